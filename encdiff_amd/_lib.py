@@ -1,0 +1,139 @@
+"""ctypes binding of libencdiff_hip.so (include/encdiff_hip.h).
+
+The library is loaded after torch so that it binds to the HIP runtime torch has
+already mapped (same SONAME libamdhip64.so.7).  There is no fallback: if the
+library is missing or a symbol is absent, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime first)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ENCDIFF_LIB", os.path.join(HERE, "libencdiff_hip.so"))
+
+# enums (mirror include/encdiff_hip.h)
+OPA_ROWK, OPA_IM2COL, OPA_ROWM = 0, 1, 2
+OPB_ROWK, OPB_ROWN, OPB_CONV_DGRAD, OPB_IM2COL = 0, 1, 2, 3
+OUT_BF16, OUT_F32, OUT_F32_ATOMIC, OUT_F32_ATOMIC_CONVW = 0, 1, 2, 3
+RESAMPLE_NONE, RESAMPLE_DOWN2, RESAMPLE_UP2 = 0, 1, 2
+(EW_COPY, EW_SILU, EW_SILU_BWD, EW_GEGLU, EW_GEGLU_BWD, EW_ADD, EW_RESAMPLE, EW_RESAMPLE_BWD,
+ EW_F32_TO_BF16, EW_BF16_TO_F32) = range(10)
+
+vp = C.c_void_p
+
+
+class ConvGeom(C.Structure):
+    _fields_ = [("batch", C.c_int), ("h", C.c_int), ("w", C.c_int), ("cin", C.c_int),
+                ("resample", C.c_int), ("pad_", C.c_int), ("ld_src", C.c_long)]
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [("M", C.c_int), ("N", C.c_int), ("K", C.c_int),
+                ("a_mode", C.c_int), ("b_mode", C.c_int), ("c_mode", C.c_int),
+                ("a", vp), ("lda", C.c_long), ("b", vp), ("ldb", C.c_long), ("c", vp), ("ldc", C.c_long),
+                ("conv", ConvGeom), ("conv_cout", C.c_int), ("convw_cin", C.c_int),
+                ("alpha", C.c_float), ("split_k", C.c_int),
+                ("bias", vp), ("resid", vp), ("ld_resid", C.c_long), ("bias_grad", vp),
+                ("tile", C.c_int), ("pad2_", C.c_int)]
+
+
+class GroupNormArgs(C.Structure):
+    _fields_ = [("batch", C.c_int), ("hw", C.c_int), ("c", C.c_int), ("groups", C.c_int),
+                ("eps", C.c_float), ("silu", C.c_int),
+                ("x", vp), ("ldx", C.c_long), ("gamma", vp), ("beta", vp),
+                ("film", vp), ("ld_film", C.c_long), ("y", vp), ("ldy", C.c_long), ("stats", vp),
+                ("dy", vp), ("lddy", C.c_long), ("dx", vp), ("lddx", C.c_long),
+                ("accumulate_dx", C.c_int), ("pad_", C.c_int),
+                ("dgamma_part", vp), ("dbeta_part", vp), ("dfilm", vp), ("ld_dfilm", C.c_long)]
+
+
+class LayerNormArgs(C.Structure):
+    _fields_ = [("rows", C.c_int), ("c", C.c_int), ("eps", C.c_float),
+                ("x", vp), ("ldx", C.c_long), ("gamma", vp), ("beta", vp), ("y", vp), ("ldy", C.c_long),
+                ("stats", vp), ("dy", vp), ("lddy", C.c_long), ("dx", vp), ("lddx", C.c_long),
+                ("accumulate_dx", C.c_int), ("dgamma_part", vp), ("dbeta_part", vp),
+                ("parts", C.c_int), ("pad_", C.c_int)]
+
+
+class AttnArgs(C.Structure):
+    _fields_ = [("batch", C.c_int), ("heads", C.c_int), ("sq", C.c_int), ("sk", C.c_int), ("dh", C.c_int),
+                ("scale", C.c_float),
+                ("q", vp), ("ldq", C.c_long), ("k", vp), ("ldk", C.c_long), ("v", vp), ("ldv", C.c_long),
+                ("o", vp), ("ldo", C.c_long), ("lse", vp),
+                ("d_o", vp), ("lddo", C.c_long), ("dq", vp), ("lddq", C.c_long),
+                ("dk", vp), ("lddk", C.c_long), ("dv", vp), ("lddv", C.c_long)]
+
+
+class EwArgs(C.Structure):
+    _fields_ = [("op", C.c_int), ("rows", C.c_int), ("cols", C.c_int),
+                ("x", vp), ("ldx", C.c_long), ("x2", vp), ("ldx2", C.c_long), ("y", vp), ("ldy", C.c_long),
+                ("accumulate", C.c_int), ("resample", C.c_int), ("batch", C.c_int), ("h", C.c_int),
+                ("w", C.c_int), ("pad_", C.c_int)]
+
+
+class SmallConvArgs(C.Structure):
+    _fields_ = [("batch", C.c_int), ("h", C.c_int), ("w", C.c_int), ("cin", C.c_int), ("cout", C.c_int),
+                ("x", vp), ("ldx", C.c_long), ("x_f32", C.c_int), ("weight", vp), ("bias", vp),
+                ("y", vp), ("ldy", C.c_long), ("y_f32", C.c_int), ("pad_", C.c_int),
+                ("dy", vp), ("lddy", C.c_long), ("dy_f32", C.c_int), ("pad2_", C.c_int),
+                ("dx", vp), ("lddx", C.c_long), ("dweight", vp), ("dbias", vp)]
+
+
+class PackJob(C.Structure):
+    _fields_ = [("src_off", C.c_longlong), ("dst_off", C.c_longlong), ("rows", C.c_int), ("cols", C.c_int),
+                ("kind", C.c_int), ("cin", C.c_int)]
+
+
+_PROTOS = {
+    "encdiff_gemm": [C.POINTER(GemmArgs), vp],
+    "encdiff_groupnorm_fwd": [C.POINTER(GroupNormArgs), vp],
+    "encdiff_groupnorm_bwd": [C.POINTER(GroupNormArgs), vp],
+    "encdiff_layernorm_fwd": [C.POINTER(LayerNormArgs), vp],
+    "encdiff_layernorm_bwd": [C.POINTER(LayerNormArgs), vp],
+    "encdiff_attention_fwd": [C.POINTER(AttnArgs), vp],
+    "encdiff_attention_bwd": [C.POINTER(AttnArgs), vp],
+    "encdiff_elementwise": [C.POINTER(EwArgs), vp],
+    "encdiff_small_conv_fwd": [C.POINTER(SmallConvArgs), vp],
+    "encdiff_small_conv_bwd": [C.POINTER(SmallConvArgs), vp],
+    "encdiff_timestep_embedding": [vp, C.c_int, C.c_int, C.c_float, vp, vp],
+    "encdiff_q_sample": [vp, vp, vp, vp, vp, C.c_int, C.c_int, vp, vp],
+    "encdiff_l1_loss": [vp, vp, vp, vp, C.c_int, C.c_int, C.c_float, vp, vp, vp],
+    "encdiff_ddim_step": [vp, vp, vp, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, vp, vp, vp],
+    "encdiff_adamw_ema": [vp, vp, vp, vp, vp, C.c_longlong, vp, C.c_longlong, vp],
+    "encdiff_pack_weights": [vp, vp, vp, C.c_int, vp],
+    "encdiff_reduce_partials": [vp, C.c_long, C.c_int, C.c_int, vp, vp, vp],
+    "encdiff_version": [],
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libencdiff_hip.so not built ({LIB_PATH}); run encdiff_amd.build.build() / "
+                          f"__graft_entry__.build()")
+    lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    for name, args in _PROTOS.items():
+        fn = getattr(lib, name)  # AttributeError == missing export: fail loudly
+        fn.argtypes = args
+        fn.restype = C.c_int
+    return lib
+
+
+lib = _load()
+EXPORTS = tuple(_PROTOS)
+
+
+class HipError(RuntimeError):
+    pass
+
+
+_ERRS = {-1: "ENCDIFF_ERR_ARG", -2: "ENCDIFF_ERR_SHAPE", -3: "ENCDIFF_ERR_UNSUPPORTED"}
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        if rc <= -1000:
+            raise HipError(f"{what}: HIP launch failure (hipError_t {-1000 - rc})")
+        raise HipError(f"{what}: {_ERRS.get(rc, rc)}")

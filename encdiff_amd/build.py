@@ -1,0 +1,72 @@
+"""Build libencdiff_hip.so (gfx950) in-tree with hipcc.
+
+The library is a plain C-ABI shared object (include/encdiff_hip.h); it is built
+next to this file so that it travels with the repository snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libencdiff_hip.so")
+OBJ = os.path.join(HERE, "_build")
+ARCH = os.environ.get("ENCDIFF_ARCH", "gfx950")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast",
+         "-I" + os.path.join(REPO, "include")]
+
+
+def _sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+
+
+def _headers():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hs.append(os.path.join(REPO, "include", "encdiff_hip.h"))
+    return hs
+
+
+def _compile(src: str, obj: str, verbose: bool):
+    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+    return obj
+
+
+def build(force: bool = False, verbose: bool = False, lib: str = LIB, sources=None, jobs: int = 8) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    srcs = sources or _sources()
+    hdr_mtime = max(os.path.getmtime(h) for h in _headers())
+    todo = []
+    objs = []
+    for s in srcs:
+        o = os.path.join(OBJ, os.path.basename(s) + f".{ARCH}.o")
+        objs.append(o)
+        if force or not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr_mtime):
+            todo.append((s, o))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=min(jobs, len(todo))) as ex:
+            list(ex.map(lambda so: _compile(so[0], so[1], verbose), todo))
+    if force or todo or not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(o) for o in objs):
+        tmp = lib + ".tmp"
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+        os.replace(tmp, lib)
+    return lib
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,59 @@
+// Shared device helpers for the EncDiff gfx950 kernels.
+// All activations are NHWC / token-major bf16 ([rows][channels] with a row
+// stride `ld` in elements); statistics and master weights are fp32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/encdiff_hip.h"
+
+typedef uint16_t bf16_t;  // raw bf16 bits in memory
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __bf16 v4bf __attribute__((ext_vector_type(4)));
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+
+#define ED_DEV __device__ __forceinline__
+
+ED_DEV float bf2f(bf16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+ED_DEV bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN preserving
+  return __builtin_bit_cast(bf16_t, b);
+}
+ED_DEV uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+
+// 8 bf16 <-> 8 float
+ED_DEV void unpack8(const uint4& u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
+  }
+}
+ED_DEV uint4 pack8(const float* f) {
+  uint4 u;
+  u.x = pack2(f[0], f[1]); u.y = pack2(f[2], f[3]);
+  u.z = pack2(f[4], f[5]); u.w = pack2(f[6], f[7]);
+  return u;
+}
+
+ED_DEV float silu_f(float z) { return z / (1.0f + __expf(-z)); }
+ED_DEV float silu_grad(float z) {
+  float s = 1.0f / (1.0f + __expf(-z));
+  return s * (1.0f + z * (1.0f - s));
+}
+
+ED_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Error codes of the C-ABI (see include/encdiff_hip.h)
+#define ED_CHECK_LAUNCH()                                   \
+  do {                                                      \
+    hipError_t _e = hipGetLastError();                      \
+    if (_e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)_e; \
+  } while (0)

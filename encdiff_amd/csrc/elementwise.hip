@@ -1,0 +1,531 @@
+// elementwise.hip -- memory-bound kernels of the EncDiff step: activations,
+// GEGLU, resampling, the UNet's 3-channel input/output convolutions, the
+// diffusion-side math (timestep embedding, q_sample, L1 loss, DDIM update) and
+// the fused AdamW + EMA + bf16 weight pack over the flat parameter arena.
+#include "common.h"
+
+namespace {
+
+ED_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+ED_DEV float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// One thread per 8 contiguous output elements of a row ([rows][cols], cols % 8 == 0).
+__global__ __launch_bounds__(256) void ew_kernel(const EncdiffEwArgs p) {
+  const int vpr = p.cols >> 3;
+  const long total = (long)p.rows * vpr;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(idx / vpr);
+    const int c = (int)(idx - (long)r * vpr) * 8;
+    const bf16_t* X = (const bf16_t*)p.x;
+    bf16_t* Y = (bf16_t*)p.y;
+    float out[8];
+    switch (p.op) {
+      case ENCDIFF_EW_COPY: unpack8(*(const uint4*)(X + (long)r * p.ldx + c), out); break;
+      case ENCDIFF_EW_SILU: {
+        unpack8(*(const uint4*)(X + (long)r * p.ldx + c), out);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) out[i] = silu_f(out[i]);
+      } break;
+      case ENCDIFF_EW_SILU_BWD: {  // x = pre-activation, x2 = dy
+        float d[8];
+        unpack8(*(const uint4*)(X + (long)r * p.ldx + c), out);
+        unpack8(*(const uint4*)((const bf16_t*)p.x2 + (long)r * p.ldx2 + c), d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) out[i] = d[i] * silu_grad(out[i]);
+      } break;
+      case ENCDIFF_EW_GEGLU: {  // x: [rows][2*cols]
+        float a[8], g[8];
+        unpack8(*(const uint4*)(X + (long)r * p.ldx + c), a);
+        unpack8(*(const uint4*)(X + (long)r * p.ldx + p.cols + c), g);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) out[i] = a[i] * gelu_erf(g[i]);
+      } break;
+      case ENCDIFF_EW_GEGLU_BWD: {  // x: [rows][2*cols] proj output, x2 = dy [rows][cols]; y: [rows][2*cols]
+        float a[8], g[8], d[8], da[8], dg[8];
+        unpack8(*(const uint4*)(X + (long)r * p.ldx + c), a);
+        unpack8(*(const uint4*)(X + (long)r * p.ldx + p.cols + c), g);
+        unpack8(*(const uint4*)((const bf16_t*)p.x2 + (long)r * p.ldx2 + c), d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          da[i] = d[i] * gelu_erf(g[i]);
+          dg[i] = d[i] * a[i] * gelu_erf_grad(g[i]);
+        }
+        *(uint4*)(Y + (long)r * p.ldy + c) = pack8(da);
+        *(uint4*)(Y + (long)r * p.ldy + p.cols + c) = pack8(dg);
+        continue;
+      }
+      case ENCDIFF_EW_ADD: {
+        float d[8];
+        unpack8(*(const uint4*)(X + (long)r * p.ldx + c), out);
+        unpack8(*(const uint4*)((const bf16_t*)p.x2 + (long)r * p.ldx2 + c), d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) out[i] += d[i];
+      } break;
+      case ENCDIFF_EW_RESAMPLE: {  // output pixel r at (h, w)
+        const int hw = p.h * p.w;
+        const int b = r / hw, rem = r - b * hw, y = rem / p.w, x = rem - (rem / p.w) * p.w;
+        if (p.resample == ENCDIFF_RESAMPLE_DOWN2) {
+          const int W2 = 2 * p.w;
+          const long r0 = ((long)b * 2 * p.h + 2 * y) * W2 + 2 * x;
+          float t[8];
+          unpack8(*(const uint4*)(X + r0 * p.ldx + c), out);
+          unpack8(*(const uint4*)(X + (r0 + 1) * p.ldx + c), t);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) out[i] += t[i];
+          unpack8(*(const uint4*)(X + (r0 + W2) * p.ldx + c), t);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) out[i] += t[i];
+          unpack8(*(const uint4*)(X + (r0 + W2 + 1) * p.ldx + c), t);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) out[i] = (out[i] + t[i]) * 0.25f;
+        } else {
+          const long rs = ((long)b * (p.h >> 1) + (y >> 1)) * (p.w >> 1) + (x >> 1);
+          unpack8(*(const uint4*)(X + rs * p.ldx + c), out);
+        }
+      } break;
+      case ENCDIFF_EW_RESAMPLE_BWD: {  // adjoint: output (h, w) = forward source dims
+        const int hw = p.h * p.w;
+        const int b = r / hw, rem = r - b * hw, y = rem / p.w, x = rem - (rem / p.w) * p.w;
+        if (p.resample == ENCDIFF_RESAMPLE_DOWN2) {  // fwd (h,w)->(h/2,w/2): dx = 0.25 dy[y/2][x/2]
+          const long rs = ((long)b * (p.h >> 1) + (y >> 1)) * (p.w >> 1) + (x >> 1);
+          unpack8(*(const uint4*)(X + rs * p.ldx + c), out);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) out[i] *= 0.25f;
+        } else {  // fwd (h,w)->(2h,2w) nearest: dx = sum of the 4 children
+          const int W2 = 2 * p.w;
+          const long r0 = ((long)b * 2 * p.h + 2 * y) * W2 + 2 * x;
+          float t[8];
+          unpack8(*(const uint4*)(X + r0 * p.ldx + c), out);
+          unpack8(*(const uint4*)(X + (r0 + 1) * p.ldx + c), t);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) out[i] += t[i];
+          unpack8(*(const uint4*)(X + (r0 + W2) * p.ldx + c), t);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) out[i] += t[i];
+          unpack8(*(const uint4*)(X + (r0 + W2 + 1) * p.ldx + c), t);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) out[i] += t[i];
+        }
+      } break;
+      case ENCDIFF_EW_F32_TO_BF16: {
+        const float* Xf = (const float*)p.x + (long)r * p.ldx + c;
+        const float4 a = *(const float4*)Xf, b = *(const float4*)(Xf + 4);
+        out[0] = a.x; out[1] = a.y; out[2] = a.z; out[3] = a.w;
+        out[4] = b.x; out[5] = b.y; out[6] = b.z; out[7] = b.w;
+      } break;
+      case ENCDIFF_EW_BF16_TO_F32: {
+        unpack8(*(const uint4*)(X + (long)r * p.ldx + c), out);
+        float* Yf = (float*)p.y + (long)r * p.ldy + c;
+        if (p.accumulate) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) Yf[i] += out[i];
+        } else {
+          *(float4*)Yf = make_float4(out[0], out[1], out[2], out[3]);
+          *(float4*)(Yf + 4) = make_float4(out[4], out[5], out[6], out[7]);
+        }
+        continue;
+      }
+      default: return;
+    }
+    bf16_t* yp = Y + (long)r * p.ldy + c;
+    if (p.accumulate) {
+      float prev[8];
+      unpack8(*(const uint4*)yp, prev);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) out[i] += prev[i];
+    }
+    *(uint4*)yp = pack8(out);
+  }
+}
+
+// ------------------------------------------------ 3-channel convolutions (VALU)
+// input conv (cin = 3): x fp32 NCHW -> y bf16 NHWC.  thread per (pixel, co)
+__global__ __launch_bounds__(256) void small_conv_in_fwd(const EncdiffSmallConvArgs p) {
+  __shared__ float w[64 * 27 + 64];
+  const int CO = p.cout, CI = p.cin, HW = p.h * p.w;
+  for (int i = threadIdx.x; i < CO * CI * 9; i += 256) w[i] = p.weight[i];
+  for (int i = threadIdx.x; i < CO; i += 256) w[CO * CI * 9 + i] = p.bias[i];
+  __syncthreads();
+  const long total = (long)p.batch * HW * CO;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const int co = (int)(idx % CO);
+    const long pix = idx / CO;
+    const int b = (int)(pix / HW), rem = (int)(pix - (long)b * HW);
+    const int y = rem / p.w, x = rem - y * p.w;
+    float acc = w[CO * CI * 9 + co];
+    const float* X = (const float*)p.x + (long)b * CI * HW;
+    for (int ci = 0; ci < CI; ++ci)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+        if (yy >= 0 && yy < p.h && xx >= 0 && xx < p.w)
+          acc += w[(co * CI + ci) * 9 + t] * X[(long)ci * HW + yy * p.w + xx];
+      }
+    ((bf16_t*)p.y)[pix * p.ldy + co] = f2bf(acc);
+  }
+}
+
+// output conv (cout = 3): x bf16 NHWC [pix][cin] -> y fp32 NCHW.  thread per pixel
+__global__ __launch_bounds__(256) void small_conv_out_fwd(const EncdiffSmallConvArgs p) {
+  __shared__ float w[3 * 9 * 512 + 3];
+  const int CO = p.cout, CI = p.cin, HW = p.h * p.w;
+  // weight reordered to [co][tap][ci]
+  for (int i = threadIdx.x; i < CO * CI * 9; i += 256) {
+    const int co = i / (CI * 9), rem = i - co * CI * 9, ci = rem / 9, t = rem - ci * 9;
+    w[(co * 9 + t) * CI + ci] = p.weight[i];
+  }
+  for (int i = threadIdx.x; i < CO; i += 256) w[CO * CI * 9 + i] = p.bias[i];
+  __syncthreads();
+  const long total = (long)p.batch * HW;
+  for (long pix = blockIdx.x * 256L + threadIdx.x; pix < total; pix += (long)gridDim.x * 256) {
+    const int b = (int)(pix / HW), rem = (int)(pix - (long)b * HW);
+    const int y = rem / p.w, x = rem - y * p.w;
+    float acc[3] = {0.f, 0.f, 0.f};
+    for (int t = 0; t < 9; ++t) {
+      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+      if (yy < 0 || yy >= p.h || xx < 0 || xx >= p.w) continue;
+      const bf16_t* src = (const bf16_t*)p.x + ((long)b * HW + yy * p.w + xx) * p.ldx;
+      for (int ci = 0; ci < CI; ci += 8) {
+        float v[8];
+        unpack8(*(const uint4*)(src + ci), v);
+#pragma unroll
+        for (int co = 0; co < 3; ++co)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) acc[co] += v[i] * w[(co * 9 + t) * CI + ci + i];
+      }
+    }
+    float* Y = (float*)p.y + (long)b * CO * HW + rem;
+    for (int co = 0; co < CO; ++co) Y[(long)co * HW] = acc[co] + w[CO * CI * 9 + co];
+  }
+}
+
+// dx of the output conv: dy fp32 NCHW [b][3][hw] -> dx bf16 NHWC [pix][cin].  thread per (pix, 8 ci)
+__global__ __launch_bounds__(256) void small_conv_out_dgrad(const EncdiffSmallConvArgs p) {
+  __shared__ float w[3 * 9 * 512];
+  const int CO = p.cout, CI = p.cin, HW = p.h * p.w;
+  for (int i = threadIdx.x; i < CO * CI * 9; i += 256) w[i] = p.weight[i];  // [co][ci][tap]
+  __syncthreads();
+  const int vpp = CI / 8;
+  const long total = (long)p.batch * HW * vpp;
+  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const long pix = idx / vpp;
+    const int ci0 = (int)(idx - pix * vpp) * 8;
+    const int b = (int)(pix / HW), rem = (int)(pix - (long)b * HW);
+    const int y = rem / p.w, x = rem - y * p.w;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float* DY = (const float*)p.dy + (long)b * CO * HW;
+    for (int t = 0; t < 9; ++t) {
+      // output pixel o = in - (t offset): y_out = y - (t/3 - 1)
+      const int yo = y - (t / 3 - 1), xo = x - (t % 3 - 1);
+      if (yo < 0 || yo >= p.h || xo < 0 || xo >= p.w) continue;
+      for (int co = 0; co < CO; ++co) {
+        const float d = DY[(long)co * HW + yo * p.w + xo];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += d * w[(co * CI + ci0 + i) * 9 + t];
+      }
+    }
+    *(uint4*)((bf16_t*)p.dx + pix * p.lddx + ci0) = pack8(acc);
+  }
+}
+
+// weight/bias gradient of either small conv.  One block per group of images; each
+// thread owns output weights o = tid + 256 k over (co, ci, tap); sums over pixels.
+// in-conv: x fp32 NCHW, dy bf16 NHWC [pix][co];  out-conv: x bf16 NHWC, dy fp32 NCHW.
+__global__ __launch_bounds__(256) void small_conv_wgrad(const EncdiffSmallConvArgs p, int imgs_per_block) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int CO = p.cout, CI = p.cin, HW = p.h * p.w;
+  float* xs = sm;              // [CI][HW]
+  float* ds = sm + CI * HW;    // [CO][HW]
+  const int NW = CO * CI * 9;
+  float acc[8];
+  float bacc = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const int b0 = blockIdx.x * imgs_per_block;
+  for (int b = b0; b < min(p.batch, b0 + imgs_per_block); ++b) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < CI * HW; i += 256) {
+      const int ci = i / HW, px = i - ci * HW;
+      xs[i] = p.x_f32 ? ((const float*)p.x)[(long)b * CI * HW + i]
+                      : bf2f(((const bf16_t*)p.x)[((long)b * HW + px) * p.ldx + ci]);
+    }
+    for (int i = threadIdx.x; i < CO * HW; i += 256) {
+      const int co = i / HW, px = i - co * HW;
+      ds[i] = p.dy_f32 ? ((const float*)p.dy)[(long)b * CO * HW + i]
+                       : bf2f(((const bf16_t*)p.dy)[((long)b * HW + px) * p.lddy + co]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int o = threadIdx.x + 256 * k;
+      if (o >= NW) break;
+      const int co = o / (CI * 9), rem = o - co * CI * 9, ci = rem / 9, t = rem - ci * 9;
+      const int dy_ = t / 3 - 1, dx_ = t % 3 - 1;
+      float a = 0.f;
+      for (int y = 0; y < p.h; ++y) {
+        const int yy = y + dy_;
+        if (yy < 0 || yy >= p.h) continue;
+        for (int x = 0; x < p.w; ++x) {
+          const int xx = x + dx_;
+          if (xx < 0 || xx >= p.w) continue;
+          a += ds[co * HW + y * p.w + x] * xs[ci * HW + yy * p.w + xx];
+        }
+      }
+      acc[k] += a;
+    }
+    if (threadIdx.x < CO) {
+      float a = 0.f;
+      for (int px = 0; px < HW; ++px) a += ds[threadIdx.x * HW + px];
+      bacc += a;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int o = threadIdx.x + 256 * k;
+    if (o < NW) atomicAdd(p.dweight + o, acc[k]);
+  }
+  if (threadIdx.x < CO && p.dbias) atomicAdd(p.dbias + threadIdx.x, bacc);
+}
+
+// ------------------------------------------------ diffusion math
+__global__ void temb_kernel(const long long* t, int batch, int dim, float max_period, bf16_t* out) {
+  const int half = dim / 2;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= batch * half) return;
+  const int b = i / half, k = i - b * half;
+  // util.py:185-189, fp32: exp(-ln(max_period) * k / half)
+  const float freq = __expf((-logf(max_period) * (float)k) / (float)half);
+  const float arg = (float)t[b] * freq;
+  out[b * dim + k] = f2bf(cosf(arg));
+  out[b * dim + half + k] = f2bf(sinf(arg));
+}
+
+__global__ void qsample_kernel(const float* x0, const float* eps, const long long* t, const float* sa,
+                               const float* s1a, int batch, int per, float* xt) {
+  const long n = (long)batch * per;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / per);
+    const long long tt = t[b];
+    xt[i] = sa[tt] * x0[i] + s1a[tt] * eps[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void l1_kernel(const float* pred, const float* eps, const long long* t,
+                                                 const float* lvlb, int batch, int per, float lsw, float* out2,
+                                                 float* grad) {
+  __shared__ float red[4];
+  const int b = blockIdx.x;
+  float s = 0.f;
+  const float gscale = lsw / ((float)batch * per);
+  for (int i = threadIdx.x; i < per; i += 256) {
+    const long j = (long)b * per + i;
+    const float d = pred[j] - eps[j];
+    s += fabsf(d);
+    if (grad) grad[j] = (d > 0.f ? gscale : (d < 0.f ? -gscale : 0.f));
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float ls = (red[0] + red[1] + red[2] + red[3]) / (float)per;  // loss_simple[b]
+    atomicAdd(out2, lsw * ls / (float)batch);
+    atomicAdd(out2 + 1, lvlb[t[b]] * ls / (float)batch);
+  }
+}
+
+__global__ void ddim_kernel(const float* x, const float* e, const float* z, int n, float a_t, float a_prev,
+                            float sigma, float s1, float* xp, float* px0) {
+  const float rs = 1.f / sqrtf(a_t);
+  const float sap = sqrtf(a_prev);
+  const float dcoef = sqrtf(1.f - a_prev - sigma * sigma);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float ee = e[i];
+    const float p0 = (x[i] - s1 * ee) * rs;
+    if (px0) px0[i] = p0;
+    xp[i] = sap * p0 + dcoef * ee + (z ? sigma * z[i] : 0.f);
+  }
+}
+
+// ------------------------------------------------ optimizer
+__global__ __launch_bounds__(256) void adamw_ema_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        float* __restrict__ ema, long long n,
+                                                        const float* __restrict__ hyper, long long ema_n) {
+  const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
+  const float step_size = hyper[5], inv_bc2_sqrt = hyper[6], omd = hyper[7];
+  const long long n4 = n >> 2;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    float4 pp = ((float4*)p)[i], gg = ((const float4*)g)[i], mm = ((float4*)m)[i], vv = ((float4*)v)[i];
+    float* pa = &pp.x; const float* ga = &gg.x; float* ma = &mm.x; float* va = &vv.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      // torch.optim.AdamW (single-tensor): decoupled decay, lerp for m, addcmul for v
+      pa[k] *= (1.f - lr * wd);
+      ma[k] = ma[k] + (1.f - b1) * (ga[k] - ma[k]);
+      va[k] = b2 * va[k] + (1.f - b2) * ga[k] * ga[k];
+      const float denom = sqrtf(va[k]) * inv_bc2_sqrt + eps;
+      pa[k] -= step_size * ma[k] / denom;
+    }
+    ((float4*)p)[i] = pp; ((float4*)m)[i] = mm; ((float4*)v)[i] = vv;
+    if (ema && 4 * i < ema_n) {  // LitEma.forward (ema.py:37-42): s -= (1 - decay) (s - p)
+      float4 ee = ((float4*)ema)[i];
+      float* ea = &ee.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (4 * i + k < ema_n) ea[k] -= omd * (ea[k] - pa[k]);
+      ((float4*)ema)[i] = ee;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst,
+                                                   const EncdiffPackJob* __restrict__ jobs) {
+  const EncdiffPackJob j = jobs[blockIdx.y];
+  const long total = (long)j.rows * j.cols;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / j.cols), c = (int)(i - (long)r * j.cols);
+    long s;
+    if (j.kind == 1) {  // conv [co][ci][3][3] -> [co][tap][ci]; c = tap*cin + ci
+      const int tap = c / j.cin, ci = c - tap * j.cin;
+      s = (long)r * j.cols + ci * 9 + tap;
+    } else {
+      s = i;
+    }
+    dst[j.dst_off + i] = f2bf(src[j.src_off + s]);
+  }
+}
+
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const float* part, long ld, int rows, int cols,
+                                                              const int* idx, float* grad) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= cols) return;
+  float s = 0.f;
+  for (int r = 0; r < rows; ++r) s += part[(long)r * ld + j];
+  grad[idx[j]] += s;
+}
+
+int grid_for(long n, int per_thread = 1) {
+  long g = (n / per_thread + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+extern "C" int encdiff_elementwise(const EncdiffEwArgs* a, void* stream) {
+  if (!a || !a->x || !a->y) return ENCDIFF_ERR_ARG;
+  if (a->cols % 8) return ENCDIFF_ERR_SHAPE;
+  hipLaunchKernelGGL(ew_kernel, dim3(grid_for((long)a->rows * a->cols, 8)), dim3(256), 0, (hipStream_t)stream, *a);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_small_conv_fwd(const EncdiffSmallConvArgs* a, void* stream) {
+  if (!a || !a->x || !a->y || !a->weight || !a->bias) return ENCDIFF_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const long pix = (long)a->batch * a->h * a->w;
+  if (a->x_f32 && !a->y_f32) {  // input conv
+    if (a->cout * a->cin * 9 + a->cout > 64 * 27 + 64) return ENCDIFF_ERR_SHAPE;
+    hipLaunchKernelGGL(small_conv_in_fwd, dim3(grid_for(pix * a->cout)), dim3(256), 0, s, *a);
+  } else if (!a->x_f32 && a->y_f32) {  // output conv
+    if (a->cout > 3 || a->cin > 512 || a->cin % 8) return ENCDIFF_ERR_SHAPE;
+    hipLaunchKernelGGL(small_conv_out_fwd, dim3(grid_for(pix)), dim3(256), 0, s, *a);
+  } else {
+    return ENCDIFF_ERR_UNSUPPORTED;
+  }
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_small_conv_bwd(const EncdiffSmallConvArgs* a, void* stream) {
+  if (!a || !a->x || !a->dy || !a->weight) return ENCDIFF_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int HW = a->h * a->w;
+  if (a->cout * a->cin * 9 > 256 * 8) return ENCDIFF_ERR_SHAPE;
+  if (a->dx) {
+    if (!a->dy_f32 || a->cout > 3 || a->cin % 8) return ENCDIFF_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(small_conv_out_dgrad, dim3(grid_for((long)a->batch * HW * (a->cin / 8))), dim3(256), 0, s,
+                       *a);
+    ED_CHECK_LAUNCH();
+  }
+  if (a->dweight) {
+    const size_t lds = (size_t)(a->cin + a->cout) * HW * sizeof(float);
+    if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
+    static const hipError_t attr = hipFuncSetAttribute((const void*)small_conv_wgrad,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)attr;
+    const int ipb = 4;
+    hipLaunchKernelGGL(small_conv_wgrad, dim3((a->batch + ipb - 1) / ipb), dim3(256), lds, s, *a, ipb);
+    ED_CHECK_LAUNCH();
+  }
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_timestep_embedding(const long long* t, int batch, int dim, float max_period, void* out,
+                                          void* stream) {
+  if (!t || !out || dim % 2) return ENCDIFF_ERR_ARG;
+  const int n = batch * dim / 2;
+  hipLaunchKernelGGL(temb_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, t, batch, dim,
+                     max_period, (bf16_t*)out);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_q_sample(const float* x0, const float* eps, const long long* t, const float* sa,
+                                const float* s1a, int batch, int per, float* xt, void* stream) {
+  if (!x0 || !eps || !t || !sa || !s1a || !xt) return ENCDIFF_ERR_ARG;
+  hipLaunchKernelGGL(qsample_kernel, dim3(grid_for((long)batch * per)), dim3(256), 0, (hipStream_t)stream, x0, eps,
+                     t, sa, s1a, batch, per, xt);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_l1_loss(const float* pred, const float* eps, const long long* t, const float* lvlb, int batch,
+                               int per, float lsw, float* out2, float* grad, void* stream) {
+  if (!pred || !eps || !t || !lvlb || !out2) return ENCDIFF_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(out2, 0, 2 * sizeof(float), s);
+  if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+  hipLaunchKernelGGL(l1_kernel, dim3(batch), dim3(256), 0, s, pred, eps, t, lvlb, batch, per, lsw, out2, grad);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_ddim_step(const float* x, const float* e, const float* noise, int n, float a_t, float a_prev,
+                                 float sigma, float s1, float* xp, float* px0, void* stream) {
+  if (!x || !e || !xp) return ENCDIFF_ERR_ARG;
+  hipLaunchKernelGGL(ddim_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, e, noise, n, a_t, a_prev,
+                     sigma, s1, xp, px0);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_adamw_ema(float* p, const float* g, float* m, float* v, float* ema, long long n,
+                                 const float* hyper, long long ema_n, void* stream) {
+  if (!p || !g || !m || !v || !hyper || n % 4) return ENCDIFF_ERR_ARG;
+  hipLaunchKernelGGL(adamw_ema_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, ema, n,
+                     hyper, ema_n);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_pack_weights(const float* src, void* dst, const EncdiffPackJob* jobs, int njobs, void* stream) {
+  if (!src || !dst || !jobs || njobs <= 0 || njobs > 65535) return ENCDIFF_ERR_ARG;
+  hipLaunchKernelGGL(pack_kernel, dim3(64, njobs), dim3(256), 0, (hipStream_t)stream, src, (bf16_t*)dst, jobs);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_reduce_partials(const float* part, long ld, int rows, int cols, const int* idx, float* grad,
+                                       void* stream) {
+  if (!part || !idx || !grad || cols <= 0) return ENCDIFF_ERR_ARG;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((cols + 255) / 256), dim3(256), 0, (hipStream_t)stream, part, ld,
+                     rows, cols, idx, grad);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}

@@ -1,0 +1,389 @@
+// gemm.hip -- one MFMA GEMM engine for every conv / linear of the EncDiff UNet.
+//
+// C[M][N] = alpha * A[M][K] * B[K][N] (+bias)(+resid), bf16 operands, fp32 accumulate,
+// v_mfma_f32_16x16x32_bf16 on gfx950.  256 threads = 4 waves in a 2x2 layout, each
+// wave owns a (BM/2)x(BN/2) sub-tile.  K is staged 64 at a time through
+// double-buffered LDS with register staging (global_load_dwordx4 -> ds_write_b128).
+//
+// Operands are loaded in their natural global layout ("k-inner": rows of K,
+// read as MFMA fragments with ds_read_b128; "k-outer": rows of M/N, read with the
+// gfx950 transpose read ds_read_b64_tr_b16), so the same engine runs
+//   forward   conv3x3  : A = implicit im2col(x) [pixels][9*Cin], B = W [Cout][9*Cin]
+//   dgrad     conv3x3  : A = im2col(dY),   B = W read through a flipped-tap map
+//   wgrad     conv3x3  : A = dY^T (k-outer), B = im2col(x) (k-outer), split-K, atomics
+//   linear fwd / dgrad / wgrad likewise with dense operands.
+// Replaces: openaimodel_enc.py:204,230,237-241,508-512,521,687; attention.py:159-167,
+// 43,58,233-259 (every Conv2d / Linear forward and their autograd backward).
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 64;
+constexpr int PADK = 8;   // k-inner tile row = BK + PADK elements (144 B: ds_read_b128 conflict-free)
+constexpr int PADN = 8;   // k-outer tile row = COLS + PADN elements
+
+enum { A_ROWK = ENCDIFF_OPA_ROWK, A_IM2COL = ENCDIFF_OPA_IM2COL, A_ROWM = ENCDIFF_OPA_ROWM };
+enum { B_ROWK = ENCDIFF_OPB_ROWK, B_ROWN = ENCDIFF_OPB_ROWN, B_CONVD = ENCDIFF_OPB_CONV_DGRAD,
+       B_IM2COL = ENCDIFF_OPB_IM2COL };
+
+template <int AM> struct AKInner { static constexpr bool v = AM != A_ROWM; };
+template <int BMd> struct BKInner { static constexpr bool v = BMd == B_ROWK; };
+
+template <int ROWS, bool KINNER>
+struct TileShape {
+  // k-inner: [ROWS][BK+PADK]; k-outer: [BK][ROWS+PADN]
+  static constexpr int LD = KINNER ? (BK + PADK) : (ROWS + PADN);
+  static constexpr int ELEMS = KINNER ? ROWS * (BK + PADK) : BK * (ROWS + PADN);
+  static constexpr int CHUNKS = ROWS * BK / 8;  // 16-byte chunks per tile
+  static constexpr int PER_THREAD = CHUNKS / 256;
+};
+
+// ---------------------------------------------------------------------------
+// implicit im2col: 8 consecutive channels [c, c+8) of tap `tap` at output pixel (b, y, x)
+ED_DEV uint4 im2col8(const bf16_t* __restrict__ src, const EncdiffConvGeom& g, int b, int y, int x,
+                     int tap, int c) {
+  const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+  uint4 z = {0u, 0u, 0u, 0u};
+  if (yy < 0 || yy >= g.h || xx < 0 || xx >= g.w) return z;
+  if (g.resample == ENCDIFF_RESAMPLE_NONE) {
+    const long row = ((long)b * g.h + yy) * g.w + xx;
+    return *(const uint4*)(src + row * g.ld_src + c);
+  } else if (g.resample == ENCDIFF_RESAMPLE_DOWN2) {
+    const int W2 = 2 * g.w;
+    const long r0 = ((long)b * 2 * g.h + 2 * yy) * W2 + 2 * xx;
+    float a[8], t[8];
+    unpack8(*(const uint4*)(src + r0 * g.ld_src + c), a);
+    unpack8(*(const uint4*)(src + (r0 + 1) * g.ld_src + c), t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] += t[i];
+    unpack8(*(const uint4*)(src + (r0 + W2) * g.ld_src + c), t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] += t[i];
+    unpack8(*(const uint4*)(src + (r0 + W2 + 1) * g.ld_src + c), t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = (a[i] + t[i]) * 0.25f;
+    return pack8(a);
+  } else {
+    const int Hh = g.h >> 1, Wh = g.w >> 1;
+    const long row = ((long)b * Hh + (yy >> 1)) * Wh + (xx >> 1);
+    return *(const uint4*)(src + row * g.ld_src + c);
+  }
+}
+
+template <int BM, int BN, int AM, int BMD>
+struct Gemm {
+  static constexpr bool AKI = AKInner<AM>::v;
+  static constexpr bool BKI = BKInner<BMD>::v;
+  using TA = TileShape<BM, AKI>;
+  using TB = TileShape<BN, BKI>;
+  static constexpr int TM = BM / 32;  // 16x16 MFMA tiles per wave along M
+  static constexpr int TN = BN / 32;
+  static constexpr int STAGE = TA::ELEMS + TB::ELEMS;  // elements per LDS stage
+};
+
+template <int BM, int BN, int AM, int BMD>
+__global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p) {
+  using G = Gemm<BM, BN, AM, BMD>;
+  using TA = typename G::TA;
+  using TB = typename G::TB;
+  constexpr bool AKI = G::AKI, BKI = G::BKI;
+  constexpr int TM = G::TM, TN = G::TN;
+
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = (wave >> 1) * (BM / 2);
+  const int wc = (wave & 1) * (BN / 2);
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+
+  // split-K range
+  const int ktiles_total = (p.K + BK - 1) / BK;
+  const int kt_per = (ktiles_total + p.split_k - 1) / p.split_k;
+  const int kt_begin = blockIdx.z * kt_per;
+  const int kt_end = min(ktiles_total, kt_begin + kt_per);
+  const int nkt = kt_end - kt_begin;
+
+  const bf16_t* __restrict__ A = (const bf16_t*)p.a;
+  const bf16_t* __restrict__ B = (const bf16_t*)p.b;
+
+  // ---- per-thread fixed coordinates for the gathers ---------------------
+  // A k-inner: row = c>>3 fixed per chunk; IM2COL needs pixel coords of that row
+  int a_pb[TA::PER_THREAD], a_py[TA::PER_THREAD], a_px[TA::PER_THREAD];
+  if constexpr (AM == A_IM2COL) {
+#pragma unroll
+    for (int i = 0; i < TA::PER_THREAD; ++i) {
+      const int c = tid + 256 * i;
+      const int m = m0 + (c >> 3);
+      const int hw = p.conv.h * p.conv.w;
+      const int b = m / hw, r = m - b * hw;
+      a_pb[i] = (m < p.M) ? b : -1;
+      a_py[i] = r / p.conv.w;
+      a_px[i] = r - a_py[i] * p.conv.w;
+    }
+  }
+  // B k-outer IM2COL: column n = (tap, ci) fixed per chunk
+  int b_tap[TB::PER_THREAD], b_ci[TB::PER_THREAD];
+  if constexpr (BMD == B_IM2COL) {
+#pragma unroll
+    for (int i = 0; i < TB::PER_THREAD; ++i) {
+      const int c = tid + 256 * i;
+      const int n = n0 + (c % (BN / 8)) * 8;
+      b_tap[i] = n / p.conv.cin;
+      b_ci[i] = n - b_tap[i] * p.conv.cin;
+    }
+  }
+
+  uint4 ra[TA::PER_THREAD], rb[TB::PER_THREAD];
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < TA::PER_THREAD; ++i) {
+      const int c = tid + 256 * i;
+      uint4 v = {0u, 0u, 0u, 0u};
+      if constexpr (AKI) {
+        const int row = c >> 3;
+        const int k = k0 + (c & 7) * 8;
+        const int m = m0 + row;
+        if constexpr (AM == A_ROWK) {
+          if (m < p.M && k < p.K) v = *(const uint4*)(A + (long)m * p.lda + k);
+        } else {  // IM2COL
+          if (a_pb[i] >= 0 && k < p.K) {
+            const int tap = k / p.conv.cin;
+            v = im2col8(A, p.conv, a_pb[i], a_py[i], a_px[i], tap, k - tap * p.conv.cin);
+          }
+        }
+      } else {  // A_ROWM: tile [BK][BM]
+        const int row = c / (BM / 8);
+        const int col = (c % (BM / 8)) * 8;
+        const int k = k0 + row, m = m0 + col;
+        if (k < p.K && m < p.M) v = *(const uint4*)(A + (long)k * p.lda + m);
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < TB::PER_THREAD; ++i) {
+      const int c = tid + 256 * i;
+      uint4 v = {0u, 0u, 0u, 0u};
+      if constexpr (BKI) {  // B_ROWK: Bt[n][k]
+        const int row = c >> 3;
+        const int k = k0 + (c & 7) * 8;
+        const int n = n0 + row;
+        if (n < p.N && k < p.K) v = *(const uint4*)(B + (long)n * p.ldb + k);
+      } else {
+        const int row = c / (BN / 8);
+        const int col = (c % (BN / 8)) * 8;
+        const int k = k0 + row, n = n0 + col;
+        if (k < p.K && n < p.N) {
+          if constexpr (BMD == B_ROWN) {
+            v = *(const uint4*)(B + (long)k * p.ldb + n);
+          } else if constexpr (BMD == B_CONVD) {
+            const int tap = k / p.conv_cout;
+            const int co = k - tap * p.conv_cout;
+            v = *(const uint4*)(B + (long)co * p.ldb + (long)(8 - tap) * p.N + n);
+          } else {  // B_IM2COL: row = pixel k
+            const int hw = p.conv.h * p.conv.w;
+            const int b = k / hw, r = k - b * hw;
+            const int y = r / p.conv.w, x = r - y * p.conv.w;
+            v = im2col8(B, p.conv, b, y, x, b_tap[i], b_ci[i]);
+          }
+        }
+      }
+      rb[i] = v;
+    }
+  };
+
+  auto store_tile = [&](bf16_t* s) {
+    bf16_t* sa = s;
+    bf16_t* sb = s + TA::ELEMS;
+#pragma unroll
+    for (int i = 0; i < TA::PER_THREAD; ++i) {
+      const int c = tid + 256 * i;
+      if constexpr (AKI) {
+        *(uint4*)(sa + (c >> 3) * TA::LD + (c & 7) * 8) = ra[i];
+      } else {
+        *(uint4*)(sa + (c / (BM / 8)) * TA::LD + (c % (BM / 8)) * 8) = ra[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TB::PER_THREAD; ++i) {
+      const int c = tid + 256 * i;
+      if constexpr (BKI) {
+        *(uint4*)(sb + (c >> 3) * TB::LD + (c & 7) * 8) = rb[i];
+      } else {
+        *(uint4*)(sb + (c / (BN / 8)) * TB::LD + (c % (BN / 8)) * 8) = rb[i];
+      }
+    }
+  };
+
+  v4f acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+
+  // optional bias-gradient: column sums of the (k-outer) A operand over K
+  const bool do_bgrad = (AM == A_ROWM) && p.bias_grad != nullptr && blockIdx.y == 0;
+  float bsum = 0.f;
+
+  const int l16 = lane & 15;
+  const int g4 = lane >> 4;
+  const int tq = l16 >> 2, tp = l16 & 3;  // transpose-read address roles
+
+  auto frag_kinner = [&](const bf16_t* s, int row, int kk) -> v8bf {
+    return *(const v8bf*)(s + row * (BK + PADK) + kk * 32 + g4 * 8);
+  };
+  auto frag_kouter = [&](const bf16_t* s, int ld, int colbase, int kk) -> v8bf {
+    typedef __attribute__((address_space(3))) v4s lds_v4s;
+    const bf16_t* p0 = s + (kk * 32 + g4 * 8 + tq) * ld + colbase + tp * 4;
+    v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p0));
+    v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p0 + 4 * ld));
+    v8s r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(v8bf, r);
+  };
+
+  if (nkt > 0) {
+    load_tile(kt_begin);
+    store_tile(smem);
+    __syncthreads();
+    for (int it = 0; it < nkt; ++it) {
+      const bf16_t* s = smem + (it & 1) * G::STAGE;
+      if (it + 1 < nkt) load_tile(kt_begin + it + 1);
+      const bf16_t* sa = s;
+      const bf16_t* sb = s + TA::ELEMS;
+      if (do_bgrad) {
+        // BM columns x BK rows; 256 threads -> 256/BM row-groups
+        constexpr int RG = 256 / BM;
+        const int col = tid % BM, rg = tid / BM;
+#pragma unroll 4
+        for (int r = rg * (BK / RG); r < (rg + 1) * (BK / RG); ++r) bsum += bf2f(sa[r * TA::LD + col]);
+      }
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        v8bf af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          if constexpr (AKI) af[i] = frag_kinner(sa, wr + 16 * i + l16, kk);
+          else af[i] = frag_kouter(sa, TA::LD, wr + 16 * i, kk);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (BKI) bfr[j] = frag_kinner(sb, wc + 16 * j + l16, kk);
+          else bfr[j] = frag_kouter(sb, TB::LD, wc + 16 * j, kk);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+      if (it + 1 < nkt) store_tile(smem + ((it + 1) & 1) * G::STAGE);
+      __syncthreads();
+    }
+  }
+
+  if (do_bgrad) {
+    const int col = tid % BM;
+    if (m0 + col < p.M) atomicAdd(p.bias_grad + m0 + col, bsum);
+  }
+
+  // ---- epilogue -------------------------------------------------------------
+  const bool add_bias = p.bias != nullptr && blockIdx.z == 0;
+  const bf16_t* R = (const bf16_t*)p.resid;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wc + 16 * j + l16;
+      if (col >= p.N) continue;
+      const float bv = add_bias ? p.bias[col] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = m0 + wr + 16 * i + 4 * g4 + q;
+        if (row >= p.M) continue;
+        float v = p.alpha * acc[i][j][q] + bv;
+        if (p.c_mode == ENCDIFF_OUT_BF16) {
+          if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
+          ((bf16_t*)p.c)[(long)row * p.ldc + col] = f2bf(v);
+        } else if (p.c_mode == ENCDIFF_OUT_F32) {
+          if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
+          ((float*)p.c)[(long)row * p.ldc + col] = v;
+        } else if (p.c_mode == ENCDIFF_OUT_F32_ATOMIC) {
+          atomicAdd((float*)p.c + (long)row * p.ldc + col, v);
+        } else {  // ATOMIC_CONVW: row = co, col = tap*cin + ci -> [co][ci][tap]
+          const int tap = col / p.convw_cin;
+          const int ci = col - tap * p.convw_cin;
+          atomicAdd((float*)p.c + (long)row * p.ldc + ci * 9 + tap, v);
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int AM, int BMD>
+hipError_t launch_t(const EncdiffGemmArgs& p, hipStream_t s) {
+  using G = Gemm<BM, BN, AM, BMD>;
+  const size_t lds = 2 * G::STAGE * sizeof(bf16_t);
+  // dynamic LDS above 64 KiB must be opted in once per instantiation (thread-safe static init)
+  static const hipError_t attr_ok = hipFuncSetAttribute(
+      (const void*)gemm_kernel<BM, BN, AM, BMD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr_ok != hipSuccess) return attr_ok;
+  dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, p.split_k);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, AM, BMD>), grid, dim3(256), lds, s, p);
+  return hipGetLastError();
+}
+
+template <int AM, int BMD>
+hipError_t launch_modes(const EncdiffGemmArgs& p, int tile, hipStream_t s) {
+  switch (tile) {
+    case 1: return launch_t<128, 128, AM, BMD>(p, s);
+    case 2: return launch_t<128, 64, AM, BMD>(p, s);
+    case 3: return launch_t<64, 128, AM, BMD>(p, s);
+    default: return launch_t<64, 64, AM, BMD>(p, s);
+  }
+}
+
+int pick_tile(const EncdiffGemmArgs& p) {
+  int bm = (p.M <= 64) ? 64 : 128;
+  int bn = (p.N <= 64) ? 64 : 128;
+  auto blocks = [&](int a, int b) { return ((p.M + a - 1) / a) * ((p.N + b - 1) / b) * p.split_k; };
+  if (blocks(bm, bn) < 512 && bm == 128) bm = 64;
+  if (blocks(bm, bn) < 512 && bn == 128) bn = 64;
+  if (bm == 128 && bn == 128) return 1;
+  if (bm == 128) return 2;
+  if (bn == 128) return 3;
+  return 4;
+}
+
+}  // namespace
+
+extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
+  if (!pa) return ENCDIFF_ERR_ARG;
+  EncdiffGemmArgs p = *pa;
+  if (p.M <= 0 || p.N <= 0 || p.K <= 0) return ENCDIFF_ERR_SHAPE;
+  if (p.split_k < 1) p.split_k = 1;
+  if (p.split_k > 1 && (p.c_mode == ENCDIFF_OUT_BF16 || p.c_mode == ENCDIFF_OUT_F32)) return ENCDIFF_ERR_ARG;
+  const bool k_inner = p.a_mode != ENCDIFF_OPA_ROWM || p.b_mode == ENCDIFF_OPB_ROWK;
+  if (k_inner && p.K % 8) return ENCDIFF_ERR_SHAPE;
+  if (p.a_mode == ENCDIFF_OPA_ROWM && p.M % 8) return ENCDIFF_ERR_SHAPE;
+  if (p.b_mode != ENCDIFF_OPB_ROWK && p.N % 8) return ENCDIFF_ERR_SHAPE;
+  if ((p.a_mode == ENCDIFF_OPA_IM2COL || p.b_mode == ENCDIFF_OPB_IM2COL) && (p.conv.cin % 8)) return ENCDIFF_ERR_SHAPE;
+  if (p.bias_grad && p.a_mode != ENCDIFF_OPA_ROWM) return ENCDIFF_ERR_ARG;
+  const int tile = p.tile ? p.tile : pick_tile(p);
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  const int am = p.a_mode, bm = p.b_mode;
+  if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_ROWK, B_ROWK>(p, tile, s);
+  else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_IM2COL, B_ROWK>(p, tile, s);
+  else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWK, B_ROWN>(p, tile, s);
+  else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_CONV_DGRAD) e = launch_modes<A_IM2COL, B_CONVD>(p, tile, s);
+  else if (am == ENCDIFF_OPA_ROWM && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWM, B_ROWN>(p, tile, s);
+  else if (am == ENCDIFF_OPA_ROWM && bm == ENCDIFF_OPB_IM2COL) e = launch_modes<A_ROWM, B_IM2COL>(p, tile, s);
+  else return ENCDIFF_ERR_UNSUPPORTED;
+  return e == hipSuccess ? ENCDIFF_OK : ENCDIFF_ERR_LAUNCH - (int)e;
+}
+
+extern "C" int encdiff_version(void) { return 1; }

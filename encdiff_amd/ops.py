@@ -1,0 +1,283 @@
+"""Thin Python wrappers over the C-ABI (one call = one or two kernel launches).
+
+Tensors are torch tensors used only as device memory; every call enqueues on
+torch's current HIP stream, so the calls compose with torch ops and can be
+captured into a HIP graph.  Activations are 2-D [rows][channels] bf16 views
+(NHWC / token-major) whose row stride is passed as the leading dimension.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+from ._lib import check, lib
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _s():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _ld(t: torch.Tensor) -> int:
+    assert t.dim() == 2 and t.stride(1) == 1, "expected a row-major 2-D view"
+    return t.stride(0)
+
+
+@dataclass
+class Geom:
+    """Image geometry of an NHWC activation: `batch` images of h x w pixels."""
+    batch: int
+    h: int
+    w: int
+
+    @property
+    def pixels(self):
+        return self.batch * self.h * self.w
+
+
+def _conv_geom(g: Geom, cin: int, resample: int, src: torch.Tensor) -> L.ConvGeom:
+    return L.ConvGeom(batch=g.batch, h=g.h, w=g.w, cin=cin, resample=resample, ld_src=_ld(src))
+
+
+def gemm(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK, c_mode=L.OUT_BF16,
+         conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=1, bias=None,
+         resid=None, ld_resid=0, bias_grad=None, tile=0):
+    args = L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=b_mode, c_mode=c_mode,
+                      a=_p(a), lda=lda, b=_p(b), ldb=ldb, c=_p(c), ldc=ldc,
+                      conv=conv if conv is not None else L.ConvGeom(),
+                      conv_cout=conv_cout, convw_cin=convw_cin, alpha=alpha, split_k=split_k,
+                      bias=_p(bias), resid=_p(resid), ld_resid=ld_resid, bias_grad=_p(bias_grad), tile=tile)
+    check(lib.encdiff_gemm(C.byref(args), _s()), "encdiff_gemm")
+
+
+def _split_for(M, N, K, bm=128, bn=128):
+    """split-K factor for reduction-heavy (wgrad) GEMMs: aim for >= 512 workgroups and
+    >= 256 reduction rows per split."""
+    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    s = 1
+    while tiles * s < 512 and K // (s * 2) >= 256:
+        s *= 2
+    return s
+
+
+# ------------------------------------------------------------------ linear layers
+def linear_fwd(x, w, out, bias=None, resid=None, alpha=1.0, out_f32=False):
+    """out[M][N] = x[M][K] w[N][K]^T (+bias)(+resid)."""
+    M, K = x.shape
+    N = w.shape[0]
+    gemm(M, N, K, x, _ld(x), w, _ld(w), out, _ld(out), c_mode=L.OUT_F32 if out_f32 else L.OUT_BF16,
+         bias=bias, resid=resid, ld_resid=_ld(resid) if resid is not None else 0, alpha=alpha)
+
+
+def linear_dgrad(dy, w, dx, resid=None):
+    """dx[M][K] = dy[M][N] w[N][K] (+resid, e.g. dx itself to accumulate)."""
+    M, N = dy.shape
+    K = w.shape[1]
+    gemm(M, K, N, dy, _ld(dy), w, _ld(w), dx, _ld(dx), b_mode=L.OPB_ROWN,
+         resid=resid, ld_resid=_ld(resid) if resid is not None else 0)
+
+
+def linear_wgrad(dy, x, dw, db=None):
+    """dw[N][K] += dy[M][N]^T x[M][K];  db[N] += sum_m dy[m][n]  (fp32 atomics)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    split = _split_for(N, K, M)
+    gemm(N, K, M, dy, _ld(dy), x, _ld(x), dw, K, a_mode=L.OPA_ROWM, b_mode=L.OPB_ROWN,
+         c_mode=L.OUT_F32_ATOMIC, split_k=split, bias_grad=db)
+
+
+# ------------------------------------------------------------------ 3x3 convolutions
+def conv3x3_fwd(x, g: Geom, cin, wf, out, bias=None, resid=None, resample=L.RESAMPLE_NONE):
+    """out[pixels][cout] = conv3x3(resample(x)) with packed weights wf [cout][9*cin]."""
+    cout = wf.shape[0]
+    gemm(g.pixels, cout, 9 * cin, x, _ld(x), wf, _ld(wf), out, _ld(out), a_mode=L.OPA_IM2COL,
+         conv=_conv_geom(g, cin, resample, x), bias=bias, resid=resid,
+         ld_resid=_ld(resid) if resid is not None else 0)
+
+
+def conv3x3_dgrad(dy, g: Geom, wf, dx, resid=None):
+    """dx[pixels][cin] = conv3x3^T(dy) (input grad at the conv resolution)."""
+    cout = wf.shape[0]
+    cin = wf.shape[1] // 9
+    gemm(g.pixels, cin, 9 * cout, dy, _ld(dy), wf, _ld(wf), dx, _ld(dx), a_mode=L.OPA_IM2COL,
+         b_mode=L.OPB_CONV_DGRAD, conv=_conv_geom(g, cout, L.RESAMPLE_NONE, dy), conv_cout=cout,
+         resid=resid, ld_resid=_ld(resid) if resid is not None else 0)
+
+
+def conv3x3_wgrad(dy, x, g: Geom, cin, dw_ref, db=None, resample=L.RESAMPLE_NONE):
+    """dw_ref[cout][cin][3][3] (fp32, reference layout) += sum_pix dy^T im2col(resample(x))."""
+    cout = dy.shape[1]
+    M, N, K = cout, 9 * cin, g.pixels
+    split = _split_for(M, N, K)
+    gemm(M, N, K, dy, _ld(dy), x, _ld(x), dw_ref, 9 * cin, a_mode=L.OPA_ROWM, b_mode=L.OPB_IM2COL,
+         c_mode=L.OUT_F32_ATOMIC_CONVW, conv=_conv_geom(g, cin, resample, x), convw_cin=cin,
+         split_k=split, bias_grad=db)
+
+
+# ------------------------------------------------------------------ normalisation
+def groupnorm_fwd(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_film=0, groups=32):
+    c = x.shape[1]
+    a = L.GroupNormArgs(batch=g.batch, hw=g.h * g.w, c=c, groups=groups, eps=eps, silu=int(silu),
+                        x=_p(x), ldx=_ld(x), gamma=_p(gamma), beta=_p(beta), film=_p(film), ld_film=ld_film,
+                        y=_p(y), ldy=_ld(y), stats=_p(stats))
+    check(lib.encdiff_groupnorm_fwd(C.byref(a), _s()), "encdiff_groupnorm_fwd")
+
+
+def groupnorm_bwd(x, g: Geom, gamma, beta, stats, eps, silu, dy, dx, dgamma_part, dbeta_part, film=None,
+                  ld_film=0, dfilm=None, ld_dfilm=0, accumulate=False, groups=32):
+    c = x.shape[1]
+    a = L.GroupNormArgs(batch=g.batch, hw=g.h * g.w, c=c, groups=groups, eps=eps, silu=int(silu),
+                        x=_p(x), ldx=_ld(x), gamma=_p(gamma), beta=_p(beta), film=_p(film), ld_film=ld_film,
+                        stats=_p(stats), dy=_p(dy), lddy=_ld(dy), dx=_p(dx), lddx=_ld(dx),
+                        accumulate_dx=int(accumulate), dgamma_part=_p(dgamma_part), dbeta_part=_p(dbeta_part),
+                        dfilm=_p(dfilm), ld_dfilm=ld_dfilm)
+    check(lib.encdiff_groupnorm_bwd(C.byref(a), _s()), "encdiff_groupnorm_bwd")
+
+
+def layernorm_parts(rows, c):
+    rpb = 256 // (c // 8)
+    return max(1, min(256, (rows + rpb - 1) // rpb))
+
+
+def layernorm_fwd(x, gamma, beta, y, stats, eps=1e-5):
+    rows, c = x.shape
+    a = L.LayerNormArgs(rows=rows, c=c, eps=eps, x=_p(x), ldx=_ld(x), gamma=_p(gamma), beta=_p(beta),
+                        y=_p(y), ldy=_ld(y), stats=_p(stats))
+    check(lib.encdiff_layernorm_fwd(C.byref(a), _s()), "encdiff_layernorm_fwd")
+
+
+def layernorm_bwd(x, gamma, stats, dy, dx, dgamma_part, dbeta_part, accumulate=False):
+    rows, c = x.shape
+    parts = layernorm_parts(rows, c)
+    assert dgamma_part.numel() >= parts * c
+    a = L.LayerNormArgs(rows=rows, c=c, eps=0.0, x=_p(x), ldx=_ld(x), gamma=_p(gamma), stats=_p(stats),
+                        dy=_p(dy), lddy=_ld(dy), dx=_p(dx), lddx=_ld(dx), accumulate_dx=int(accumulate),
+                        dgamma_part=_p(dgamma_part), dbeta_part=_p(dbeta_part), parts=parts)
+    check(lib.encdiff_layernorm_bwd(C.byref(a), _s()), "encdiff_layernorm_bwd")
+
+
+# ------------------------------------------------------------------ attention
+def attention_fwd(q, k, v, o, lse, batch, heads, sq, sk, dh):
+    a = L.AttnArgs(batch=batch, heads=heads, sq=sq, sk=sk, dh=dh, scale=dh ** -0.5,
+                   q=_p(q), ldq=_ld(q), k=_p(k), ldk=_ld(k), v=_p(v), ldv=_ld(v), o=_p(o), ldo=_ld(o),
+                   lse=_p(lse))
+    check(lib.encdiff_attention_fwd(C.byref(a), _s()), "encdiff_attention_fwd")
+
+
+def attention_bwd(q, k, v, o, lse, d_o, dq, dk, dv, batch, heads, sq, sk, dh):
+    a = L.AttnArgs(batch=batch, heads=heads, sq=sq, sk=sk, dh=dh, scale=dh ** -0.5,
+                   q=_p(q), ldq=_ld(q), k=_p(k), ldk=_ld(k), v=_p(v), ldv=_ld(v), o=_p(o), ldo=_ld(o),
+                   lse=_p(lse), d_o=_p(d_o), lddo=_ld(d_o), dq=_p(dq), lddq=_ld(dq), dk=_p(dk), lddk=_ld(dk),
+                   dv=_p(dv), lddv=_ld(dv))
+    check(lib.encdiff_attention_bwd(C.byref(a), _s()), "encdiff_attention_bwd")
+
+
+# ------------------------------------------------------------------ elementwise
+def ew(op, x, y, x2=None, rows=None, cols=None, accumulate=False, resample=0, g: Optional[Geom] = None):
+    rows = rows if rows is not None else y.shape[0]
+    cols = cols if cols is not None else y.shape[1]
+    a = L.EwArgs(op=op, rows=rows, cols=cols, x=_p(x), ldx=_ld(x), x2=_p(x2), ldx2=_ld(x2) if x2 is not None else 0,
+                 y=_p(y), ldy=_ld(y), accumulate=int(accumulate), resample=resample,
+                 batch=g.batch if g else 0, h=g.h if g else 0, w=g.w if g else 0)
+    check(lib.encdiff_elementwise(C.byref(a), _s()), "encdiff_elementwise")
+
+
+def geglu_fwd(f, y):
+    ew(L.EW_GEGLU, f, y, cols=y.shape[1])
+
+
+def geglu_bwd(f, dy, df):
+    ew(L.EW_GEGLU_BWD, f, df, x2=dy, rows=dy.shape[0], cols=dy.shape[1])
+
+
+def resample(x, y, g_out: Geom, mode, accumulate=False):
+    ew(L.EW_RESAMPLE, x, y, resample=mode, g=g_out, accumulate=accumulate)
+
+
+def resample_bwd(dy, dx, g_src: Geom, mode, accumulate=False):
+    """dx (at the forward source resolution g_src) (+)= adjoint of `mode` applied to dy."""
+    ew(L.EW_RESAMPLE_BWD, dy, dx, resample=mode, g=g_src, accumulate=accumulate)
+
+
+def small_conv_in_fwd(x_nchw, g: Geom, weight, bias, y):
+    cout, cin = weight.shape[0], weight.shape[1]
+    a = L.SmallConvArgs(batch=g.batch, h=g.h, w=g.w, cin=cin, cout=cout, x=_p(x_nchw), ldx=0, x_f32=1,
+                        weight=_p(weight), bias=_p(bias), y=_p(y), ldy=_ld(y), y_f32=0)
+    check(lib.encdiff_small_conv_fwd(C.byref(a), _s()), "encdiff_small_conv_fwd")
+
+
+def small_conv_in_wgrad(x_nchw, g: Geom, weight, dy, dweight, dbias):
+    cout, cin = weight.shape[0], weight.shape[1]
+    a = L.SmallConvArgs(batch=g.batch, h=g.h, w=g.w, cin=cin, cout=cout, x=_p(x_nchw), x_f32=1,
+                        weight=_p(weight), dy=_p(dy), lddy=_ld(dy), dy_f32=0, dweight=_p(dweight), dbias=_p(dbias))
+    check(lib.encdiff_small_conv_bwd(C.byref(a), _s()), "encdiff_small_conv_bwd(in)")
+
+
+def small_conv_out_fwd(x, g: Geom, weight, bias, y_nchw):
+    cout, cin = weight.shape[0], weight.shape[1]
+    a = L.SmallConvArgs(batch=g.batch, h=g.h, w=g.w, cin=cin, cout=cout, x=_p(x), ldx=_ld(x), x_f32=0,
+                        weight=_p(weight), bias=_p(bias), y=_p(y_nchw), ldy=0, y_f32=1)
+    check(lib.encdiff_small_conv_fwd(C.byref(a), _s()), "encdiff_small_conv_fwd")
+
+
+def small_conv_out_bwd(x, g: Geom, weight, dy_nchw, dx, dweight, dbias):
+    cout, cin = weight.shape[0], weight.shape[1]
+    a = L.SmallConvArgs(batch=g.batch, h=g.h, w=g.w, cin=cin, cout=cout, x=_p(x), ldx=_ld(x), x_f32=0,
+                        weight=_p(weight), dy=_p(dy_nchw), lddy=0, dy_f32=1, dx=_p(dx),
+                        lddx=_ld(dx) if dx is not None else 0, dweight=_p(dweight), dbias=_p(dbias))
+    check(lib.encdiff_small_conv_bwd(C.byref(a), _s()), "encdiff_small_conv_bwd(out)")
+
+
+# ------------------------------------------------------------------ diffusion / optimizer
+def timestep_embedding(t, dim, out, max_period=10000.0):
+    check(lib.encdiff_timestep_embedding(_p(t), t.shape[0], dim, max_period, _p(out), _s()),
+          "encdiff_timestep_embedding")
+
+
+def q_sample(x0, eps, t, sqrt_ac, sqrt_1mac, xt):
+    b = x0.shape[0]
+    check(lib.encdiff_q_sample(_p(x0), _p(eps), _p(t), _p(sqrt_ac), _p(sqrt_1mac), b, x0.numel() // b, _p(xt),
+                               _s()), "encdiff_q_sample")
+
+
+def l1_loss(pred, eps, t, lvlb, out2, grad=None, l_simple_weight=1.0):
+    b = pred.shape[0]
+    check(lib.encdiff_l1_loss(_p(pred), _p(eps), _p(t), _p(lvlb), b, pred.numel() // b, l_simple_weight,
+                              _p(out2), _p(grad), _s()), "encdiff_l1_loss")
+
+
+def ddim_step(x, e, noise, a_t, a_prev, sigma, s1, x_prev, pred_x0=None):
+    check(lib.encdiff_ddim_step(_p(x), _p(e), _p(noise), x.numel(), float(a_t), float(a_prev), float(sigma),
+                                float(s1), _p(x_prev), _p(pred_x0), _s()), "encdiff_ddim_step")
+
+
+def adamw_ema(p, g, m, v, hyper, ema=None, ema_n=0):
+    check(lib.encdiff_adamw_ema(_p(p), _p(g), _p(m), _p(v), _p(ema), p.numel(), _p(hyper), ema_n, _s()),
+          "encdiff_adamw_ema")
+
+
+def adamw_hyper(lr, step, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=1e-2, ema_one_minus_decay=0.0):
+    """Host-side (float64) scalars exactly as torch.optim.AdamW computes them."""
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    return [lr, beta1, beta2, eps, weight_decay, lr / bc1, 1.0 / math.sqrt(bc2), ema_one_minus_decay]
+
+
+def pack_weights(src_f32, dst_bf16, jobs_dev, njobs):
+    check(lib.encdiff_pack_weights(_p(src_f32), _p(dst_bf16), _p(jobs_dev), njobs, _s()), "encdiff_pack_weights")
+
+
+def reduce_partials(part, ld, rows, cols, col_index, grad):
+    check(lib.encdiff_reduce_partials(_p(part), ld, rows, cols, _p(col_index), _p(grad), _s()),
+          "encdiff_reduce_partials")

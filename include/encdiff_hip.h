@@ -1,0 +1,280 @@
+/*
+ * encdiff_hip.h -- C-ABI of libencdiff_hip.so, the MI355X (gfx950) kernels of the
+ * EncDiff denoising path.
+ *
+ * The reference (SelenaGeRuiqi/EncDiff) has no FFI: its hot path is PyTorch eager
+ * ops inside ldm/modules/diffusionmodules/openaimodel_enc.py, ldm/modules/attention.py,
+ * ldm/models/diffusion/ddpm_enc.py and ldm/models/diffusion/ddim.py.  Each entry point
+ * below names the reference computation it replaces (file:line).  The Python
+ * module-level mirror of the reference API (encdiff_amd/ldm/...) calls these
+ * through ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Caller owns all memory: device pointers + leading dimensions (in elements).
+ *    The library never allocates.
+ *  - Stream ordered: every launch goes on the `stream` argument (a hipStream_t,
+ *    e.g. torch.cuda.current_stream().cuda_stream); no implicit synchronisation,
+ *    so every call is hipGraph-capturable.
+ *  - Errors: 0 on success, a negative ENCDIFF_ERR_* on bad arguments, and
+ *    ENCDIFF_ERR_LAUNCH - hipError_t on a launch failure.
+ *  - Threading: reentrant, no global mutable state.
+ *  - Layout: activations are [rows][channels] bf16 (NHWC for images, token-major
+ *    for transformer tokens) with a row stride `ld`; statistics / master weights /
+ *    gradients are fp32.
+ */
+#ifndef ENCDIFF_HIP_H
+#define ENCDIFF_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ENCDIFF_OK 0
+#define ENCDIFF_ERR_ARG (-1)
+#define ENCDIFF_ERR_SHAPE (-2)
+#define ENCDIFF_ERR_UNSUPPORTED (-3)
+#define ENCDIFF_ERR_LAUNCH (-1000)
+
+/* ---------------------------------------------------------------- GEMM / conv
+ * C[M][N] = alpha * sum_k A[m][k] * B[k][n]  (+ bias[n]) (+ resid[m][n])
+ * Replaces every nn.Linear / 1x1 Conv2d / 3x3 Conv2d forward and backward on the
+ * path: openaimodel_enc.py:204,230,237-241,508-512,521,687 (conv/linear),
+ * attention.py:159-167,43,58 (q/k/v/out, GEGLU, FF), attention.py:233-259 (proj_in/out).
+ */
+enum {
+  ENCDIFF_OPA_ROWK = 0,   /* A[m][k] at a + m*lda + k                                  */
+  ENCDIFF_OPA_IM2COL = 1, /* A[m][k] = im2col3x3(src)[pixel m][tap*cin + c] (conv fwd / dgrad) */
+  ENCDIFF_OPA_ROWM = 2    /* A stored transposed: A[m][k] at a + k*lda + m (wgrad of dY)   */
+};
+enum {
+  ENCDIFF_OPB_ROWK = 0,       /* B[k][n] at b + n*ldb + k (weights [out][in])               */
+  ENCDIFF_OPB_ROWN = 1,       /* B[k][n] at b + k*ldb + n                                    */
+  ENCDIFF_OPB_CONV_DGRAD = 2, /* B[(tap,co)][ci] = Wf[co][8-tap][ci], Wf packed [co][9][cin] */
+  ENCDIFF_OPB_IM2COL = 3      /* B[pixel][tap*cin + c] = im2col3x3(src) (conv wgrad)          */
+};
+enum {
+  ENCDIFF_OUT_BF16 = 0,
+  ENCDIFF_OUT_F32 = 1,
+  ENCDIFF_OUT_F32_ATOMIC = 2,       /* atomicAdd into fp32 C (split-K / grad accumulate)   */
+  ENCDIFF_OUT_F32_ATOMIC_CONVW = 3  /* atomicAdd, column n=(tap,ci) scattered to the reference
+                                       Conv2d weight layout [co][ci][3][3]                   */
+};
+enum {
+  ENCDIFF_RESAMPLE_NONE = 0,
+  ENCDIFF_RESAMPLE_DOWN2 = 1, /* source is (2h,2w); AvgPool2d(2) on the fly  (openaimodel_enc.py:156) */
+  ENCDIFF_RESAMPLE_UP2 = 2    /* source is (h/2,w/2); nearest x2 on the fly (openaimodel_enc.py:116) */
+};
+
+typedef struct EncdiffConvGeom {
+  int batch;     /* images                                                       */
+  int h, w;      /* spatial size of the conv input after resampling (== output)  */
+  int cin;       /* channels of the im2col source                                */
+  int resample;  /* ENCDIFF_RESAMPLE_*                                           */
+  int pad_;
+  long ld_src;   /* pixel stride of the source tensor, elements                  */
+} EncdiffConvGeom;
+
+typedef struct EncdiffGemmArgs {
+  int M, N, K;
+  int a_mode, b_mode, c_mode;
+  const void* a; long lda;   /* bf16 */
+  const void* b; long ldb;   /* bf16 */
+  void* c; long ldc;         /* bf16 or fp32 per c_mode */
+  EncdiffConvGeom conv;      /* for IM2COL operands                                */
+  int conv_cout;             /* OPB_CONV_DGRAD: forward conv's output channels     */
+  int convw_cin;             /* OUT_F32_ATOMIC_CONVW: forward conv's input channels */
+  float alpha;
+  int split_k;               /* >= 1; > 1 needs an atomic c_mode                  */
+  const float* bias;         /* [N] fp32 or NULL                                   */
+  const void* resid; long ld_resid;  /* bf16 [M][N] or NULL                        */
+  float* bias_grad;          /* OPA_ROWM only: += sum_k A[m][k] into bias_grad[m]  */
+  int tile;                  /* 0 = auto, else 1:128x128 2:128x64 3:64x128 4:64x64 */
+  int pad2_;
+} EncdiffGemmArgs;
+
+int encdiff_gemm(const EncdiffGemmArgs* args, void* stream);
+
+/* ---------------------------------------------------------------- GroupNorm
+ * y = act( GN(x) * (1 + scale[b,c]) + shift[b,c] )
+ * Replaces GroupNorm32 + SiLU (+ FiLM) of ResBlock in/out_layers and UNet.out
+ * (openaimodel_enc.py:201-205,225-232,267-271,684-686; util.py:242-244) and the
+ * SpatialTransformer Normalize (attention.py:76-77, eps 1e-6, no act).
+ */
+typedef struct EncdiffGroupNormArgs {
+  int batch, hw, c, groups;
+  float eps;
+  int silu;                  /* apply SiLU after the affine/FiLM                   */
+  const void* x; long ldx;   /* bf16 [batch*hw][c]                                 */
+  const float* gamma;
+  const float* beta;
+  const float* film; long ld_film;   /* optional fp32 [batch][ld_film]: scale at [c], shift at [C + c] */
+  void* y; long ldy;         /* bf16 out                                           */
+  float* stats;              /* fp32 [batch][groups][2] (mean, rstd)               */
+  /* backward only */
+  const void* dy; long lddy;
+  void* dx; long lddx;       /* bf16                                                */
+  int accumulate_dx;         /* dx += result                                        */
+  int pad_;
+  float* dgamma_part;        /* fp32 [batch][c] per-image partial sums (reduced later) */
+  float* dbeta_part;
+  float* dfilm; long ld_dfilm;       /* fp32 [batch][ld_dfilm]: dscale at [c], dshift at [C + c] */
+} EncdiffGroupNormArgs;
+
+int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* args, void* stream);
+int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* args, void* stream);
+
+/* ---------------------------------------------------------------- LayerNorm
+ * BasicTransformerBlock norm1/2/3 (attention.py:206-208, 211-215), eps 1e-5.
+ */
+typedef struct EncdiffLayerNormArgs {
+  int rows, c;
+  float eps;
+  const void* x; long ldx;
+  const float* gamma; const float* beta;
+  void* y; long ldy;
+  float* stats;              /* fp32 [rows][2] (mean, rstd) */
+  const void* dy; long lddy; /* backward */
+  void* dx; long lddx;
+  int accumulate_dx;         /* dx += (residual branch)                            */
+  float* dgamma_part;        /* fp32 [parts][c]                                    */
+  float* dbeta_part;
+  int parts;                 /* number of partial rows (grid size of the backward) */
+  int pad_;
+} EncdiffLayerNormArgs;
+
+int encdiff_layernorm_fwd(const EncdiffLayerNormArgs* args, void* stream);
+int encdiff_layernorm_bwd(const EncdiffLayerNormArgs* args, void* stream);
+
+/* ---------------------------------------------------------------- Attention
+ * softmax(q k^T * dh^-0.5) v per head, q/k/v/o as [rows][ld] with head h at
+ * columns [h*dh, (h+1)*dh) ('b n (h d)', attention.py:170-193).  Self-attention
+ * (keys = the same tokens) and cross-attention to the concept tokens (keys = 20).
+ */
+typedef struct EncdiffAttnArgs {
+  int batch, heads, sq, sk, dh;
+  float scale;
+  const void* q; long ldq;
+  const void* k; long ldk;
+  const void* v; long ldv;
+  void* o; long ldo;
+  float* lse;                /* fp32 [batch*heads][sq] log-sum-exp (for backward)  */
+  const void* d_o; long lddo;  /* backward */
+  void* dq; long lddq;
+  void* dk; long lddk;
+  void* dv; long lddv;
+} EncdiffAttnArgs;
+
+int encdiff_attention_fwd(const EncdiffAttnArgs* args, void* stream);
+int encdiff_attention_bwd(const EncdiffAttnArgs* args, void* stream);
+
+/* ---------------------------------------------------------------- elementwise */
+enum {
+  ENCDIFF_EW_COPY = 0,        /* y = x                                               */
+  ENCDIFF_EW_SILU = 1,        /* y = silu(x)                        (emb_layers[0]) */
+  ENCDIFF_EW_SILU_BWD = 2,    /* y = dy * silu'(x)                                   */
+  ENCDIFF_EW_GEGLU = 3,       /* y[:, j] = x[:, j] * gelu(x[:, n + j])  (attention.py:42-44) */
+  ENCDIFF_EW_GEGLU_BWD = 4,   /* dx[:, j], dx[:, n+j] from dy and x                  */
+  ENCDIFF_EW_ADD = 5,         /* y = x + x2                                          */
+  ENCDIFF_EW_RESAMPLE = 6,    /* y = resample(x) (down: avgpool2, up: nearest2)      */
+  ENCDIFF_EW_RESAMPLE_BWD = 7,/* y (+)= adjoint of resample applied to x             */
+  ENCDIFF_EW_F32_TO_BF16 = 8,
+  ENCDIFF_EW_BF16_TO_F32 = 9
+};
+typedef struct EncdiffEwArgs {
+  int op;
+  int rows, cols;            /* output logical shape [rows][cols]                  */
+  const void* x; long ldx;
+  const void* x2; long ldx2;
+  void* y; long ldy;
+  int accumulate;            /* y += result                                        */
+  int resample;              /* ENCDIFF_RESAMPLE_* for RESAMPLE ops                */
+  int batch, h, w;           /* output spatial dims for RESAMPLE ops               */
+  int pad_;
+} EncdiffEwArgs;
+
+int encdiff_elementwise(const EncdiffEwArgs* args, void* stream);
+
+/* ---------------------------------------------------------------- small convs
+ * UNet input conv 3->64 (openaimodel_enc.py:521) and output conv 64->3
+ * (openaimodel_enc.py:687): channel counts not multiples of 8.  NHWC bf16
+ * activations, fp32 weights in the reference layout [co][ci][3][3].
+ */
+typedef struct EncdiffSmallConvArgs {
+  int batch, h, w, cin, cout;
+  const void* x; long ldx;        /* bf16 (or fp32 when x_f32)                     */
+  int x_f32;                      /* input x is fp32 NCHW (the UNet input tensor) */
+  const float* weight;            /* [cout][cin][3][3] fp32                        */
+  const float* bias;
+  void* y; long ldy;              /* bf16 NHWC, or fp32 NCHW when y_f32            */
+  int y_f32;
+  int pad_;
+  /* backward */
+  const void* dy; long lddy;      /* bf16 NHWC or fp32 NCHW (dy_f32)               */
+  int dy_f32;
+  int pad2_;
+  void* dx; long lddx;            /* bf16 NHWC (or NULL)                           */
+  float* dweight;                 /* fp32 atomic accumulate, reference layout      */
+  float* dbias;
+} EncdiffSmallConvArgs;
+
+int encdiff_small_conv_fwd(const EncdiffSmallConvArgs* args, void* stream);
+int encdiff_small_conv_bwd(const EncdiffSmallConvArgs* args, void* stream);
+
+/* ---------------------------------------------------------------- diffusion
+ * timestep_embedding (util.py:179-199) -> bf16 [batch][dim]
+ */
+int encdiff_timestep_embedding(const long long* t, int batch, int dim, float max_period,
+                               void* out_bf16, void* stream);
+
+/* q_sample (ddpm_enc.py:292-295): x_t = sqrt_ac[t] x0 + sqrt_1mac[t] eps.
+ * x0, eps, x_t fp32 NCHW [batch][3*hw]. */
+int encdiff_q_sample(const float* x0, const float* eps, const long long* t, const float* sqrt_ac,
+                     const float* sqrt_1mac, int batch, int per_sample, float* x_t, void* stream);
+
+/* p_losses L1 (ddpm_enc.py:1194-1213): loss_simple[b] = mean|eps - pred|,
+ * out[0] = mean_b loss_simple (= loss with logvar 0), out[1] = mean_b lvlb[t_b] loss_simple[b];
+ * grad_pred = sign(pred - eps) / (batch * per_sample) * l_simple_weight. */
+int encdiff_l1_loss(const float* pred, const float* eps, const long long* t, const float* lvlb,
+                    int batch, int per_sample, float l_simple_weight, float* out2, float* grad_pred,
+                    void* stream);
+
+/* DDIM update (ddim.py:197-206) for one step with scalar coefficients:
+ * pred_x0 = (x - s1 e) / sqrt(a_t); x' = sqrt(a_prev) pred_x0 + sqrt(1-a_prev-sigma^2) e + sigma z. */
+int encdiff_ddim_step(const float* x, const float* e, const float* noise, int n, float a_t,
+                      float a_prev, float sigma, float sqrt_one_minus_at, float* x_prev, float* pred_x0,
+                      void* stream);
+
+/* ---------------------------------------------------------------- optimizer / EMA
+ * Fused AdamW (torch defaults; ddpm_enc.py:1615) + optional LitEma update
+ * (ema.py:25-44) over one flat fp32 parameter arena, plus the bf16 packing of
+ * the updated weights into the compute layouts (pack table).
+ */
+/* hyper (device fp32[8], read at execution time so a captured step graph can be
+ * replayed with a new lr / step): [lr, beta1, beta2, eps, weight_decay,
+ * lr / (1 - beta1^step), 1 / sqrt(1 - beta2^step), ema (1 - decay)].
+ * The EMA covers the first ema_n elements of the arena (the UNet parameters). */
+int encdiff_adamw_ema(float* p, const float* g, float* m, float* v, float* ema, long long n,
+                      const float* hyper, long long ema_n, void* stream);
+
+/* Pack fp32 master weights into bf16 compute layouts.  Each job copies `rows x cols`
+ * elements: dst[r*dst_ld + c] = src[src_index(r, c)], kind 0: src[r*cols + c]
+ * (identity), kind 1: conv [co][ci][3][3] -> [co][tap][ci] (r=co, c=tap*cin+ci). */
+typedef struct EncdiffPackJob {
+  long long src_off, dst_off;
+  int rows, cols, kind, cin;
+} EncdiffPackJob;
+int encdiff_pack_weights(const float* src, void* dst_bf16, const EncdiffPackJob* jobs, int njobs,
+                         void* stream);
+
+/* Reduce per-part partial sums into the fp32 gradient arena:
+ * grad[col_index[j]] += sum_{r < rows} part[r * ld + j], j < cols. */
+int encdiff_reduce_partials(const float* part, long ld, int rows, int cols, const int* col_index,
+                            float* grad, void* stream);
+
+/* Library/device information (for tests): returns the number of exported kernels. */
+int encdiff_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ENCDIFF_HIP_H */

@@ -1,0 +1,67 @@
+"""CPU tests of the drop-in boundary: the C-ABI library loads, exports every
+symbol the header declares, and the ctypes mirror of each struct has exactly the
+C layout (compiled with gcc against include/encdiff_hip.h)."""
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(REPO, "include", "encdiff_hip.h")
+
+
+def header_functions():
+    txt = open(HDR).read()
+    return sorted(set(re.findall(r"\bint\s+(encdiff_\w+)\s*\(", txt)))
+
+
+def test_header_exports_match_library():
+    import encdiff_amd._lib as L
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (encdiff_\w+)", out))
+    declared = set(header_functions())
+    assert declared, "no functions parsed from the header"
+    assert declared <= exported, f"missing exports: {declared - exported}"
+    assert set(L.EXPORTS) == declared, "ctypes prototypes out of sync with the header"
+
+
+STRUCTS = {
+    "EncdiffConvGeom": "ConvGeom", "EncdiffGemmArgs": "GemmArgs", "EncdiffGroupNormArgs": "GroupNormArgs",
+    "EncdiffLayerNormArgs": "LayerNormArgs", "EncdiffAttnArgs": "AttnArgs", "EncdiffEwArgs": "EwArgs",
+    "EncdiffSmallConvArgs": "SmallConvArgs", "EncdiffPackJob": "PackJob",
+}
+
+
+def test_struct_layouts_match_c():
+    import encdiff_amd._lib as L
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HDR}"', "int main(void){"]
+    for cname, pyname in STRUCTS.items():
+        lines.append(f'printf("{pyname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in getattr(L, pyname)._fields_:
+            lines.append(f'printf("{pyname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0;}")
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "probe.c"), os.path.join(d, "probe")
+        open(src, "w").write("\n".join(lines))
+        subprocess.run(["gcc", "-std=c99", "-o", exe, src], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout
+    for line in out.strip().splitlines():
+        pyname, field, val = line.split()
+        cls = getattr(L, pyname)
+        if field == "size":
+            assert C.sizeof(cls) == int(val), pyname
+        else:
+            assert getattr(cls, field).offset == int(val), f"{pyname}.{field}"
+
+
+def test_product_path_has_no_oracle_or_fallback():
+    """The product package never imports the oracle nor a CPU fallback."""
+    pkg = os.path.join(REPO, "encdiff_amd")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                txt = open(os.path.join(root, f)).read()
+                assert "from oracle" not in txt and "import oracle" not in txt, f

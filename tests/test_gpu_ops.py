@@ -1,0 +1,368 @@
+"""Per-kernel numerics on the MI355X: every HIP op against a plain PyTorch fp32
+reference of the same op, evaluated on the same (bf16-rounded) inputs.
+
+Tolerances: bf16-output kernels rel-L2 <= 1e-2 (one bf16 rounding of the output,
+fp32 accumulation); fp32-output kernels (weight gradients) rel-L2 <= 2e-3.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def rel(a, b):
+    a = a.double(); b = b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def O():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from encdiff_amd import ops
+    return ops
+
+
+def bf(*shape, scale=1.0):
+    return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
+
+
+def nhwc(x, g):  # [pix][c] -> NCHW fp32
+    return x.float().reshape(g.batch, g.h, g.w, -1).permute(0, 3, 1, 2)
+
+
+def to_rows(x):  # NCHW -> [pix][c]
+    return x.permute(0, 2, 3, 1).reshape(-1, x.shape[1])
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 256, 256), (1000, 72, 64), (32768, 64, 64), (130, 2048, 256),
+                                   (128, 10240, 256), (2560, 128, 16)])
+def test_linear(O, M, N, K):
+    torch.manual_seed(0)
+    x, w = bf(M, K), bf(N, K, scale=K ** -0.5)
+    b = torch.randn(N, device=dev)
+    r = bf(M, N)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    O.linear_fwd(x, w, out, bias=b, resid=r)
+    ref = x.float() @ w.float().t() + b + r.float()
+    assert rel(out, ref) < 1e-2
+    # fp32 output
+    out32 = torch.empty(M, N, device=dev)
+    O.linear_fwd(x, w, out32, bias=b, out_f32=True)
+    assert rel(out32, x.float() @ w.float().t() + b) < 1e-4
+    dy = bf(M, N)
+    dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+    O.linear_dgrad(dy, w, dx)
+    assert rel(dx, dy.float() @ w.float()) < 1e-2
+    dw = torch.zeros(N, K, device=dev)
+    db = torch.zeros(N, device=dev)
+    O.linear_wgrad(dy, x, dw, db)
+    assert rel(dw, dy.float().t() @ x.float()) < 2e-3
+    assert rel(db, dy.float().sum(0)) < 2e-3
+
+
+def test_linear_strided_views(O):
+    """q/k/v slices of a fused [M][3C] projection output are strided views."""
+    torch.manual_seed(1)
+    M, C = 4096, 128
+    x = bf(M, 3 * C)[:, C:2 * C]
+    w = bf(C, C, scale=C ** -0.5)
+    outbuf = torch.zeros(M, 2 * C, device=dev, dtype=torch.bfloat16)
+    out = outbuf[:, C:]
+    O.linear_fwd(x, w, out)
+    assert rel(out, x.float() @ w.float().t()) < 1e-2
+    assert outbuf[:, :C].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("B,H,cin,cout,mode", [(4, 16, 64, 64, 0), (2, 16, 192, 64, 0), (3, 8, 128, 256, 0),
+                                               (2, 8, 64, 64, 1), (2, 8, 256, 256, 2), (8, 2, 256, 256, 0),
+                                               (2, 4, 512, 256, 0)])
+def test_conv3x3(O, B, H, cin, cout, mode):
+    from encdiff_amd.ops import Geom
+    torch.manual_seed(2)
+    g = Geom(B, H, H)
+    src_h = 2 * H if mode == 1 else (H // 2 if mode == 2 else H)
+    gs = Geom(B, src_h, src_h)
+    x = bf(gs.pixels, cin)
+    wt = torch.randn(cout, cin, 3, 3, device=dev) / math.sqrt(9 * cin)
+    wf = wt.permute(0, 2, 3, 1).reshape(cout, 9 * cin).to(torch.bfloat16).contiguous()
+    wq = wf.float().reshape(cout, 3, 3, cin).permute(0, 3, 1, 2)
+    bias = torch.randn(cout, device=dev)
+    out = torch.empty(g.pixels, cout, device=dev, dtype=torch.bfloat16)
+    O.conv3x3_fwd(x, g, cin, wf, out, bias=bias, resample=mode)
+    xin = nhwc(x, gs)
+    if mode == 1:
+        xin = F.avg_pool2d(xin, 2)
+    elif mode == 2:
+        xin = F.interpolate(xin, scale_factor=2, mode="nearest")
+    xin = xin.to(torch.bfloat16).float() if mode == 1 else xin
+    xin.requires_grad_(True)
+    wq.requires_grad_(True)
+    ref = F.conv2d(xin, wq, bias, padding=1)
+    assert rel(nhwc(out, g), ref) < 1e-2
+    dy = bf(g.pixels, cout)
+    ref.backward(nhwc(dy, g))
+    # dgrad at the conv resolution
+    dx = torch.empty(g.pixels, cin, device=dev, dtype=torch.bfloat16)
+    O.conv3x3_dgrad(dy, g, wf, dx)
+    assert rel(nhwc(dx, g), xin.grad) < 1e-2
+    dw = torch.zeros(cout, cin, 3, 3, device=dev)
+    db = torch.zeros(cout, device=dev)
+    O.conv3x3_wgrad(dy, x, g, cin, dw, db, resample=mode)
+    assert rel(dw, wq.grad) < 5e-3
+    assert rel(db, nhwc(dy, g).sum((0, 2, 3))) < 2e-3
+
+
+@pytest.mark.parametrize("C,H,film,silu,eps", [(64, 16, True, True, 1e-5), (192, 16, False, True, 1e-5),
+                                                (384, 8, True, True, 1e-5), (256, 4, False, False, 1e-6),
+                                                (512, 2, True, True, 1e-5)])
+def test_groupnorm(O, C, H, film, silu, eps):
+    from encdiff_amd.ops import Geom
+    torch.manual_seed(3)
+    B = 6
+    g = Geom(B, H, H)
+    x = (torch.randn(g.pixels, C, device=dev) * 2 + 0.5).to(torch.bfloat16)
+    gamma = 1 + 0.1 * torch.randn(C, device=dev)
+    beta = 0.1 * torch.randn(C, device=dev)
+    E = torch.randn(B, 2 * C + 32, device=dev) * 0.3 if film else None
+    y = torch.empty_like(x)
+    stats = torch.empty(B, 32, 2, device=dev)
+    O.groupnorm_fwd(x, g, gamma, beta, y, stats, eps, silu, film=E, ld_film=E.shape[1] if film else 0)
+    xr = nhwc(x, g).requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    Er = E.clone().requires_grad_(True) if film else None
+    ref = F.group_norm(xr, 32, gr, br, eps)
+    if film:
+        ref = ref * (1 + Er[:, :C, None, None]) + Er[:, C:2 * C, None, None]
+    if silu:
+        ref = F.silu(ref)
+    assert rel(nhwc(y, g), ref) < 1e-2
+    dy = bf(g.pixels, C)
+    ref.backward(nhwc(dy, g))
+    dx = torch.empty_like(x)
+    dgp = torch.empty(B, C, device=dev)
+    dbp = torch.empty(B, C, device=dev)
+    dE = torch.zeros(B, 2 * C + 32, device=dev) if film else None
+    O.groupnorm_bwd(x, g, gamma, beta, stats, eps, silu, dy, dx, dgp, dbp, film=E,
+                    ld_film=E.shape[1] if film else 0, dfilm=dE, ld_dfilm=dE.shape[1] if film else 0)
+    assert rel(nhwc(dx, g), xr.grad) < 1e-2
+    assert rel(dgp.sum(0), gr.grad) < 2e-3
+    assert rel(dbp.sum(0), br.grad) < 2e-3
+    if film:
+        assert rel(dE[:, :2 * C], Er.grad[:, :2 * C]) < 2e-3
+
+
+@pytest.mark.parametrize("rows,C", [(32768, 64), (8192, 128), (2048, 256), (512, 256), (1000, 128)])
+def test_layernorm(O, rows, C):
+    torch.manual_seed(4)
+    x = (torch.randn(rows, C, device=dev) + 0.3).to(torch.bfloat16)
+    gamma = 1 + 0.1 * torch.randn(C, device=dev)
+    beta = 0.1 * torch.randn(C, device=dev)
+    y = torch.empty_like(x)
+    st = torch.empty(rows, 2, device=dev)
+    O.layernorm_fwd(x, gamma, beta, y, st)
+    xr = x.float().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    ref = F.layer_norm(xr, (C,), gr, br, 1e-5)
+    assert rel(y, ref) < 1e-2
+    dy = bf(rows, C)
+    ref.backward(dy.float())
+    dx = bf(rows, C)
+    base = dx.float().clone()
+    parts = O.layernorm_parts(rows, C)
+    dgp = torch.empty(parts, C, device=dev)
+    dbp = torch.empty(parts, C, device=dev)
+    O.layernorm_bwd(x, gamma, st, dy, dx, dgp, dbp, accumulate=True)
+    assert rel(dx.float() - base, xr.grad) < 2e-2
+    assert rel(dgp.sum(0), gr.grad) < 2e-3
+    assert rel(dbp.sum(0), br.grad) < 2e-3
+
+
+@pytest.mark.parametrize("B,heads,sq,sk,dh,cross", [(4, 8, 256, 256, 8, False), (4, 8, 64, 64, 16, False),
+                                                    (4, 8, 16, 16, 32, False), (4, 8, 4, 4, 32, False),
+                                                    (4, 8, 256, 20, 8, True), (4, 8, 16, 20, 32, True)])
+def test_attention(O, B, heads, sq, sk, dh, cross):
+    torch.manual_seed(5)
+    C = heads * dh
+    if cross:
+        q = bf(B * sq, C)
+        kv = bf(B * sk, 2 * C)
+        k, v = kv[:, :C], kv[:, C:]
+    else:
+        qkv = bf(B * sq, 3 * C)
+        q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    o = torch.empty(B * sq, C, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * heads, sq, device=dev)
+    O.attention_fwd(q, k, v, o, lse, B, heads, sq, sk, dh)
+
+    def split(t, s):
+        return t.float().reshape(B, s, heads, dh).permute(0, 2, 1, 3).reshape(B * heads, s, dh)
+    qr, kr, vr = (split(q, sq).requires_grad_(True), split(k, sk).requires_grad_(True),
+                  split(v, sk).requires_grad_(True))
+    att = (qr @ kr.transpose(1, 2) * dh ** -0.5).softmax(-1)
+    ref = att @ vr
+    refm = ref.reshape(B, heads, sq, dh).permute(0, 2, 1, 3).reshape(B * sq, C)
+    assert rel(o, refm) < 1e-2
+    d_o = bf(B * sq, C)
+    refm.backward(d_o.float())
+    dq = torch.empty_like(o)
+    dkv = torch.empty(B * sk, 2 * C, device=dev, dtype=torch.bfloat16)
+    O.attention_bwd(q, k, v, o, lse, d_o, dq, dkv[:, :C], dkv[:, C:], B, heads, sq, sk, dh)
+    assert rel(split(dq, sq), qr.grad) < 2e-2
+    assert rel(split(dkv[:, :C], sk), kr.grad) < 2e-2
+    assert rel(split(dkv[:, C:], sk), vr.grad) < 2e-2
+
+
+def test_elementwise(O):
+    from encdiff_amd.ops import Geom
+    import encdiff_amd._lib as L
+    torch.manual_seed(6)
+    M, n = 4096, 256
+    f = bf(M, 2 * n)
+    y = torch.empty(M, n, device=dev, dtype=torch.bfloat16)
+    O.geglu_fwd(f, y)
+    fr = f.float().requires_grad_(True)
+    a, gt = fr.chunk(2, -1)
+    ref = a * F.gelu(gt)
+    assert rel(y, ref) < 1e-2
+    dy = bf(M, n)
+    ref.backward(dy.float())
+    df = torch.empty_like(f)
+    O.geglu_bwd(f, dy, df)
+    assert rel(df, fr.grad) < 1e-2
+    # resample down / up and adjoints
+    g = Geom(3, 8, 8)
+    x = bf(3 * 16 * 16, 64)
+    yd = torch.empty(g.pixels, 64, device=dev, dtype=torch.bfloat16)
+    O.resample(x, yd, g, L.RESAMPLE_DOWN2)
+    assert rel(nhwc(yd, g), F.avg_pool2d(nhwc(x, Geom(3, 16, 16)), 2)) < 1e-2
+    gu = Geom(3, 16, 16)
+    xu = bf(3 * 64, 64)
+    yu = torch.empty(gu.pixels, 64, device=dev, dtype=torch.bfloat16)
+    O.resample(xu, yu, gu, L.RESAMPLE_UP2)
+    assert rel(nhwc(yu, gu), F.interpolate(nhwc(xu, Geom(3, 8, 8)), scale_factor=2, mode="nearest")) < 1e-2
+    # adjoint of down: grad at 16x16 from dy at 8x8
+    xs = nhwc(x, Geom(3, 16, 16)).requires_grad_(True)
+    dyd = bf(g.pixels, 64)
+    F.avg_pool2d(xs, 2).backward(nhwc(dyd, g))
+    dxs = torch.empty_like(x)
+    O.resample_bwd(dyd, dxs, Geom(3, 16, 16), L.RESAMPLE_DOWN2)
+    assert rel(nhwc(dxs, Geom(3, 16, 16)), xs.grad) < 1e-2
+    xs2 = nhwc(xu, Geom(3, 8, 8)).requires_grad_(True)
+    dyu = bf(gu.pixels, 64)
+    F.interpolate(xs2, scale_factor=2, mode="nearest").backward(nhwc(dyu, gu))
+    dxu = torch.empty_like(xu)
+    O.resample_bwd(dyu, dxu, Geom(3, 8, 8), L.RESAMPLE_UP2)
+    assert rel(nhwc(dxu, Geom(3, 8, 8)), xs2.grad) < 1e-2
+
+
+def test_small_convs(O):
+    from encdiff_amd.ops import Geom
+    torch.manual_seed(7)
+    B = 5
+    g = Geom(B, 16, 16)
+    x = torch.randn(B, 3, 16, 16, device=dev)
+    w = torch.randn(64, 3, 3, 3, device=dev) * 0.2
+    b = torch.randn(64, device=dev)
+    y = torch.empty(g.pixels, 64, device=dev, dtype=torch.bfloat16)
+    O.small_conv_in_fwd(x, g, w, b, y)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    ref = F.conv2d(x, wr, br, padding=1)
+    assert rel(nhwc(y, g), ref) < 1e-2
+    dy = bf(g.pixels, 64)
+    ref.backward(nhwc(dy, g))
+    dw = torch.zeros_like(w); db = torch.zeros_like(b)
+    O.small_conv_in_wgrad(x, g, w, dy, dw, db)
+    assert rel(dw, wr.grad) < 2e-3 and rel(db, br.grad) < 2e-3
+    # output conv 64 -> 3
+    h = bf(g.pixels, 64)
+    w2 = torch.randn(3, 64, 3, 3, device=dev) * 0.05
+    b2 = torch.randn(3, device=dev)
+    out = torch.empty(B, 3, 16, 16, device=dev)
+    O.small_conv_out_fwd(h, g, w2, b2, out)
+    hr = nhwc(h, g).requires_grad_(True)
+    w2r = w2.clone().requires_grad_(True); b2r = b2.clone().requires_grad_(True)
+    ref2 = F.conv2d(hr, w2r, b2r, padding=1)
+    assert rel(out, ref2) < 1e-4
+    d2 = torch.randn(B, 3, 16, 16, device=dev)
+    ref2.backward(d2)
+    dh = torch.empty_like(h)
+    dw2 = torch.zeros_like(w2); db2 = torch.zeros_like(b2)
+    O.small_conv_out_bwd(h, g, w2, d2, dh, dw2, db2)
+    assert rel(nhwc(dh, g), hr.grad) < 1e-2
+    assert rel(dw2, w2r.grad) < 2e-3 and rel(db2, b2r.grad) < 2e-3
+
+
+def test_diffusion_math(O):
+    from oracle import encdiff_oracle as OR
+    torch.manual_seed(8)
+    B = 16
+    t = torch.randint(0, 1000, (B,), device=dev)
+    emb = torch.empty(B, 64, device=dev, dtype=torch.bfloat16)
+    O.timestep_embedding(t, 64, emb)
+    assert rel(emb, OR.timestep_embedding(t.cpu(), 64).to(dev)) < 1e-2
+    sch = {k: v.to(dev) for k, v in OR.sched_fp32(OR.register_schedule()).items()}
+    x0 = torch.randn(B, 3, 16, 16, device=dev)
+    eps = torch.randn_like(x0)
+    xt = torch.empty_like(x0)
+    O.q_sample(x0, eps, t, sch["sqrt_alphas_cumprod"], sch["sqrt_one_minus_alphas_cumprod"], xt)
+    assert rel(xt, OR.q_sample(sch, x0, t, eps)) < 1e-6
+    pred = torch.randn_like(x0).requires_grad_(True)
+    out2 = torch.empty(2, device=dev)
+    grad = torch.empty_like(x0)
+    O.l1_loss(pred.detach(), eps, t, sch["lvlb_weights"], out2, grad)
+    loss, ld = OR.p_losses_from_output(sch, pred, eps, t, logvar=torch.zeros(1000, device=dev))
+    loss.backward()
+    assert abs(out2[0].item() - loss.item()) < 1e-5 and abs(out2[1].item() - ld["loss_vlb"].item()) < 1e-5 * max(
+        1, abs(ld["loss_vlb"].item()))
+    assert rel(grad, pred.grad) < 1e-6
+    z = torch.randn_like(x0)
+    xp = torch.empty_like(x0); px = torch.empty_like(x0)
+    O.ddim_step(xt, pred.detach(), z, 0.5, 0.7, 0.1, math.sqrt(0.5), xp, px)
+    rx, rp = OR.ddim_step(xt.cpu(), pred.detach().cpu(), 0.5, 0.7, 0.1, math.sqrt(0.5), z.cpu())
+    assert rel(xp.cpu(), rx) < 1e-6 and rel(px.cpu(), rp) < 1e-6
+
+
+def test_adamw_ema_pack_reduce(O):
+    from oracle import encdiff_oracle as OR
+    import encdiff_amd._lib as L
+    torch.manual_seed(9)
+    n = 4096
+    p = torch.randn(n, device=dev); g = torch.randn(n, device=dev)
+    m = torch.zeros(n, device=dev); v = torch.zeros(n, device=dev)
+    ema = p.clone()
+    rp, rm, rv = p.cpu().clone(), m.cpu().clone(), v.cpu().clone()
+    rema = {"x": ema.cpu().clone()}
+    nu = 0
+    for step in range(1, 4):
+        hy = torch.tensor(O.adamw_hyper(1e-3, step, ema_one_minus_decay=1 - min(0.9999, (1 + step) / (10 + step))),
+                          device=dev)
+        O.adamw_ema(p, g, m, v, hy, ema=ema, ema_n=n - 100)
+        rp, rm, rv = OR.adamw_step(rp, g.cpu(), rm, rv, step, 1e-3)
+        new, nu = OR.ema_update(rema, {"x": rp}, nu)
+        rema["x"][: n - 100] = new["x"][: n - 100]
+    assert (p.cpu() - rp).abs().max().item() < 1e-6
+    assert (ema.cpu() - rema["x"]).abs().max().item() < 1e-6
+    # pack conv weight [co][ci][3][3] -> [co][tap][ci] bf16
+    w = torch.randn(32, 16, 3, 3, device=dev)
+    dst = torch.zeros(32 * 9 * 16 + 100, device=dev, dtype=torch.bfloat16)
+    jobs = (L.PackJob * 2)(L.PackJob(src_off=0, dst_off=0, rows=32, cols=144, kind=1, cin=16),
+                           L.PackJob(src_off=0, dst_off=32 * 144, rows=1, cols=100, kind=0, cin=0))
+    jt = torch.frombuffer(bytearray(jobs), dtype=torch.uint8).to(dev)
+    O.pack_weights(w.reshape(-1), dst, jt, 2)
+    assert torch.equal(dst[: 32 * 144].reshape(32, 3, 3, 16), w.permute(0, 2, 3, 1).to(torch.bfloat16))
+    assert torch.equal(dst[32 * 144:], w.reshape(-1)[:100].to(torch.bfloat16))
+    part = torch.randn(7, 50, device=dev)
+    idx = torch.randperm(200, device=dev)[:50].to(torch.int32)
+    gr = torch.zeros(200, device=dev)
+    O.reduce_partials(part, 50, 7, 50, idx, gr)
+    ref = torch.zeros(200, device=dev)
+    ref[idx.long()] = part.sum(0)
+    assert rel(gr, ref) < 1e-6
