@@ -47,14 +47,15 @@ class GroupNormArgs(C.Structure):
                 ("film", vp), ("ld_film", C.c_long), ("y", vp), ("ldy", C.c_long), ("stats", vp),
                 ("dy", vp), ("lddy", C.c_long), ("dx", vp), ("lddx", C.c_long),
                 ("accumulate_dx", C.c_int), ("pad_", C.c_int),
-                ("dgamma_part", vp), ("dbeta_part", vp), ("dfilm", vp), ("ld_dfilm", C.c_long)]
+                ("dgamma_part", vp), ("dbeta_part", vp), ("ld_part", C.c_long), ("dfilm", vp),
+                ("ld_dfilm", C.c_long)]
 
 
 class LayerNormArgs(C.Structure):
     _fields_ = [("rows", C.c_int), ("c", C.c_int), ("eps", C.c_float),
                 ("x", vp), ("ldx", C.c_long), ("gamma", vp), ("beta", vp), ("y", vp), ("ldy", C.c_long),
                 ("stats", vp), ("dy", vp), ("lddy", C.c_long), ("dx", vp), ("lddx", C.c_long),
-                ("accumulate_dx", C.c_int), ("dgamma_part", vp), ("dbeta_part", vp),
+                ("accumulate_dx", C.c_int), ("dgamma_part", vp), ("dbeta_part", vp), ("ld_part", C.c_long),
                 ("parts", C.c_int), ("pad_", C.c_int)]
 
 

@@ -1,0 +1,184 @@
+"""Flat parameter arena for the MI355X training step.
+
+All trainable parameters of the denoiser (and, when training, of the concept
+encoder) live in ONE fp32 buffer; each ``nn.Parameter`` keeps its reference name
+and shape but its ``.data`` / ``.grad`` become views into the arena.  That makes
+
+  * the optimizer one fused AdamW + EMA kernel over a contiguous array,
+  * gradient all-reduce one (bucketable) contiguous buffer,
+  * the per-step bf16 repack of GEMM weights one kernel driven by a job table.
+
+The arena order is free (state_dict names are unaffected), so parameters that
+the executor consumes together are laid out contiguously: the 28 ResBlock
+emb_layers projections form one [sum 2C][256] matrix (one GEMM per step), the
+16 cross-attention to_k/to_v projections one [sum 2C][context_dim] matrix, and
+each self-attention's to_q/to_k/to_v one [3C][C] matrix.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib as L
+
+
+class ParamArena:
+    def __init__(self, order: Sequence[Tuple[str, torch.nn.Parameter]], device, ema_names: Sequence[str] = (),
+                 align: int = 8):
+        self.device = torch.device(device)
+        self.names: List[str] = []
+        self.offsets: Dict[str, Tuple[int, Tuple[int, ...]]] = {}
+        self.params: Dict[str, torch.nn.Parameter] = {}
+        off = 0
+        ema_set = set(ema_names)
+        # EMA-tracked params first so the EMA covers a prefix of the arena
+        ordered = [o for o in order if o[0] in ema_set] + [o for o in order if o[0] not in ema_set]
+        self.ema_numel = 0
+        for name, p in ordered:
+            if name in self.offsets:
+                continue
+            off = (off + align - 1) // align * align
+            self.offsets[name] = (off, tuple(p.shape))
+            self.params[name] = p
+            self.names.append(name)
+            off += p.numel()
+            if name in ema_set:
+                self.ema_numel = off
+        self.numel = (off + 3) // 4 * 4
+        self.master = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
+        self.grad = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
+        self.exp_avg = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
+        self.exp_avg_sq = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
+        self.ema: Optional[torch.Tensor] = None
+        with torch.no_grad():
+            for name in self.names:
+                p = self.params[name]
+                o, shp = self.offsets[name]
+                view = self.master[o:o + p.numel()].view(shp)
+                view.copy_(p.detach().to(self.device, torch.float32))
+                p.data = view
+                p.grad = self.grad[o:o + p.numel()].view(shp)
+        self.step = 0
+        self.hyper = torch.zeros(8, device=self.device, dtype=torch.float32)
+
+    # -------------------------------------------------------------- views
+    def f32(self, name: str) -> torch.Tensor:
+        o, shp = self.offsets[name]
+        n = 1
+        for s in shp:
+            n *= s
+        return self.master[o:o + n].view(shp)
+
+    def grad_of(self, name: str) -> torch.Tensor:
+        o, shp = self.offsets[name]
+        n = 1
+        for s in shp:
+            n *= s
+        return self.grad[o:o + n].view(shp)
+
+    def span(self, names: Sequence[str]) -> Tuple[int, int]:
+        """(offset, numel) of a group of params laid out back-to-back (checked)."""
+        o0, _ = self.offsets[names[0]]
+        cur = o0
+        for n in names:
+            o, shp = self.offsets[n]
+            assert o == cur, f"{n} not contiguous in the arena"
+            k = 1
+            for s in shp:
+                k *= s
+            cur = o + k
+        return o0, cur - o0
+
+    def attach_grads(self):
+        """Make every parameter's .grad the arena view again (an optimizer's
+        zero_grad(set_to_none=True) detaches them); re-attached slices start at zero."""
+        for name in self.names:
+            p = self.params[name]
+            g = p.grad
+            o, shp = self.offsets[name]
+            if g is None or g.data_ptr() != self.grad.data_ptr() + 4 * o:
+                view = self.grad[o:o + p.numel()].view(shp)
+                view.zero_()
+                p.grad = view
+
+    def zero_grad(self):
+        self.attach_grads()
+        self.grad.zero_()
+
+    def enable_ema(self):
+        if self.ema is None:
+            self.ema = self.master[: self.ema_numel].clone()
+        return self.ema
+
+
+class PackTable:
+    """bf16 compute copies of the GEMM weights, refreshed from the fp32 arena by one
+    kernel (encdiff_pack_weights) after every optimizer step."""
+
+    def __init__(self, arena: ParamArena):
+        self.arena = arena
+        self.jobs: List[L.PackJob] = []
+        self.views: Dict[str, Tuple[int, int, int]] = {}  # key -> (dst_off, rows, cols)
+        self.numel = 0
+
+    def add(self, key: str, src_off: int, rows: int, cols: int, kind: int = 0, cin: int = 0):
+        off = (self.numel + 7) // 8 * 8
+        self.jobs.append(L.PackJob(src_off=src_off, dst_off=off, rows=rows, cols=cols, kind=kind, cin=cin))
+        self.views[key] = (off, rows, cols)
+        self.numel = off + rows * cols
+
+    def finalize(self):
+        dev = self.arena.device
+        self.buf = torch.zeros(max(self.numel, 8), device=dev, dtype=torch.bfloat16)
+        arr = (L.PackJob * len(self.jobs))(*self.jobs)
+        self.jobs_dev = torch.frombuffer(bytearray(arr), dtype=torch.uint8).to(dev)
+        self.njobs = len(self.jobs)
+
+    def view(self, key: str) -> torch.Tensor:
+        off, rows, cols = self.views[key]
+        return self.buf[off:off + rows * cols].view(rows, cols)
+
+    def repack(self):
+        from . import ops
+        ops.pack_weights(self.arena.master, self.buf, self.jobs_dev, self.njobs)
+
+
+class NormPartials:
+    """Per-layer GroupNorm/LayerNorm gamma/beta partial sums laid out as columns of one
+    fp32 matrix [rows][cols]; one encdiff_reduce_partials per step folds them into
+    the gradient arena."""
+
+    def __init__(self, arena: ParamArena, rows: int):
+        self.arena = arena
+        self.rows = rows
+        self.cols = 0
+        self.index: List[int] = []
+        self.slots: Dict[str, int] = {}
+
+    def add(self, gamma_name: str, beta_name: str) -> int:
+        og, shg = self.arena.offsets[gamma_name]
+        ob, shb = self.arena.offsets[beta_name]
+        c = shg[0]
+        base = self.cols
+        self.index.extend(range(og, og + c))
+        self.index.extend(range(ob, ob + c))
+        self.cols += 2 * c
+        self.slots[gamma_name] = base
+        return base
+
+    def finalize(self):
+        dev = self.arena.device
+        self.ld = max(self.cols, 1)
+        self.buf = torch.zeros(self.rows, self.ld, device=dev, dtype=torch.float32)
+        self.index_dev = torch.tensor(self.index if self.index else [0], device=dev, dtype=torch.int32)
+
+    def parts(self, gamma_name: str, c: int):
+        base = self.slots[gamma_name]
+        return self.buf[:, base:base + c], self.buf[:, base + c:base + 2 * c]
+
+    def reduce(self):
+        from . import ops
+        if self.cols:
+            ops.reduce_partials(self.buf, self.ld, self.rows, self.cols, self.index_dev, self.arena.grad)

@@ -170,8 +170,8 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
       for (int r = 0; r < L.np; ++r) a += red[(k * L.np + r) * C + c];
       chs[k * C + c] = a;
     }
-    p.dbeta_part[(long)b * C + c] = chs[c];
-    p.dgamma_part[(long)b * C + c] = chs[C + c];
+    p.dbeta_part[(long)b * p.ld_part + c] = chs[c];
+    p.dgamma_part[(long)b * p.ld_part + c] = chs[C + c];
     if (film) {
       p.dfilm[(long)b * p.ld_dfilm + c] = chs[3 * C + c];       // d scale = sum dz * n
       p.dfilm[(long)b * p.ld_dfilm + C + c] = chs[2 * C + c];   // d shift = sum dz
@@ -294,8 +294,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const EncdiffLayerNormArgs 
   for (int c = threadIdx.x; c < C; c += 256) {
     float a = 0.f, bsum = 0.f;
     for (int r = 0; r < RPB; ++r) { a += red[0][r][c]; bsum += red[1][r][c]; }
-    p.dgamma_part[(long)blockIdx.x * C + c] = a;
-    p.dbeta_part[(long)blockIdx.x * C + c] = bsum;
+    p.dgamma_part[(long)blockIdx.x * p.ld_part + c] = a;
+    p.dbeta_part[(long)blockIdx.x * p.ld_part + c] = bsum;
   }
 }
 

@@ -1,0 +1,236 @@
+"""UNetModel (the EncDiff denoiser) and the as-is concept encoder Encoder4.
+
+Mirrors ldm/modules/diffusionmodules/openaimodel_enc.py:
+  * ``UNetModel`` (:413-748): same constructor kwargs, same submodule / parameter
+    names (state_dicts interchange with the reference), same forward signature
+    ``forward(x, timesteps, context=[c], y=None, **kwargs)``.  The forward runs the
+    MI355X executor (encdiff_amd/unet.py) through a torch.autograd.Function, so
+    ``loss.backward()`` reaches the concept encoder through d(context); the UNet's
+    own weight gradients are written straight into the parameter arena.
+    There is no CPU path: calling it on a CPU tensor raises.
+  * ``Encoder4`` / ``EncResBlock`` / ``View`` (:969-1049): plain PyTorch, called
+    as-is (north_star: the concept-token image encoder is not re-implemented).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import nn
+
+from encdiff_amd import _lib as L
+from encdiff_amd.arena import ParamArena
+from encdiff_amd.unet import ConvSpec, ResSpec, STSpec, UNetExecutor, UNetSpec
+from ..attention import SpatialTransformer
+from .util import normalization, zero_module
+
+
+class TimestepBlock(nn.Module):
+    pass
+
+
+class TimestepEmbedSequential(nn.Sequential, TimestepBlock):
+    """openaimodel_enc.py:74-88 (container; the executor walks the layers)."""
+
+
+class ResBlock(TimestepBlock):
+    """openaimodel_enc.py:163-275 -- parameter container with the reference names."""
+
+    def __init__(self, channels, emb_channels, dropout, out_channels=None, use_conv=False,
+                 use_scale_shift_norm=False, dims=2, use_checkpoint=False, up=False, down=False):
+        super().__init__()
+        self.channels = channels
+        self.out_channels = out_channels or channels
+        self.use_scale_shift_norm = use_scale_shift_norm
+        self.updown = up or down
+        self.in_layers = nn.Sequential(normalization(channels), nn.SiLU(),
+                                       nn.Conv2d(channels, self.out_channels, 3, padding=1))
+        self.emb_layers = nn.Sequential(
+            nn.SiLU(), nn.Linear(emb_channels, 2 * self.out_channels if use_scale_shift_norm else self.out_channels))
+        self.out_layers = nn.Sequential(normalization(self.out_channels), nn.SiLU(), nn.Dropout(p=dropout),
+                                        zero_module(nn.Conv2d(self.out_channels, self.out_channels, 3, padding=1)))
+        if self.out_channels == channels:
+            self.skip_connection = nn.Identity()
+        elif use_conv:
+            self.skip_connection = nn.Conv2d(channels, self.out_channels, 3, padding=1)
+        else:
+            self.skip_connection = nn.Conv2d(channels, self.out_channels, 1)
+
+    def forward(self, x, emb):
+        raise RuntimeError("ResBlock runs inside the HIP UNet executor; call UNetModel.forward")
+
+
+class _UNetFn(torch.autograd.Function):
+    """eps = UNet(x_t, t, context); backward returns d(context) only (x_t needs no
+    gradient in the EncDiff objective); weight grads go to the arena."""
+
+    @staticmethod
+    def forward(ctx, x, t, c, ex: UNetExecutor):
+        ctx.ex = ex
+        return ex.forward(x, t, c).clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        dc = ctx.ex.backward(g.float())
+        return None, None, dc.clone(), None
+
+
+_SUPPORTED = dict(dims=2, num_classes=None, use_fp16=False, num_head_channels=-1, transformer_depth=1,
+                  use_spatial_transformer=True, use_scale_shift_norm=True, resblock_updown=True, n_embed=None,
+                  legacy=True)
+
+
+class UNetModel(nn.Module):
+    """openaimodel_enc.py:413-748 for the EncDiff configuration family
+    (spatial transformer, scale-shift norm, ResBlock up/down)."""
+
+    def __init__(self, image_size, in_channels, model_channels, out_channels, num_res_blocks,
+                 attention_resolutions, latent_unit, dropout=0, channel_mult=(1, 2, 4, 8), conv_resample=True,
+                 dims=2, num_classes=None, use_checkpoint=False, use_fp16=False, num_heads=-1,
+                 num_head_channels=-1, num_heads_upsample=-1, use_scale_shift_norm=False, resblock_updown=False,
+                 use_new_attention_order=False, use_spatial_transformer=False, transformer_depth=1,
+                 context_dim=None, n_embed=None, legacy=True):
+        super().__init__()
+        given = dict(dims=dims, num_classes=num_classes, use_fp16=use_fp16, num_head_channels=num_head_channels,
+                     transformer_depth=transformer_depth, use_spatial_transformer=use_spatial_transformer,
+                     use_scale_shift_norm=use_scale_shift_norm, resblock_updown=resblock_updown, n_embed=n_embed,
+                     legacy=legacy)
+        bad = {k: v for k, v in given.items() if v != _SUPPORTED[k]}
+        if bad or dropout:
+            raise NotImplementedError(f"HIP UNet path supports the EncDiff config family only; unsupported: {bad}")
+        if isinstance(context_dim, (list, tuple)):
+            context_dim = context_dim[0]
+        self.image_size = image_size
+        self.in_channels = in_channels
+        self.model_channels = model_channels
+        self.out_channels = out_channels
+        self.num_res_blocks = num_res_blocks
+        self.attention_resolutions = list(attention_resolutions)
+        self.channel_mult = list(channel_mult)
+        self.num_heads = num_heads
+        self.context_dim = context_dim
+        self.latent_unit = latent_unit
+        self.dtype = torch.float32
+        self.num_classes = None
+        self.predict_codebook_ids = False
+        cfg = dict(image_size=image_size, in_channels=in_channels, out_channels=out_channels,
+                   model_channels=model_channels, attention_resolutions=self.attention_resolutions,
+                   num_res_blocks=num_res_blocks, channel_mult=self.channel_mult, num_heads=num_heads,
+                   context_dim=context_dim, latent_unit=latent_unit)
+        self._spec = UNetSpec.from_config(cfg)
+        ted = model_channels * 4
+        self.time_embed = nn.Sequential(nn.Linear(model_channels, ted), nn.SiLU(), nn.Linear(ted, ted))
+
+        def make(layer):
+            if isinstance(layer, ConvSpec):
+                return nn.Conv2d(layer.cin, layer.cout, 3, padding=1)
+            if isinstance(layer, ResSpec):
+                return ResBlock(layer.cin, ted, 0, out_channels=layer.cout, use_scale_shift_norm=True,
+                                up=layer.updown == L.RESAMPLE_UP2, down=layer.updown == L.RESAMPLE_DOWN2)
+            return SpatialTransformer(layer.c, layer.heads, layer.dh, context_dim=context_dim)
+
+        self.input_blocks = nn.ModuleList([TimestepEmbedSequential(*[make(l) for l in b])
+                                           for b in self._spec.input_blocks])
+        self.middle_block = TimestepEmbedSequential(*[make(l) for l in self._spec.middle])
+        self.output_blocks = nn.ModuleList([TimestepEmbedSequential(*[make(l) for l in b])
+                                            for b in self._spec.output_blocks])
+        self.out = nn.Sequential(normalization(self._spec.out_ch), nn.SiLU(),
+                                 zero_module(nn.Conv2d(model_channels, out_channels, 3, padding=1)))
+        self._arena: Optional[ParamArena] = None
+        self._ex: Optional[UNetExecutor] = None
+        self._packed_version = -1
+
+    # ------------------------------------------------------------- HIP binding
+    def bind_arena(self, arena: Optional[ParamArena] = None):
+        """Put the parameters into `arena` (shared with other trainables) or a private one."""
+        named = dict(self.named_parameters())
+        if arena is None:
+            dev = next(self.parameters()).device
+            arena = ParamArena(self._spec.arena_order(named), dev, ema_names=list(named))
+        self._arena = arena
+        self._ex = None
+        return arena
+
+    def arena_order(self):
+        return self._spec.arena_order(dict(self.named_parameters()))
+
+    def executor(self) -> UNetExecutor:
+        if self._arena is None:
+            self.bind_arena()
+        if self._ex is None or self._ex.arena is not self._arena:
+            self._ex = UNetExecutor(self._spec, self._arena)
+            self._packed_version = self._arena.master._version
+        elif self._arena.master._version != self._packed_version:
+            # parameters were modified in place (load_state_dict, EMA swap...): refresh bf16 copies
+            self._ex.pack.repack()
+            self._packed_version = self._arena.master._version
+        return self._ex
+
+    def mark_repacked(self):
+        if self._arena is not None:
+            self._packed_version = self._arena.master._version
+
+    def forward(self, x, timesteps=None, context=None, y=None, **kwargs):
+        if not x.is_cuda:
+            raise RuntimeError("UNetModel runs on the MI355X HIP path only (no CPU fallback)")
+        c = context[0] if isinstance(context, (list, tuple)) else context
+        c = c.reshape(x.shape[0], -1).float()
+        ex = self.executor()
+        if torch.is_grad_enabled():
+            self._arena.attach_grads()
+        return _UNetFn.apply(x.float(), timesteps.long(), c, ex)
+
+
+# --------------------------------------------------------------------------- Encoder4 (as-is)
+class EncResBlock(nn.Module):
+    """openaimodel_enc.py:969-989."""
+
+    def __init__(self, in_channels, out_channels, mid_channels=None, bn=False):
+        super().__init__()
+        mid = mid_channels or out_channels
+        layers = [nn.ReLU(), nn.Conv2d(in_channels, mid, 3, 1, 1), nn.ReLU(), nn.Conv2d(mid, out_channels, 1, 1, 0)]
+        if bn:
+            layers.insert(2, nn.BatchNorm2d(out_channels))
+        self.convs = nn.Sequential(*layers)
+
+    def forward(self, x):
+        return x + self.convs(x)
+
+
+class View(nn.Module):
+    def __init__(self, size):
+        super().__init__()
+        self.size = size
+
+    def forward(self, tensor):
+        return tensor.view(self.size)
+
+
+class Encoder4(nn.Module):
+    """openaimodel_enc.py:991-1041: image -> latent_unit scalars -> per-unit MLP warp
+    to context_dim-d concept tokens, concatenated to (B, latent_unit*context_dim)."""
+
+    def __init__(self, d, context_dim, latent_unit, bn=True, num_channels=3):
+        super().__init__()
+        self.context_dim = context_dim
+        self.latent_unit = latent_unit
+        self.encoder = nn.Sequential(
+            nn.Conv2d(num_channels, d, 4, 2, 1), nn.BatchNorm2d(d), nn.ReLU(True),
+            nn.Conv2d(d, d, 4, 2, 1), nn.BatchNorm2d(d), nn.ReLU(True),
+            nn.Conv2d(d, d, 4, 2, 1), nn.BatchNorm2d(d),
+            nn.Conv2d(d, d, 4, 2, 1), nn.BatchNorm2d(d), nn.ReLU(True),
+            EncResBlock(d, d, bn=bn), nn.BatchNorm2d(d), nn.ReLU(True),
+            EncResBlock(d, d, bn=bn),
+            View((-1, 128 * 4 * 4)),
+            nn.Linear(2048, latent_unit))
+        self.net = nn.ModuleList([nn.Sequential(nn.Linear(1, 64), nn.ELU(True), nn.Linear(64, 128), nn.ELU(True),
+                                                nn.Linear(128, context_dim)) for _ in range(latent_unit)])
+
+    def warp(self, u):
+        return torch.cat([self.net[i](u[:, i][:, None]) for i in range(self.latent_unit)], dim=1)
+
+    def forward(self, x):
+        return self.warp(self.encoder(x))
+
+    def encoding(self, x):
+        return self.encoder(x)

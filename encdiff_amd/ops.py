@@ -135,19 +135,21 @@ def groupnorm_fwd(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_fi
 
 
 def groupnorm_bwd(x, g: Geom, gamma, beta, stats, eps, silu, dy, dx, dgamma_part, dbeta_part, film=None,
-                  ld_film=0, dfilm=None, ld_dfilm=0, accumulate=False, groups=32):
+                  ld_film=0, dfilm=None, ld_dfilm=0, accumulate=False, groups=32, ld_part=None):
     c = x.shape[1]
     a = L.GroupNormArgs(batch=g.batch, hw=g.h * g.w, c=c, groups=groups, eps=eps, silu=int(silu),
                         x=_p(x), ldx=_ld(x), gamma=_p(gamma), beta=_p(beta), film=_p(film), ld_film=ld_film,
                         stats=_p(stats), dy=_p(dy), lddy=_ld(dy), dx=_p(dx), lddx=_ld(dx),
                         accumulate_dx=int(accumulate), dgamma_part=_p(dgamma_part), dbeta_part=_p(dbeta_part),
-                        dfilm=_p(dfilm), ld_dfilm=ld_dfilm)
+                        ld_part=c if ld_part is None else ld_part, dfilm=_p(dfilm), ld_dfilm=ld_dfilm)
     check(lib.encdiff_groupnorm_bwd(C.byref(a), _s()), "encdiff_groupnorm_bwd")
 
 
+LN_PARTS = 256  # fixed partial-row count of the LayerNorm backward (blocks without rows write zeros)
+
+
 def layernorm_parts(rows, c):
-    rpb = 256 // (c // 8)
-    return max(1, min(256, (rows + rpb - 1) // rpb))
+    return LN_PARTS
 
 
 def layernorm_fwd(x, gamma, beta, y, stats, eps=1e-5):
@@ -157,13 +159,13 @@ def layernorm_fwd(x, gamma, beta, y, stats, eps=1e-5):
     check(lib.encdiff_layernorm_fwd(C.byref(a), _s()), "encdiff_layernorm_fwd")
 
 
-def layernorm_bwd(x, gamma, stats, dy, dx, dgamma_part, dbeta_part, accumulate=False):
+def layernorm_bwd(x, gamma, stats, dy, dx, dgamma_part, dbeta_part, accumulate=False, ld_part=None):
     rows, c = x.shape
     parts = layernorm_parts(rows, c)
-    assert dgamma_part.numel() >= parts * c
+    ld_part = c if ld_part is None else ld_part
     a = L.LayerNormArgs(rows=rows, c=c, eps=0.0, x=_p(x), ldx=_ld(x), gamma=_p(gamma), stats=_p(stats),
                         dy=_p(dy), lddy=_ld(dy), dx=_p(dx), lddx=_ld(dx), accumulate_dx=int(accumulate),
-                        dgamma_part=_p(dgamma_part), dbeta_part=_p(dbeta_part), parts=parts)
+                        dgamma_part=_p(dgamma_part), dbeta_part=_p(dbeta_part), ld_part=ld_part, parts=parts)
     check(lib.encdiff_layernorm_bwd(C.byref(a), _s()), "encdiff_layernorm_bwd")
 
 

@@ -115,8 +115,9 @@ typedef struct EncdiffGroupNormArgs {
   void* dx; long lddx;       /* bf16                                                */
   int accumulate_dx;         /* dx += result                                        */
   int pad_;
-  float* dgamma_part;        /* fp32 [batch][c] per-image partial sums (reduced later) */
+  float* dgamma_part;        /* fp32 [batch][ld_part] per-image partial sums (reduced later) */
   float* dbeta_part;
+  long ld_part;
   float* dfilm; long ld_dfilm;       /* fp32 [batch][ld_dfilm]: dscale at [c], dshift at [C + c] */
 } EncdiffGroupNormArgs;
 
@@ -136,8 +137,9 @@ typedef struct EncdiffLayerNormArgs {
   const void* dy; long lddy; /* backward */
   void* dx; long lddx;
   int accumulate_dx;         /* dx += (residual branch)                            */
-  float* dgamma_part;        /* fp32 [parts][c]                                    */
+  float* dgamma_part;        /* fp32 [parts][ld_part]                              */
   float* dbeta_part;
+  long ld_part;
   int parts;                 /* number of partial rows (grid size of the backward) */
   int pad_;
 } EncdiffLayerNormArgs;

@@ -1,0 +1,67 @@
+"""CPU tests of the host side of the UNet mirror: config instantiation, module /
+parameter names and shapes identical to the reference state_dict, the executor's
+static schedule and the arena layout."""
+import json
+import os
+
+import pytest
+import torch
+
+import encdiff_amd  # noqa: F401  (installs the ldm alias)
+from oracle import encdiff_oracle as O
+
+UNET_PARAMS = dict(image_size=16, in_channels=3, out_channels=3, model_channels=64, attention_resolutions=[1, 2, 4],
+                   num_res_blocks=2, channel_mult=[1, 2, 4, 4], num_heads=8, use_scale_shift_norm=True,
+                   resblock_updown=True, use_spatial_transformer=True, context_dim=16, latent_unit=20)
+
+
+def test_instantiate_from_config_alias():
+    from ldm.util import instantiate_from_config
+    m = instantiate_from_config({"target": "ldm.modules.diffusionmodules.openaimodel_enc.UNetModel",
+                                 "params": UNET_PARAMS})
+    from encdiff_amd.ldm.modules.diffusionmodules.openaimodel_enc import UNetModel
+    assert isinstance(m, UNetModel)
+
+
+def test_unet_state_dict_matches_reference(golden_dir):
+    from encdiff_amd.ldm.modules.diffusionmodules.openaimodel_enc import UNetModel
+    m = UNetModel(**UNET_PARAMS)
+    ref = json.load(open(os.path.join(golden_dir, "unet_state_dict_shapes.json")))
+    mine = {k: list(v.shape) for k, v in m.state_dict().items()}
+    assert mine == ref
+    assert sum(p.numel() for p in m.parameters()) == 37469635
+
+
+def test_load_reference_named_weights():
+    from encdiff_amd.ldm.modules.diffusionmodules.openaimodel_enc import UNetModel
+    m = UNetModel(**UNET_PARAMS)
+    P = O.recipe_params(O.param_shapes(O.build_plan()))
+    m.load_state_dict(P, strict=True)
+
+
+def test_spec_counts_and_arena_layout():
+    from encdiff_amd.unet import UNetSpec
+    from encdiff_amd.arena import ParamArena
+    from encdiff_amd.ldm.modules.diffusionmodules.openaimodel_enc import UNetModel
+    s = UNetSpec.from_config(UNET_PARAMS)
+    assert len(s.res) == 28 and len(s.sts) == 16
+    assert s.film_total == 10240 and s.kv_total == 4992
+    assert [t.h for t in s.sts] == [16] * 2 + [8] * 2 + [4] * 2 + [2] + [4] * 3 + [8] * 3 + [16] * 3
+    m = UNetModel(**UNET_PARAMS)
+    named = dict(m.named_parameters())
+    arena = ParamArena(s.arena_order(named), "cpu", ema_names=list(named))
+    assert arena.ema_numel >= 37469635
+    # params are views of the arena, grads too
+    for n, p in named.items():
+        o, _ = arena.offsets[n]
+        assert p.data_ptr() == arena.master.data_ptr() + 4 * o
+        assert p.grad.data_ptr() == arena.grad.data_ptr() + 4 * o
+    o, n = arena.span([r.prefix + "emb_layers.1.weight" for r in s.res])
+    assert n == 10240 * 256
+
+
+def test_unet_refuses_cpu():
+    from encdiff_amd.ldm.modules.diffusionmodules.openaimodel_enc import UNetModel
+    m = UNetModel(**UNET_PARAMS)
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 3, 16, 16), torch.zeros(1, dtype=torch.long), [torch.zeros(1, 320)])
