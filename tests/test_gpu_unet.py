@@ -41,6 +41,7 @@ def test_unet_matches_reference_fixture(unet, golden_dir):
     x = torch.tensor(fx["x"]).cuda()
     t = torch.tensor(fx["t"]).cuda()
     ctx = torch.tensor(fx["ctx"]).cuda().requires_grad_(True)
+    unet.executor()
     unet._arena.zero_grad()
     eps = unet(x, t, context=[ctx])
     e = rel(eps.detach(), fx["eps"])
