@@ -1,0 +1,189 @@
+"""EncDiff training benchmark on MI355X (driver contract: one JSON line on rank 0).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (data-parallel, RCCL)
+
+Metric (BASELINE.json): training imgs/sec on Shapes3D 64x64 (VQ-f4, 16x16 latent),
+configs[1]: batch 128 per GPU, bf16 HIP path.  A step = one full LatentDiffusion
+training step: frozen VQ encode + Encoder4 + q_sample + UNet fwd/bwd + L1 + AdamW +
+EMA (+ RCCL gradient all-reduce when N > 1).  Inputs: synthetic images resident in HBM
+(no dataset / checkpoint is available offline).  Also reported: DDIM sampling steps/s,
+the roofline of the dominant kernel measured live with HIP events, and the CPU
+oracle (the repo's restatement of the reference) timed on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+# MI355X peaks (MI355X_MICROARCH.md, chip-level parameters): dense bf16 MFMA, HBM3E spec
+PEAK_BF16_TFLOPS = 2500.0
+PEAK_HBM_GBS = 8000.0
+F_UNET_FWD_PER_IMG = 1.98671e9  # SURVEY.md §8(d), FlopCounterMode on the reference UNet
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--ddim-steps", type=int, default=200)
+    ap.add_argument("--ddim-batch", type=int, default=8)
+    ap.add_argument("--skip-ddim", action="store_true")
+    ap.add_argument("--skip-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist.get_rank(), ws
+    torch.cuda.set_device(0)
+    return 0, 1
+
+
+def build_ldm():
+    import encdiff_amd  # noqa: F401
+    from encdiff_amd.configs import model_config
+    from encdiff_amd.ldm.util import instantiate_from_config
+    cfg = model_config("shapes3d")
+    torch.manual_seed(0)
+    return instantiate_from_config(cfg).cuda(), cfg
+
+
+def kernel_roofline(B):
+    """Live HIP-event timing of the dominant kernel: the conv3x3 implicit-GEMM forward
+    at the 16x16 level (M = B*256 pixels, N = 64, K = 9*64)."""
+    from encdiff_amd import ops
+    from encdiff_amd.ops import Geom
+    g = Geom(B, 16, 16)
+    cin = cout = 64
+    x = (torch.randn(g.pixels, cin, device="cuda") * 0.5).to(torch.bfloat16)
+    w = (torch.randn(cout, 9 * cin, device="cuda") * 0.04).to(torch.bfloat16)
+    y = torch.empty(g.pixels, cout, device="cuda", dtype=torch.bfloat16)
+    bias = torch.zeros(cout, device="cuda")
+    for _ in range(20):
+        ops.conv3x3_fwd(x, g, cin, w, y, bias=bias)
+    n = 200
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(n):
+        ops.conv3x3_fwd(x, g, cin, w, y, bias=bias)
+    e1.record()
+    torch.cuda.synchronize()
+    avg_s = e0.elapsed_time(e1) / 1e3 / n
+    flops = 2.0 * g.pixels * cout * 9 * cin
+    return {"kernel": "gemm_kernel<IM2COL,ROWK> conv3x3 fwd 16x16x64->64", "bound": "mfma",
+            "achieved": flops / avg_s / 1e12, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": flops / avg_s / 1e12 / PEAK_BF16_TFLOPS, "traffic": None,
+            "avg_us": avg_s * 1e6, "flops_per_launch": flops}
+
+
+def ddim_rate(ldm, B, S):
+    from encdiff_amd.ldm.models.diffusion.ddim import DDIMSampler
+    cond = torch.randn(B, 320, device="cuda")
+    sampler = DDIMSampler(ldm)
+    x_T = torch.randn(B, 3, 16, 16, device="cuda")
+    with torch.no_grad():
+        sampler.sample(S, B, (3, 16, 16), cond, eta=0.0, verbose=False, x_T=x_T)  # capture + warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sampler.sample(S, B, (3, 16, 16), cond, eta=0.0, verbose=False, x_T=x_T)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    return S / dt
+
+
+def cpu_baseline(budget_s):
+    """The CPU oracle (repo restatement of the reference, pinned to reference fixtures),
+    full training step on latents (Encoder4 + UNet fwd/bwd + AdamW + EMA), B=4 fp32."""
+    from oracle import encdiff_oracle as O
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(min(cores, 64))
+    tr = O.OracleTrainer(O.build_plan(), lr=4 * 2e-6)
+    g = torch.Generator().manual_seed(1234)
+    B = 4
+
+    def batch():
+        return (torch.randn(B, 3, 16, 16, generator=g), torch.rand(B, 3, 64, 64, generator=g) * 2 - 1,
+                torch.randint(0, 1000, (B,), generator=g), torch.randn(B, 3, 16, 16, generator=g))
+    tr.step(*batch())
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or n < 2:
+        tr.step(*batch())
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": B * n / dt, "unit": "imgs/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} oracle training steps at batch {B} (fp32, Encoder4+UNet fwd/bwd+AdamW+EMA) "
+                      f"in {dt:.1f}s"}
+
+
+def main():
+    args = parse()
+    rank, world = setup_dist(args)
+    from encdiff_amd.trainer import HipTrainer, time_steps
+    ldm, cfg = build_ldm()
+    tr = HipTrainer(ldm, args.batch, graph=not args.no_graph)
+    tr.init_scale_factor()
+    tr.capture(warmup=3)
+    for _ in range(args.warmup):
+        tr.step()
+    dt = time_steps(tr, args.steps)
+    if world > 1:
+        t = torch.tensor([dt], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    imgs = args.batch * world * args.steps
+    value = imgs / dt
+    loss = tr.loss()
+    extra = {}
+    if rank == 0:
+        extra["roofline"] = kernel_roofline(args.batch)
+        f_step = 3 * F_UNET_FWD_PER_IMG * args.batch
+        extra["step_roofline"] = {"bound": "mfma", "unit": "TFLOP/s",
+                                  "achieved": f_step * args.steps / dt / 1e12,
+                                  "peak": PEAK_BF16_TFLOPS,
+                                  "frac": f_step * args.steps / dt / 1e12 / PEAK_BF16_TFLOPS,
+                                  "flops_per_img": 3 * F_UNET_FWD_PER_IMG}
+        if not args.skip_ddim:
+            extra["ddim_steps_per_sec"] = {"value": ddim_rate(ldm, args.ddim_batch, args.ddim_steps),
+                                           "batch": args.ddim_batch, "S": args.ddim_steps, "eta": 0.0}
+        if not args.skip_cpu:
+            extra["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        out = {"metric": "training imgs/sec (node) Shapes3D 64x64 LDM", "value": value, "unit": "imgs/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+               "config": {"workload": "configs[1]: Shapes3D VQ-f4 16x16 latent LatentDiffusion training step "
+                                      "(shapes3d-vq-4-16-encdiff)", "global_batch": args.batch * world,
+                          "per_gpu_batch": args.batch, "parallelism": f"dp{world}",
+                          "graph": not args.no_graph},
+               "loss_simple_last": loss}
+        out.update(extra)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -103,6 +103,7 @@ _PROTOS = {
     "encdiff_q_sample": [vp, vp, vp, vp, vp, C.c_int, C.c_int, vp, vp],
     "encdiff_l1_loss": [vp, vp, vp, vp, C.c_int, C.c_int, C.c_float, vp, vp, vp],
     "encdiff_ddim_step": [vp, vp, vp, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, vp, vp, vp],
+    "encdiff_ddim_step_indexed": [vp, vp, vp, C.c_int, vp, vp, C.c_int, vp, vp, vp],
     "encdiff_adamw_ema": [vp, vp, vp, vp, vp, C.c_longlong, vp, C.c_longlong, vp],
     "encdiff_pack_weights": [vp, vp, vp, C.c_int, vp],
     "encdiff_reduce_partials": [vp, C.c_long, C.c_int, C.c_int, vp, vp, vp],

@@ -1,0 +1,58 @@
+"""Model configurations of the EncDiff denoising path as Python data.
+
+SHAPES3D is the drop-in contract configs/latent-diffusion/shapes3d-vq-4-16-encdiff.yaml
+(model section; the reference YAML itself loads unchanged through
+encdiff_amd.config.load_config when it is available).  The VQ checkpoint path of the
+reference config is absolute and unavailable, so ``ckpt_path`` is omitted
+(random-init, frozen first stage).
+"""
+from __future__ import annotations
+
+import copy
+
+SHAPES3D = {
+    "base_learning_rate": 2.0e-6,
+    "target": "ldm.models.diffusion.ddpm_enc.LatentDiffusion",
+    "params": {
+        "linear_start": 0.0015, "linear_end": 0.0155, "num_timesteps_cond": 1, "log_every_t": 200,
+        "timesteps": 1000, "loss_type": "l1", "first_stage_key": "image", "cond_stage_key": "image",
+        "image_size": 16, "channels": 3, "cond_stage_trainable": True, "concat_mode": False,
+        "scale_by_std": True, "monitor": "train/loss_simple", "conditioning_key": "crossattn",
+        "eval_name": "shapes3d",
+        "scheduler_config": {"target": "ldm.lr_scheduler.LambdaLinearScheduler",
+                             "params": {"warm_up_steps": [10000], "cycle_lengths": [10000000000000],
+                                        "f_start": [1.e-6], "f_max": [1.], "f_min": [1.]}},
+        "unet_config": {"target": "ldm.modules.diffusionmodules.openaimodel_enc.UNetModel",
+                        "params": {"image_size": 16, "in_channels": 3, "out_channels": 3, "model_channels": 64,
+                                   "attention_resolutions": [1, 2, 4], "num_res_blocks": 2,
+                                   "channel_mult": [1, 2, 4, 4], "num_heads": 8, "use_scale_shift_norm": True,
+                                   "resblock_updown": True, "use_spatial_transformer": True, "context_dim": 16,
+                                   "latent_unit": 20}},
+        "first_stage_config": {"target": "ldm.models.autoencoder.VQModelInterface",
+                               "params": {"embed_dim": 3, "n_embed": 2048, "use_disentangled_concat": True,
+                                          "disentangled_dim": 20, "monitor": "train/rec_loss",
+                                          "ddconfig": {"double_z": False, "z_channels": 3, "resolution": 64,
+                                                       "in_channels": 3, "out_ch": 3, "ch": 32,
+                                                       "ch_mult": [1, 2, 4], "num_res_blocks": 2,
+                                                       "attn_resolutions": [], "dropout": 0.0},
+                                          "lossconfig": {"target": "torch.nn.Identity"}}},
+        "cond_stage_config": {"target": "ldm.modules.diffusionmodules.openaimodel_enc.Encoder4",
+                              "params": {"d": 128, "context_dim": 16, "latent_unit": 20}},
+    },
+}
+SHAPES3D_BATCH = 128  # data.params.batch_size
+
+
+def model_config(name: str = "shapes3d") -> dict:
+    if name in ("shapes3d", "mpi3d", "cars3d"):
+        cfg = copy.deepcopy(SHAPES3D)
+        cfg["params"]["eval_name"] = name
+        return cfg
+    raise KeyError(name)
+
+
+def load_config(path: str) -> dict:
+    """OmegaConf-free YAML loader for reference configs (yaml.safe_load)."""
+    import yaml
+    with open(path) as f:
+        return yaml.safe_load(f)

@@ -350,6 +350,23 @@ __global__ void ddim_kernel(const float* x, const float* e, const float* z, int 
   }
 }
 
+__global__ void ddim_indexed_kernel(const float* x, const float* e, const float* z, int n, const float* coef,
+                                    const int* index, float* xp, float* px0) {
+  const int idx = *index;
+  const float a_t = coef[4 * idx], a_prev = coef[4 * idx + 1], sigma = coef[4 * idx + 2], s1 = coef[4 * idx + 3];
+  const float rs = 1.f / sqrtf(a_t);
+  const float sap = sqrtf(a_prev);
+  const float dcoef = sqrtf(1.f - a_prev - sigma * sigma);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float ee = e[i];
+    const float p0 = (x[i] - s1 * ee) * rs;
+    if (px0) px0[i] = p0;
+    xp[i] = sap * p0 + dcoef * ee + (z ? sigma * z[i] : 0.f);
+  }
+}
+
+__global__ void index_dec_kernel(int* index) { *index -= 1; }
+
 // ------------------------------------------------ optimizer
 __global__ __launch_bounds__(256) void adamw_ema_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
@@ -502,6 +519,19 @@ extern "C" int encdiff_ddim_step(const float* x, const float* e, const float* no
   hipLaunchKernelGGL(ddim_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, e, noise, n, a_t, a_prev,
                      sigma, s1, xp, px0);
   ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_ddim_step_indexed(const float* x, const float* e, const float* noise, int n, const float* coef,
+                                         int* index, int advance, float* xp, float* px0, void* stream) {
+  if (!x || !e || !xp || !coef || !index) return ENCDIFF_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(ddim_indexed_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, e, noise, n, coef, index, xp, px0);
+  ED_CHECK_LAUNCH();
+  if (advance) {
+    hipLaunchKernelGGL(index_dec_kernel, dim3(1), dim3(1), 0, s, index);
+    ED_CHECK_LAUNCH();
+  }
   return ENCDIFF_OK;
 }
 

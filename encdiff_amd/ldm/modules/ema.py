@@ -1,0 +1,83 @@
+"""LitEma -- mirror of ldm/modules/ema.py:5-76 (buffer names, decay rule,
+store/restore/copy_to).
+
+When the tracked model lives in a parameter arena, the shadow buffers become views
+of one contiguous fp32 EMA array that the fused HIP AdamW+EMA kernel updates in
+the same pass as the optimizer (encdiff_adamw_ema); ``forward`` then only advances
+``num_updates``/decay bookkeeping unless called stand-alone.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+
+class LitEma(nn.Module):
+    def __init__(self, model, decay=0.9999, use_num_upates=True):
+        super().__init__()
+        if decay < 0.0 or decay > 1.0:
+            raise ValueError("Decay must be between 0 and 1")
+        self.m_name2s_name = {}
+        self.register_buffer("decay", torch.tensor(decay, dtype=torch.float32))
+        self.register_buffer("num_updates", torch.tensor(0, dtype=torch.int) if use_num_upates
+                             else torch.tensor(-1, dtype=torch.int))
+        for name, p in model.named_parameters():
+            if p.requires_grad:
+                s_name = name.replace(".", "")
+                self.m_name2s_name[name] = s_name
+                self.register_buffer(s_name, p.clone().detach().data)
+        self.collected_params = []
+        self._arena = None
+        self._prefix = ""
+
+    # ------------------------------------------------------------ arena binding
+    def bind_arena(self, arena, prefix: str = ""):
+        """Re-home the shadow buffers as views of arena.ema (names keep the reference form)."""
+        ema = arena.enable_ema()
+        with torch.no_grad():
+            for name, s_name in self.m_name2s_name.items():
+                o, shp = arena.offsets[prefix + name]
+                n = 1
+                for s in shp:
+                    n *= s
+                view = ema[o:o + n].view(shp)
+                view.copy_(self._buffers[s_name].to(view.device))
+                self._buffers[s_name] = view
+        self._arena, self._prefix = arena, prefix
+
+    def next_decay(self) -> float:
+        """ema.py:29-33: decay = min(decay, (1 + n) / (10 + n)) after n += 1 (returns 1 - decay)."""
+        decay = float(self.decay)
+        if int(self.num_updates) >= 0:
+            self.num_updates += 1
+            n = int(self.num_updates)
+            decay = min(decay, (1 + n) / (10 + n))
+        return float(1.0 - torch.tensor(decay, dtype=torch.float32))
+
+    def forward(self, model):
+        omd = self.next_decay()
+        with torch.no_grad():
+            if self._arena is not None:
+                a = self._arena
+                a.ema.sub_(omd * (a.ema - a.master[: a.ema_numel]))
+                return
+            m_param = dict(model.named_parameters())
+            shadow = dict(self.named_buffers())
+            for key, p in m_param.items():
+                if p.requires_grad:
+                    s = shadow[self.m_name2s_name[key]]
+                    s.sub_(omd * (s - p))
+
+    def copy_to(self, model):
+        m_param = dict(model.named_parameters())
+        shadow = dict(self.named_buffers())
+        for key, p in m_param.items():
+            if p.requires_grad:
+                p.data.copy_(shadow[self.m_name2s_name[key]].data)
+
+    def store(self, parameters):
+        self.collected_params = [p.clone() for p in parameters]
+
+    def restore(self, parameters):
+        for c, p in zip(self.collected_params, parameters):
+            p.data.copy_(c.data)

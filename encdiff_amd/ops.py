@@ -264,6 +264,11 @@ def ddim_step(x, e, noise, a_t, a_prev, sigma, s1, x_prev, pred_x0=None):
                                 float(s1), _p(x_prev), _p(pred_x0), _s()), "encdiff_ddim_step")
 
 
+def ddim_step_indexed(x, e, noise, coef, index, x_prev, pred_x0=None, advance=True):
+    check(lib.encdiff_ddim_step_indexed(_p(x), _p(e), _p(noise), x.numel(), _p(coef), _p(index), int(advance),
+                                        _p(x_prev), _p(pred_x0), _s()), "encdiff_ddim_step_indexed")
+
+
 def adamw_ema(p, g, m, v, hyper, ema=None, ema_n=0):
     check(lib.encdiff_adamw_ema(_p(p), _p(g), _p(m), _p(v), _p(ema), p.numel(), _p(hyper), ema_n, _s()),
           "encdiff_adamw_ema")

@@ -246,6 +246,13 @@ int encdiff_ddim_step(const float* x, const float* e, const float* noise, int n,
                       float a_prev, float sigma, float sqrt_one_minus_at, float* x_prev, float* pred_x0,
                       void* stream);
 
+/* Same update, coefficients read at execution time from a device table
+ * coef[index][4] = {a_t, a_prev, sigma, sqrt(1 - a_t)} with `index` a device int --
+ * one captured step graph replays the whole DDIM loop (ddim.py:135-162). The kernel
+ * also decrements *index after the update when `advance` != 0. */
+int encdiff_ddim_step_indexed(const float* x, const float* e, const float* noise, int n, const float* coef,
+                              int* index, int advance, float* x_prev, float* pred_x0, void* stream);
+
 /* ---------------------------------------------------------------- optimizer / EMA
  * Fused AdamW (torch defaults; ddpm_enc.py:1615) + optional LitEma update
  * (ema.py:25-44) over one flat fp32 parameter arena, plus the bf16 packing of
