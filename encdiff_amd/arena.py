@@ -25,12 +25,18 @@ from . import _lib as L
 
 
 class ParamArena:
+    """``channels_last``: names of [co][ci][kh][kw] conv weights stored as [co][kh][kw][ci]
+    (the GEMM B layout, so the weight gradient is written coalesced and the bf16 pack is a
+    plain cast); the parameter / grad / EMA views keep the reference shape through a
+    permuted (strided) view."""
+
     def __init__(self, order: Sequence[Tuple[str, torch.nn.Parameter]], device, ema_names: Sequence[str] = (),
-                 align: int = 8):
+                 align: int = 8, channels_last: Sequence[str] = ()):
         self.device = torch.device(device)
         self.names: List[str] = []
         self.offsets: Dict[str, Tuple[int, Tuple[int, ...]]] = {}
         self.params: Dict[str, torch.nn.Parameter] = {}
+        self.cl = set(channels_last)
         off = 0
         ema_set = set(ema_names)
         # EMA-tracked params first so the EMA covers a prefix of the arena
@@ -55,28 +61,45 @@ class ParamArena:
         with torch.no_grad():
             for name in self.names:
                 p = self.params[name]
-                o, shp = self.offsets[name]
-                view = self.master[o:o + p.numel()].view(shp)
+                view = self.view_in(self.master, name)
                 view.copy_(p.detach().to(self.device, torch.float32))
                 p.data = view
-                p.grad = self.grad[o:o + p.numel()].view(shp)
+                p.grad = self.view_in(self.grad, name)
         self.step = 0
         self.hyper = torch.zeros(8, device=self.device, dtype=torch.float32)
 
     # -------------------------------------------------------------- views
-    def f32(self, name: str) -> torch.Tensor:
+    def alias(self, local: str, name: str):
+        """Address `name` also as `local` (e.g. UNet-local names inside a model arena)."""
+        self.offsets[local] = self.offsets[name]
+        if name in self.cl:
+            self.cl.add(local)
+
+    def view_in(self, base: torch.Tensor, name: str) -> torch.Tensor:
+        """Reference-shaped view of `name` inside an arena-shaped buffer (master/grad/ema)."""
         o, shp = self.offsets[name]
         n = 1
         for s in shp:
             n *= s
-        return self.master[o:o + n].view(shp)
+        flat = base[o:o + n]
+        if name in self.cl:
+            co, ci, kh, kw = shp
+            return flat.view(co, kh, kw, ci).permute(0, 3, 1, 2)
+        return flat.view(shp)
+
+    def raw(self, base: torch.Tensor, name: str) -> torch.Tensor:
+        """Storage-order 2-D view [rows][cols] (conv weights: [co][kh*kw*ci])."""
+        o, shp = self.offsets[name]
+        n = 1
+        for s in shp:
+            n *= s
+        return base[o:o + n].view(shp[0], n // shp[0])
+
+    def f32(self, name: str) -> torch.Tensor:
+        return self.view_in(self.master, name)
 
     def grad_of(self, name: str) -> torch.Tensor:
-        o, shp = self.offsets[name]
-        n = 1
-        for s in shp:
-            n *= s
-        return self.grad[o:o + n].view(shp)
+        return self.view_in(self.grad, name)
 
     def span(self, names: Sequence[str]) -> Tuple[int, int]:
         """(offset, numel) of a group of params laid out back-to-back (checked)."""
@@ -99,7 +122,7 @@ class ParamArena:
             g = p.grad
             o, shp = self.offsets[name]
             if g is None or g.data_ptr() != self.grad.data_ptr() + 4 * o:
-                view = self.grad[o:o + p.numel()].view(shp)
+                view = self.view_in(self.grad, name)
                 view.zero_()
                 p.grad = view
 

@@ -81,6 +81,7 @@ class FusedArenaAdamW(torch.optim.Optimizer):
     def stage_hyper(self):
         """Host -> device copy of this step's scalars (outside any captured graph)."""
         self.step_count += 1
+        self._opt_called = True  # tells torch LR schedulers the optimizer stepped (launch() bypasses step())
         vals = self.hyper_values()
         if self._host is not None:
             self._host.copy_(torch.tensor(vals, dtype=torch.float32))
@@ -438,11 +439,13 @@ class LatentDiffusion(DDPM):
         unet = self.model.diffusion_model
         order = self.hip_trainables()
         ema_names = ["model.diffusion_model." + n for n, _ in unet.named_parameters()]
-        arena = ParamArena(order, self.device, ema_names=ema_names)
+        cl = ["model.diffusion_model." + n for n in unet._spec.conv_weights()]
+        arena = ParamArena(order, self.device, ema_names=ema_names, channels_last=cl)
 
         # the UNet executor addresses its parameters by their UNet-local names
-        arena.offsets.update({n[len("model.diffusion_model."):]: v for n, v in list(arena.offsets.items())
-                              if n.startswith("model.diffusion_model.")})
+        for n in list(arena.offsets):
+            if n.startswith("model.diffusion_model."):
+                arena.alias(n[len("model.diffusion_model."):], n)
         unet.bind_arena(arena)
         if self.use_ema:
             self.model_ema.bind_arena(arena, prefix="model.")

@@ -146,7 +146,8 @@ class UNetModel(nn.Module):
         named = dict(self.named_parameters())
         if arena is None:
             dev = next(self.parameters()).device
-            arena = ParamArena(self._spec.arena_order(named), dev, ema_names=list(named))
+            arena = ParamArena(self._spec.arena_order(named), dev, ema_names=list(named),
+                               channels_last=self._spec.conv_weights())
         self._arena = arena
         self._ex = None
         return arena

@@ -36,11 +36,7 @@ class LitEma(nn.Module):
         ema = arena.enable_ema()
         with torch.no_grad():
             for name, s_name in self.m_name2s_name.items():
-                o, shp = arena.offsets[prefix + name]
-                n = 1
-                for s in shp:
-                    n *= s
-                view = ema[o:o + n].view(shp)
+                view = arena.view_in(ema, prefix + name)
                 view.copy_(self._buffers[s_name].to(view.device))
                 self._buffers[s_name] = view
         self._arena, self._prefix = arena, prefix

@@ -125,6 +125,21 @@ def conv3x3_wgrad(dy, x, g: Geom, cin, dw_ref, db=None, resample=L.RESAMPLE_NONE
          split_k=split, bias_grad=db)
 
 
+def conv3x3_wgrad_cl(dy, x, g: Geom, cin, dw_cl, db=None, resample=L.RESAMPLE_NONE):
+    """dw_cl[cout][9*cin] (fp32, channels-last [co][kh][kw][ci]) += dy^T im2col(resample(x)):
+    coalesced fp32 atomics, split-K sized for ~2 waves of workgroups."""
+    cout = dy.shape[1]
+    M, N, K = cout, 9 * cin, g.pixels
+    bm = 64
+    bn = 64
+    tiles = math.ceil(M / bm) * math.ceil(N / bn)
+    split = 1
+    while tiles * split < 320 and K // (split * 2) >= 512:
+        split *= 2
+    gemm(M, N, K, dy, _ld(dy), x, _ld(x), dw_cl, _ld(dw_cl), a_mode=L.OPA_ROWM, b_mode=L.OPB_IM2COL,
+         c_mode=L.OUT_F32_ATOMIC, conv=_conv_geom(g, cin, resample, x), split_k=split, bias_grad=db, tile=4)
+
+
 # ------------------------------------------------------------------ normalisation
 def groupnorm_fwd(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_film=0, groups=32):
     c = x.shape[1]

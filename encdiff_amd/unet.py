@@ -139,6 +139,13 @@ class UNetSpec:
         return s
 
     # ---------------------------------------------------------------- arena order
+    def conv_weights(self):
+        """3x3 conv weights run by the GEMM engine (stored channels-last in the arena)."""
+        out = []
+        for r in self.res:
+            out += [r.prefix + "in_layers.2.weight", r.prefix + "out_layers.3.weight"]
+        return out
+
     def arena_order(self, named: Dict[str, torch.nn.Parameter]):
         """Arena layout: [emb W][emb b][cross K/V W][per-ST qkv W]...rest (named order)."""
         order = []
@@ -208,7 +215,9 @@ class UNetExecutor:
         pk.add("time_embed.2.weight", a.offsets["time_embed.2.weight"][0], 4 * self.mc, 4 * self.mc)
         for r in spec.res:
             for w, cin in (("in_layers.2.weight", r.cin), ("out_layers.3.weight", r.cout)):
-                pk.add(r.prefix + w, a.offsets[r.prefix + w][0], r.cout, 9 * cin, kind=1, cin=cin)
+                # arena stores these [co][kh][kw][ci] (channels_last) -> identity pack
+                kind = 0 if (r.prefix + w) in a.cl else 1
+                pk.add(r.prefix + w, a.offsets[r.prefix + w][0], r.cout, 9 * cin, kind=kind, cin=cin)
             if r.cin != r.cout:
                 pk.add(r.prefix + "skip_connection.weight", a.offsets[r.prefix + "skip_connection.weight"][0],
                        r.cout, r.cin)
@@ -252,6 +261,12 @@ class UNetExecutor:
 
     def G(self, name):
         return self.arena.grad_of(name)
+
+    def conv_wgrad(self, dy, x, g, cin, name, db, resample=0):
+        if name in self.arena.cl:
+            ops.conv3x3_wgrad_cl(dy, x, g, cin, self.arena.raw(self.arena.grad, name), db, resample=resample)
+        else:
+            ops.conv3x3_wgrad(dy, x, g, cin, self.G(name), db, resample=resample)
 
     def _t(self, rows, cols, dtype=BF16):  # noqa: D401
         return torch.empty(rows, cols, device=self.dev, dtype=dtype)
@@ -540,7 +555,7 @@ class UNetExecutor:
         pre = r.prefix
         # conv2
         ops.conv3x3_dgrad(dout, go, self.W(pre + "out_layers.3.weight"), S["d_a2"])
-        ops.conv3x3_wgrad(dout, S["a2"], go, r.cout, self.G(pre + "out_layers.3.weight"), self.G(pre + "out_layers.3.bias"))
+        self.conv_wgrad(dout, S["a2"], go, r.cout, pre + "out_layers.3.weight", self.G(pre + "out_layers.3.bias"))
         # GN2 + FiLM + SiLU
         dg, db = self.gn.parts(pre + "out_layers.0.weight", r.cout)
         ops.groupnorm_bwd(S["h1"], go, self.P(pre + "out_layers.0.weight"), self.P(pre + "out_layers.0.bias"),
@@ -548,8 +563,8 @@ class UNetExecutor:
                           ld_film=self.E.shape[1], dfilm=self.dE[:, r.film_off:], ld_dfilm=self.dE.shape[1],
                           ld_part=self.gn.ld)
         # conv1 (on the resampled GN1 output)
-        ops.conv3x3_wgrad(S["d_h1"], S["a1"], go, r.cin, self.G(pre + "in_layers.2.weight"),
-                          self.G(pre + "in_layers.2.bias"), resample=r.updown)
+        self.conv_wgrad(S["d_h1"], S["a1"], go, r.cin, pre + "in_layers.2.weight", self.G(pre + "in_layers.2.bias"),
+                        resample=r.updown)
         dg, db = self.gn.parts(pre + "in_layers.0.weight", r.cin)
         if r.updown:
             ops.conv3x3_dgrad(S["d_h1"], go, self.W(pre + "in_layers.2.weight"), S["d_a1r"])
