@@ -37,7 +37,7 @@ class GemmArgs(C.Structure):
                 ("conv", ConvGeom), ("conv_cout", C.c_int), ("convw_cin", C.c_int),
                 ("alpha", C.c_float), ("split_k", C.c_int),
                 ("bias", vp), ("resid", vp), ("ld_resid", C.c_long), ("bias_grad", vp),
-                ("tile", C.c_int), ("pad2_", C.c_int)]
+                ("tile", C.c_int), ("pad2_", C.c_int), ("workspace", vp)]
 
 
 class GroupNormArgs(C.Structure):

@@ -323,6 +323,21 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p) {
   }
 }
 
+// split-K finalize: C = alpha * ws (+bias)(+resid); ws re-zeroed for the next user
+__global__ __launch_bounds__(256) void gemm_finalize_kernel(const EncdiffGemmArgs p) {
+  const long total = (long)p.M * p.N;
+  const bf16_t* R = (const bf16_t*)p.resid;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int row = (int)(i / p.N), col = (int)(i - (long)row * p.N);
+    float v = p.alpha * p.workspace[i];
+    p.workspace[i] = 0.f;
+    if (p.bias) v += p.bias[col];
+    if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
+    if (p.c_mode == ENCDIFF_OUT_BF16) ((bf16_t*)p.c)[(long)row * p.ldc + col] = f2bf(v);
+    else ((float*)p.c)[(long)row * p.ldc + col] = v;
+  }
+}
+
 template <int BM, int BN, int AM, int BMD>
 hipError_t launch_t(const EncdiffGemmArgs& p, hipStream_t s) {
   using G = Gemm<BM, BN, AM, BMD>;
@@ -365,7 +380,8 @@ extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
   EncdiffGemmArgs p = *pa;
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return ENCDIFF_ERR_SHAPE;
   if (p.split_k < 1) p.split_k = 1;
-  if (p.split_k > 1 && (p.c_mode == ENCDIFF_OUT_BF16 || p.c_mode == ENCDIFF_OUT_F32)) return ENCDIFF_ERR_ARG;
+  const bool ws_path = p.split_k > 1 && (p.c_mode == ENCDIFF_OUT_BF16 || p.c_mode == ENCDIFF_OUT_F32);
+  if (ws_path && !p.workspace) return ENCDIFF_ERR_ARG;
   const bool k_inner = p.a_mode != ENCDIFF_OPA_ROWM || p.b_mode == ENCDIFF_OPB_ROWK;
   if (k_inner && p.K % 8) return ENCDIFF_ERR_SHAPE;
   if (p.a_mode == ENCDIFF_OPA_ROWM && p.M % 8) return ENCDIFF_ERR_SHAPE;
@@ -376,6 +392,11 @@ extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   const int am = p.a_mode, bm = p.b_mode;
+  const EncdiffGemmArgs user = p;
+  if (ws_path) {  // accumulate partials in the fp32 workspace; epilogue in the finalize pass
+    p.c = p.workspace; p.ldc = p.N; p.c_mode = ENCDIFF_OUT_F32_ATOMIC; p.alpha = 1.f;
+    p.bias = nullptr; p.resid = nullptr;
+  }
   if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_ROWK, B_ROWK>(p, tile, s);
   else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_IM2COL, B_ROWK>(p, tile, s);
   else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWK, B_ROWN>(p, tile, s);
@@ -383,7 +404,16 @@ extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
   else if (am == ENCDIFF_OPA_ROWM && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWM, B_ROWN>(p, tile, s);
   else if (am == ENCDIFF_OPA_ROWM && bm == ENCDIFF_OPB_IM2COL) e = launch_modes<A_ROWM, B_IM2COL>(p, tile, s);
   else return ENCDIFF_ERR_UNSUPPORTED;
-  return e == hipSuccess ? ENCDIFF_OK : ENCDIFF_ERR_LAUNCH - (int)e;
+  if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+  if (ws_path) {
+    long total = (long)user.M * user.N;
+    long g = (total + 255) / 256;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(gemm_finalize_kernel, dim3((unsigned)g), dim3(256), 0, s, user);
+    e = hipGetLastError();
+    if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+  }
+  return ENCDIFF_OK;
 }
 
 extern "C" int encdiff_version(void) { return 1; }

@@ -50,25 +50,76 @@ def _conv_geom(g: Geom, cin: int, resample: int, src: torch.Tensor) -> L.ConvGeo
     return L.ConvGeom(batch=g.batch, h=g.h, w=g.w, cin=cin, resample=resample, ld_src=_ld(src))
 
 
+_WS = {}
+WS_FLOATS = 8 * 1024 * 1024          # fp32 split-K scratch (zero-initialised, self-cleaning)
+_TILES = None
+_TILE_SHAPES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64)}
+
+
+def _workspace():
+    dev = torch.cuda.current_device()
+    ws = _WS.get(dev)
+    if ws is None:
+        ws = _WS[dev] = torch.zeros(WS_FLOATS, device=f"cuda:{dev}", dtype=torch.float32)
+    return ws
+
+
+def _tile_table():
+    global _TILES
+    if _TILES is None:
+        import json
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tiles.json")
+        _TILES = json.load(open(path)) if os.path.exists(path) else {}
+    return _TILES
+
+
+def plan(M, N, K, a_mode, b_mode, c_mode):
+    """(tile, split_k) for a GEMM: measured table (tools/gemm_profile.py --write-table) first,
+    else a heuristic aiming at >= 256 workgroups with bounded split-K traffic."""
+    hit = _tile_table().get(f"{a_mode},{b_mode},{c_mode},{M},{N},{K}")
+    if hit is not None:
+        return int(hit[0]), int(hit[1])
+    atomic = c_mode in (L.OUT_F32_ATOMIC, L.OUT_F32_ATOMIC_CONVW)
+    bm = 64 if M <= 64 else 128
+    bn = 64 if N <= 64 else 128
+
+    def blocks(a, b):
+        return math.ceil(M / a) * math.ceil(N / b)
+    if blocks(bm, bn) < 512 and bm == 128:
+        bm = 64
+    if blocks(bm, bn) < 512 and bn == 128:
+        bn = 64
+    tile = {(128, 128): 1, (128, 64): 2, (64, 128): 3, (64, 64): 4}[(bm, bn)]
+    nb = blocks(bm, bn)
+    split = 1
+    if atomic:
+        while nb * split < 256 and K // (split * 2) >= 256 and (split * 2) * M * N * 4 <= (8 << 20):
+            split *= 2
+    elif M * N <= WS_FLOATS:
+        while nb * split < 192 and K // (split * 2) >= 512:
+            split *= 2
+    return tile, split
+
+
 def gemm(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK, c_mode=L.OUT_BF16,
-         conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=1, bias=None,
+         conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=None, bias=None,
          resid=None, ld_resid=0, bias_grad=None, tile=0):
+    if split_k is None or tile == 0:
+        t, sp = plan(M, N, K, a_mode, b_mode, c_mode)
+        tile = tile or t
+        split_k = split_k or sp
+    ws = None
+    if split_k > 1 and c_mode in (L.OUT_BF16, L.OUT_F32):
+        assert M * N <= WS_FLOATS
+        ws = _workspace()
     args = L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=b_mode, c_mode=c_mode,
                       a=_p(a), lda=lda, b=_p(b), ldb=ldb, c=_p(c), ldc=ldc,
                       conv=conv if conv is not None else L.ConvGeom(),
                       conv_cout=conv_cout, convw_cin=convw_cin, alpha=alpha, split_k=split_k,
-                      bias=_p(bias), resid=_p(resid), ld_resid=ld_resid, bias_grad=_p(bias_grad), tile=tile)
+                      bias=_p(bias), resid=_p(resid), ld_resid=ld_resid, bias_grad=_p(bias_grad), tile=tile,
+                      workspace=_p(ws))
     check(lib.encdiff_gemm(C.byref(args), _s()), "encdiff_gemm")
-
-
-def _split_for(M, N, K, bm=128, bn=128):
-    """split-K factor for reduction-heavy (wgrad) GEMMs: aim for >= 512 workgroups and
-    >= 256 reduction rows per split."""
-    tiles = math.ceil(M / bm) * math.ceil(N / bn)
-    s = 1
-    while tiles * s < 512 and K // (s * 2) >= 256:
-        s *= 2
-    return s
 
 
 # ------------------------------------------------------------------ linear layers
@@ -92,9 +143,8 @@ def linear_wgrad(dy, x, dw, db=None):
     """dw[N][K] += dy[M][N]^T x[M][K];  db[N] += sum_m dy[m][n]  (fp32 atomics)."""
     M, N = dy.shape
     K = x.shape[1]
-    split = _split_for(N, K, M)
     gemm(N, K, M, dy, _ld(dy), x, _ld(x), dw, K, a_mode=L.OPA_ROWM, b_mode=L.OPB_ROWN,
-         c_mode=L.OUT_F32_ATOMIC, split_k=split, bias_grad=db)
+         c_mode=L.OUT_F32_ATOMIC, bias_grad=db)
 
 
 # ------------------------------------------------------------------ 3x3 convolutions
@@ -119,25 +169,16 @@ def conv3x3_wgrad(dy, x, g: Geom, cin, dw_ref, db=None, resample=L.RESAMPLE_NONE
     """dw_ref[cout][cin][3][3] (fp32, reference layout) += sum_pix dy^T im2col(resample(x))."""
     cout = dy.shape[1]
     M, N, K = cout, 9 * cin, g.pixels
-    split = _split_for(M, N, K)
     gemm(M, N, K, dy, _ld(dy), x, _ld(x), dw_ref, 9 * cin, a_mode=L.OPA_ROWM, b_mode=L.OPB_IM2COL,
-         c_mode=L.OUT_F32_ATOMIC_CONVW, conv=_conv_geom(g, cin, resample, x), convw_cin=cin,
-         split_k=split, bias_grad=db)
+         c_mode=L.OUT_F32_ATOMIC_CONVW, conv=_conv_geom(g, cin, resample, x), convw_cin=cin, bias_grad=db)
 
 
 def conv3x3_wgrad_cl(dy, x, g: Geom, cin, dw_cl, db=None, resample=L.RESAMPLE_NONE):
-    """dw_cl[cout][9*cin] (fp32, channels-last [co][kh][kw][ci]) += dy^T im2col(resample(x)):
-    coalesced fp32 atomics, split-K sized for ~2 waves of workgroups."""
+    """dw_cl[cout][9*cin] (fp32, channels-last [co][kh][kw][ci]) += dy^T im2col(resample(x))
+    (coalesced fp32 atomics)."""
     cout = dy.shape[1]
-    M, N, K = cout, 9 * cin, g.pixels
-    bm = 64
-    bn = 64
-    tiles = math.ceil(M / bm) * math.ceil(N / bn)
-    split = 1
-    while tiles * split < 320 and K // (split * 2) >= 512:
-        split *= 2
-    gemm(M, N, K, dy, _ld(dy), x, _ld(x), dw_cl, _ld(dw_cl), a_mode=L.OPA_ROWM, b_mode=L.OPB_IM2COL,
-         c_mode=L.OUT_F32_ATOMIC, conv=_conv_geom(g, cin, resample, x), split_k=split, bias_grad=db, tile=4)
+    gemm(cout, 9 * cin, g.pixels, dy, _ld(dy), x, _ld(x), dw_cl, _ld(dw_cl), a_mode=L.OPA_ROWM,
+         b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32_ATOMIC, conv=_conv_geom(g, cin, resample, x), bias_grad=db)
 
 
 # ------------------------------------------------------------------ normalisation

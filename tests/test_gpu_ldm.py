@@ -52,8 +52,10 @@ def test_p_losses_matches_reference(ldm, golden_dir):
 
 
 def test_training_gradients_match_oracle(ldm):
-    """One p_losses backward through UNet (HIP) and Encoder4 (torch): arena gradients vs
-    the oracle's autograd gradients on identical (x0, img, t, noise)."""
+    """Backward through UNet (HIP) and Encoder4 (torch): arena gradients vs the oracle's
+    autograd gradients on identical (x0, img, t, noise).  Both sides get the SAME upstream
+    seed (the L1 seed sign(eps_hat - eps) is discontinuous, so a bf16/fp32 eps difference
+    would otherwise flip seed entries); the loss value itself is compared separately."""
     from oracle import encdiff_oracle as O
     ldm.train()
     ldm.setup_hip_training()
@@ -64,7 +66,6 @@ def test_training_gradients_match_oracle(ldm):
     ldm._arena.zero_grad()
     c = ldm.get_learned_conditioning(img.cuda())
     loss, _ = ldm.p_losses(x0.cuda(), c, t.cuda(), noise=noise.cuda())
-    loss.backward()
     P = {k: v.requires_grad_(True) for k, v in O.recipe_params(O.param_shapes(O.build_plan())).items()}
     E = O.encoder4_params()
     E = {k: (v.requires_grad_(True) if v.is_floating_point() and "running" not in k else v) for k, v in E.items()}
@@ -72,17 +73,20 @@ def test_training_gradients_match_oracle(ldm):
     cr = O.encoder4_forward(E, img)
     out = O.unet_forward(P, O.build_plan(), O.q_sample(sched, x0, t, noise), t, [cr])
     lref, _ = O.p_losses_from_output(sched, out, noise, t)
-    lref.backward()
     assert abs(float(loss.detach()) - float(lref.detach())) / float(lref) < 1e-2
+    # shared upstream gradient for the model outputs
+    seed = torch.sign(out.detach() - noise) / out.numel()
+    ldm._arena.zero_grad()
+    c = ldm.get_learned_conditioning(img.cuda())
+    eps = ldm.apply_model(ldm.q_sample(x0.cuda(), t.cuda(), noise.cuda()), t.cuda(), c)
+    eps.backward(seed.cuda())
+    out.backward(seed)
     unet = dict(ldm.model.diffusion_model.named_parameters())
-    worst = 0.0
     for n in ["time_embed.0.weight", "input_blocks.1.0.in_layers.2.weight", "middle_block.1.proj_in.weight",
               "output_blocks.8.2.out_layers.3.weight", "out.2.weight", "output_blocks.3.1.norm.bias"]:
         r = rel(unet[n].grad, P[n].grad)
-        worst = max(worst, r)
         print(n, r)
-        # the time-MLP weights sit at the end of all 28 FiLM gradient paths (bf16 activations): 8e-2
-        assert r < (8e-2 if n.startswith("time_embed") else 5e-2), n
+        assert r < 5e-2, n
     cond = dict(ldm.cond_stage_model.named_parameters())
     for n in ["encoder.0.weight", "encoder.16.weight", "net.3.4.weight"]:
         r = rel(cond[n].grad, E[n].grad)

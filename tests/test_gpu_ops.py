@@ -66,6 +66,20 @@ def test_linear(O, M, N, K):
     assert rel(db, dy.float().sum(0)) < 2e-3
 
 
+@pytest.mark.parametrize("split", [2, 8])
+def test_split_k_workspace(O, split):
+    """bf16-output GEMM with split-K: fp32 workspace partials + finalize (bias, resid)."""
+    torch.manual_seed(11)
+    M, N, K = 512, 256, 4608
+    x, w = bf(M, K), bf(N, K, scale=K ** -0.5)
+    b = torch.randn(N, device=dev)
+    r = bf(M, N)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    for _ in range(2):  # second call checks the workspace was left zeroed
+        O.gemm(M, N, K, x, K, w, K, out, N, bias=b, resid=r, ld_resid=N, split_k=split, tile=4)
+        assert rel(out, x.float() @ w.float().t() + b + r.float()) < 1e-2
+
+
 def test_linear_strided_views(O):
     """q/k/v slices of a fused [M][3C] projection output are strided views."""
     torch.manual_seed(1)
@@ -116,6 +130,12 @@ def test_conv3x3(O, B, H, cin, cout, mode):
     O.conv3x3_wgrad(dy, x, g, cin, dw, db, resample=mode)
     assert rel(dw, wq.grad) < 5e-3
     assert rel(db, nhwc(dy, g).sum((0, 2, 3))) < 2e-3
+    # channels-last weight gradient ([co][kh][kw][ci], the arena layout)
+    dwc = torch.zeros(cout, 9 * cin, device=dev)
+    db2 = torch.zeros(cout, device=dev)
+    O.conv3x3_wgrad_cl(dy, x, g, cin, dwc, db2, resample=mode)
+    assert rel(dwc.view(cout, 3, 3, cin).permute(0, 3, 1, 2), wq.grad) < 5e-3
+    assert rel(db2, db) < 1e-5
 
 
 @pytest.mark.parametrize("C,H,film,silu,eps", [(64, 16, True, True, 1e-5), (192, 16, False, True, 1e-5),

@@ -1,0 +1,159 @@
+"""Record every GEMM of one EncDiff training step and time each under every tile shape.
+
+    python tools/gemm_profile.py [--batch 128] [--write-table]
+
+Prints per-category totals (current heuristic vs best tile) and, with --write-table,
+stores the best tile per GEMM signature in encdiff_amd/gemm_tiles.json (read by
+ops.gemm at run time).  Also prints a phase breakdown of the eager step (HIP events).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+from collections import defaultdict
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--write-table", action="store_true")
+    args = ap.parse_args()
+    import encdiff_amd  # noqa: F401
+    from encdiff_amd import _lib as L
+    from encdiff_amd import ops
+    from encdiff_amd.configs import model_config
+    from encdiff_amd.ldm.util import instantiate_from_config
+    from encdiff_amd.trainer import HipTrainer
+
+    torch.manual_seed(0)
+    ldm = instantiate_from_config(model_config("shapes3d")).cuda()
+    tr = HipTrainer(ldm, args.batch, graph=False)
+    tr.init_scale_factor()
+    tr.step_eager()
+    torch.cuda.synchronize()
+
+    # ---- phase breakdown (eager) --------------------------------------------------
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    e = [ev() for _ in range(8)]
+    img = tr.img
+    e[0].record()
+    with torch.no_grad():
+        z = ldm.get_first_stage_encoding(ldm.encode_first_stage(img))
+    e[1].record()
+    c = ldm.get_learned_conditioning(img)
+    e[2].record()
+    t = torch.randint(0, 1000, (args.batch,), device="cuda")
+    noise = torch.randn_like(z)
+    xn = ldm.q_sample(z, t, noise)
+    unet = ldm.model.diffusion_model
+    ex = unet.executor()
+    eps = ex.forward(xn, t, c.detach())
+    e[3].record()
+    d_c = ex.backward(torch.sign(eps - noise) / eps.numel())
+    e[4].record()
+    c.backward(d_c)
+    e[5].record()
+    tr.opt.stage_hyper()
+    tr.opt.launch()
+    e[6].record()
+    torch.cuda.synchronize()
+    names = ["vq_encode", "encoder4_fwd", "unet_fwd(+q_sample)", "unet_bwd", "encoder4_bwd", "adamw+ema+pack"]
+    for i, n in enumerate(names):
+        print(f"phase {n:22s} {e[i].elapsed_time(e[i + 1]):8.3f} ms")
+
+    # ---- record GEMMs ---------------------------------------------------------------
+    calls = []
+    orig = L.lib.encdiff_gemm
+
+    class Rec:
+        def __call__(self, argp, stream):
+            a = L.GemmArgs()
+            C.memmove(C.byref(a), argp, C.sizeof(L.GemmArgs))
+            calls.append(a)
+            return orig(argp, stream)
+    L.lib.encdiff_gemm = Rec()
+    try:
+        eps = ex.forward(xn, t, c.detach())
+        ex.backward(torch.sign(eps - noise) / eps.numel())
+        torch.cuda.synchronize()
+    finally:
+        L.lib.encdiff_gemm = orig
+    print(f"{len(calls)} GEMM launches per UNet fwd+bwd")
+
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    ws = ops._workspace()
+
+    def timeit(a, tile, split=None):
+        a2 = L.GemmArgs()
+        C.memmove(C.byref(a2), C.byref(a), C.sizeof(L.GemmArgs))
+        a2.tile = tile
+        if split is not None:
+            a2.split_k = split
+            a2.workspace = ws.data_ptr() if split > 1 else None
+            if split > 1 and a2.c_mode in (L.OUT_BF16, L.OUT_F32) and a2.M * a2.N > ops.WS_FLOATS:
+                return float("inf")
+        for _ in range(2):
+            rc = orig(C.byref(a2), stream)
+            if rc != 0:
+                return float("inf")
+        s, f = ev(), ev()
+        s.record()
+        for _ in range(args.reps):
+            orig(C.byref(a2), stream)
+        f.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(f) / args.reps * 1e3
+
+    def cat(a):
+        modes = (a.a_mode, a.b_mode)
+        return {(1, 0): "conv_fwd", (1, 2): "conv_dgrad", (2, 3): "conv_wgrad", (0, 0): "lin_fwd",
+                (0, 1): "lin_dgrad", (2, 1): "lin_wgrad"}.get(modes, str(modes))
+
+    tot_cur, tot_best = defaultdict(float), defaultdict(float)
+    flops = defaultdict(float)
+    table = {}
+    rows = []
+    for a in calls:
+        cur = timeit(a, a.tile)
+        best_t, best_tile, best_split = cur, a.tile, a.split_k
+        for tile in (1, 2, 3, 4):
+            for split in (1, 2, 4, 8, 16, 32, 64):
+                if a.K // split < 128 or (split > 1 and a.K // split < 64):
+                    continue
+                tt = timeit(a, tile, split)
+                if tt < best_t:
+                    best_t, best_tile, best_split = tt, tile, split
+        k = cat(a)
+        tot_cur[k] += cur
+        tot_best[k] += best_t
+        flops[k] += 2.0 * a.M * a.N * a.K
+        key = f"{a.a_mode},{a.b_mode},{a.c_mode},{a.M},{a.N},{a.K}"
+        if key not in table or table[key][2] > best_t:
+            table[key] = [best_tile, best_split, best_t]
+        rows.append((k, a.M, a.N, a.K, a.split_k, a.tile, cur, f"{best_tile}/{best_split}", best_t))
+    for r in sorted(rows, key=lambda r: -r[6])[:30]:
+        k, M, N, K, s, tile, cur, bt, bb = r
+        print(f"{k:10s} M={M:6d} N={N:5d} K={K:6d} split={s:3d} tile={tile} {cur:8.1f}us -> {bt} {bb:8.1f}us "
+              f"({2 * M * N * K / bb / 1e6:7.1f} TF/s)")
+    print("category     current_us   best_us   TFLOP/s(best)")
+    for k in tot_cur:
+        print(f"{k:12s} {tot_cur[k]:9.1f} {tot_best[k]:9.1f} {flops[k] / tot_best[k] / 1e6:8.1f}")
+    print(f"TOTAL        {sum(tot_cur.values()):9.1f} {sum(tot_best.values()):9.1f}")
+    if args.write_table:
+        path = os.path.join(REPO, "encdiff_amd", "gemm_tiles.json")
+        json.dump(table, open(path, "w"), indent=0, sort_keys=True)
+        print("wrote", path)
+
+
+if __name__ == "__main__":
+    main()
