@@ -291,46 +291,105 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p) {
   }
 
   // ---- epilogue -------------------------------------------------------------
+  // Stage the fp32 tile through LDS (the staging buffers are free after the last barrier),
+  // then write whole 16-byte row segments (bf16/fp32 outputs) or lane-contiguous fp32 atomics.
   const bool add_bias = p.bias != nullptr && blockIdx.z == 0;
   const bf16_t* R = (const bf16_t*)p.resid;
+  if (p.c_mode == ENCDIFF_OUT_F32_ATOMIC_CONVW) {  // reference-layout scatter (rare path)
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wc + 16 * j + l16;
-      if (col >= p.N) continue;
-      const float bv = add_bias ? p.bias[col] : 0.f;
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wc + 16 * j + l16;
+        if (col >= p.N) continue;
+        const float bv = add_bias ? p.bias[col] : 0.f;
+        const int tap = col / p.convw_cin;
+        const int ci = col - tap * p.convw_cin;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = m0 + wr + 16 * i + 4 * g4 + q;
-        if (row >= p.M) continue;
-        float v = p.alpha * acc[i][j][q] + bv;
-        if (p.c_mode == ENCDIFF_OUT_BF16) {
-          if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
-          ((bf16_t*)p.c)[(long)row * p.ldc + col] = f2bf(v);
-        } else if (p.c_mode == ENCDIFF_OUT_F32) {
-          if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
-          ((float*)p.c)[(long)row * p.ldc + col] = v;
-        } else if (p.c_mode == ENCDIFF_OUT_F32_ATOMIC) {
-          atomicAdd((float*)p.c + (long)row * p.ldc + col, v);
-        } else {  // ATOMIC_CONVW: row = co, col = tap*cin + ci -> [co][ci][tap]
-          const int tap = col / p.convw_cin;
-          const int ci = col - tap * p.convw_cin;
-          atomicAdd((float*)p.c + (long)row * p.ldc + ci * 9 + tap, v);
+        for (int q = 0; q < 4; ++q) {
+          const int row = m0 + wr + 16 * i + 4 * g4 + q;
+          if (row < p.M) atomicAdd((float*)p.c + (long)row * p.ldc + ci * 9 + tap, p.alpha * acc[i][j][q] + bv);
         }
       }
+    return;
+  }
+  float* p_c_slab = (float*)p.c;
+  constexpr int SLD = BN + 4;
+  static_assert(BM * SLD * 4 <= 2 * G::STAGE * 2, "epilogue staging must fit the LDS allocation");
+  float* sc = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sc[(wr + 16 * i + 4 * g4 + q) * SLD + wc + 16 * j + l16] = acc[i][j][q];
+  __syncthreads();
+  if (p.c_mode == ENCDIFF_OUT_F32_ATOMIC) {
+    // lanes along columns: one wave instruction = 64 consecutive floats of one row
+    for (int e = tid; e < BM * BN; e += 256) {
+      const int r = e / BN, cc = e - r * BN;
+      const int row = m0 + r, col = n0 + cc;
+      if (row < p.M && col < p.N)
+        atomicAdd((float*)p.c + (long)row * p.ldc + col, p.alpha * sc[r * SLD + cc] + (add_bias ? p.bias[col] : 0.f));
+    }
+    return;
+  }
+  if (p.split_k > 1 && p.c_mode == ENCDIFF_OUT_F32)  // split-K slab of this z (workspace path)
+    p_c_slab = (float*)p.c + (long)blockIdx.z * p.M * p.N;
+  const bool vec = (p.N % 8 == 0) && (p.ldc % 8 == 0) && (((uintptr_t)p.c & 15) == 0) &&
+                   (!add_bias || (((uintptr_t)p.bias & 15) == 0)) &&
+                   (!R || ((p.ld_resid % 8 == 0) && (((uintptr_t)R & 15) == 0)));
+  if (vec) {
+    constexpr int CPR = BN / 8;  // 8-column chunks per row
+    for (int e = tid; e < BM * CPR; e += 256) {
+      const int r = e / CPR, c8 = (e - r * CPR) * 8;
+      const int row = m0 + r, col = n0 + c8;
+      if (row >= p.M || col >= p.N) continue;
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = p.alpha * sc[r * SLD + c8 + k];
+      if (add_bias) {
+        const float4 b0 = *(const float4*)(p.bias + col), b1 = *(const float4*)(p.bias + col + 4);
+        v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+        v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+      }
+      if (R) {
+        float rr[8];
+        unpack8(*(const uint4*)(R + (long)row * p.ld_resid + col), rr);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] += rr[k];
+      }
+      if (p.c_mode == ENCDIFF_OUT_BF16) {
+        *(uint4*)((bf16_t*)p.c + (long)row * p.ldc + col) = pack8(v);
+      } else {
+        float* cp = p_c_slab + (long)row * p.ldc + col;
+        *(float4*)cp = make_float4(v[0], v[1], v[2], v[3]);
+        *(float4*)(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    }
+  } else {
+    for (int e = tid; e < BM * BN; e += 256) {
+      const int r = e / BN, cc = e - r * BN;
+      const int row = m0 + r, col = n0 + cc;
+      if (row >= p.M || col >= p.N) continue;
+      float v = p.alpha * sc[r * SLD + cc] + (add_bias ? p.bias[col] : 0.f);
+      if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
+      if (p.c_mode == ENCDIFF_OUT_BF16) ((bf16_t*)p.c)[(long)row * p.ldc + col] = f2bf(v);
+      else p_c_slab[(long)row * p.ldc + col] = v;
     }
   }
 }
 
-// split-K finalize: C = alpha * ws (+bias)(+resid); ws re-zeroed for the next user
+// split-K finalize: C = alpha * sum_z slab[z] (+bias)(+resid), slabs summed in a fixed
+// order (bitwise reproducible; no atomics).
 __global__ __launch_bounds__(256) void gemm_finalize_kernel(const EncdiffGemmArgs p) {
   const long total = (long)p.M * p.N;
   const bf16_t* R = (const bf16_t*)p.resid;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const int row = (int)(i / p.N), col = (int)(i - (long)row * p.N);
-    float v = p.alpha * p.workspace[i];
-    p.workspace[i] = 0.f;
+    float acc = 0.f;
+    for (int z = 0; z < p.split_k; ++z) acc += p.workspace[(long)z * total + i];
+    float v = p.alpha * acc;
     if (p.bias) v += p.bias[col];
     if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
     if (p.c_mode == ENCDIFF_OUT_BF16) ((bf16_t*)p.c)[(long)row * p.ldc + col] = f2bf(v);
@@ -393,8 +452,8 @@ extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
   hipError_t e;
   const int am = p.a_mode, bm = p.b_mode;
   const EncdiffGemmArgs user = p;
-  if (ws_path) {  // accumulate partials in the fp32 workspace; epilogue in the finalize pass
-    p.c = p.workspace; p.ldc = p.N; p.c_mode = ENCDIFF_OUT_F32_ATOMIC; p.alpha = 1.f;
+  if (ws_path) {  // per-split fp32 slabs (plain stores); epilogue in the finalize pass
+    p.c = p.workspace; p.ldc = p.N; p.c_mode = ENCDIFF_OUT_F32; p.alpha = 1.f;
     p.bias = nullptr; p.resid = nullptr;
   }
   if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_ROWK, B_ROWK>(p, tile, s);

@@ -20,10 +20,31 @@ struct GnLayout {
   ED_DEV GnLayout(int c) {
     nv = c >> 3;
     np = GN_THREADS / nv;
+    while (np & (np - 1)) np &= np - 1;  // power-of-two pixel lanes (tree reduction)
     tv = threadIdx.x % nv;
     tp = threadIdx.x / nv;
   }
 };
+
+// Tree-reduce NR arrays red[k][np][C] over the np rows into row 0 (log2(np) steps).
+// Every thread of the block must call it.
+ED_DEV void tree_reduce_rows(float* red, int NR, const GnLayout& L, int C) {
+  for (int stride = L.np >> 1; stride > 0; stride >>= 1) {
+    __syncthreads();
+    if (L.tp < stride) {
+      for (int k = 0; k < NR; ++k) {
+        float4* a = (float4*)(red + (k * L.np + L.tp) * C + L.tv * 8);
+        const float4* b = (const float4*)(red + (k * L.np + L.tp + stride) * C + L.tv * 8);
+        float4 a0 = a[0], a1 = a[1];
+        const float4 b0 = b[0], b1 = b[1];
+        a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
+        a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
+        a[0] = a0; a[1] = a1;
+      }
+    }
+  }
+  __syncthreads();
+}
 
 __global__ __launch_bounds__(GN_THREADS) void gn_fwd_kernel(const EncdiffGroupNormArgs p) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
@@ -54,11 +75,10 @@ __global__ __launch_bounds__(GN_THREADS) void gn_fwd_kernel(const EncdiffGroupNo
       red[(L.np + L.tp) * C + L.tv * 8 + i] = ss[i];
     }
   }
-  __syncthreads();
+  tree_reduce_rows(red, 2, L, C);
   for (int c = threadIdx.x; c < C; c += GN_THREADS) {
-    float a = 0.f, q = 0.f;
-    for (int r = 0; r < L.np; ++r) { a += red[r * C + c]; q += red[(L.np + r) * C + c]; }
-    ch_s[c] = a; ch_ss[c] = q;
+    ch_s[c] = red[c];
+    ch_ss[c] = red[L.np * C + c];
   }
   __syncthreads();
   if (threadIdx.x < p.groups) {
@@ -163,13 +183,9 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
       }
     }
   }
-  __syncthreads();
+  tree_reduce_rows(red, NR, L, C);
   for (int c = threadIdx.x; c < C; c += GN_THREADS) {
-    for (int k = 0; k < NR; ++k) {
-      float a = 0.f;
-      for (int r = 0; r < L.np; ++r) a += red[(k * L.np + r) * C + c];
-      chs[k * C + c] = a;
-    }
+    for (int k = 0; k < NR; ++k) chs[k * C + c] = red[(k * L.np) * C + c];
     p.dbeta_part[(long)b * p.ld_part + c] = chs[c];
     p.dgamma_part[(long)b * p.ld_part + c] = chs[C + c];
     if (film) {

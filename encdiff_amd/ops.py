@@ -79,7 +79,9 @@ def plan(M, N, K, a_mode, b_mode, c_mode):
     else a heuristic aiming at >= 256 workgroups with bounded split-K traffic."""
     hit = _tile_table().get(f"{a_mode},{b_mode},{c_mode},{M},{N},{K}")
     if hit is not None:
-        return int(hit[0]), int(hit[1])
+        tile, split = int(hit[0]), int(hit[1])
+        if split == 1 or c_mode in (L.OUT_F32_ATOMIC, L.OUT_F32_ATOMIC_CONVW) or split * M * N <= WS_FLOATS:
+            return tile, split
     atomic = c_mode in (L.OUT_F32_ATOMIC, L.OUT_F32_ATOMIC_CONVW)
     bm = 64 if M <= 64 else 128
     bn = 64 if N <= 64 else 128
@@ -96,8 +98,8 @@ def plan(M, N, K, a_mode, b_mode, c_mode):
     if atomic:
         while nb * split < 256 and K // (split * 2) >= 256 and (split * 2) * M * N * 4 <= (8 << 20):
             split *= 2
-    elif M * N <= WS_FLOATS:
-        while nb * split < 192 and K // (split * 2) >= 512:
+    else:
+        while nb * split < 192 and K // (split * 2) >= 512 and (split * 2) * M * N <= WS_FLOATS:
             split *= 2
     return tile, split
 
@@ -111,7 +113,7 @@ def gemm(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROW
         split_k = split_k or sp
     ws = None
     if split_k > 1 and c_mode in (L.OUT_BF16, L.OUT_F32):
-        assert M * N <= WS_FLOATS
+        assert split_k * M * N <= WS_FLOATS, "split-K slabs exceed the workspace"
         ws = _workspace()
     args = L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=b_mode, c_mode=c_mode,
                       a=_p(a), lda=lda, b=_p(b), ldb=ldb, c=_p(c), ldc=ldc,

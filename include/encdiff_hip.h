@@ -90,9 +90,9 @@ typedef struct EncdiffGemmArgs {
   float* bias_grad;          /* OPA_ROWM only: += sum_k A[m][k] into bias_grad[m]  */
   int tile;                  /* 0 = auto, else 1:128x128 2:128x64 3:64x128 4:64x64 */
   int pad2_;
-  float* workspace;          /* split_k > 1 with a BF16/F32 c_mode: zero-initialised fp32 [M][N]
-                                scratch; the partials are accumulated there and a finalize pass
-                                applies alpha/bias/resid, writes C and re-zeroes the scratch   */
+  float* workspace;          /* split_k > 1 with a BF16/F32 c_mode: fp32 scratch of split_k*M*N;
+                                each split writes its own [M][N] slab, a finalize pass sums the
+                                slabs in order (reproducible) and applies alpha/bias/resid    */
 } EncdiffGemmArgs;
 
 int encdiff_gemm(const EncdiffGemmArgs* args, void* stream);

@@ -25,7 +25,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--write-table", action="store_true")
+    ap.add_argument("--write-table", default="", help="path for the measured (tile, split) table, e.g. "
+                    "gpurun_out/gemm_tiles.json (copy it to encdiff_amd/gemm_tiles.json)")
     args = ap.parse_args()
     import encdiff_amd  # noqa: F401
     from encdiff_amd import _lib as L
@@ -100,7 +101,7 @@ def main():
         if split is not None:
             a2.split_k = split
             a2.workspace = ws.data_ptr() if split > 1 else None
-            if split > 1 and a2.c_mode in (L.OUT_BF16, L.OUT_F32) and a2.M * a2.N > ops.WS_FLOATS:
+            if split > 1 and a2.c_mode in (L.OUT_BF16, L.OUT_F32) and split * a2.M * a2.N > ops.WS_FLOATS:
                 return float("inf")
         for _ in range(2):
             rc = orig(C.byref(a2), stream)
@@ -150,9 +151,9 @@ def main():
         print(f"{k:12s} {tot_cur[k]:9.1f} {tot_best[k]:9.1f} {flops[k] / tot_best[k] / 1e6:8.1f}")
     print(f"TOTAL        {sum(tot_cur.values()):9.1f} {sum(tot_best.values()):9.1f}")
     if args.write_table:
-        path = os.path.join(REPO, "encdiff_amd", "gemm_tiles.json")
-        json.dump(table, open(path, "w"), indent=0, sort_keys=True)
-        print("wrote", path)
+        os.makedirs(os.path.dirname(os.path.abspath(args.write_table)), exist_ok=True)
+        json.dump(table, open(args.write_table, "w"), indent=0, sort_keys=True)
+        print("wrote", args.write_table)
 
 
 if __name__ == "__main__":
