@@ -10,6 +10,8 @@
 // Sizes on the path: self S in {256, 64, 16, 4} with dh {8, 16, 32, 32}, cross Sk = 20.
 #include "common.h"
 
+int encdiff_attention_mfma(const EncdiffAttnArgs* a, bool bwd, void* stream);
+
 namespace {
 
 ED_DEV void load_row(const bf16_t* __restrict__ src, int dh, float* dst) {
@@ -204,6 +206,10 @@ int attn_launch(const EncdiffAttnArgs& a, bool bwd, hipStream_t s) {
 int attn_dispatch(const EncdiffAttnArgs* a, bool bwd, void* stream) {
   if (!a || !a->q || !a->k || !a->v || !a->o) return ENCDIFF_ERR_ARG;
   if (bwd && (!a->d_o || !a->dq || !a->dk || !a->dv || !a->lse)) return ENCDIFF_ERR_ARG;
+  // MFMA path (attn_mfma.hip) for every shape whose tiles fit LDS; the VALU kernels
+  // below remain for head groups too large for one workgroup's LDS.
+  const int rc = encdiff_attention_mfma(a, bwd, stream);
+  if (rc != ENCDIFF_ERR_SHAPE) return rc;
   if (a->sq > 256) return ENCDIFF_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   switch (a->dh) {
