@@ -146,7 +146,11 @@ def main():
     tr.capture(warmup=3)
     for _ in range(args.warmup):
         tr.step()
+    # marker kernels (torch's spin_kernel) bracket the timed region so a kernel trace can
+    # be cut to it (tools/trace_window.py); they run outside the timed region
+    torch.cuda._sleep(1000)
     dt = time_steps(tr, args.steps)
+    torch.cuda._sleep(1000)
     if world > 1:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

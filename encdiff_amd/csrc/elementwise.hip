@@ -233,62 +233,49 @@ __global__ __launch_bounds__(256) void small_conv_out_dgrad(const EncdiffSmallCo
 }
 
 // weight/bias gradient of either small conv.  One block per group of images; each
-// thread owns output weights o = tid + 256 k over (co, ci, tap); sums over pixels.
+// grid (ceil(NW/256), ceil(batch/ipb)): a thread owns ONE output weight o = (co, ci, tap)
+// and sums over the pixels of the block's images; partial sums are atomically added.
 // in-conv: x fp32 NCHW, dy bf16 NHWC [pix][co];  out-conv: x bf16 NHWC, dy fp32 NCHW.
 __global__ __launch_bounds__(256) void small_conv_wgrad(const EncdiffSmallConvArgs p, int imgs_per_block) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int CO = p.cout, CI = p.cin, HW = p.h * p.w;
+  const int CO = p.cout, CI = p.cin, H = p.h, W = p.w, HW = H * W;
   float* xs = sm;              // [CI][HW]
   float* ds = sm + CI * HW;    // [CO][HW]
   const int NW = CO * CI * 9;
-  float acc[8];
-  float bacc = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-  const int b0 = blockIdx.x * imgs_per_block;
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  const bool live = o < NW;
+  const int co = live ? o / (CI * 9) : 0, rem = o - co * CI * 9, ci = rem / 9, t = rem - ci * 9;
+  const int oy = t / 3 - 1, ox = t % 3 - 1;
+  const int y0 = max(0, -oy), y1 = min(H, H - oy), x0 = max(0, -ox), x1 = min(W, W - ox);
+  const bool do_bias = blockIdx.x == 0 && threadIdx.x < CO && p.dbias;
+  float acc = 0.f, bacc = 0.f;
+  const int b0 = blockIdx.y * imgs_per_block;
   for (int b = b0; b < min(p.batch, b0 + imgs_per_block); ++b) {
     __syncthreads();
     for (int i = threadIdx.x; i < CI * HW; i += 256) {
-      const int ci = i / HW, px = i - ci * HW;
+      const int c = i / HW, px = i - c * HW;
       xs[i] = p.x_f32 ? ((const float*)p.x)[(long)b * CI * HW + i]
-                      : bf2f(((const bf16_t*)p.x)[((long)b * HW + px) * p.ldx + ci]);
+                      : bf2f(((const bf16_t*)p.x)[((long)b * HW + px) * p.ldx + c]);
     }
     for (int i = threadIdx.x; i < CO * HW; i += 256) {
-      const int co = i / HW, px = i - co * HW;
+      const int c = i / HW, px = i - c * HW;
       ds[i] = p.dy_f32 ? ((const float*)p.dy)[(long)b * CO * HW + i]
-                       : bf2f(((const bf16_t*)p.dy)[((long)b * HW + px) * p.lddy + co]);
+                       : bf2f(((const bf16_t*)p.dy)[((long)b * HW + px) * p.lddy + c]);
     }
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int o = threadIdx.x + 256 * k;
-      if (o >= NW) break;
-      const int co = o / (CI * 9), rem = o - co * CI * 9, ci = rem / 9, t = rem - ci * 9;
-      const int dy_ = t / 3 - 1, dx_ = t % 3 - 1;
-      float a = 0.f;
-      for (int y = 0; y < p.h; ++y) {
-        const int yy = y + dy_;
-        if (yy < 0 || yy >= p.h) continue;
-        for (int x = 0; x < p.w; ++x) {
-          const int xx = x + dx_;
-          if (xx < 0 || xx >= p.w) continue;
-          a += ds[co * HW + y * p.w + x] * xs[ci * HW + yy * p.w + xx];
-        }
-      }
-      acc[k] += a;
+    if (live) {
+      const float* dr = ds + co * HW;
+      const float* xr = xs + ci * HW + oy * W + ox;
+      for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) acc += dr[y * W + x] * xr[y * W + x];
     }
-    if (threadIdx.x < CO) {
-      float a = 0.f;
-      for (int px = 0; px < HW; ++px) a += ds[threadIdx.x * HW + px];
-      bacc += a;
+    if (do_bias) {
+      const float* dr = ds + threadIdx.x * HW;
+      for (int px = 0; px < HW; ++px) bacc += dr[px];
     }
   }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int o = threadIdx.x + 256 * k;
-    if (o < NW) atomicAdd(p.dweight + o, acc[k]);
-  }
-  if (threadIdx.x < CO && p.dbias) atomicAdd(p.dbias + threadIdx.x, bacc);
+  if (live) atomicAdd(p.dweight + o, acc);
+  if (do_bias) atomicAdd(p.dbias + threadIdx.x, bacc);
 }
 
 // ------------------------------------------------ diffusion math
@@ -476,8 +463,9 @@ extern "C" int encdiff_small_conv_bwd(const EncdiffSmallConvArgs* a, void* strea
     static const hipError_t attr = hipFuncSetAttribute((const void*)small_conv_wgrad,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)attr;
-    const int ipb = 4;
-    hipLaunchKernelGGL(small_conv_wgrad, dim3((a->batch + ipb - 1) / ipb), dim3(256), lds, s, *a, ipb);
+    const int ipb = 2, nw = a->cout * a->cin * 9;
+    hipLaunchKernelGGL(small_conv_wgrad, dim3((nw + 255) / 256, (a->batch + ipb - 1) / ipb), dim3(256), lds, s, *a,
+                       ipb);
     ED_CHECK_LAUNCH();
   }
   return ENCDIFF_OK;
