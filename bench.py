@@ -51,9 +51,15 @@ def setup_dist(args):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        # one process per GPU over RCCL ("nccl").  ENCDIFF_DIST_BACKEND=gloo rehearses the
+        # DP path with several ranks sharing the GPUs of a smaller box (ranks wrap around).
+        local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("ENCDIFF_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         return dist.get_rank(), ws
     torch.cuda.set_device(0)
     return 0, 1

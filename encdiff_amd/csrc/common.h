@@ -39,9 +39,11 @@ ED_DEV uint4 pack8(const float* f) {
   return u;
 }
 
-ED_DEV float silu_f(float z) { return z / (1.0f + __expf(-z)); }
+// sigmoid via the hardware reciprocal (v_rcp_f32, 1 ulp): results are rounded to bf16
+ED_DEV float sigmoid_f(float z) { return __builtin_amdgcn_rcpf(1.0f + __expf(-z)); }
+ED_DEV float silu_f(float z) { return z * sigmoid_f(z); }
 ED_DEV float silu_grad(float z) {
-  float s = 1.0f / (1.0f + __expf(-z));
+  const float s = sigmoid_f(z);
   return s * (1.0f + z * (1.0f - s));
 }
 

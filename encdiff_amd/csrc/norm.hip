@@ -1,10 +1,8 @@
 // norm.hip -- GroupNorm(+FiLM)(+SiLU) and LayerNorm, forward and backward, NHWC bf16.
 //
-// GroupNorm: one workgroup per image (512 threads).  Threads are laid out as
-// (C/8 channel vectors) x (pixel lanes); each thread streams 16-byte vectors of its
-// 8 channels over its pixels, sums are combined through LDS into per-channel and
-// per-group statistics (fp32, as GroupNorm32 does: util.py:242-244), then a second
-// pass (L2-resident re-read) writes the normalised, FiLM-modulated, SiLU-activated
+// GroupNorm: one workgroup per (image, slice of whole groups); the slice is held in
+// registers between the statistics (fp32, two-pass, as GroupNorm32 computes in fp32:
+// util.py:242-244) and the write of the normalised, FiLM-modulated, SiLU-activated
 // output (openaimodel_enc.py:201-205, 225-232, 267-271, 684-686; attention.py:76-77).
 // The backward recomputes the forward from x and the saved statistics and emits
 // per-image partial sums for dgamma/dbeta (reduced once per step by
@@ -13,224 +11,285 @@
 
 namespace {
 
-constexpr int GN_THREADS = 512;
+constexpr int GN_THREADS = 256;
+constexpr int GN_TILE = 1024;  // 16-byte vectors of a slice kept in LDS (16 KB per operand)
 
-struct GnLayout {
-  int nv, np, tv, tp;
-  ED_DEV GnLayout(int c) {
-    nv = c >> 3;
-    np = GN_THREADS / nv;
-    while (np & (np - 1)) np &= np - 1;  // power-of-two pixel lanes (tree reduction)
-    tv = threadIdx.x % nv;
-    tp = threadIdx.x / nv;
+// A workgroup owns (image b, channel slice [c0, c0 + cs)); cs is a multiple of 8 and of
+// channels-per-group, so every group lies inside one slice and the slices are independent.
+// Threads: tv = channel vector (8 channels) of the slice, tp = pixel lane.  The slice is
+// read from HBM once into an LDS tile (slices larger than GN_TILE vectors re-read HBM/L2),
+// per-channel partials are reduced deterministically (wave shuffles + ordered LDS sums),
+// statistics are two-pass (mean, then centred sum of squares).  Loops stay rolled (4-way
+// unrolled) so the kernels are a few hundred instructions: a cold instruction cache is
+// otherwise the dominant latency of these small launches.
+struct GnSlice {
+  int S, b, c0, cs, nvc, np, tv, tp, cpg, gs, g0, cb;
+  bool active, tiled;
+  ED_DEV GnSlice(const EncdiffGroupNormArgs& p, int cs_) {
+    cs = cs_;
+    S = p.c / cs;
+    b = blockIdx.x / S;
+    c0 = (blockIdx.x - b * S) * cs;
+    nvc = cs >> 3;
+    np = GN_THREADS / nvc;
+    tv = threadIdx.x % nvc;
+    tp = threadIdx.x / nvc;
+    active = tp < np;
+    cpg = p.c / p.groups;
+    gs = cs / cpg;
+    g0 = c0 / cpg;
+    cb = c0 + tv * 8;
+    tiled = nvc * p.hw <= GN_TILE;
   }
 };
 
-// Tree-reduce NR arrays red[k][np][C] over the np rows into row 0 (log2(np) steps).
-// Every thread of the block must call it.
-ED_DEV void tree_reduce_rows(float* red, int NR, const GnLayout& L, int C) {
-  for (int stride = L.np >> 1; stride > 0; stride >>= 1) {
-    __syncthreads();
-    if (L.tp < stride) {
-      for (int k = 0; k < NR; ++k) {
-        float4* a = (float4*)(red + (k * L.np + L.tp) * C + L.tv * 8);
-        const float4* b = (const float4*)(red + (k * L.np + L.tp + stride) * C + L.tv * 8);
-        float4 a0 = a[0], a1 = a[1];
-        const float4 b0 = b[0], b1 = b[1];
-        a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
-        a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
-        a[0] = a0; a[1] = a1;
-      }
+ED_DEV void load8f(const float* p, float* v) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// Deterministic reduction of per-thread channel partials q[NQ][8] over the pixel lanes of
+// the slice into out[NQ][cs] (LDS).  Power-of-two nvc: xor-shuffles inside each wave, then
+// the wave rows are added in order; otherwise every pixel-lane row goes through LDS and a
+// thread per channel adds the rows in order.  Ends with a barrier.
+template <int NQ>
+ED_DEV void slice_reduce(float (&q)[NQ][8], const GnSlice& L, float* red, float* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool pow2 = (L.nvc & (L.nvc - 1)) == 0;
+  int rows;
+  if (pow2) {
+    for (int off = L.nvc; off < 64; off <<= 1) {
+#pragma unroll
+      for (int k = 0; k < NQ; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) q[k][i] += __shfl_xor(q[k][i], off, 64);
     }
+    if (lane < L.nvc) {
+#pragma unroll
+      for (int k = 0; k < NQ; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) red[(wave * NQ + k) * L.cs + L.tv * 8 + i] = q[k][i];
+    }
+    rows = L.nvc >= 64 ? GN_THREADS / L.nvc : GN_THREADS / 64;
+  } else {
+    if (L.active) {
+#pragma unroll
+      for (int k = 0; k < NQ; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) red[(L.tp * NQ + k) * L.cs + L.tv * 8 + i] = q[k][i];
+    }
+    rows = L.np;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < NQ * L.cs; e += GN_THREADS) {
+    const int k = e / L.cs, c = e - k * L.cs;
+    float a = 0.f;
+    for (int r = 0; r < rows; ++r) a += red[(r * NQ + k) * L.cs + c];
+    out[k * L.cs + c] = a;
   }
   __syncthreads();
 }
 
-__global__ __launch_bounds__(GN_THREADS) void gn_fwd_kernel(const EncdiffGroupNormArgs p) {
-  extern __shared__ __attribute__((aligned(16))) float sh[];
-  const int b = blockIdx.x;
-  const int C = p.c, HW = p.hw, cpg = C / p.groups;
-  GnLayout L(C);
-  float* red = sh;                      // [np][C] x2
-  float* ch_s = sh + 2 * L.np * C;      // [C]
-  float* ch_ss = ch_s + C;              // [C]
-  float* g_mean = ch_ss + C;            // [groups]
-  float* g_rstd = g_mean + p.groups;    // [groups]
+// Row px of the thread's channel vector: from the LDS tile when the slice fits, else HBM/L2.
+ED_DEV uint4 gn_row(const GnSlice& L, const uint4* tile, const bf16_t* g, long ld, int px) {
+  return L.tiled ? tile[px * L.nvc + L.tv] : *(const uint4*)(g + (long)px * ld);
+}
 
-  const bf16_t* X = (const bf16_t*)p.x + (long)b * HW * p.ldx;
-  const bool active = L.tp < L.np;
-  float s[8], ss[8];
+// phase 0: stream the slice from HBM (4 loads in flight per thread), fill the tile, sum.
+ED_DEV void gn_stream_in(const GnSlice& L, uint4* tile, const bf16_t* X, long ld, int HW, float* s) {
+#pragma unroll 4
+  for (int px = L.tp; px < HW; px += L.np) {
+    const uint4 u = *(const uint4*)(X + (long)px * ld);
+    if (L.tiled) tile[px * L.nvc + L.tv] = u;
+    float v[8];
+    unpack8(u, v);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { s[i] = 0.f; ss[i] = 0.f; }
-  if (active) {
+    for (int i = 0; i < 8; ++i) s[i] += v[i];
+  }
+}
+
+__global__ __launch_bounds__(GN_THREADS) void gn_fwd_kernel(const EncdiffGroupNormArgs p, int cs) {
+  __shared__ uint4 tile[GN_TILE];
+  __shared__ float red[2048], chs[512], gsh[2 * 64];
+  const GnSlice L(p, cs);
+  const int HW = p.hw;
+  const float inv_n = 1.f / ((float)HW * L.cpg);
+  const bf16_t* X = (const bf16_t*)p.x + (long)L.b * HW * p.ldx + L.cb;
+  float s[1][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[0][i] = 0.f;
+  if (L.active) gn_stream_in(L, tile, X, p.ldx, HW, s[0]);
+  // per-channel affine / FiLM constants (independent of the statistics)
+  float ga[8], be[8], sc[8], sf[8];
+  load8f(p.gamma + L.cb, ga);
+  load8f(p.beta + L.cb, be);
+  if (p.film) {
+    load8f(p.film + (long)L.b * p.ld_film + L.cb, sc);
+    load8f(p.film + (long)L.b * p.ld_film + p.c + L.cb, sf);
+  }
+  slice_reduce<1>(s, L, red, chs);
+  if (threadIdx.x < L.gs) {
+    float a = 0.f;
+    for (int c = threadIdx.x * L.cpg; c < (threadIdx.x + 1) * L.cpg; ++c) a += chs[c];
+    gsh[threadIdx.x] = a * inv_n;
+  }
+  __syncthreads();
+  float mean[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { mean[i] = gsh[(L.tv * 8 + i) / L.cpg]; s[0][i] = 0.f; }
+  if (L.active) {
+#pragma unroll 2
     for (int px = L.tp; px < HW; px += L.np) {
       float v[8];
-      unpack8(*(const uint4*)(X + (long)px * p.ldx + L.tv * 8), v);
+      unpack8(gn_row(L, tile, X, p.ldx, px), v);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) { s[i] += v[i]; ss[i] += v[i] * v[i]; }
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      red[L.tp * C + L.tv * 8 + i] = s[i];
-      red[(L.np + L.tp) * C + L.tv * 8 + i] = ss[i];
+      for (int i = 0; i < 8; ++i) { const float d = v[i] - mean[i]; s[0][i] += d * d; }
     }
   }
-  tree_reduce_rows(red, 2, L, C);
-  for (int c = threadIdx.x; c < C; c += GN_THREADS) {
-    ch_s[c] = red[c];
-    ch_ss[c] = red[L.np * C + c];
+  slice_reduce<1>(s, L, red, chs);
+  if (threadIdx.x < L.gs) {
+    float q = 0.f;
+    for (int c = threadIdx.x * L.cpg; c < (threadIdx.x + 1) * L.cpg; ++c) q += chs[c];
+    const float rstd = rsqrtf(q * inv_n + p.eps);
+    gsh[64 + threadIdx.x] = rstd;
+    const long gi = (long)L.b * p.groups + L.g0 + threadIdx.x;
+    p.stats[2 * gi] = gsh[threadIdx.x];
+    p.stats[2 * gi + 1] = rstd;
   }
   __syncthreads();
-  if (threadIdx.x < p.groups) {
-    const int g = threadIdx.x;
-    float a = 0.f, q = 0.f;
-    for (int c = g * cpg; c < (g + 1) * cpg; ++c) { a += ch_s[c]; q += ch_ss[c]; }
-    const float n = (float)HW * cpg;
-    const float mean = a / n;
-    const float var = fmaxf(q / n - mean * mean, 0.f);
-    const float rstd = rsqrtf(var + p.eps);
-    g_mean[g] = mean; g_rstd[g] = rstd;
-    p.stats[(b * p.groups + g) * 2] = mean;
-    p.stats[(b * p.groups + g) * 2 + 1] = rstd;
-  }
-  __syncthreads();
-  if (!active) return;
-  // per-thread channel constants
+  if (!L.active) return;
   float mul[8], add[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int c = L.tv * 8 + i;
-    const int g = c / cpg;
-    float ga = p.gamma[c], be = p.beta[c];
-    float m = g_mean[g], r = g_rstd[g];
+    const float r = gsh[64 + (L.tv * 8 + i) / L.cpg];
     // y = ((x - m) r ga + be)(1 + sc) + sh
-    float a = r * ga, bb = be - m * r * ga;
+    float a = r * ga[i], bb = be[i] - mean[i] * a;
     if (p.film) {
-      const float sc = p.film[(long)b * p.ld_film + c];
-      const float sf = p.film[(long)b * p.ld_film + C + c];
-      a *= (1.f + sc);
-      bb = bb * (1.f + sc) + sf;
+      a *= (1.f + sc[i]);
+      bb = bb * (1.f + sc[i]) + sf[i];
     }
     mul[i] = a; add[i] = bb;
   }
-  bf16_t* Y = (bf16_t*)p.y + (long)b * HW * p.ldy;
+  bf16_t* Y = (bf16_t*)p.y + (long)L.b * HW * p.ldy + L.cb;
+  const bool silu = p.silu;
+#pragma unroll 2
   for (int px = L.tp; px < HW; px += L.np) {
     float v[8];
-    unpack8(*(const uint4*)(X + (long)px * p.ldx + L.tv * 8), v);
+    unpack8(gn_row(L, tile, X, p.ldx, px), v);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      float z = v[i] * mul[i] + add[i];
-      v[i] = p.silu ? silu_f(z) : z;
+      const float z = v[i] * mul[i] + add[i];
+      v[i] = silu ? silu_f(z) : z;
     }
-    *(uint4*)(Y + (long)px * p.ldy + L.tv * 8) = pack8(v);
+    *(uint4*)(Y + (long)px * p.ldy) = pack8(v);
   }
 }
 
-__global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNormArgs p) {
-  extern __shared__ __attribute__((aligned(16))) float sh[];
-  const int b = blockIdx.x;
-  const int C = p.c, HW = p.hw, cpg = C / p.groups;
-  GnLayout L(C);
-  const bool film = p.film != nullptr;
-  const int NR = film ? 4 : 2;           // reductions per channel
-  float* red = sh;                       // [NR][np][C]
-  float* chs = sh + NR * L.np * C;       // [NR][C]
-  float* gs = chs + NR * C;              // [groups][2]
-  const float* st = p.stats + b * p.groups * 2;
-
-  const bf16_t* X = (const bf16_t*)p.x + (long)b * HW * p.ldx;
-  const bf16_t* DY = (const bf16_t*)p.dy + (long)b * HW * p.lddy;
-  const bool active = L.tp < L.np;
-
+__global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNormArgs p, int cs) {
+  __shared__ uint4 tx[GN_TILE], td[GN_TILE];
+  __shared__ float red[4 * 2048], chs[4 * 512], gsh[2 * 64];
+  const GnSlice L(p, cs);
+  const int HW = p.hw;
+  const bool film = p.film != nullptr, silu = p.silu;
+  const float inv_n = 1.f / ((float)HW * L.cpg);
+  const long off = (long)L.b * HW;
+  const bf16_t* X = (const bf16_t*)p.x + off * p.ldx + L.cb;
+  const bf16_t* DY = (const bf16_t*)p.dy + off * p.lddy + L.cb;
+  // per-channel constants
   float xm[8], xr[8], ga[8], be[8], sc1[8], sf[8];
+  load8f(p.gamma + L.cb, ga);
+  load8f(p.beta + L.cb, be);
+  if (film) {
+    load8f(p.film + (long)L.b * p.ld_film + L.cb, sc1);
+    load8f(p.film + (long)L.b * p.ld_film + p.c + L.cb, sf);
+  }
+  const float* st = p.stats + ((long)L.b * p.groups) * 2;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int c = L.tv * 8 + i;
-    const int g = c / cpg;
+    const int g = (L.cb + i) / L.cpg;
     xm[i] = st[2 * g]; xr[i] = st[2 * g + 1];
-    ga[i] = p.gamma[c]; be[i] = p.beta[c];
-    sc1[i] = film ? 1.f + p.film[(long)b * p.ld_film + c] : 1.f;
-    sf[i] = film ? p.film[(long)b * p.ld_film + C + c] : 0.f;
+    sc1[i] = film ? 1.f + sc1[i] : 1.f;
+    sf[i] = film ? sf[i] : 0.f;
   }
-  // pass 1: per-channel sums of dn, dn*xhat (and dz, dz*n for FiLM)
-  float a_dn[8], a_dnx[8], a_dz[8], a_dzn[8];
+  // pass 1: per-channel sums of dn, dn*xhat, dz, dz*n
+  float acc[4][8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { a_dn[i] = a_dnx[i] = a_dz[i] = a_dzn[i] = 0.f; }
-  if (active) {
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[k][i] = 0.f;
+  if (L.active) {
+#pragma unroll 2
     for (int px = L.tp; px < HW; px += L.np) {
+      const uint4 ux = *(const uint4*)(X + (long)px * p.ldx);
+      const uint4 ud = *(const uint4*)(DY + (long)px * p.lddy);
+      if (L.tiled) { tx[px * L.nvc + L.tv] = ux; td[px * L.nvc + L.tv] = ud; }
       float v[8], d[8];
-      unpack8(*(const uint4*)(X + (long)px * p.ldx + L.tv * 8), v);
-      unpack8(*(const uint4*)(DY + (long)px * p.lddy + L.tv * 8), d);
+      unpack8(ux, v);
+      unpack8(ud, d);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float xh = (v[i] - xm[i]) * xr[i];
         const float n = xh * ga[i] + be[i];
         const float z = n * sc1[i] + sf[i];
-        const float dz = p.silu ? d[i] * silu_grad(z) : d[i];
+        const float dz = silu ? d[i] * silu_grad(z) : d[i];
         const float dn = dz * sc1[i];
-        a_dn[i] += dn; a_dnx[i] += dn * xh;
-        a_dz[i] += dz; a_dzn[i] += dz * n;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = L.tv * 8 + i;
-      red[(0 * L.np + L.tp) * C + c] = a_dn[i];
-      red[(1 * L.np + L.tp) * C + c] = a_dnx[i];
-      if (film) {
-        red[(2 * L.np + L.tp) * C + c] = a_dz[i];
-        red[(3 * L.np + L.tp) * C + c] = a_dzn[i];
+        acc[0][i] += dn; acc[1][i] += dn * xh;
+        acc[2][i] += dz; acc[3][i] += dz * n;
       }
     }
   }
-  tree_reduce_rows(red, NR, L, C);
-  for (int c = threadIdx.x; c < C; c += GN_THREADS) {
-    for (int k = 0; k < NR; ++k) chs[k * C + c] = red[(k * L.np) * C + c];
-    p.dbeta_part[(long)b * p.ld_part + c] = chs[c];
-    p.dgamma_part[(long)b * p.ld_part + c] = chs[C + c];
+  slice_reduce<4>(acc, L, red, chs);
+  // per-channel outputs + gamma-weighted sums for the group terms
+  float* gch = red;  // [2][cs] (red is free after the reduction)
+  for (int cl = threadIdx.x; cl < L.cs; cl += GN_THREADS) {
+    const int c = L.c0 + cl;
+    const float gam = p.gamma[c];
+    p.dbeta_part[(long)L.b * p.ld_part + c] = chs[cl];
+    p.dgamma_part[(long)L.b * p.ld_part + c] = chs[L.cs + cl];
     if (film) {
-      p.dfilm[(long)b * p.ld_dfilm + c] = chs[3 * C + c];       // d scale = sum dz * n
-      p.dfilm[(long)b * p.ld_dfilm + C + c] = chs[2 * C + c];   // d shift = sum dz
+      p.dfilm[(long)L.b * p.ld_dfilm + c] = chs[3 * L.cs + cl];         // d scale = sum dz * n
+      p.dfilm[(long)L.b * p.ld_dfilm + p.c + c] = chs[2 * L.cs + cl];   // d shift = sum dz
     }
+    gch[cl] = gam * chs[cl];
+    gch[L.cs + cl] = gam * chs[L.cs + cl];
   }
   __syncthreads();
-  if (threadIdx.x < p.groups) {
-    const int g = threadIdx.x;
+  if (threadIdx.x < L.gs) {
     float s1 = 0.f, s2 = 0.f;
-    for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
-      s1 += p.gamma[c] * chs[c];
-      s2 += p.gamma[c] * chs[C + c];
+    for (int cl = threadIdx.x * L.cpg; cl < (threadIdx.x + 1) * L.cpg; ++cl) {
+      s1 += gch[cl];
+      s2 += gch[L.cs + cl];
     }
-    const float inv_n = 1.f / ((float)HW * cpg);
-    gs[2 * g] = s1 * inv_n;
-    gs[2 * g + 1] = s2 * inv_n;
+    gsh[threadIdx.x] = s1 * inv_n;
+    gsh[64 + threadIdx.x] = s2 * inv_n;
   }
   __syncthreads();
-  if (!active) return;
+  if (!L.active) return;
   float m1[8], m2[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int g = (L.tv * 8 + i) / cpg;
-    m1[i] = gs[2 * g]; m2[i] = gs[2 * g + 1];
+    const int g = (L.tv * 8 + i) / L.cpg;
+    m1[i] = gsh[g]; m2[i] = gsh[64 + g];
   }
-  bf16_t* DX = (bf16_t*)p.dx + (long)b * HW * p.lddx;
+  bf16_t* DX = (bf16_t*)p.dx + off * p.lddx + L.cb;
+  const bool accum = p.accumulate_dx;
+#pragma unroll 1
   for (int px = L.tp; px < HW; px += L.np) {
-    float v[8], d[8];
-    unpack8(*(const uint4*)(X + (long)px * p.ldx + L.tv * 8), v);
-    unpack8(*(const uint4*)(DY + (long)px * p.lddy + L.tv * 8), d);
-    float o[8];
-    if (p.accumulate_dx) unpack8(*(const uint4*)(DX + (long)px * p.lddx + L.tv * 8), o);
+    float v[8], d[8], o[8];
+    unpack8(gn_row(L, tx, X, p.ldx, px), v);
+    unpack8(gn_row(L, td, DY, p.lddy, px), d);
+    if (accum) unpack8(*(const uint4*)(DX + (long)px * p.lddx), o);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float xh = (v[i] - xm[i]) * xr[i];
       const float n = xh * ga[i] + be[i];
       const float z = n * sc1[i] + sf[i];
-      const float dz = p.silu ? d[i] * silu_grad(z) : d[i];
+      const float dz = silu ? d[i] * silu_grad(z) : d[i];
       const float dn = dz * sc1[i];
       const float r = xr[i] * (dn * ga[i] - m1[i] - xh * m2[i]);
-      o[i] = p.accumulate_dx ? o[i] + r : r;
+      o[i] = accum ? o[i] + r : r;
     }
-    *(uint4*)(DX + (long)px * p.lddx + L.tv * 8) = pack8(o);
+    *(uint4*)(DX + (long)px * p.lddx) = pack8(o);
   }
 }
 
@@ -315,27 +374,30 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const EncdiffLayerNormArgs 
   }
 }
 
-size_t gn_fwd_lds(int C, int groups) {
-  const int np = GN_THREADS / (C / 8);
-  return (2 * np * C + 2 * C + 2 * groups) * sizeof(float);
+// channel-slice width: the narrowest multiple of lcm(8, channels-per-group) dividing C whose
+// slice holds >= 4096 elements (so small images still fill a workgroup), else all of C.
+int gn_slice(int C, int HW, int cpg) {
+  int unit = 8;
+  while (unit % cpg) unit += 8;
+  for (int w = unit; w < C; w += unit)
+    if (C % w == 0 && (long)w * HW >= 4096) return w;
+  return C;
 }
-size_t gn_bwd_lds(int C, int groups, bool film) {
-  const int np = GN_THREADS / (C / 8);
-  const int NR = film ? 4 : 2;
-  return (NR * np * C + NR * C + 2 * groups) * sizeof(float);
+
+int gn_check(const EncdiffGroupNormArgs* a) {
+  if (a->c % 8 || a->groups <= 0 || a->c % a->groups) return ENCDIFF_ERR_SHAPE;
+  const int cs = gn_slice(a->c, a->hw, a->c / a->groups);
+  if (cs > 512 || cs / (a->c / a->groups) > 64) return ENCDIFF_ERR_UNSUPPORTED;
+  return cs;
 }
 
 }  // namespace
 
 extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream) {
   if (!a || !a->x || !a->y || !a->stats || !a->gamma || !a->beta) return ENCDIFF_ERR_ARG;
-  if (a->c % 8 || a->c % a->groups || a->c > 8 * GN_THREADS || a->groups > GN_THREADS) return ENCDIFF_ERR_SHAPE;
-  const size_t lds = gn_fwd_lds(a->c, a->groups);
-  static const hipError_t attr = hipFuncSetAttribute((const void*)gn_fwd_kernel,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)attr;
-  if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
-  hipLaunchKernelGGL(gn_fwd_kernel, dim3(a->batch), dim3(GN_THREADS), lds, (hipStream_t)stream, *a);
+  const int cs = gn_check(a);
+  if (cs < 0) return cs;
+  hipLaunchKernelGGL(gn_fwd_kernel, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream, *a, cs);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
@@ -343,13 +405,9 @@ extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream
 extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream) {
   if (!a || !a->x || !a->dy || !a->dx || !a->stats || !a->dgamma_part || !a->dbeta_part) return ENCDIFF_ERR_ARG;
   if (a->film && !a->dfilm) return ENCDIFF_ERR_ARG;
-  if (a->c % 8 || a->c % a->groups || a->c > 8 * GN_THREADS || a->groups > GN_THREADS) return ENCDIFF_ERR_SHAPE;
-  const size_t lds = gn_bwd_lds(a->c, a->groups, a->film != nullptr);
-  static const hipError_t attr = hipFuncSetAttribute((const void*)gn_bwd_kernel,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)attr;
-  if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
-  hipLaunchKernelGGL(gn_bwd_kernel, dim3(a->batch), dim3(GN_THREADS), lds, (hipStream_t)stream, *a);
+  const int cs = gn_check(a);
+  if (cs < 0) return cs;
+  hipLaunchKernelGGL(gn_bwd_kernel, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream, *a, cs);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }

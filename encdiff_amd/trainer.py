@@ -7,12 +7,13 @@ Step = (per rank)
   eps_hat = UNet(x_t, t, c)          (HIP executor, forward)
   L1 loss + gradient seed            (HIP)
   backward: UNet (HIP) -> d c -> Encoder4 (torch autograd)
-  [world > 1: RCCL all-reduce (mean) of the flat gradient arena]
+  [world > 1: RCCL all-reduce (mean) of the gradient arena in two buckets (dp.py):
+   the UNet bucket on a side stream while Encoder4's backward runs, then Encoder4's]
   AdamW + EMA over the flat arena, bf16 repack of GEMM weights   (HIP)
 
 The device work of a step is replayed from captured graphs: one graph for the
-single-GPU step, or (forward+backward) and (optimizer) graphs around the
-all-reduce when data-parallel.  Only the per-step scalars (lr, bias corrections,
+single-GPU step; with DP three graphs sharing one memory pool -- (forward + UNet
+backward), (Encoder4 backward), (optimizer) -- around the bucket all-reduces.  Only the per-step scalars (lr, bias corrections,
 EMA decay) cross the host->device boundary, through a pinned 8-float buffer.
 Reference: ddpm_enc.py:360-375, 399-401, 1040-1053, 1183-1253, 1598-1639;
 main_val.py:818-842 (lr = ngpu * batch * base_lr).
@@ -25,6 +26,8 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from .dp import GradBuckets, rank_seed, scaled_lr, world_info
+
 
 class HipTrainer:
     def __init__(self, ldm, batch_size: int, base_lr: Optional[float] = None, graph: bool = True,
@@ -33,20 +36,21 @@ class HipTrainer:
         self.ldm = ldm
         self.dev = ldm.device
         self.B = batch_size
-        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
-        self.rank = dist.get_rank() if self.world > 1 else 0
+        self.rank, self.world = world_info()
         ldm.train()
         arena = ldm.setup_hip_training()
         self.arena = arena
         base = base_lr if base_lr is not None else 2.0e-6
-        ldm.learning_rate = self.world * batch_size * base  # main_val.py:834-838 (scale_lr)
+        ldm.learning_rate = scaled_lr(base, batch_size, self.world)  # main_val.py:834-838 (scale_lr)
         opt = ldm.configure_optimizers()
         if isinstance(opt, tuple) or isinstance(opt, list):
             self.opt = opt[0][0]
             self.sched = opt[1][0]["scheduler"]
         else:
             self.opt, self.sched = opt, None
-        g = torch.Generator(device=self.dev).manual_seed(seed + self.rank)
+        self.buckets = GradBuckets.from_arena(arena)
+        self._comm = torch.cuda.Stream() if self.world > 1 else None
+        g = torch.Generator(device=self.dev).manual_seed(rank_seed(seed, self.rank))
         if data_pool is None:  # synthetic Shapes3D-shaped images in [-1, 1], resident in HBM
             data_pool = torch.rand(pool_size, 3, 64, 64, device=self.dev, generator=g) * 2 - 1
         self.pool = data_pool
@@ -54,8 +58,10 @@ class HipTrainer:
         self.loss_buf = torch.zeros(4, device=self.dev)
         self.graph = graph
         self._g_fb = None
+        self._g_cond = None
         self._g_opt = None
-        torch.manual_seed(seed + self.rank)
+        self._c = self._dc = None
+        torch.manual_seed(rank_seed(seed, self.rank))
 
     # ---------------------------------------------------------------- device work
     def _draw_batch(self):
@@ -63,6 +69,10 @@ class HipTrainer:
         torch.index_select(self.pool, 0, idx, out=self.img)
 
     def _fwd_bwd(self):
+        """Everything up to the UNet backward.  At world size 1 Encoder4's backward runs
+        inside it (plain loss.backward()); with DP the autograd graph is cut at the concept
+        tokens so the UNet gradient bucket can be all-reduced while Encoder4's backward runs
+        (`_cond_bwd`)."""
         ldm = self.ldm
         self.arena.grad.zero_()
         self._draw_batch()
@@ -71,14 +81,32 @@ class HipTrainer:
         c = ldm.get_learned_conditioning(self.img)
         t = torch.randint(0, ldm.num_timesteps, (self.B,), device=self.dev)
         noise = torch.randn_like(z)
-        loss, ld = ldm.p_losses(z, c, t, noise)
-        loss.backward()
+        if self.world == 1:
+            loss, ld = ldm.p_losses(z, c, t, noise)
+            loss.backward()
+        else:
+            c_det = c.detach().requires_grad_(True)
+            loss, ld = ldm.p_losses(z, c_det, t, noise)
+            loss.backward()
+            self._c, self._dc = c, c_det.grad
         self.loss_buf[0].copy_(ld["train/loss_simple"])
         self.loss_buf[1].copy_(ld["train/loss_vlb"])
 
-    def _allreduce(self):
-        if self.world > 1:
-            dist.all_reduce(self.arena.grad, op=dist.ReduceOp.AVG)
+    def _cond_bwd(self):
+        self._c.backward(self._dc)
+
+    def _exchange(self, cond_bwd):
+        """DP gradient mean: bucket 0 (UNet) on the side stream overlapped with the cond
+        stage backward, then bucket 1 (cond stage); the current stream waits for both."""
+        cur = torch.cuda.current_stream()
+        self._comm.wait_stream(cur)
+        with torch.cuda.stream(self._comm):
+            w0 = self.buckets.start(0)
+        cond_bwd()
+        w1 = self.buckets.start(1) if len(self.buckets) > 1 else None
+        self.buckets.finish(0, w0)
+        if len(self.buckets) > 1:
+            self.buckets.finish(1, w1)
 
     # ---------------------------------------------------------------- setup
     def init_scale_factor(self):
@@ -106,8 +134,12 @@ class HipTrainer:
                 if self.world == 1:
                     self.opt.launch()
             if self.world > 1:
+                pool = self._g_fb.pool()
+                self._g_cond = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self._g_cond, stream=s, pool=pool):
+                    self._cond_bwd()
                 self._g_opt = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self._g_opt, stream=s):
+                with torch.cuda.graph(self._g_opt, stream=s, pool=pool):
                     self.opt.launch()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
@@ -116,7 +148,8 @@ class HipTrainer:
     def step_eager(self):
         self.opt.stage_hyper()
         self._fwd_bwd()
-        self._allreduce()
+        if self.world > 1:
+            self._exchange(self._cond_bwd)
         self.opt.launch()
         self._post()
 
@@ -126,7 +159,7 @@ class HipTrainer:
         self.opt.stage_hyper()
         self._g_fb.replay()
         if self.world > 1:
-            self._allreduce()
+            self._exchange(self._g_cond.replay)
             self._g_opt.replay()
         self._post()
 

@@ -140,7 +140,8 @@ def test_conv3x3(O, B, H, cin, cout, mode):
 
 @pytest.mark.parametrize("C,H,film,silu,eps", [(64, 16, True, True, 1e-5), (192, 16, False, True, 1e-5),
                                                 (384, 8, True, True, 1e-5), (256, 4, False, False, 1e-6),
-                                                (512, 2, True, True, 1e-5)])
+                                                (512, 2, True, True, 1e-5), (64, 64, True, True, 1e-5),
+                                                (128, 8, False, True, 1e-5)])
 def test_groupnorm(O, C, H, film, silu, eps):
     from encdiff_amd.ops import Geom
     torch.manual_seed(3)
