@@ -74,33 +74,88 @@ def build_ldm():
     return instantiate_from_config(cfg).cuda(), cfg
 
 
-def kernel_roofline(B):
-    """Live HIP-event timing of the dominant kernel: the conv3x3 implicit-GEMM forward
-    at the 16x16 level (M = B*256 pixels, N = 64, K = 9*64)."""
-    from encdiff_amd import ops
-    from encdiff_amd.ops import Geom
-    g = Geom(B, 16, 16)
-    cin = cout = 64
-    x = (torch.randn(g.pixels, cin, device="cuda") * 0.5).to(torch.bfloat16)
-    w = (torch.randn(cout, 9 * cin, device="cuda") * 0.04).to(torch.bfloat16)
-    y = torch.empty(g.pixels, cout, device="cuda", dtype=torch.bfloat16)
-    bias = torch.zeros(cout, device="cuda")
-    for _ in range(20):
-        ops.conv3x3_fwd(x, g, cin, w, y, bias=bias)
-    n = 200
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+def record_gemms(tr):
+    """Arguments of every encdiff_gemm launch of one eager training step (the UNet's conv
+    and linear forward / dgrad / wgrad GEMMs), in launch order."""
+    import ctypes as C
+    from encdiff_amd import _lib as L
+    calls = []
+    orig = L.lib.encdiff_gemm
+
+    class Rec:
+        def __call__(self, argp, stream):
+            a = L.GemmArgs()
+            C.memmove(C.byref(a), argp, C.sizeof(L.GemmArgs))
+            calls.append(a)
+            return orig(argp, stream)
+    L.lib.encdiff_gemm = Rec()
+    try:
+        tr.step_eager()
+    finally:
+        L.lib.encdiff_gemm = orig
     torch.cuda.synchronize()
-    e0.record()
-    for _ in range(n):
-        ops.conv3x3_fwd(x, g, cin, w, y, bias=bias)
-    e1.record()
-    torch.cuda.synchronize()
-    avg_s = e0.elapsed_time(e1) / 1e3 / n
-    flops = 2.0 * g.pixels * cout * 9 * cin
-    return {"kernel": "gemm_kernel<IM2COL,ROWK> conv3x3 fwd 16x16x64->64", "bound": "mfma",
-            "achieved": flops / avg_s / 1e12, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": flops / avg_s / 1e12 / PEAK_BF16_TFLOPS, "traffic": None,
-            "avg_us": avg_s * 1e6, "flops_per_launch": flops}
+    return calls
+
+
+def gemm_alg_bytes(a):
+    """Algorithmic HBM bytes of one GEMM launch: each operand tensor read once (an im2col
+    operand is its source image, not the 9x-expanded matrix), the output written once."""
+    def src():
+        pix = a.conv.batch * a.conv.h * a.conv.w
+        pix = pix * 4 if a.conv.resample == 1 else (pix // 4 if a.conv.resample == 2 else pix)
+        return 2.0 * pix * a.conv.cin
+    abytes = src() if a.a_mode == 1 else 2.0 * a.M * a.K
+    bbytes = src() if a.b_mode == 3 else 2.0 * a.N * a.K
+    return abytes + bbytes + (2.0 if a.c_mode == 0 else 4.0) * a.M * a.N
+
+
+def replay_gemms(calls, reps=1):
+    import ctypes as C
+    from encdiff_amd import _lib as L
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for _ in range(reps):
+        for a in calls:
+            L.check(L.lib.encdiff_gemm(C.byref(a), stream), "encdiff_gemm")
+
+
+def kernel_roofline(tr, reps=10):
+    """Dominant kernel by time: the GEMM family (gemm_kernel<*> + its split-K finalize)
+    that runs every conv / linear of the UNet, fwd + dgrad + wgrad.  The exact launches of
+    one training step are recorded, captured into a HIP graph and replayed `reps` times
+    between HIP events on the replay stream: achieved = algorithmic flops (sum 2*M*N*K)
+    / GPU time, per launch averages reported beside it."""
+    calls = record_gemms(tr)
+    flops = sum(2.0 * a.M * a.N * a.K for a in calls)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        replay_gemms(calls)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            replay_gemms(calls)
+        g.replay()
+        s.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            g.replay()
+        e1.record(s)
+        s.synchronize()
+    t_set = e0.elapsed_time(e1) / 1e3 / reps
+    out = {"kernel": f"gemm_kernel<*> family: {len(calls)} UNet conv/linear GEMM launches per step "
+                     "(fwd+dgrad+wgrad, incl. split-K finalize)",
+           "bound": "mfma", "achieved": flops / t_set / 1e12, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+           "frac": flops / t_set / 1e12 / PEAK_BF16_TFLOPS, "traffic": None,
+           "avg_us": t_set / len(calls) * 1e6, "flops_per_launch": flops / len(calls),
+           "launches_per_step": len(calls), "gemm_ms_per_step": t_set * 1e3,
+           "alg_bytes_per_launch": sum(gemm_alg_bytes(a) for a in calls) / len(calls)}
+    prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "gemm_traffic.json")
+    if os.path.exists(prof):  # HBM bytes per launch from the committed rocprofv3 PMC passes
+        with open(prof) as f:
+            pm = json.load(f)
+        out["traffic"] = pm.get("bytes_per_launch")
+        out["traffic_source"] = f"profiles/gemm_traffic.json ({pm.get('source', '')})"
+    return out
 
 
 def ddim_rate(ldm, B, S):
@@ -165,8 +220,9 @@ def main():
     value = imgs / dt
     loss = tr.loss()
     extra = {}
+    roof = kernel_roofline(tr)  # every rank (its recording step runs the DP exchange)
     if rank == 0:
-        extra["roofline"] = kernel_roofline(args.batch)
+        extra["roofline"] = roof
         f_step = 3 * F_UNET_FWD_PER_IMG * args.batch
         extra["step_roofline"] = {"bound": "mfma", "unit": "TFLOP/s",
                                   "achieved": f_step * args.steps / dt / 1e12,

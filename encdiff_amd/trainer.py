@@ -94,6 +94,9 @@ class HipTrainer:
 
     def _cond_bwd(self):
         self._c.backward(self._dc)
+        # drop the autograd graph: a graph kept alive across steps pins AccumulateGrad
+        # nodes created on another stream, which breaks the next capture
+        self._c = self._dc = None
 
     def _exchange(self, cond_bwd):
         """DP gradient mean: bucket 0 (UNet) on the side stream overlapped with the cond

@@ -1,0 +1,114 @@
+"""HBM traffic of the GEMM family (bench.py's roofline kernel) from rocprofv3 PMC passes.
+
+Run (GPU box), one counter per pass as MI355X_MICROARCH.md prescribes (FETCH_SIZE and
+WRITE_SIZE do not fit one pass):
+
+    cd /tmp && export TMPDIR=/tmp
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_f -o run -- python3 $R/tools/gemm_traffic.py run
+    rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_w -o run -- python3 $R/tools/gemm_traffic.py run
+    python tools/gemm_traffic.py summarize gpurun_out/pmc_f gpurun_out/pmc_w --out profiles/gemm_traffic.json
+
+`run` records the GEMM launches of one eager training step (B=128) and replays them once
+between torch spin_kernel markers, preceded by a calibration copy of known size (the
+ENCDIFF_EW_COPY kernel, 16-B lanes, 256 MiB read + 256 MiB write).  `summarize` sums the
+counters of the gemm dispatches between the markers, converts them with the calibration
+copy's bytes-per-unit (the guide: FETCH_SIZE reports 1/2 of a 16-B-lane streaming read on
+gfx950), and writes bytes per launch next to the algorithmic bytes per launch.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+CAL_BYTES = 256 << 20
+
+
+def run(batch: int):
+    import torch
+    import bench
+    from encdiff_amd import ops
+    from encdiff_amd.trainer import HipTrainer
+    torch.cuda.set_device(0)
+    ldm, _ = bench.build_ldm()
+    tr = HipTrainer(ldm, batch, graph=False)
+    tr.init_scale_factor()
+    tr.step_eager()
+    calls = bench.record_gemms(tr)
+    n = CAL_BYTES // 2
+    src = torch.randn(n // 64, 64, device="cuda").to(torch.bfloat16)
+    dst = torch.empty_like(src)
+    torch.cuda.synchronize()
+    torch.cuda._sleep(1000)
+    ops.ew(0, src, dst)                      # calibration: ENCDIFF_EW_COPY
+    bench.replay_gemms(calls)
+    torch.cuda._sleep(1000)
+    torch.cuda.synchronize()
+    alg = sum(bench.gemm_alg_bytes(a) for a in calls)
+    with open(os.path.join(REPO, "gpurun_out", "gemm_traffic_calls.json"), "w") as f:
+        json.dump({"launches": len(calls), "alg_bytes": alg,
+                   "flops": sum(2.0 * a.M * a.N * a.K for a in calls)}, f)
+    print(f"replayed {len(calls)} gemm launches")
+
+
+def _rows(d):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    assert files, f"no counter_collection.csv under {d}"
+    out = []
+    for fn in files:
+        with open(fn) as f:
+            for r in csv.DictReader(f):
+                out.append((int(r["Dispatch_Id"]), r["Kernel_Name"], r["Counter_Name"], float(r["Counter_Value"])))
+    out.sort()
+    return out
+
+
+def _window(rows, counter):
+    marks = [i for i, r in enumerate(rows) if "spin_kernel" in r[1]]
+    assert len(marks) >= 2, "markers missing"
+    win = rows[marks[-2] + 1:marks[-1]]
+    cal = [r for r in win if "ew_kernel" in r[1] and r[2] == counter]
+    gem = [r for r in win if ("gemm_kernel" in r[1] or "gemm_finalize" in r[1]) and r[2] == counter]
+    launches = len({r[0] for r in win if "gemm_kernel" in r[1]})
+    return sum(r[3] for r in cal), sum(r[3] for r in gem), launches
+
+
+def summarize(fdir, wdir, out):
+    f_cal, f_gemm, n1 = _window(_rows(fdir), "FETCH_SIZE")
+    w_cal, w_gemm, n2 = _window(_rows(wdir), "WRITE_SIZE")
+    assert n1 == n2, (n1, n2)
+    rd = f_gemm * CAL_BYTES / f_cal        # calibrated: units of the counter -> bytes
+    wr = w_gemm * CAL_BYTES / w_cal
+    meta = json.load(open(os.path.join(REPO, "gpurun_out", "gemm_traffic_calls.json")))
+    res = {"launches": n1, "read_bytes_per_step": rd, "write_bytes_per_step": wr,
+           "bytes_per_launch": (rd + wr) / n1, "alg_bytes_per_launch": meta["alg_bytes"] / n1,
+           "traffic_over_alg": (rd + wr) / meta["alg_bytes"],
+           "fetch_units_per_cal_byte": f_cal / CAL_BYTES, "write_units_per_cal_byte": w_cal / CAL_BYTES,
+           "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of tools/gemm_traffic.py run (B=128), "
+                     "calibrated on a 256 MiB 16-B-lane copy"}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["run", "summarize"])
+    ap.add_argument("dirs", nargs="*")
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "gemm_traffic.json"))
+    a = ap.parse_args()
+    if a.mode == "run":
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        run(a.batch)
+    else:
+        summarize(a.dirs[0], a.dirs[1], a.out)
+
+
+if __name__ == "__main__":
+    main()
