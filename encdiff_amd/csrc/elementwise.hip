@@ -354,6 +354,40 @@ __global__ void ddim_indexed_kernel(const float* x, const float* e, const float*
 
 __global__ void index_dec_kernel(int* index) { *index -= 1; }
 
+// ------------------------------------------------ input path
+// Block per image: the uint8 HWC image is staged through LDS with 16-byte loads, then
+// written as fp32 CHW with float4 stores.
+__global__ __launch_bounds__(256) void gather_u8_kernel(const uint8_t* __restrict__ pool, long long n_images,
+                                                        int hw, int c, const long long* __restrict__ perm,
+                                                        const long long* step, int steps_per_epoch,
+                                                        float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t img[];
+  const int b = blockIdx.x, B = gridDim.x;
+  const long long s = step ? *step : 0;
+  const long long id = perm[(s % steps_per_epoch) * B + b];
+  const int nbytes = hw * c;
+  const uint8_t* src = pool + (id < 0 ? 0 : (id >= n_images ? n_images - 1 : id)) * (long long)nbytes;
+  if ((nbytes & 15) == 0 && (((uintptr_t)src) & 15) == 0) {
+    for (int i = threadIdx.x; i < nbytes / 16; i += 256) ((uint4*)img)[i] = ((const uint4*)src)[i];
+  } else {
+    for (int i = threadIdx.x; i < nbytes; i += 256) img[i] = src[i];
+  }
+  __syncthreads();
+  float* o = out + (long long)b * nbytes;
+  const int n4 = nbytes >> 2;  // hw % 4 == 0 checked on the host
+  for (int i = threadIdx.x; i < n4; i += 256) {
+    const int e = i * 4, ch = e / hw, px = e - ch * hw;
+    float4 v;
+    v.x = ((float)img[(px + 0) * c + ch] / 255.f - 0.5f) / 0.5f;
+    v.y = ((float)img[(px + 1) * c + ch] / 255.f - 0.5f) / 0.5f;
+    v.z = ((float)img[(px + 2) * c + ch] / 255.f - 0.5f) / 0.5f;
+    v.w = ((float)img[(px + 3) * c + ch] / 255.f - 0.5f) / 0.5f;
+    ((float4*)o)[i] = v;
+  }
+}
+
+__global__ void counter_inc_kernel(long long* counter) { *counter += 1; }
+
 // ------------------------------------------------ optimizer
 __global__ __launch_bounds__(256) void adamw_ema_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
@@ -518,6 +552,23 @@ extern "C" int encdiff_ddim_step_indexed(const float* x, const float* e, const f
   ED_CHECK_LAUNCH();
   if (advance) {
     hipLaunchKernelGGL(index_dec_kernel, dim3(1), dim3(1), 0, s, index);
+    ED_CHECK_LAUNCH();
+  }
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_gather_images_u8(const void* pool, long long n_images, int h, int w, int c,
+                                        const long long* perm, long long* step, int steps_per_epoch, int batch,
+                                        int advance, float* out, void* stream) {
+  if (!pool || !perm || !out || batch <= 0 || steps_per_epoch <= 0 || n_images <= 0) return ENCDIFF_ERR_ARG;
+  if ((h * w) % 4 || (long)h * w * c > 64 * 1024) return ENCDIFF_ERR_SHAPE;
+  if (advance && !step) return ENCDIFF_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(gather_u8_kernel, dim3(batch), dim3(256), (size_t)h * w * c, s, (const uint8_t*)pool, n_images,
+                     h * w, c, perm, step, steps_per_epoch, out);
+  ED_CHECK_LAUNCH();
+  if (advance) {
+    hipLaunchKernelGGL(counter_inc_kernel, dim3(1), dim3(1), 0, s, step);
     ED_CHECK_LAUNCH();
   }
   return ENCDIFF_OK;

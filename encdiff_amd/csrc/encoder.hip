@@ -1,0 +1,227 @@
+// encoder.hip -- concept-encoder kernels (Encoder4 in HIP).
+//
+// Encoder4.warp (openaimodel_enc.py:1015-1041): latent_unit independent MLPs
+//   u_i (B scalars) -> Linear(1,64) -> ELU -> Linear(64,128) -> ELU -> Linear(128,16)
+// whose outputs are concatenated to (B, latent_unit*16).  The reference runs them as
+// 100 forward / ~300 backward tiny launches; here one workgroup per unit runs the whole
+// MLP in fp32 (VALU FMA, weights and 32-row activation chunks in LDS), forward in one
+// launch and backward (recomputing the activations) in one launch.  The backward adds
+// the weight gradients of unit i straight into the fp32 gradient arena (one workgroup
+// owns them: deterministic) and writes d u.
+#include "common.h"
+
+namespace {
+
+constexpr int WT = 256;   // threads
+constexpr int WR = 32;    // batch rows per chunk
+constexpr int H1 = 64, H2 = 128;
+
+ED_DEV float elu_f(float z) { return z > 0.f ? z : expm1f(z); }
+ED_DEV float elu_d(float out) { return out > 0.f ? 1.f : out + 1.f; }  // torch elu_backward(is_result)
+
+struct WarpSmem {
+  float w1[H1], b1[H1], b2[H2];
+  float w2[H2][H1 + 1];        // +1: conflict-free column walks
+  float w3[16][H2 + 1];
+  float b3[16];
+  float h1[WR][H1 + 1];
+  float h2[WR][H2 + 1];
+  float u[WR];
+};
+
+// parameter block of unit i: [W1 64][b1 64][W2 128x64][b2 128][W3 D x 128][b3 D]
+ED_DEV void load_unit(WarpSmem& s, const float* P, int D) {
+  const float* W1 = P;
+  const float* B1 = W1 + H1;
+  const float* W2 = B1 + H1;
+  const float* B2 = W2 + H2 * H1;
+  const float* W3 = B2 + H2;
+  const float* B3 = W3 + D * H2;
+  for (int i = threadIdx.x; i < H1; i += WT) { s.w1[i] = W1[i]; s.b1[i] = B1[i]; }
+  for (int i = threadIdx.x; i < H2; i += WT) s.b2[i] = B2[i];
+  for (int i = threadIdx.x; i < H2 * H1; i += WT) s.w2[i / H1][i % H1] = W2[i];
+  for (int i = threadIdx.x; i < D * H2; i += WT) s.w3[i / H2][i % H2] = W3[i];
+  for (int i = threadIdx.x; i < D; i += WT) s.b3[i] = B3[i];
+}
+
+// rows [r0, r0 + nr) of unit `unit`: h1, h2 (post-ELU) into LDS
+ED_DEV void warp_hidden(WarpSmem& s, const float* u, long ldu, int unit, int r0, int nr) {
+  for (int i = threadIdx.x; i < WR; i += WT) s.u[i] = i < nr ? u[(long)(r0 + i) * ldu + unit] : 0.f;
+  __syncthreads();
+  for (int e = threadIdx.x; e < WR * H1; e += WT) {
+    const int r = e / H1, j = e % H1;
+    s.h1[r][j] = elu_f(s.u[r] * s.w1[j] + s.b1[j]);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < WR * H2; e += WT) {
+    const int r = e / H2, k = e % H2;
+    float a = s.b2[k];
+#pragma unroll 8
+    for (int j = 0; j < H1; ++j) a += s.h1[r][j] * s.w2[k][j];
+    s.h2[r][k] = elu_f(a);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(WT) void warp_fwd_kernel(const float* __restrict__ u, long ldu, int batch,
+                                                      const float* __restrict__ params, long unit_stride, int D,
+                                                      float* __restrict__ out, long ldo) {
+  extern __shared__ __attribute__((aligned(16))) float smem_raw[];
+  WarpSmem& s = *reinterpret_cast<WarpSmem*>(smem_raw);
+  const int unit = blockIdx.x;
+  load_unit(s, params + unit * unit_stride, D);
+  for (int r0 = 0; r0 < batch; r0 += WR) {
+    const int nr = min(WR, batch - r0);
+    warp_hidden(s, u, ldu, unit, r0, nr);
+    for (int e = threadIdx.x; e < nr * D; e += WT) {
+      const int r = e / D, m = e % D;
+      float a = s.b3[m];
+#pragma unroll 8
+      for (int k = 0; k < H2; ++k) a += s.h2[r][k] * s.w3[m][k];
+      out[(long)(r0 + r) * ldo + unit * D + m] = a;
+    }
+    __syncthreads();
+  }
+}
+
+struct WarpBwdSmem {
+  WarpSmem f;
+  float dout[WR][17];
+  float dz2[WR][H2 + 1];
+  float dz1[WR][H1 + 1];
+};
+
+__global__ __launch_bounds__(WT) void warp_bwd_kernel(const float* __restrict__ u, long ldu, int batch,
+                                                      const float* __restrict__ params, long unit_stride, int D,
+                                                      const float* __restrict__ dout, long lddo,
+                                                      float* __restrict__ du, long lddu,
+                                                      float* __restrict__ grads) {
+  extern __shared__ __attribute__((aligned(16))) float smem_raw[];
+  WarpBwdSmem& s = *reinterpret_cast<WarpBwdSmem*>(smem_raw);
+  const int unit = blockIdx.x, tid = threadIdx.x;
+  load_unit(s.f, params + unit * unit_stride, D);
+  // register-resident weight-gradient accumulators (fixed ownership -> deterministic)
+  float gW2[H2 * H1 / WT];   // 32: entries tid + WT*q of W2 (row-major [k][j])
+  float gW3[16 * H2 / WT];   // 8 : entries tid + WT*q of W3 ([m][k], D <= 16)
+  float gb2 = 0.f, gW1 = 0.f, gb1 = 0.f, gb3 = 0.f;
+#pragma unroll
+  for (int q = 0; q < H2 * H1 / WT; ++q) gW2[q] = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16 * H2 / WT; ++q) gW3[q] = 0.f;
+  for (int r0 = 0; r0 < batch; r0 += WR) {
+    const int nr = min(WR, batch - r0);
+    warp_hidden(s.f, u, ldu, unit, r0, nr);
+    for (int e = tid; e < WR * D; e += WT) {
+      const int r = e / D, m = e % D;
+      s.dout[r][m] = r < nr ? dout[(long)(r0 + r) * lddo + unit * D + m] : 0.f;
+    }
+    __syncthreads();
+    // dW3[m][k] += sum_r dout[r][m] h2[r][k]; db3
+#pragma unroll
+    for (int q = 0; q < 16 * H2 / WT; ++q) {
+      const int e = tid + WT * q, m = e / H2, k = e % H2;
+      if (m < D) {
+        float a = 0.f;
+        for (int r = 0; r < nr; ++r) a += s.dout[r][m] * s.f.h2[r][k];
+        gW3[q] += a;
+      }
+    }
+    if (tid < D) {
+      float a = 0.f;
+      for (int r = 0; r < nr; ++r) a += s.dout[r][tid];
+      gb3 += a;
+    }
+    // dz2[r][k] = (sum_m dout[r][m] W3[m][k]) * elu'(h2)
+    for (int e = tid; e < WR * H2; e += WT) {
+      const int r = e / H2, k = e % H2;
+      float a = 0.f;
+      for (int m = 0; m < D; ++m) a += s.dout[r][m] * s.f.w3[m][k];
+      s.dz2[r][k] = r < nr ? a * elu_d(s.f.h2[r][k]) : 0.f;
+    }
+    __syncthreads();
+    // dW2[k][j] += sum_r dz2[r][k] h1[r][j]; db2
+#pragma unroll
+    for (int q = 0; q < H2 * H1 / WT; ++q) {
+      const int e = tid + WT * q, k = e / H1, j = e % H1;
+      float a = 0.f;
+      for (int r = 0; r < nr; ++r) a += s.dz2[r][k] * s.f.h1[r][j];
+      gW2[q] += a;
+    }
+    if (tid < H2) {
+      float a = 0.f;
+      for (int r = 0; r < nr; ++r) a += s.dz2[r][tid];
+      gb2 += a;
+    }
+    // dz1[r][j] = (sum_k dz2[r][k] W2[k][j]) * elu'(h1)
+    for (int e = tid; e < WR * H1; e += WT) {
+      const int r = e / H1, j = e % H1;
+      float a = 0.f;
+#pragma unroll 8
+      for (int k = 0; k < H2; ++k) a += s.dz2[r][k] * s.f.w2[k][j];
+      s.dz1[r][j] = r < nr ? a * elu_d(s.f.h1[r][j]) : 0.f;
+    }
+    __syncthreads();
+    // dW1[j] += sum_r dz1[r][j] u[r]; db1[j] += sum_r dz1[r][j]
+    if (tid < H1) {
+      float a = 0.f, c = 0.f;
+      for (int r = 0; r < nr; ++r) { a += s.dz1[r][tid] * s.f.u[r]; c += s.dz1[r][tid]; }
+      gW1 += a;
+      gb1 += c;
+    }
+    // du[r] = sum_j dz1[r][j] W1[j]
+    if (tid < nr) {
+      float a = 0.f;
+      for (int j = 0; j < H1; ++j) a += s.dz1[tid][j] * s.f.w1[j];
+      du[(long)(r0 + tid) * lddu + unit] = a;
+    }
+    __syncthreads();
+  }
+  float* G = grads + unit * unit_stride;
+  float* gW1p = G;
+  float* gb1p = gW1p + H1;
+  float* gW2p = gb1p + H1;
+  float* gb2p = gW2p + H2 * H1;
+  float* gW3p = gb2p + H2;
+  float* gb3p = gW3p + D * H2;
+  if (tid < H1) { gW1p[tid] += gW1; gb1p[tid] += gb1; }
+  if (tid < H2) gb2p[tid] += gb2;
+  if (tid < D) gb3p[tid] += gb3;
+#pragma unroll
+  for (int q = 0; q < H2 * H1 / WT; ++q) gW2p[tid + WT * q] += gW2[q];
+#pragma unroll
+  for (int q = 0; q < 16 * H2 / WT; ++q) {
+    const int e = tid + WT * q;
+    if (e < D * H2) gW3p[e] += gW3[q];
+  }
+}
+
+}  // namespace
+
+extern "C" int encdiff_encoder_warp_fwd(const float* u, long ldu, int batch, int units, const float* params,
+                                        long unit_stride, int context_dim, float* out, long ldo, void* stream) {
+  if (!u || !params || !out || batch <= 0 || units <= 0) return ENCDIFF_ERR_ARG;
+  if (context_dim <= 0 || context_dim > 16) return ENCDIFF_ERR_UNSUPPORTED;
+  if (unit_stride < 2 * H1 + H2 * H1 + H2 + context_dim * H2 + context_dim) return ENCDIFF_ERR_SHAPE;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)warp_fwd_kernel,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)attr;
+  hipLaunchKernelGGL(warp_fwd_kernel, dim3(units), dim3(WT), sizeof(WarpSmem), (hipStream_t)stream, u, ldu, batch,
+                     params, unit_stride, context_dim, out, ldo);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_encoder_warp_bwd(const float* u, long ldu, int batch, int units, const float* params,
+                                        long unit_stride, int context_dim, const float* dout, long lddo, float* du,
+                                        long lddu, float* grads, void* stream) {
+  if (!u || !params || !dout || !du || !grads || batch <= 0 || units <= 0) return ENCDIFF_ERR_ARG;
+  if (context_dim <= 0 || context_dim > 16) return ENCDIFF_ERR_UNSUPPORTED;
+  if (unit_stride < 2 * H1 + H2 * H1 + H2 + context_dim * H2 + context_dim) return ENCDIFF_ERR_SHAPE;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)warp_bwd_kernel,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)attr;
+  hipLaunchKernelGGL(warp_bwd_kernel, dim3(units), dim3(WT), sizeof(WarpBwdSmem), (hipStream_t)stream, u, ldu,
+                     batch, params, unit_stride, context_dim, dout, lddo, du, lddu, grads);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}

@@ -447,6 +447,9 @@ class LatentDiffusion(DDPM):
             if n.startswith("model.diffusion_model."):
                 arena.alias(n[len("model.diffusion_model."):], n)
         unet.bind_arena(arena)
+        cs = self.cond_stage_model
+        if self.cond_stage_trainable and cs is not None and hasattr(cs, "bind_arena"):
+            cs.bind_arena(arena, "cond_stage_model.")   # Encoder4.warp on HIP (§8(f) row 2)
         if self.use_ema:
             self.model_ema.bind_arena(arena, prefix="model.")
             self._ema_fused = True

@@ -19,6 +19,7 @@ import torch
 from torch import nn
 
 from encdiff_amd import _lib as L
+from encdiff_amd import ops
 from encdiff_amd.arena import ParamArena
 from encdiff_amd.unet import ConvSpec, ResSpec, STSpec, UNetExecutor, UNetSpec
 from ..attention import SpatialTransformer
@@ -207,6 +208,31 @@ class View(nn.Module):
         return tensor.view(self.size)
 
 
+class _WarpFn(torch.autograd.Function):
+    """Encoder4.warp on encdiff_encoder_warp_fwd/bwd; weight gradients go to the arena
+    directly (the module's .grad views), only d u flows back through autograd."""
+
+    @staticmethod
+    def forward(ctx, u, enc):
+        arena, base, stride = enc._warp_bind
+        u = u.contiguous()
+        out = torch.empty(u.shape[0], enc.latent_unit * enc.context_dim, device=u.device, dtype=torch.float32)
+        ops.encoder_warp_fwd(u, arena.master[base:], stride, enc.latent_unit, enc.context_dim, out)
+        ctx.enc = enc
+        ctx.save_for_backward(u)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (u,) = ctx.saved_tensors
+        enc = ctx.enc
+        arena, base, stride = enc._warp_bind
+        du = torch.empty_like(u)
+        ops.encoder_warp_bwd(u, arena.master[base:], stride, enc.latent_unit, enc.context_dim, dout.contiguous(), du,
+                             arena.grad[base:])
+        return du, None
+
+
 class Encoder4(nn.Module):
     """openaimodel_enc.py:991-1041: image -> latent_unit scalars -> per-unit MLP warp
     to context_dim-d concept tokens, concatenated to (B, latent_unit*context_dim)."""
@@ -226,8 +252,30 @@ class Encoder4(nn.Module):
             nn.Linear(2048, latent_unit))
         self.net = nn.ModuleList([nn.Sequential(nn.Linear(1, 64), nn.ELU(True), nn.Linear(64, 128), nn.ELU(True),
                                                 nn.Linear(128, context_dim)) for _ in range(latent_unit)])
+        self._warp_bind = None
+
+    def bind_arena(self, arena, prefix: str):
+        """Run warp() on the HIP kernels (encdiff_encoder_warp_*): the per-unit MLP
+        parameters must sit in the fp32 arena contiguously, unit after unit, with one
+        stride (the arena lays out named_parameters() in order, so they do); weight
+        gradients are then written straight into the arena's gradient buffer."""
+        sizes = [p.numel() for p in self.net[0].parameters()]
+        base = arena.offsets[prefix + "net.0.0.weight"][0]
+        stride = None
+        for i in range(self.latent_unit):
+            names = [prefix + f"net.{i}.{n}" for n, _ in self.net[i].named_parameters()]
+            offs = [arena.offsets[n][0] for n in names]
+            if any(o2 != o1 + s1 for o1, o2, s1 in zip(offs, offs[1:], sizes)):
+                raise ValueError("Encoder4.net params are not contiguous in the arena")
+            if i == 1:
+                stride = offs[0] - base
+            if i > 0 and offs[0] != base + i * stride:
+                raise ValueError("Encoder4.net units do not have a constant arena stride")
+        self._warp_bind = (arena, base, stride or sum(sizes))
 
     def warp(self, u):
+        if self._warp_bind is not None:
+            return _WarpFn.apply(u, self)
         return torch.cat([self.net[i](u[:, i][:, None]) for i in range(self.latent_unit)], dim=1)
 
     def forward(self, x):

@@ -346,3 +346,29 @@ def pack_weights(src_f32, dst_bf16, jobs_dev, njobs):
 def reduce_partials(part, ld, rows, cols, col_index, grad):
     check(lib.encdiff_reduce_partials(_p(part), ld, rows, cols, _p(col_index), _p(grad), _s()),
           "encdiff_reduce_partials")
+
+
+def gather_images_u8(pool_u8, perm, step, batch, out, advance=True):
+    """Batch gather from the HBM-resident uint8 dataset + ToTensor/Normalize/CHW
+    (disdata.py:82-88, ddpm_enc.py:347-353) -> out fp32 [batch][c][h][w]."""
+    n, h, w, c = pool_u8.shape
+    assert pool_u8.is_cuda and perm.is_cuda and step.is_cuda and out.is_cuda, "HIP device tensors required"
+    assert pool_u8.dtype == torch.uint8 and pool_u8.is_contiguous() and out.is_contiguous()
+    assert out.shape == (batch, c, h, w) and out.dtype == torch.float32
+    spe = perm.numel() // batch
+    check(lib.encdiff_gather_images_u8(_p(pool_u8), n, h, w, c, _p(perm), _p(step), spe, batch, int(advance),
+                                       _p(out), _s()), "encdiff_gather_images_u8")
+
+
+def encoder_warp_fwd(u, params, unit_stride, units, context_dim, out):
+    """Encoder4.warp forward (openaimodel_enc.py:1015-1041) -> out fp32 [B, units*context_dim]."""
+    assert u.is_cuda and params.is_cuda and out.is_cuda, "HIP device tensors required"
+    check(lib.encdiff_encoder_warp_fwd(_p(u), u.stride(0), u.shape[0], units, _p(params), unit_stride, context_dim,
+                                       _p(out), out.stride(0), _s()), "encdiff_encoder_warp_fwd")
+
+
+def encoder_warp_bwd(u, params, unit_stride, units, context_dim, dout, du, grads):
+    assert dout.stride(1) == 1 and du.stride(1) == 1
+    check(lib.encdiff_encoder_warp_bwd(_p(u), u.stride(0), u.shape[0], units, _p(params), unit_stride, context_dim,
+                                       _p(dout), dout.stride(0), _p(du), du.stride(0), _p(grads), _s()),
+          "encdiff_encoder_warp_bwd")

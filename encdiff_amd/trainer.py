@@ -26,12 +26,13 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from .data import ImagePool
 from .dp import GradBuckets, rank_seed, scaled_lr, world_info
 
 
 class HipTrainer:
     def __init__(self, ldm, batch_size: int, base_lr: Optional[float] = None, graph: bool = True,
-                 data_pool: Optional[torch.Tensor] = None, pool_size: int = 2048, seed: int = 1234,
+                 data: Optional[ImagePool] = None, pool_size: int = 480000, seed: int = 1234,
                  bucket_mb: float = 0.0):
         self.ldm = ldm
         self.dev = ldm.device
@@ -50,10 +51,9 @@ class HipTrainer:
             self.opt, self.sched = opt, None
         self.buckets = GradBuckets.from_arena(arena)
         self._comm = torch.cuda.Stream() if self.world > 1 else None
-        g = torch.Generator(device=self.dev).manual_seed(rank_seed(seed, self.rank))
-        if data_pool is None:  # synthetic Shapes3D-shaped images in [-1, 1], resident in HBM
-            data_pool = torch.rand(pool_size, 3, 64, 64, device=self.dev, generator=g) * 2 - 1
-        self.pool = data_pool
+        if data is None:  # synthetic uint8 images of the Shapes3D shape/size, resident in HBM
+            data = ImagePool.synthetic(pool_size, batch_size, self.dev, seed=seed, rank=self.rank, world=self.world)
+        self.data = data
         self.img = torch.empty(batch_size, 3, 64, 64, device=self.dev)
         self.loss_buf = torch.zeros(4, device=self.dev)
         self.graph = graph
@@ -65,8 +65,7 @@ class HipTrainer:
 
     # ---------------------------------------------------------------- device work
     def _draw_batch(self):
-        idx = torch.randint(0, self.pool.shape[0], (self.B,), device=self.dev)
-        torch.index_select(self.pool, 0, idx, out=self.img)
+        self.data.draw(self.img)
 
     def _fwd_bwd(self):
         """Everything up to the UNet backward.  At world size 1 Encoder4's backward runs
@@ -167,6 +166,7 @@ class HipTrainer:
         self._post()
 
     def _post(self):
+        self.data.after_step()
         if self.sched is not None:
             self.sched.step()
         self.ldm.global_step += 1

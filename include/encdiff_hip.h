@@ -283,6 +283,33 @@ int encdiff_pack_weights(const float* src, void* dst_bf16, const EncdiffPackJob*
 int encdiff_reduce_partials(const float* part, long ld, int rows, int cols, const int* col_index,
                             float* grad, void* stream);
 
+/* ---------------------------------------------------------------- input path
+ * GPU-resident dataset: uint8 images [n_images][h][w][c] (Shapes3D layout, disdata.py:45-97)
+ * stay in HBM; one launch gathers a batch and applies ToTensor + Normalize(0.5, 0.5)
+ * (disdata.py:82-88) and get_input's 'b h w c -> b c h w' float (ddpm_enc.py:347-353):
+ *   out[b][ch][y][x] = (pool[id][y][x][ch] / 255 - 0.5) / 0.5,
+ *   id = perm[(*step mod steps_per_epoch) * batch + b]          (shuffled epoch order)
+ * perm: device int64 [steps_per_epoch * batch]; step: device int64 counter (NULL = 0),
+ * advanced by one after the gather when `advance` != 0, so a captured step graph walks
+ * the epoch by itself. */
+int encdiff_gather_images_u8(const void* pool, long long n_images, int h, int w, int c,
+                             const long long* perm, long long* step, int steps_per_epoch, int batch,
+                             int advance, float* out, void* stream);
+
+/* ---------------------------------------------------------------- concept encoder (§8(f) row 2)
+ * Encoder4.warp (openaimodel_enc.py:1015-1041): `units` independent MLPs
+ * u[:, i] -> Linear(1,64) -> ELU -> Linear(64,128) -> ELU -> Linear(128,context_dim),
+ * out[:, i*context_dim + m].  fp32 throughout (the reference's precision).
+ * params: unit i's tensors contiguous at params + i*unit_stride in nn.Sequential order
+ * [W1 64][b1 64][W2 128x64][b2 128][W3 context_dim x 128][b3 context_dim] (the layout
+ * of the parameter arena).  The backward ADDS the weight gradients into `grads` (same
+ * layout) and writes du; one workgroup per unit, deterministic. context_dim <= 16. */
+int encdiff_encoder_warp_fwd(const float* u, long ldu, int batch, int units, const float* params,
+                             long unit_stride, int context_dim, float* out, long ldo, void* stream);
+int encdiff_encoder_warp_bwd(const float* u, long ldu, int batch, int units, const float* params,
+                             long unit_stride, int context_dim, const float* dout, long lddo, float* du,
+                             long lddu, float* grads, void* stream);
+
 /* Library/device information (for tests): returns the number of exported kernels. */
 int encdiff_version(void);
 

@@ -522,6 +522,19 @@ def encoder4_forward(P, x, latent_unit=20, train=True):
 # of the end-to-end step): q_sample -> UNet -> L1 loss -> backward -> AdamW -> EMA.
 # ----------------------------------------------------------------------------
 
+def images_to_input(images_u8: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """Training input of one batch: Shapes3D uint8 HWC images
+    (disdata.py:45-97) -> transforms.ToTensor() (x / 255, CHW) -> Normalize((0.5,)*3,
+    (0.5,)*3) ((x - 0.5) / 0.5) -> .permute(1, 2, 0) (disdata.py:82-94) -> get_input's
+    'b h w c -> b c h w' .float() (ddpm_enc.py:347-353).  torchvision is not installed
+    here; ToTensor/Normalize are restated from torchvision's published definitions (the
+    reference pins torchvision via encdiff_h100.yaml), so this row is "parity unpinned"
+    by reference fixtures."""
+    x = images_u8[idx].permute(0, 3, 1, 2).contiguous().to(torch.float32).div(255)
+    x = x.sub(0.5).div(0.5)
+    return x
+
+
 class OracleTrainer:
     """CPU restatement of one LatentDiffusion training step on latents
     (ddpm_enc.py:1040-1053, 1183-1253, 399-401, 1598-1639).  The frozen VQ

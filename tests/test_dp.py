@@ -111,3 +111,19 @@ def test_gloo_world2():
         assert r["dp_grad_err"] < 1e-6
         assert r["opt_rank_diff"] == 0.0
         assert r["scale_factor"] == 0.5
+
+
+def test_image_pool_shards():
+    """DistributedSampler semantics of the HBM dataset: same permutation on every rank,
+    disjoint strided shards, new permutation per epoch (host side, CPU tensors)."""
+    from encdiff_amd.data import ImagePool
+    imgs = torch.zeros(103, 4, 4, 3, dtype=torch.uint8)
+    p0 = ImagePool(imgs, 8, "cpu", seed=5, rank=0, world=2)
+    p1 = ImagePool(imgs, 8, "cpu", seed=5, rank=1, world=2)
+    assert p0.steps_per_epoch == 6 and p0.perm.numel() == 48
+    a, b = set(p0.perm.tolist()), set(p1.perm.tolist())
+    assert not (a & b) and a | b <= set(range(103))
+    first = p0.perm.clone()
+    for _ in range(p0.steps_per_epoch):
+        p0.after_step()
+    assert p0.epoch == 1 and not torch.equal(first, p0.perm)

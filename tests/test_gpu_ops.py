@@ -387,3 +387,44 @@ def test_adamw_ema_pack_reduce(O):
     ref = torch.zeros(200, device=dev)
     ref[idx.long()] = part.sum(0)
     assert rel(gr, ref) < 1e-6
+
+
+def test_gather_images_u8(O):
+    """GPU-resident dataset gather + ToTensor/Normalize/CHW == oracle bit-exact, with the
+    device step counter walking the epoch (and wrapping) on its own."""
+    from encdiff_amd.data import ImagePool
+    from oracle import encdiff_oracle as Orc
+    pool = ImagePool.synthetic(37, 8, dev, seed=3)
+    out = torch.empty(8, 3, 64, 64, device=dev)
+    for s in range(pool.steps_per_epoch + 2):
+        pool.draw(out)
+        k = s % pool.steps_per_epoch
+        idx = pool.perm[k * 8:(k + 1) * 8].cpu()
+        ref = Orc.images_to_input(pool.images.cpu(), idx)
+        assert torch.equal(out.cpu(), ref)
+    assert int(pool.step) == pool.steps_per_epoch + 2
+
+
+@pytest.mark.parametrize("B", [128, 50])
+def test_encoder_warp(O, B):
+    """Encoder4.warp on HIP (fp32) vs the as-is torch modules (fp32) on the same params:
+    outputs, d u and every per-unit weight/bias gradient."""
+    import copy
+    from encdiff_amd.arena import ParamArena
+    from encdiff_amd.ldm.modules.diffusionmodules.openaimodel_enc import Encoder4
+    torch.manual_seed(9)
+    enc = Encoder4(128, 16, 20).to(dev)
+    ref = copy.deepcopy(enc)
+    arena = ParamArena([("cond_stage_model." + n, p) for n, p in enc.named_parameters()], dev)
+    enc.bind_arena(arena, "cond_stage_model.")
+    u = torch.randn(B, 20, device=dev, requires_grad=True)
+    u2 = u.detach().clone().requires_grad_(True)
+    out, outr = enc.warp(u), ref.warp(u2)
+    assert rel(out, outr) < 1e-5
+    g = torch.randn_like(out)
+    arena.grad.zero_()
+    out.backward(g)
+    outr.backward(g)
+    assert rel(u.grad, u2.grad) < 1e-5
+    for (n, p), (_, pr) in zip(enc.net.named_parameters(), ref.net.named_parameters()):
+        assert rel(p.grad, pr.grad) < 1e-4, n
