@@ -79,6 +79,9 @@ struct Gemm {
   static constexpr int TM = BM / 32;  // 16x16 MFMA tiles per wave along M
   static constexpr int TN = BN / 32;
   static constexpr int STAGE = TA::ELEMS + TB::ELEMS;  // elements per LDS stage
+  // global->register prefetch depth: hides HBM latency behind PF-1 tiles of MFMA work
+  static constexpr int CH = TA::PER_THREAD + TB::PER_THREAD;
+  static constexpr int PF = CH <= 4 ? 4 : 3;
 };
 
 template <int BM, int BN, int AM, int BMD>
@@ -136,9 +139,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p) {
     }
   }
 
-  uint4 ra[TA::PER_THREAD], rb[TB::PER_THREAD];
+  // register ring: PF tiles in flight (global -> registers), LDS double buffer
+  constexpr int PF = G::PF;
+  uint4 ra_s[PF][TA::PER_THREAD], rb_s[PF][TB::PER_THREAD];
 
-  auto load_tile = [&](int kt) {
+  auto load_tile = [&](int kt, uint4 (&ra)[TA::PER_THREAD], uint4 (&rb)[TB::PER_THREAD]) {
     const int k0 = kt * BK;
 #pragma unroll
     for (int i = 0; i < TA::PER_THREAD; ++i) {
@@ -196,7 +201,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p) {
     }
   };
 
-  auto store_tile = [&](bf16_t* s) {
+  auto store_tile = [&](bf16_t* s, const uint4 (&ra)[TA::PER_THREAD], const uint4 (&rb)[TB::PER_THREAD]) {
     bf16_t* sa = s;
     bf16_t* sb = s + TA::ELEMS;
 #pragma unroll
@@ -245,43 +250,58 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p) {
     return __builtin_bit_cast(v8bf, r);
   };
 
-  if (nkt > 0) {
-    load_tile(kt_begin);
-    store_tile(smem);
-    __syncthreads();
-    for (int it = 0; it < nkt; ++it) {
-      const bf16_t* s = smem + (it & 1) * G::STAGE;
-      if (it + 1 < nkt) load_tile(kt_begin + it + 1);
-      const bf16_t* sa = s;
-      const bf16_t* sb = s + TA::ELEMS;
-      if (do_bgrad) {
-        // BM columns x BK rows; 256 threads -> 256/BM row-groups
-        constexpr int RG = 256 / BM;
-        const int col = tid % BM, rg = tid / BM;
+  auto compute = [&](const bf16_t* s) {
+    const bf16_t* sa = s;
+    const bf16_t* sb = s + TA::ELEMS;
+    if (do_bgrad) {
+      // BM columns x BK rows; 256 threads -> 256/BM row-groups
+      constexpr int RG = 256 / BM;
+      const int col = tid % BM, rg = tid / BM;
 #pragma unroll 4
-        for (int r = rg * (BK / RG); r < (rg + 1) * (BK / RG); ++r) bsum += bf2f(sa[r * TA::LD + col]);
+      for (int r = rg * (BK / RG); r < (rg + 1) * (BK / RG); ++r) bsum += bf2f(sa[r * TA::LD + col]);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      v8bf af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if constexpr (AKI) af[i] = frag_kinner(sa, wr + 16 * i + l16, kk);
+        else af[i] = frag_kouter(sa, TA::LD, wr + 16 * i, kk);
       }
 #pragma unroll
-      for (int kk = 0; kk < BK / 32; ++kk) {
-        v8bf af[TM], bfr[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          if constexpr (AKI) af[i] = frag_kinner(sa, wr + 16 * i + l16, kk);
-          else af[i] = frag_kouter(sa, TA::LD, wr + 16 * i, kk);
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          if constexpr (BKI) bfr[j] = frag_kinner(sb, wc + 16 * j + l16, kk);
-          else bfr[j] = frag_kouter(sb, TB::LD, wc + 16 * j, kk);
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (BKI) bfr[j] = frag_kinner(sb, wc + 16 * j + l16, kk);
+        else bfr[j] = frag_kouter(sb, TB::LD, wc + 16 * j, kk);
       }
-      if (it + 1 < nkt) store_tile(smem + ((it + 1) & 1) * G::STAGE);
-      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (nkt > 0) {
+    // prologue: PF tiles in flight
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+      if (u < nkt) load_tile(kt_begin + u, ra_s[u], rb_s[u]);
+    store_tile(smem, ra_s[0], rb_s[0]);
+    __syncthreads();
+    // main loop, unrolled by PF so every register stage index is a compile-time constant:
+    // iteration i computes LDS buffer i&1, refills ring slot i%PF with tile i+PF and moves
+    // tile i+1 (slot (i+1)%PF) into the other LDS buffer.
+    for (int base = 0; base < nkt; base += PF) {
+#pragma unroll
+      for (int u = 0; u < PF; ++u) {
+        const int it = base + u;
+        if (it < nkt) {
+          if (it + PF < nkt) load_tile(kt_begin + it + PF, ra_s[u], rb_s[u]);
+          compute(smem + (it & 1) * G::STAGE);
+          if (it + 1 < nkt) store_tile(smem + ((it + 1) & 1) * G::STAGE, ra_s[(u + 1) % PF], rb_s[(u + 1) % PF]);
+          __syncthreads();
+        }
+      }
     }
   }
 
@@ -363,6 +383,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p) {
         *(uint4*)((bf16_t*)p.c + (long)row * p.ldc + col) = pack8(v);
       } else {
         float* cp = p_c_slab + (long)row * p.ldc + col;
+        if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) {
+          const float4 c0 = *(const float4*)cp, c1 = *(const float4*)(cp + 4);
+          v[0] += c0.x; v[1] += c0.y; v[2] += c0.z; v[3] += c0.w;
+          v[4] += c1.x; v[5] += c1.y; v[6] += c1.z; v[7] += c1.w;
+        }
         *(float4*)cp = make_float4(v[0], v[1], v[2], v[3]);
         *(float4*)(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
       }
@@ -375,25 +400,43 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p) {
       float v = p.alpha * sc[r * SLD + cc] + (add_bias ? p.bias[col] : 0.f);
       if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
       if (p.c_mode == ENCDIFF_OUT_BF16) ((bf16_t*)p.c)[(long)row * p.ldc + col] = f2bf(v);
+      else if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) p_c_slab[(long)row * p.ldc + col] += v;
       else p_c_slab[(long)row * p.ldc + col] = v;
     }
   }
 }
 
-// split-K finalize: C = alpha * sum_z slab[z] (+bias)(+resid), slabs summed in a fixed
-// order (bitwise reproducible; no atomics).
+// split-K finalize: C = alpha * sum_z slab[z] (+bias)(+resid).  A workgroup owns 64
+// consecutive outputs; its 4 wave-rows each sum every 4th slab (8 loads in flight per
+// lane), then the 4 partials are added in a fixed order: bitwise reproducible, no atomics,
+// and a deep split (e.g. 128 slabs of a 64x64 weight gradient) stays bandwidth-bound.
+constexpr int FIN_ZG = 4, FIN_OPB = 64;
 __global__ __launch_bounds__(256) void gemm_finalize_kernel(const EncdiffGemmArgs p) {
+  __shared__ float part[FIN_ZG][FIN_OPB];
   const long total = (long)p.M * p.N;
   const bf16_t* R = (const bf16_t*)p.resid;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int row = (int)(i / p.N), col = (int)(i - (long)row * p.N);
+  const int o = threadIdx.x % FIN_OPB, zg = threadIdx.x / FIN_OPB;
+  for (long t0 = (long)blockIdx.x * FIN_OPB; t0 < total; t0 += (long)gridDim.x * FIN_OPB) {
+    const long i = t0 + o;
     float acc = 0.f;
-    for (int z = 0; z < p.split_k; ++z) acc += p.workspace[(long)z * total + i];
-    float v = p.alpha * acc;
-    if (p.bias) v += p.bias[col];
-    if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
-    if (p.c_mode == ENCDIFF_OUT_BF16) ((bf16_t*)p.c)[(long)row * p.ldc + col] = f2bf(v);
-    else ((float*)p.c)[(long)row * p.ldc + col] = v;
+    if (i < total) {
+      const float* w = p.workspace + i;
+#pragma unroll 8
+      for (int z = zg; z < p.split_k; z += FIN_ZG) acc += w[(long)z * total];
+    }
+    part[zg][o] = acc;
+    __syncthreads();
+    if (zg == 0 && i < total) {
+      const float sum = ((part[0][o] + part[1][o]) + part[2][o]) + part[3][o];
+      const int row = (int)(i / p.N), col = (int)(i - (long)row * p.N);
+      float v = p.alpha * sum;
+      if (p.bias) v += p.bias[col];
+      if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
+      if (p.c_mode == ENCDIFF_OUT_BF16) ((bf16_t*)p.c)[(long)row * p.ldc + col] = f2bf(v);
+      else if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) ((float*)p.c)[(long)row * p.ldc + col] += v;
+      else ((float*)p.c)[(long)row * p.ldc + col] = v;
+    }
+    __syncthreads();
   }
 }
 
@@ -439,7 +482,8 @@ extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
   EncdiffGemmArgs p = *pa;
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return ENCDIFF_ERR_SHAPE;
   if (p.split_k < 1) p.split_k = 1;
-  const bool ws_path = p.split_k > 1 && (p.c_mode == ENCDIFF_OUT_BF16 || p.c_mode == ENCDIFF_OUT_F32);
+  const bool ws_path = p.split_k > 1 && (p.c_mode == ENCDIFF_OUT_BF16 || p.c_mode == ENCDIFF_OUT_F32 ||
+                                         p.c_mode == ENCDIFF_OUT_F32_ACCUM);
   if (ws_path && !p.workspace) return ENCDIFF_ERR_ARG;
   const bool k_inner = p.a_mode != ENCDIFF_OPA_ROWM || p.b_mode == ENCDIFF_OPB_ROWK;
   if (k_inner && p.K % 8) return ENCDIFF_ERR_SHAPE;
@@ -466,8 +510,8 @@ extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
   if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
   if (ws_path) {
     long total = (long)user.M * user.N;
-    long g = (total + 255) / 256;
-    if (g > 2048) g = 2048;
+    long g = (total + FIN_OPB - 1) / FIN_OPB;
+    if (g > 8192) g = 8192;
     hipLaunchKernelGGL(gemm_finalize_kernel, dim3((unsigned)g), dim3(256), 0, s, user);
     e = hipGetLastError();
     if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;

@@ -98,8 +98,8 @@ def plan(M, N, K, a_mode, b_mode, c_mode):
     if atomic:
         while nb * split < 256 and K // (split * 2) >= 256 and (split * 2) * M * N * 4 <= (8 << 20):
             split *= 2
-    else:
-        while nb * split < 192 and K // (split * 2) >= 512 and (split * 2) * M * N <= WS_FLOATS:
+    else:  # slab split-K (bf16 / f32 / f32-accumulate outputs)
+        while nb * split < 256 and K // (split * 2) >= 256 and (split * 2) * M * N <= WS_FLOATS:
             split *= 2
     return tile, split
 
@@ -112,7 +112,7 @@ def gemm(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROW
         tile = tile or t
         split_k = split_k or sp
     ws = None
-    if split_k > 1 and c_mode in (L.OUT_BF16, L.OUT_F32):
+    if split_k > 1 and c_mode in (L.OUT_BF16, L.OUT_F32, L.OUT_F32_ACCUM):
         assert split_k * M * N <= WS_FLOATS, "split-K slabs exceed the workspace"
         ws = _workspace()
     args = L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=b_mode, c_mode=c_mode,
@@ -142,11 +142,12 @@ def linear_dgrad(dy, w, dx, resid=None):
 
 
 def linear_wgrad(dy, x, dw, db=None):
-    """dw[N][K] += dy[M][N]^T x[M][K];  db[N] += sum_m dy[m][n]  (fp32 atomics)."""
+    """dw[N][K] += dy[M][N]^T x[M][K] (split-K slabs summed in order: reproducible);
+    db[N] += sum_m dy[m][n] (fp32 atomics)."""
     M, N = dy.shape
     K = x.shape[1]
     gemm(N, K, M, dy, _ld(dy), x, _ld(x), dw, K, a_mode=L.OPA_ROWM, b_mode=L.OPB_ROWN,
-         c_mode=L.OUT_F32_ATOMIC, bias_grad=db)
+         c_mode=L.OUT_F32_ACCUM, bias_grad=db)
 
 
 # ------------------------------------------------------------------ 3x3 convolutions
@@ -177,10 +178,10 @@ def conv3x3_wgrad(dy, x, g: Geom, cin, dw_ref, db=None, resample=L.RESAMPLE_NONE
 
 def conv3x3_wgrad_cl(dy, x, g: Geom, cin, dw_cl, db=None, resample=L.RESAMPLE_NONE):
     """dw_cl[cout][9*cin] (fp32, channels-last [co][kh][kw][ci]) += dy^T im2col(resample(x))
-    (coalesced fp32 atomics)."""
+    (split-K slabs summed in order: reproducible)."""
     cout = dy.shape[1]
     gemm(cout, 9 * cin, g.pixels, dy, _ld(dy), x, _ld(x), dw_cl, _ld(dw_cl), a_mode=L.OPA_ROWM,
-         b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32_ATOMIC, conv=_conv_geom(g, cin, resample, x), bias_grad=db)
+         b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32_ACCUM, conv=_conv_geom(g, cin, resample, x), bias_grad=db)
 
 
 # ------------------------------------------------------------------ normalisation

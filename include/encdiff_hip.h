@@ -56,8 +56,11 @@ enum {
   ENCDIFF_OUT_BF16 = 0,
   ENCDIFF_OUT_F32 = 1,
   ENCDIFF_OUT_F32_ATOMIC = 2,       /* atomicAdd into fp32 C (split-K / grad accumulate)   */
-  ENCDIFF_OUT_F32_ATOMIC_CONVW = 3  /* atomicAdd, column n=(tap,ci) scattered to the reference
+  ENCDIFF_OUT_F32_ATOMIC_CONVW = 3, /* atomicAdd, column n=(tap,ci) scattered to the reference
                                        Conv2d weight layout [co][ci][3][3]                   */
+  ENCDIFF_OUT_F32_ACCUM = 4         /* fp32 C += result, single writer per element (weight
+                                       gradients): with split_k > 1 the slabs are summed in a
+                                       fixed order -> bitwise reproducible                   */
 };
 enum {
   ENCDIFF_RESAMPLE_NONE = 0,
@@ -84,13 +87,13 @@ typedef struct EncdiffGemmArgs {
   int conv_cout;             /* OPB_CONV_DGRAD: forward conv's output channels     */
   int convw_cin;             /* OUT_F32_ATOMIC_CONVW: forward conv's input channels */
   float alpha;
-  int split_k;               /* >= 1; > 1 needs an atomic c_mode                  */
+  int split_k;               /* >= 1; > 1 needs an atomic c_mode or a workspace     */
   const float* bias;         /* [N] fp32 or NULL                                   */
   const void* resid; long ld_resid;  /* bf16 [M][N] or NULL                        */
   float* bias_grad;          /* OPA_ROWM only: += sum_k A[m][k] into bias_grad[m]  */
   int tile;                  /* 0 = auto, else 1:128x128 2:128x64 3:64x128 4:64x64 */
   int pad2_;
-  float* workspace;          /* split_k > 1 with a BF16/F32 c_mode: fp32 scratch of split_k*M*N;
+  float* workspace;          /* split_k > 1 with a BF16/F32/F32_ACCUM c_mode: fp32 scratch of split_k*M*N;
                                 each split writes its own [M][N] slab, a finalize pass sums the
                                 slabs in order (reproducible) and applies alpha/bias/resid    */
 } EncdiffGemmArgs;

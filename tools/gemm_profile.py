@@ -101,16 +101,25 @@ def main():
         if split is not None:
             a2.split_k = split
             a2.workspace = ws.data_ptr() if split > 1 else None
-            if split > 1 and a2.c_mode in (L.OUT_BF16, L.OUT_F32) and split * a2.M * a2.N > ops.WS_FLOATS:
+            if split > 1 and a2.c_mode in (L.OUT_BF16, L.OUT_F32, L.OUT_F32_ACCUM) and split * a2.M * a2.N > ops.WS_FLOATS:
                 return float("inf")
         for _ in range(2):
             rc = orig(C.byref(a2), stream)
             if rc != 0:
                 return float("inf")
+        # GPU time: the reps are captured in a graph (no host launch gaps)
+        gs = torch.cuda.Stream()
+        gs.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=gs):
+            st = C.c_void_p(gs.cuda_stream)
+            for _ in range(args.reps):
+                orig(C.byref(a2), st)
+        g.replay()
+        torch.cuda.synchronize()
         s, f = ev(), ev()
         s.record()
-        for _ in range(args.reps):
-            orig(C.byref(a2), stream)
+        g.replay()
         f.record()
         torch.cuda.synchronize()
         return s.elapsed_time(f) / args.reps * 1e3
@@ -128,8 +137,8 @@ def main():
         cur = timeit(a, a.tile)
         best_t, best_tile, best_split = cur, a.tile, a.split_k
         for tile in (1, 2, 3, 4):
-            for split in (1, 2, 4, 8, 16, 32, 64):
-                if a.K // split < 128 or (split > 1 and a.K // split < 64):
+            for split in (1, 2, 4, 8, 16, 32, 64, 128, 256):
+                if split > 1 and a.K // split < 64:
                     continue
                 tt = timeit(a, tile, split)
                 if tt < best_t:
@@ -142,10 +151,12 @@ def main():
         if key not in table or table[key][2] > best_t:
             table[key] = [best_tile, best_split, best_t]
         rows.append((k, a.M, a.N, a.K, a.split_k, a.tile, cur, f"{best_tile}/{best_split}", best_t))
-    for r in sorted(rows, key=lambda r: -r[6])[:30]:
-        k, M, N, K, s, tile, cur, bt, bb = r
-        print(f"{k:10s} M={M:6d} N={N:5d} K={K:6d} split={s:3d} tile={tile} {cur:8.1f}us -> {bt} {bb:8.1f}us "
-              f"({2 * M * N * K / bb / 1e6:7.1f} TF/s)")
+    for cat_name in sorted(tot_cur):
+        sel = sorted([r for r in rows if r[0] == cat_name], key=lambda r: -r[6])[:8]
+        for r in sel:
+            k, M, N, K, s, tile, cur, bt, bb = r
+            print(f"{k:10s} M={M:6d} N={N:5d} K={K:6d} split={s:3d} tile={tile} {cur:8.1f}us -> {bt} {bb:8.1f}us "
+                  f"({2 * M * N * K / bb / 1e6:7.1f} TF/s)")
     print("category     current_us   best_us   TFLOP/s(best)")
     for k in tot_cur:
         print(f"{k:12s} {tot_cur[k]:9.1f} {tot_best[k]:9.1f} {flops[k] / tot_best[k] / 1e6:8.1f}")
