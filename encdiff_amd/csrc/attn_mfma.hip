@@ -302,26 +302,33 @@ int mfma_hpb(const EncdiffAttnArgs& a) {
 }
 
 template <int DH>
-int launch_mfma(const EncdiffAttnArgs& a, bool bwd, hipStream_t s) {
+int launch_mfma_fwd(const EncdiffAttnArgs& a, hipStream_t s) {
+  constexpr int DP = DH < 16 ? 16 : DH;
+  const int hpb = mfma_hpb(a);
+  const int SKP = (a.sk + 15) & ~15;
+  const int nblk = a.batch * a.heads / hpb;
+  const size_t lds = (size_t)hpb * 2 * SKP * DP * sizeof(bf16_t);
+  if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)attn_fwd_mfma<DH>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)attr;
+  hipLaunchKernelGGL(attn_fwd_mfma<DH>, dim3(nblk), dim3(256), lds, s, a, hpb);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+template <int DH>
+int launch_mfma_bwd(const EncdiffAttnArgs& a, hipStream_t s) {
   constexpr int DP = DH < 16 ? 16 : DH;
   const int hpb = mfma_hpb(a);
   const int SQP = (a.sq + 15) & ~15, SKP = (a.sk + 15) & ~15;
   const int nblk = a.batch * a.heads / hpb;
-  if (!bwd) {
-    const size_t lds = (size_t)hpb * 2 * SKP * DP * sizeof(bf16_t);
-    if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
-    static const hipError_t attr = hipFuncSetAttribute((const void*)attn_fwd_mfma<DH>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)attr;
-    hipLaunchKernelGGL(attn_fwd_mfma<DH>, dim3(nblk), dim3(256), lds, s, a, hpb);
-  } else {
-    const size_t lds = (size_t)hpb * ((4 * SQP + 3 * SKP) * DP * sizeof(bf16_t) + 2 * SQP * sizeof(float));
-    if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
-    static const hipError_t attr = hipFuncSetAttribute((const void*)attn_bwd_mfma<DH>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)attr;
-    hipLaunchKernelGGL(attn_bwd_mfma<DH>, dim3(nblk), dim3(256), lds, s, a, hpb);
-  }
+  const size_t lds = (size_t)hpb * ((4 * SQP + 3 * SKP) * DP * sizeof(bf16_t) + 2 * SQP * sizeof(float));
+  if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)attn_bwd_mfma<DH>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)attr;
+  hipLaunchKernelGGL(attn_bwd_mfma<DH>, dim3(nblk), dim3(256), lds, s, a, hpb);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
@@ -333,9 +340,11 @@ int encdiff_attention_mfma(const EncdiffAttnArgs* a, bool bwd, void* stream) {
   if (a->batch * a->heads % mfma_hpb(*a)) return ENCDIFF_ERR_SHAPE;
   hipStream_t s = (hipStream_t)stream;
   switch (a->dh) {
-    case 8: return launch_mfma<8>(*a, bwd, s);
-    case 16: return launch_mfma<16>(*a, bwd, s);
-    case 32: return launch_mfma<32>(*a, bwd, s);
+    case 8: return bwd ? launch_mfma_bwd<8>(*a, s) : launch_mfma_fwd<8>(*a, s);
+    case 16: return bwd ? launch_mfma_bwd<16>(*a, s) : launch_mfma_fwd<16>(*a, s);
+    case 32: return bwd ? launch_mfma_bwd<32>(*a, s) : launch_mfma_fwd<32>(*a, s);
+    case 128:  // single-head AttnBlock of the VQ encoder (model.py AttnBlock): forward only (frozen)
+      return bwd ? ENCDIFF_ERR_UNSUPPORTED : launch_mfma_fwd<128>(*a, s);
     default: return ENCDIFF_ERR_UNSUPPORTED;
   }
 }

@@ -42,8 +42,14 @@ struct TileShape {
 // implicit im2col: 8 consecutive channels [c, c+8) of tap `tap` at output pixel (b, y, x)
 ED_DEV uint4 im2col8(const bf16_t* __restrict__ src, const EncdiffConvGeom& g, int b, int y, int x,
                      int tap, int c) {
-  const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
   uint4 z = {0u, 0u, 0u, 0u};
+  if (g.resample == ENCDIFF_RESAMPLE_STRIDE2) {  // VQ Downsample: pad (0,1,0,1), k3 s2 p0
+    const int ys = 2 * y + tap / 3, xs = 2 * x + tap % 3;
+    if (ys >= 2 * g.h || xs >= 2 * g.w) return z;
+    const long row = ((long)b * 2 * g.h + ys) * (2 * g.w) + xs;
+    return *(const uint4*)(src + row * g.ld_src + c);
+  }
+  const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
   if (yy < 0 || yy >= g.h || xx < 0 || xx >= g.w) return z;
   if (g.resample == ENCDIFF_RESAMPLE_NONE) {
     const long row = ((long)b * g.h + yy) * g.w + xx;

@@ -88,8 +88,19 @@ class VQModelInterface(VQModel):
     def __init__(self, embed_dim, *args, **kwargs):
         super().__init__(embed_dim=embed_dim, *args, **kwargs)
         self.embed_dim = embed_dim
+        self._hip_encoder = None
+
+    def enable_hip(self):
+        """Route encode() through the HIP executor of the frozen encoder
+        (encdiff_amd/vq.py).  Called by LatentDiffusion when it sets
+        up HIP training; the module itself stays the reference's (state_dict, decode)."""
+        from encdiff_amd.vq import VQEncoderExecutor
+        self._hip_encoder = VQEncoderExecutor(self)
+        return self
 
     def encode(self, x):
+        if self._hip_encoder is not None:
+            return self._hip_encoder.encode(x)
         return self.quant_conv(self.encoder(x))
 
     def decode(self, h, force_not_quantize=False, disentangled_repr=None):

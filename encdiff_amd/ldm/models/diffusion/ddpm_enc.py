@@ -447,6 +447,9 @@ class LatentDiffusion(DDPM):
             if n.startswith("model.diffusion_model."):
                 arena.alias(n[len("model.diffusion_model."):], n)
         unet.bind_arena(arena)
+        fs = self.first_stage_model
+        if hasattr(fs, "enable_hip") and getattr(fs, "_hip_encoder", None) is None:
+            fs.enable_hip()                              # frozen VQ encoder on HIP (§8(f) row 2)
         cs = self.cond_stage_model
         if self.cond_stage_trainable and cs is not None and hasattr(cs, "bind_arena"):
             cs.bind_arena(arena, "cond_stage_model.")   # Encoder4.warp on HIP (§8(f) row 2)

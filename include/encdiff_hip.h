@@ -65,7 +65,9 @@ enum {
 enum {
   ENCDIFF_RESAMPLE_NONE = 0,
   ENCDIFF_RESAMPLE_DOWN2 = 1, /* source is (2h,2w); AvgPool2d(2) on the fly  (openaimodel_enc.py:156) */
-  ENCDIFF_RESAMPLE_UP2 = 2    /* source is (h/2,w/2); nearest x2 on the fly (openaimodel_enc.py:116) */
+  ENCDIFF_RESAMPLE_UP2 = 2,   /* source is (h/2,w/2); nearest x2 on the fly (openaimodel_enc.py:116) */
+  ENCDIFF_RESAMPLE_STRIDE2 = 3 /* source is (2h,2w); 3x3 taps at (2y+ky, 2x+kx), zero pad right/bottom
+                                  only: F.pad(x,(0,1,0,1)) + Conv2d(k3, s2, p0) (model.py Downsample) */
 };
 
 typedef struct EncdiffConvGeom {
