@@ -144,28 +144,41 @@ __global__ __launch_bounds__(256) void ew_kernel(const EncdiffEwArgs p) {
 
 // ------------------------------------------------ 3-channel convolutions (VALU)
 // input conv (cin = 3): x fp32 NCHW -> y bf16 NHWC.  thread per (pixel, co)
+// input conv (cin <= 4, fp32 NCHW) -> bf16 NHWC: thread per output pixel, the cin*9 input
+// taps in registers, all cout outputs accumulated 8 at a time and written as 16-byte vectors.
 __global__ __launch_bounds__(256) void small_conv_in_fwd(const EncdiffSmallConvArgs p) {
-  __shared__ float w[64 * 27 + 64];
-  const int CO = p.cout, CI = p.cin, HW = p.h * p.w;
-  for (int i = threadIdx.x; i < CO * CI * 9; i += 256) w[i] = p.weight[i];
-  for (int i = threadIdx.x; i < CO; i += 256) w[CO * CI * 9 + i] = p.bias[i];
+  __shared__ float w[64 * 36 + 64];
+  const int CO = p.cout, CI = p.cin, HW = p.h * p.w, KW = CI * 9;
+  for (int i = threadIdx.x; i < CO * KW; i += 256) w[i] = p.weight[i];
+  for (int i = threadIdx.x; i < CO; i += 256) w[CO * KW + i] = p.bias[i];
   __syncthreads();
-  const long total = (long)p.batch * HW * CO;
-  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
-    const int co = (int)(idx % CO);
-    const long pix = idx / CO;
+  const long total = (long)p.batch * HW;
+  for (long pix = blockIdx.x * 256L + threadIdx.x; pix < total; pix += (long)gridDim.x * 256) {
     const int b = (int)(pix / HW), rem = (int)(pix - (long)b * HW);
     const int y = rem / p.w, x = rem - y * p.w;
-    float acc = w[CO * CI * 9 + co];
     const float* X = (const float*)p.x + (long)b * CI * HW;
-    for (int ci = 0; ci < CI; ++ci)
+    float in[36];
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci)
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-        if (yy >= 0 && yy < p.h && xx >= 0 && xx < p.w)
-          acc += w[(co * CI + ci) * 9 + t] * X[(long)ci * HW + yy * p.w + xx];
+        in[ci * 9 + t] = (ci < CI && yy >= 0 && yy < p.h && xx >= 0 && xx < p.w) ? X[(long)ci * HW + yy * p.w + xx] : 0.f;
       }
-    ((bf16_t*)p.y)[pix * p.ldy + co] = f2bf(acc);
+    bf16_t* Y = (bf16_t*)p.y + pix * p.ldy;
+    for (int c0 = 0; c0 < CO; c0 += 8) {
+      float acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float* wr = w + (c0 + j) * KW;
+        float a = w[CO * KW + c0 + j];
+#pragma unroll
+        for (int k = 0; k < 36; ++k)
+          if (k < KW) a += wr[k] * in[k];
+        acc[j] = a;
+      }
+      *(uint4*)(Y + c0) = pack8(acc);
+    }
   }
 }
 
@@ -468,8 +481,8 @@ extern "C" int encdiff_small_conv_fwd(const EncdiffSmallConvArgs* a, void* strea
   hipStream_t s = (hipStream_t)stream;
   const long pix = (long)a->batch * a->h * a->w;
   if (a->x_f32 && !a->y_f32) {  // input conv
-    if (a->cout * a->cin * 9 + a->cout > 64 * 27 + 64) return ENCDIFF_ERR_SHAPE;
-    hipLaunchKernelGGL(small_conv_in_fwd, dim3(grid_for(pix * a->cout)), dim3(256), 0, s, *a);
+    if (a->cin > 4 || a->cout > 64 || a->cout % 8 || a->ldy % 8) return ENCDIFF_ERR_SHAPE;
+    hipLaunchKernelGGL(small_conv_in_fwd, dim3(grid_for(pix)), dim3(256), 0, s, *a);
   } else if (!a->x_f32 && a->y_f32) {  // output conv
     if (a->cout > 3 || a->cin > 512 || a->cin % 8) return ENCDIFF_ERR_SHAPE;
     hipLaunchKernelGGL(small_conv_out_fwd, dim3(grid_for(pix)), dim3(256), 0, s, *a);

@@ -39,41 +39,46 @@ struct TileShape {
 };
 
 // ---------------------------------------------------------------------------
-// implicit im2col: 8 consecutive channels [c, c+8) of tap `tap` at output pixel (b, y, x)
-ED_DEV uint4 im2col8(const bf16_t* __restrict__ src, const EncdiffConvGeom& g, int b, int y, int x,
-                     int tap, int c) {
-  uint4 z = {0u, 0u, 0u, 0u};
-  if (g.resample == ENCDIFF_RESAMPLE_STRIDE2) {  // VQ Downsample: pad (0,1,0,1), k3 s2 p0
-    const int ys = 2 * y + tap / 3, xs = 2 * x + tap % 3;
-    if (ys >= 2 * g.h || xs >= 2 * g.w) return z;
-    const long row = ((long)b * 2 * g.h + ys) * (2 * g.w) + xs;
-    return *(const uint4*)(src + row * g.ld_src + c);
+// Exact division by a launch constant without a divider: n / d == (n * mul) >> 40 for
+// n * d < 2^40 (pixels < 2^24, divisors < 2^16 here); mul = 2^40 / d + 1 from the host.
+struct FDiv {
+  unsigned long long mul;
+  uint32_t d, pad_;
+};
+ED_DEV uint32_t fdiv(uint32_t n, const FDiv& f) { return (uint32_t)(((unsigned long long)n * f.mul) >> 40); }
+
+struct GemmAux {
+  FDiv cin;   // A/B im2col: k (or n) -> (tap, channel)
+  FDiv cout;  // B_CONVD: k -> (tap, co)
+  FDiv hw;    // pixel -> (image, in-image index)
+  FDiv w;     // in-image index -> (y, x)
+};
+
+// Implicit im2col, branch-free.  The launch's resample mode is folded into uniform
+// constants once per thread; per chunk the source pixel of output pixel (b, y, x) and
+// 3x3 tap (ty, tx) is  ys = sy*y + ty + oy  (limits lh x lw), then >> sh (nearest-up
+// source), row = (b*hs + ys)*ws + xs.  Padding gives ok = false and row 0: the load is
+// still issued (and masked when written to LDS), so no branch or early wait is needed.
+struct Im2colMode {
+  int sy, oy, lh, lw, sh, hs, ws;
+  ED_DEV Im2colMode(const EncdiffConvGeom& g) {
+    const bool s2 = g.resample == ENCDIFF_RESAMPLE_STRIDE2;  // VQ Downsample: pad (0,1,0,1), k3 s2 p0
+    const bool up = g.resample == ENCDIFF_RESAMPLE_UP2;      // nearest x2 (openaimodel_enc.py:116)
+    sy = s2 ? 2 : 1;
+    oy = s2 ? 0 : -1;
+    lh = s2 ? 2 * g.h : g.h;
+    lw = s2 ? 2 * g.w : g.w;
+    sh = up ? 1 : 0;
+    hs = lh >> sh;
+    ws = lw >> sh;
   }
-  const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
-  if (yy < 0 || yy >= g.h || xx < 0 || xx >= g.w) return z;
-  if (g.resample == ENCDIFF_RESAMPLE_NONE) {
-    const long row = ((long)b * g.h + yy) * g.w + xx;
-    return *(const uint4*)(src + row * g.ld_src + c);
-  } else if (g.resample == ENCDIFF_RESAMPLE_DOWN2) {
-    const int W2 = 2 * g.w;
-    const long r0 = ((long)b * 2 * g.h + 2 * yy) * W2 + 2 * xx;
-    float a[8], t[8];
-    unpack8(*(const uint4*)(src + r0 * g.ld_src + c), a);
-    unpack8(*(const uint4*)(src + (r0 + 1) * g.ld_src + c), t);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] += t[i];
-    unpack8(*(const uint4*)(src + (r0 + W2) * g.ld_src + c), t);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] += t[i];
-    unpack8(*(const uint4*)(src + (r0 + W2 + 1) * g.ld_src + c), t);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] = (a[i] + t[i]) * 0.25f;
-    return pack8(a);
-  } else {
-    const int Hh = g.h >> 1, Wh = g.w >> 1;
-    const long row = ((long)b * Hh + (yy >> 1)) * Wh + (xx >> 1);
-    return *(const uint4*)(src + row * g.ld_src + c);
-  }
+};
+
+ED_DEV uint32_t im2col_row(const Im2colMode& md, uint32_t b, int y, int x, int ty, int tx, bool& ok) {
+  const int ys = md.sy * y + ty + md.oy, xs = md.sy * x + tx + md.oy;
+  ok = (unsigned)ys < (unsigned)md.lh && (unsigned)xs < (unsigned)md.lw;
+  const uint32_t row = (b * (uint32_t)md.hs + (uint32_t)(ys >> md.sh)) * (uint32_t)md.ws + (uint32_t)(xs >> md.sh);
+  return ok ? row : 0u;
 }
 
 template <int BM, int BN, int AM, int BMD>
@@ -91,7 +96,7 @@ struct Gemm {
 };
 
 template <int BM, int BN, int AM, int BMD>
-__global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p) {
+__global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, const GemmAux aux) {
   using G = Gemm<BM, BN, AM, BMD>;
   using TA = typename G::TA;
   using TB = typename G::TB;
@@ -118,114 +123,142 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p) {
   const bf16_t* __restrict__ A = (const bf16_t*)p.a;
   const bf16_t* __restrict__ B = (const bf16_t*)p.b;
 
-  // ---- per-thread fixed coordinates for the gathers ---------------------
-  // A k-inner: row = c>>3 fixed per chunk; IM2COL needs pixel coords of that row
-  int a_pb[TA::PER_THREAD], a_py[TA::PER_THREAD], a_px[TA::PER_THREAD];
+  // ---- per-thread fixed coordinates of the gathers (K-loop invariant) ------
+  // A im2col (k-inner): the chunk's row = one output pixel (b, y, x)
+  uint32_t a_b[TA::PER_THREAD];
+  int a_y[TA::PER_THREAD], a_x[TA::PER_THREAD];
+  bool a_in[TA::PER_THREAD];
   if constexpr (AM == A_IM2COL) {
 #pragma unroll
     for (int i = 0; i < TA::PER_THREAD; ++i) {
       const int c = tid + 256 * i;
-      const int m = m0 + (c >> 3);
-      const int hw = p.conv.h * p.conv.w;
-      const int b = m / hw, r = m - b * hw;
-      a_pb[i] = (m < p.M) ? b : -1;
-      a_py[i] = r / p.conv.w;
-      a_px[i] = r - a_py[i] * p.conv.w;
+      const uint32_t m = (uint32_t)(m0 + (c >> 3));
+      a_in[i] = m < (uint32_t)p.M;
+      const uint32_t mm = a_in[i] ? m : 0u;
+      a_b[i] = fdiv(mm, aux.hw);
+      const uint32_t r = mm - a_b[i] * (uint32_t)(p.conv.h * p.conv.w);
+      a_y[i] = (int)fdiv(r, aux.w);
+      a_x[i] = (int)(r - (uint32_t)a_y[i] * (uint32_t)p.conv.w);
     }
   }
-  // B k-outer IM2COL: column n = (tap, ci) fixed per chunk
-  int b_tap[TB::PER_THREAD], b_ci[TB::PER_THREAD];
+  // B im2col (k-outer, wgrad): the chunk's column n = (tap, ci) is fixed
+  int b_ty[TB::PER_THREAD], b_tx[TB::PER_THREAD], b_ci[TB::PER_THREAD];
   if constexpr (BMD == B_IM2COL) {
 #pragma unroll
     for (int i = 0; i < TB::PER_THREAD; ++i) {
       const int c = tid + 256 * i;
-      const int n = n0 + (c % (BN / 8)) * 8;
-      b_tap[i] = n / p.conv.cin;
-      b_ci[i] = n - b_tap[i] * p.conv.cin;
+      const uint32_t n = (uint32_t)(n0 + (c % (BN / 8)) * 8);
+      const uint32_t tap = fdiv(n, aux.cin);
+      b_ci[i] = (int)(n - tap * (uint32_t)p.conv.cin);
+      b_ty[i] = (int)((tap * 11u) >> 5);  // tap / 3 for tap < 9
+      b_tx[i] = (int)tap - 3 * b_ty[i];
     }
   }
 
-  // register ring: PF tiles in flight (global -> registers), LDS double buffer
+  const Im2colMode md(p.conv);
+
+  // register ring: PF tiles in flight (global -> registers), LDS double buffer.  Every
+  // global load is unconditional (out-of-range / padding chunks load a valid address and
+  // are zeroed when written to LDS), so hipcc keeps counted vmcnt waits and the PF-1
+  // younger tiles stay in flight.
   constexpr int PF = G::PF;
   uint4 ra_s[PF][TA::PER_THREAD], rb_s[PF][TB::PER_THREAD];
+  uint32_t am_s[PF], bm_s[PF];  // per-chunk validity bits of each ring slot
 
-  auto load_tile = [&](int kt, uint4 (&ra)[TA::PER_THREAD], uint4 (&rb)[TB::PER_THREAD]) {
+  auto load_tile = [&](int kt, uint4 (&ra)[TA::PER_THREAD], uint4 (&rb)[TB::PER_THREAD], uint32_t& amask,
+                       uint32_t& bmask) {
     const int k0 = kt * BK;
+    amask = 0u;
+    bmask = 0u;
 #pragma unroll
     for (int i = 0; i < TA::PER_THREAD; ++i) {
       const int c = tid + 256 * i;
-      uint4 v = {0u, 0u, 0u, 0u};
+      bool ok;
+      size_t off;
       if constexpr (AKI) {
-        const int row = c >> 3;
         const int k = k0 + (c & 7) * 8;
-        const int m = m0 + row;
         if constexpr (AM == A_ROWK) {
-          if (m < p.M && k < p.K) v = *(const uint4*)(A + (long)m * p.lda + k);
+          const int m = m0 + (c >> 3);
+          ok = m < p.M && k < p.K;
+          off = (size_t)(ok ? m : 0) * p.lda + (ok ? k : 0);
         } else {  // IM2COL
-          if (a_pb[i] >= 0 && k < p.K) {
-            const int tap = k / p.conv.cin;
-            v = im2col8(A, p.conv, a_pb[i], a_py[i], a_px[i], tap, k - tap * p.conv.cin);
-          }
+          const uint32_t kk = k < p.K ? (uint32_t)k : 0u;
+          const uint32_t tap = fdiv(kk, aux.cin);
+          const uint32_t ch = kk - tap * (uint32_t)p.conv.cin;
+          const int ty = (int)((tap * 11u) >> 5), tx = (int)tap - 3 * ty;
+          bool inb;
+          const uint32_t row = im2col_row(md, a_b[i], a_y[i], a_x[i], ty, tx, inb);
+          ok = a_in[i] && k < p.K && inb;
+          off = (size_t)(ok ? row : 0u) * p.conv.ld_src + (ok ? ch : 0u);
         }
       } else {  // A_ROWM: tile [BK][BM]
-        const int row = c / (BM / 8);
-        const int col = (c % (BM / 8)) * 8;
-        const int k = k0 + row, m = m0 + col;
-        if (k < p.K && m < p.M) v = *(const uint4*)(A + (long)k * p.lda + m);
+        const int k = k0 + c / (BM / 8), m = m0 + (c % (BM / 8)) * 8;
+        ok = k < p.K && m < p.M;
+        off = (size_t)(ok ? k : 0) * p.lda + (ok ? m : 0);
       }
-      ra[i] = v;
+      ra[i] = *(const uint4*)(A + off);
+      amask |= (ok ? 1u : 0u) << i;
     }
 #pragma unroll
     for (int i = 0; i < TB::PER_THREAD; ++i) {
       const int c = tid + 256 * i;
-      uint4 v = {0u, 0u, 0u, 0u};
+      bool ok;
+      size_t off;
       if constexpr (BKI) {  // B_ROWK: Bt[n][k]
-        const int row = c >> 3;
-        const int k = k0 + (c & 7) * 8;
-        const int n = n0 + row;
-        if (n < p.N && k < p.K) v = *(const uint4*)(B + (long)n * p.ldb + k);
+        const int n = n0 + (c >> 3), k = k0 + (c & 7) * 8;
+        ok = n < p.N && k < p.K;
+        off = (size_t)(ok ? n : 0) * p.ldb + (ok ? k : 0);
       } else {
-        const int row = c / (BN / 8);
-        const int col = (c % (BN / 8)) * 8;
-        const int k = k0 + row, n = n0 + col;
-        if (k < p.K && n < p.N) {
-          if constexpr (BMD == B_ROWN) {
-            v = *(const uint4*)(B + (long)k * p.ldb + n);
-          } else if constexpr (BMD == B_CONVD) {
-            const int tap = k / p.conv_cout;
-            const int co = k - tap * p.conv_cout;
-            v = *(const uint4*)(B + (long)co * p.ldb + (long)(8 - tap) * p.N + n);
-          } else {  // B_IM2COL: row = pixel k
-            const int hw = p.conv.h * p.conv.w;
-            const int b = k / hw, r = k - b * hw;
-            const int y = r / p.conv.w, x = r - y * p.conv.w;
-            v = im2col8(B, p.conv, b, y, x, b_tap[i], b_ci[i]);
-          }
+        const int k = k0 + c / (BN / 8), n = n0 + (c % (BN / 8)) * 8;
+        const bool kn = k < p.K && n < p.N;
+        if constexpr (BMD == B_ROWN) {
+          ok = kn;
+          off = (size_t)(ok ? k : 0) * p.ldb + (ok ? n : 0);
+        } else if constexpr (BMD == B_CONVD) {
+          const uint32_t kk = kn ? (uint32_t)k : 0u;
+          const uint32_t tap = fdiv(kk, aux.cout);
+          const uint32_t co = kk - tap * (uint32_t)p.conv_cout;
+          ok = kn;
+          off = (size_t)co * p.ldb + (size_t)(8 - tap) * p.N + (ok ? n : 0);
+        } else {  // B_IM2COL: row = output pixel k
+          const uint32_t kk = kn ? (uint32_t)k : 0u;
+          const uint32_t b = fdiv(kk, aux.hw);
+          const uint32_t r = kk - b * (uint32_t)(p.conv.h * p.conv.w);
+          const int y = (int)fdiv(r, aux.w), x = (int)(r - (uint32_t)y * (uint32_t)p.conv.w);
+          bool inb;
+          const uint32_t row = im2col_row(md, b, y, x, b_ty[i], b_tx[i], inb);
+          ok = kn && inb;
+          off = (size_t)(ok ? row : 0u) * p.conv.ld_src + (ok ? (uint32_t)b_ci[i] : 0u);
         }
       }
-      rb[i] = v;
+      rb[i] = *(const uint4*)(B + off);
+      bmask |= (ok ? 1u : 0u) << i;
     }
   };
 
-  auto store_tile = [&](bf16_t* s, const uint4 (&ra)[TA::PER_THREAD], const uint4 (&rb)[TB::PER_THREAD]) {
+  auto store_tile = [&](bf16_t* s, const uint4 (&ra)[TA::PER_THREAD], const uint4 (&rb)[TB::PER_THREAD],
+                        uint32_t amask, uint32_t bmask) {
+    const uint4 z = {0u, 0u, 0u, 0u};
     bf16_t* sa = s;
     bf16_t* sb = s + TA::ELEMS;
 #pragma unroll
     for (int i = 0; i < TA::PER_THREAD; ++i) {
       const int c = tid + 256 * i;
+      const uint4 v = ((amask >> i) & 1u) ? ra[i] : z;
       if constexpr (AKI) {
-        *(uint4*)(sa + (c >> 3) * TA::LD + (c & 7) * 8) = ra[i];
+        *(uint4*)(sa + (c >> 3) * TA::LD + (c & 7) * 8) = v;
       } else {
-        *(uint4*)(sa + (c / (BM / 8)) * TA::LD + (c % (BM / 8)) * 8) = ra[i];
+        *(uint4*)(sa + (c / (BM / 8)) * TA::LD + (c % (BM / 8)) * 8) = v;
       }
     }
 #pragma unroll
     for (int i = 0; i < TB::PER_THREAD; ++i) {
       const int c = tid + 256 * i;
+      const uint4 v = ((bmask >> i) & 1u) ? rb[i] : z;
       if constexpr (BKI) {
-        *(uint4*)(sb + (c >> 3) * TB::LD + (c & 7) * 8) = rb[i];
+        *(uint4*)(sb + (c >> 3) * TB::LD + (c & 7) * 8) = v;
       } else {
-        *(uint4*)(sb + (c / (BN / 8)) * TB::LD + (c % (BN / 8)) * 8) = rb[i];
+        *(uint4*)(sb + (c / (BN / 8)) * TB::LD + (c % (BN / 8)) * 8) = v;
       }
     }
   };
@@ -291,8 +324,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p) {
     // prologue: PF tiles in flight
 #pragma unroll
     for (int u = 0; u < PF; ++u)
-      if (u < nkt) load_tile(kt_begin + u, ra_s[u], rb_s[u]);
-    store_tile(smem, ra_s[0], rb_s[0]);
+      if (u < nkt) load_tile(kt_begin + u, ra_s[u], rb_s[u], am_s[u], bm_s[u]);
+    store_tile(smem, ra_s[0], rb_s[0], am_s[0], bm_s[0]);
     __syncthreads();
     // main loop, unrolled by PF so every register stage index is a compile-time constant:
     // iteration i computes LDS buffer i&1, refills ring slot i%PF with tile i+PF and moves
@@ -302,9 +335,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p) {
       for (int u = 0; u < PF; ++u) {
         const int it = base + u;
         if (it < nkt) {
-          if (it + PF < nkt) load_tile(kt_begin + it + PF, ra_s[u], rb_s[u]);
+          if (it + PF < nkt) load_tile(kt_begin + it + PF, ra_s[u], rb_s[u], am_s[u], bm_s[u]);
           compute(smem + (it & 1) * G::STAGE);
-          if (it + 1 < nkt) store_tile(smem + ((it + 1) & 1) * G::STAGE, ra_s[(u + 1) % PF], rb_s[(u + 1) % PF]);
+          if (it + 1 < nkt)
+            store_tile(smem + ((it + 1) & 1) * G::STAGE, ra_s[(u + 1) % PF], rb_s[(u + 1) % PF], am_s[(u + 1) % PF],
+                       bm_s[(u + 1) % PF]);
           __syncthreads();
         }
       }
@@ -447,7 +482,7 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const EncdiffGemmArg
 }
 
 template <int BM, int BN, int AM, int BMD>
-hipError_t launch_t(const EncdiffGemmArgs& p, hipStream_t s) {
+hipError_t launch_t(const EncdiffGemmArgs& p, const GemmAux& aux, hipStream_t s) {
   using G = Gemm<BM, BN, AM, BMD>;
   const size_t lds = 2 * G::STAGE * sizeof(bf16_t);
   // dynamic LDS above 64 KiB must be opted in once per instantiation (thread-safe static init)
@@ -455,18 +490,26 @@ hipError_t launch_t(const EncdiffGemmArgs& p, hipStream_t s) {
       (const void*)gemm_kernel<BM, BN, AM, BMD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr_ok != hipSuccess) return attr_ok;
   dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, p.split_k);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, AM, BMD>), grid, dim3(256), lds, s, p);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, AM, BMD>), grid, dim3(256), lds, s, p, aux);
   return hipGetLastError();
 }
 
 template <int AM, int BMD>
-hipError_t launch_modes(const EncdiffGemmArgs& p, int tile, hipStream_t s) {
+hipError_t launch_modes(const EncdiffGemmArgs& p, const GemmAux& aux, int tile, hipStream_t s) {
   switch (tile) {
-    case 1: return launch_t<128, 128, AM, BMD>(p, s);
-    case 2: return launch_t<128, 64, AM, BMD>(p, s);
-    case 3: return launch_t<64, 128, AM, BMD>(p, s);
-    default: return launch_t<64, 64, AM, BMD>(p, s);
+    case 1: return launch_t<128, 128, AM, BMD>(p, aux, s);
+    case 2: return launch_t<128, 64, AM, BMD>(p, aux, s);
+    case 3: return launch_t<64, 128, AM, BMD>(p, aux, s);
+    default: return launch_t<64, 64, AM, BMD>(p, aux, s);
   }
+}
+
+FDiv make_fdiv(int d) {
+  FDiv f;
+  f.d = d > 0 ? (uint32_t)d : 1u;
+  f.mul = (1ull << 40) / f.d + 1;
+  f.pad_ = 0;
+  return f;
 }
 
 int pick_tile(const EncdiffGemmArgs& p) {
@@ -495,7 +538,13 @@ extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
   if (k_inner && p.K % 8) return ENCDIFF_ERR_SHAPE;
   if (p.a_mode == ENCDIFF_OPA_ROWM && p.M % 8) return ENCDIFF_ERR_SHAPE;
   if (p.b_mode != ENCDIFF_OPB_ROWK && p.N % 8) return ENCDIFF_ERR_SHAPE;
-  if ((p.a_mode == ENCDIFF_OPA_IM2COL || p.b_mode == ENCDIFF_OPB_IM2COL) && (p.conv.cin % 8)) return ENCDIFF_ERR_SHAPE;
+  const bool im2col = p.a_mode == ENCDIFF_OPA_IM2COL || p.b_mode == ENCDIFF_OPB_IM2COL;
+  if (im2col && (p.conv.cin % 8)) return ENCDIFF_ERR_SHAPE;
+  // exact fdiv range (pixel indices < 2^24, divisors < 2^16) and single-load im2col modes
+  if (im2col && ((long)p.conv.batch * p.conv.h * p.conv.w >= (1L << 24) || p.conv.h * p.conv.w >= (1 << 16)))
+    return ENCDIFF_ERR_SHAPE;
+  if (im2col && p.conv.resample == ENCDIFF_RESAMPLE_DOWN2) return ENCDIFF_ERR_UNSUPPORTED;
+  if (p.K >= (1 << 24)) return ENCDIFF_ERR_SHAPE;
   if (p.bias_grad && p.a_mode != ENCDIFF_OPA_ROWM) return ENCDIFF_ERR_ARG;
   const int tile = p.tile ? p.tile : pick_tile(p);
   hipStream_t s = (hipStream_t)stream;
@@ -506,12 +555,18 @@ extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
     p.c = p.workspace; p.ldc = p.N; p.c_mode = ENCDIFF_OUT_F32; p.alpha = 1.f;
     p.bias = nullptr; p.resid = nullptr;
   }
-  if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_ROWK, B_ROWK>(p, tile, s);
-  else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_IM2COL, B_ROWK>(p, tile, s);
-  else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWK, B_ROWN>(p, tile, s);
-  else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_CONV_DGRAD) e = launch_modes<A_IM2COL, B_CONVD>(p, tile, s);
-  else if (am == ENCDIFF_OPA_ROWM && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWM, B_ROWN>(p, tile, s);
-  else if (am == ENCDIFF_OPA_ROWM && bm == ENCDIFF_OPB_IM2COL) e = launch_modes<A_ROWM, B_IM2COL>(p, tile, s);
+  GemmAux aux;
+  aux.cin = make_fdiv(p.conv.cin);
+  aux.cout = make_fdiv(p.conv_cout);
+  aux.hw = make_fdiv(p.conv.h * p.conv.w);
+  aux.w = make_fdiv(p.conv.w);
+  if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_ROWK, B_ROWK>(p, aux, tile, s);
+  else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_IM2COL, B_ROWK>(p, aux, tile, s);
+  else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWK, B_ROWN>(p, aux, tile, s);
+  else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_CONV_DGRAD)
+    e = launch_modes<A_IM2COL, B_CONVD>(p, aux, tile, s);
+  else if (am == ENCDIFF_OPA_ROWM && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWM, B_ROWN>(p, aux, tile, s);
+  else if (am == ENCDIFF_OPA_ROWM && bm == ENCDIFF_OPB_IM2COL) e = launch_modes<A_ROWM, B_IM2COL>(p, aux, tile, s);
   else return ENCDIFF_ERR_UNSUPPORTED;
   if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
   if (ws_path) {

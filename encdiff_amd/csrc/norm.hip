@@ -12,7 +12,8 @@
 namespace {
 
 constexpr int GN_THREADS = 256;
-constexpr int GN_TILE = 1024;  // 16-byte vectors of a slice kept in LDS (16 KB per operand)
+constexpr int GN_TILE = 1024;      // backward: 16-byte vectors of a slice kept in LDS per operand (16 KB)
+constexpr int GN_TILE_FWD = 6144;  // forward: dynamic LDS tile up to 96 KB (the VQ encoder's 64x64 levels)
 
 // A workgroup owns (image b, channel slice [c0, c0 + cs)); cs is a multiple of 8 and of
 // channels-per-group, so every group lies inside one slice and the slices are independent.
@@ -25,7 +26,7 @@ constexpr int GN_TILE = 1024;  // 16-byte vectors of a slice kept in LDS (16 KB 
 struct GnSlice {
   int S, b, c0, cs, nvc, np, tv, tp, cpg, gs, g0, cb;
   bool active, tiled;
-  ED_DEV GnSlice(const EncdiffGroupNormArgs& p, int cs_) {
+  ED_DEV GnSlice(const EncdiffGroupNormArgs& p, int cs_, int tile_cap = GN_TILE) {
     cs = cs_;
     S = p.c / cs;
     b = blockIdx.x / S;
@@ -39,7 +40,7 @@ struct GnSlice {
     gs = cs / cpg;
     g0 = c0 / cpg;
     cb = c0 + tv * 8;
-    tiled = nvc * p.hw <= GN_TILE;
+    tiled = nvc * p.hw <= tile_cap;
   }
 };
 
@@ -108,10 +109,10 @@ ED_DEV void gn_stream_in(const GnSlice& L, uint4* tile, const bf16_t* X, long ld
   }
 }
 
-__global__ __launch_bounds__(GN_THREADS) void gn_fwd_kernel(const EncdiffGroupNormArgs p, int cs) {
-  __shared__ uint4 tile[GN_TILE];
+__global__ __launch_bounds__(GN_THREADS) void gn_fwd_kernel(const EncdiffGroupNormArgs p, int cs, int tile_cap) {
+  extern __shared__ uint4 tile[];  // tile_cap vectors (0: untiled, re-read from L2/HBM)
   __shared__ float red[2048], chs[512], gsh[2 * 64];
-  const GnSlice L(p, cs);
+  const GnSlice L(p, cs, tile_cap);
   const int HW = p.hw;
   const float inv_n = 1.f / ((float)HW * L.cpg);
   const bf16_t* X = (const bf16_t*)p.x + (long)L.b * HW * p.ldx + L.cb;
@@ -397,7 +398,13 @@ extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream
   if (!a || !a->x || !a->y || !a->stats || !a->gamma || !a->beta) return ENCDIFF_ERR_ARG;
   const int cs = gn_check(a);
   if (cs < 0) return cs;
-  hipLaunchKernelGGL(gn_fwd_kernel, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream, *a, cs);
+  const long need = (long)(cs / 8) * a->hw;  // 16-byte vectors of one slice
+  const int cap = need <= GN_TILE_FWD ? (int)need : 0;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)gn_fwd_kernel,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+  (void)attr;
+  hipLaunchKernelGGL(gn_fwd_kernel, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), (size_t)cap * 16,
+                     (hipStream_t)stream, *a, cs, cap);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }

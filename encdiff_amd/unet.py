@@ -340,6 +340,8 @@ class UNetExecutor:
                  out=t(Mo, r.cout), d_a2=t(Mo, r.cout), d_h1=t(Mo, r.cout), d_in=t(Mi, r.cin), d_a1=t(Mi, r.cin))
         if r.updown:
             d["d_a1r"] = t(Mo, r.cin)
+        if r.updown == L.RESAMPLE_DOWN2:
+            d["a1r"] = t(Mo, r.cin)  # AvgPool2d(2) of the GN1 output (the conv's input)
         if r.updown and r.cin == r.cout:
             d["xr"] = t(Mo, r.cout)
         return d
@@ -413,8 +415,9 @@ class UNetExecutor:
         gi, go = Geom(B, r.hin, r.hin), Geom(B, r.hout, r.hout)
         ops.groupnorm_fwd(x, gi, self.P(r.prefix + "in_layers.0.weight"), self.P(r.prefix + "in_layers.0.bias"),
                           S["a1"], S["st1"], GN_EPS, True)
-        ops.conv3x3_fwd(S["a1"], go, r.cin, self.W(r.prefix + "in_layers.2.weight"), S["h1"],
-                        bias=self.P(r.prefix + "in_layers.2.bias"), resample=r.updown)
+        a1, rs = self._conv1_input(r, S, go)
+        ops.conv3x3_fwd(a1, go, r.cin, self.W(r.prefix + "in_layers.2.weight"), S["h1"],
+                        bias=self.P(r.prefix + "in_layers.2.bias"), resample=rs)
         film = self.E[:, r.film_off:]
         ops.groupnorm_fwd(S["h1"], go, self.P(r.prefix + "out_layers.0.weight"), self.P(r.prefix + "out_layers.0.bias"),
                           S["a2"], S["st2"], GN_EPS, True, film=film, ld_film=self.E.shape[1])
@@ -432,6 +435,16 @@ class UNetExecutor:
         ops.conv3x3_fwd(S["a2"], go, r.cout, self.W(r.prefix + "out_layers.3.weight"), out,
                         bias=self.P(r.prefix + "out_layers.3.bias"), resid=resid)
         return out
+
+    @staticmethod
+    def _conv1_input(r: ResSpec, S, go: Geom):
+        """in_layers conv input: the GN1 output, avg-pooled first for a down block
+        (openaimodel_enc.py:256-261: in_rest -> h_upd -> in_conv) -- the pooled copy is
+        kept for the weight gradient; nearest-up is read through the im2col gather."""
+        if r.updown == L.RESAMPLE_DOWN2:
+            ops.resample(S["a1"], S["a1r"], go, L.RESAMPLE_DOWN2)
+            return S["a1r"], L.RESAMPLE_NONE
+        return S["a1"], r.updown
 
     def _st_fwd(self, s: STSpec, x):
         """attention.py:250-261 (+ BasicTransformerBlock :211-215)."""
@@ -563,8 +576,12 @@ class UNetExecutor:
                           ld_film=self.E.shape[1], dfilm=self.dE[:, r.film_off:], ld_dfilm=self.dE.shape[1],
                           ld_part=self.gn.ld)
         # conv1 (on the resampled GN1 output)
-        self.conv_wgrad(S["d_h1"], S["a1"], go, r.cin, pre + "in_layers.2.weight", self.G(pre + "in_layers.2.bias"),
-                        resample=r.updown)
+        if r.updown == L.RESAMPLE_DOWN2:
+            a1, rs = S["a1r"], L.RESAMPLE_NONE
+        else:
+            a1, rs = S["a1"], r.updown
+        self.conv_wgrad(S["d_h1"], a1, go, r.cin, pre + "in_layers.2.weight", self.G(pre + "in_layers.2.bias"),
+                        resample=rs)
         dg, db = self.gn.parts(pre + "in_layers.0.weight", r.cin)
         if r.updown:
             ops.conv3x3_dgrad(S["d_h1"], go, self.W(pre + "in_layers.2.weight"), S["d_a1r"])

@@ -93,14 +93,26 @@ def test_linear_strided_views(O):
     assert outbuf[:, :C].abs().max().item() == 0
 
 
+def test_conv3x3_down2_is_rejected(O):
+    """AvgPool2d-then-conv is pooled by the executor (one resample launch), not in the GEMM gather."""
+    import encdiff_amd._lib as L
+    from encdiff_amd.ops import Geom
+    g = Geom(2, 8, 8)
+    x = bf(2 * 16 * 16, 64)
+    wf = bf(64, 9 * 64)
+    out = torch.empty(g.pixels, 64, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(L.HipError):
+        O.conv3x3_fwd(x, g, 64, wf, out, resample=L.RESAMPLE_DOWN2)
+
+
 @pytest.mark.parametrize("B,H,cin,cout,mode", [(4, 16, 64, 64, 0), (2, 16, 192, 64, 0), (3, 8, 128, 256, 0),
-                                               (2, 8, 64, 64, 1), (2, 8, 256, 256, 2), (8, 2, 256, 256, 0),
-                                               (2, 4, 512, 256, 0)])
+                                               (2, 8, 32, 32, 3), (2, 8, 256, 256, 2), (8, 2, 256, 256, 0),
+                                               (2, 4, 512, 256, 0), (2, 32, 64, 32, 3)])
 def test_conv3x3(O, B, H, cin, cout, mode):
     from encdiff_amd.ops import Geom
     torch.manual_seed(2)
     g = Geom(B, H, H)
-    src_h = 2 * H if mode == 1 else (H // 2 if mode == 2 else H)
+    src_h = 2 * H if mode in (1, 3) else (H // 2 if mode == 2 else H)
     gs = Geom(B, src_h, src_h)
     x = bf(gs.pixels, cin)
     wt = torch.randn(cout, cin, 3, 3, device=dev) / math.sqrt(9 * cin)
@@ -117,6 +129,10 @@ def test_conv3x3(O, B, H, cin, cout, mode):
     xin = xin.to(torch.bfloat16).float() if mode == 1 else xin
     xin.requires_grad_(True)
     wq.requires_grad_(True)
+    if mode == 3:  # VQ Downsample: F.pad(0,1,0,1) + conv k3 s2 p0 (forward only: the VQ encoder is frozen)
+        ref = F.conv2d(F.pad(xin, (0, 1, 0, 1)), wq, bias, stride=2)
+        assert rel(nhwc(out, g), ref) < 1e-2
+        return
     ref = F.conv2d(xin, wq, bias, padding=1)
     assert rel(nhwc(out, g), ref) < 1e-2
     dy = bf(g.pixels, cout)
