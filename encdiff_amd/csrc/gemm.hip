@@ -19,8 +19,6 @@
 namespace {
 
 constexpr int BK = 64;
-constexpr int PADK = 8;   // k-inner tile row = BK + PADK elements (144 B: ds_read_b128 conflict-free)
-constexpr int PADN = 8;   // k-outer tile row = COLS + PADN elements
 
 enum { A_ROWK = ENCDIFF_OPA_ROWK, A_IM2COL = ENCDIFF_OPA_IM2COL, A_ROWM = ENCDIFF_OPA_ROWM };
 enum { B_ROWK = ENCDIFF_OPB_ROWK, B_ROWN = ENCDIFF_OPB_ROWN, B_CONVD = ENCDIFF_OPB_CONV_DGRAD,
@@ -29,14 +27,24 @@ enum { B_ROWK = ENCDIFF_OPB_ROWK, B_ROWN = ENCDIFF_OPB_ROWN, B_CONVD = ENCDIFF_O
 template <int AM> struct AKInner { static constexpr bool v = AM != A_ROWM; };
 template <int BMd> struct BKInner { static constexpr bool v = BMd == B_ROWK; };
 
+// LDS tiles are unpadded rows of 16-byte chunks, filled by LDS-DMA (global_load_lds_dwordx4:
+// one wave instruction writes 1 KiB lane-linearly).  Bank conflicts of the fragment reads are
+// removed by an XOR swizzle applied on the SOURCE side: the chunk stored at LDS slot s of
+// row r is the global chunk s ^ (r & 7), and reads apply the same involution.
 template <int ROWS, bool KINNER>
 struct TileShape {
-  // k-inner: [ROWS][BK+PADK]; k-outer: [BK][ROWS+PADN]
-  static constexpr int LD = KINNER ? (BK + PADK) : (ROWS + PADN);
-  static constexpr int ELEMS = KINNER ? ROWS * (BK + PADK) : BK * (ROWS + PADN);
+  // k-inner: [ROWS][BK]; k-outer: [BK][ROWS]
+  static constexpr int LD = KINNER ? BK : ROWS;            // elements per LDS row
+  static constexpr int SLOTS = LD / 8;                      // 16-byte chunks per row
+  static constexpr int ELEMS = ROWS * BK;
   static constexpr int CHUNKS = ROWS * BK / 8;  // 16-byte chunks per tile
   static constexpr int PER_THREAD = CHUNKS / 256;
 };
+ED_DEV int swz(int row, int slot) { return slot ^ (row & 7); }
+
+// 16 zero bytes in global memory: the source of masked (padding / out-of-range) chunks,
+// so LDS-DMA lanes never need a branch.
+__device__ __attribute__((aligned(16))) const uint4 g_zero16 = {0u, 0u, 0u, 0u};
 
 // ---------------------------------------------------------------------------
 // Exact division by a launch constant without a divider: n / d == (n * mul) >> 40 for
@@ -90,9 +98,8 @@ struct Gemm {
   static constexpr int TM = BM / 32;  // 16x16 MFMA tiles per wave along M
   static constexpr int TN = BN / 32;
   static constexpr int STAGE = TA::ELEMS + TB::ELEMS;  // elements per LDS stage
-  // global->register prefetch depth: hides HBM latency behind PF-1 tiles of MFMA work
-  static constexpr int CH = TA::PER_THREAD + TB::PER_THREAD;
-  static constexpr int PF = CH <= 4 ? 4 : 3;
+  // two staging buffers, reused by the fp32 epilogue tile [BM][BN + 4]
+  static constexpr int LDS_BYTES = (2 * STAGE * 2 > BM * (BN + 4) * 4) ? 2 * STAGE * 2 : BM * (BN + 4) * 4;
 };
 
 template <int BM, int BN, int AM, int BMD>
@@ -123,93 +130,67 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
   const bf16_t* __restrict__ A = (const bf16_t*)p.a;
   const bf16_t* __restrict__ B = (const bf16_t*)p.b;
 
-  // ---- per-thread fixed coordinates of the gathers (K-loop invariant) ------
-  // A im2col (k-inner): the chunk's row = one output pixel (b, y, x)
-  uint32_t a_b[TA::PER_THREAD];
-  int a_y[TA::PER_THREAD], a_x[TA::PER_THREAD];
-  bool a_in[TA::PER_THREAD];
-  if constexpr (AM == A_IM2COL) {
-#pragma unroll
-    for (int i = 0; i < TA::PER_THREAD; ++i) {
-      const int c = tid + 256 * i;
-      const uint32_t m = (uint32_t)(m0 + (c >> 3));
-      a_in[i] = m < (uint32_t)p.M;
-      const uint32_t mm = a_in[i] ? m : 0u;
-      a_b[i] = fdiv(mm, aux.hw);
-      const uint32_t r = mm - a_b[i] * (uint32_t)(p.conv.h * p.conv.w);
-      a_y[i] = (int)fdiv(r, aux.w);
-      a_x[i] = (int)(r - (uint32_t)a_y[i] * (uint32_t)p.conv.w);
-    }
-  }
-  // B im2col (k-outer, wgrad): the chunk's column n = (tap, ci) is fixed
-  int b_ty[TB::PER_THREAD], b_tx[TB::PER_THREAD], b_ci[TB::PER_THREAD];
-  if constexpr (BMD == B_IM2COL) {
-#pragma unroll
-    for (int i = 0; i < TB::PER_THREAD; ++i) {
-      const int c = tid + 256 * i;
-      const uint32_t n = (uint32_t)(n0 + (c % (BN / 8)) * 8);
-      const uint32_t tap = fdiv(n, aux.cin);
-      b_ci[i] = (int)(n - tap * (uint32_t)p.conv.cin);
-      b_ty[i] = (int)((tap * 11u) >> 5);  // tap / 3 for tap < 9
-      b_tx[i] = (int)tap - 3 * b_ty[i];
-    }
-  }
-
   const Im2colMode md(p.conv);
 
-  // register ring: PF tiles in flight (global -> registers), LDS double buffer.  Every
-  // global load is unconditional (out-of-range / padding chunks load a valid address and
-  // are zeroed when written to LDS), so hipcc keeps counted vmcnt waits and the PF-1
-  // younger tiles stay in flight.
-  constexpr int PF = G::PF;
-  uint4 ra_s[PF][TA::PER_THREAD], rb_s[PF][TB::PER_THREAD];
-  uint32_t am_s[PF], bm_s[PF];  // per-chunk validity bits of each ring slot
-
-  auto load_tile = [&](int kt, uint4 (&ra)[TA::PER_THREAD], uint4 (&rb)[TB::PER_THREAD], uint32_t& amask,
-                       uint32_t& bmask) {
+  // LDS-DMA staging: every chunk's global address is computed branch-free (masked chunks
+  // read g_zero16) and copied straight into the lane-linear LDS image; tile t+1 is in
+  // flight while tile t is multiplied (depth-1 prefetch, no staging VGPRs).
+  typedef __attribute__((address_space(3))) void lds_void;
+  typedef __attribute__((address_space(1))) const void gbl_void;
+  auto stage = [&](bf16_t* s, int kt) {
     const int k0 = kt * BK;
-    amask = 0u;
-    bmask = 0u;
+    bf16_t* sa = s;
+    bf16_t* sb = s + TA::ELEMS;
 #pragma unroll
     for (int i = 0; i < TA::PER_THREAD; ++i) {
-      const int c = tid + 256 * i;
+      const int c = tid + 256 * i;               // LDS chunk position (lane-linear)
+      const int row = c / TA::SLOTS, slot = c % TA::SLOTS;
+      const int gs = swz(row, slot);              // global chunk held at this slot
       bool ok;
       size_t off;
       if constexpr (AKI) {
-        const int k = k0 + (c & 7) * 8;
+        const int k = k0 + gs * 8;
         if constexpr (AM == A_ROWK) {
-          const int m = m0 + (c >> 3);
+          const int m = m0 + row;
           ok = m < p.M && k < p.K;
           off = (size_t)(ok ? m : 0) * p.lda + (ok ? k : 0);
-        } else {  // IM2COL
+        } else {  // IM2COL: this row = output pixel, fixed per (thread, i) only when SLOTS == 8
+          const uint32_t mm0 = (uint32_t)(m0 + row);
+          const bool min = mm0 < (uint32_t)p.M;
+          const uint32_t mm = min ? mm0 : 0u;
+          const uint32_t bb = fdiv(mm, aux.hw);
+          const uint32_t r = mm - bb * (uint32_t)(p.conv.h * p.conv.w);
+          const int y = (int)fdiv(r, aux.w), x = (int)(r - (uint32_t)y * (uint32_t)p.conv.w);
           const uint32_t kk = k < p.K ? (uint32_t)k : 0u;
           const uint32_t tap = fdiv(kk, aux.cin);
           const uint32_t ch = kk - tap * (uint32_t)p.conv.cin;
           const int ty = (int)((tap * 11u) >> 5), tx = (int)tap - 3 * ty;
           bool inb;
-          const uint32_t row = im2col_row(md, a_b[i], a_y[i], a_x[i], ty, tx, inb);
-          ok = a_in[i] && k < p.K && inb;
-          off = (size_t)(ok ? row : 0u) * p.conv.ld_src + (ok ? ch : 0u);
+          const uint32_t prow = im2col_row(md, bb, y, x, ty, tx, inb);
+          ok = min && k < p.K && inb;
+          off = (size_t)(ok ? prow : 0u) * p.conv.ld_src + (ok ? ch : 0u);
         }
-      } else {  // A_ROWM: tile [BK][BM]
-        const int k = k0 + c / (BM / 8), m = m0 + (c % (BM / 8)) * 8;
+      } else {  // A_ROWM: tile [BK][BM], row = k
+        const int k = k0 + row, m = m0 + gs * 8;
         ok = k < p.K && m < p.M;
         off = (size_t)(ok ? k : 0) * p.lda + (ok ? m : 0);
       }
-      ra[i] = *(const uint4*)(A + off);
-      amask |= (ok ? 1u : 0u) << i;
+      const void* src = ok ? (const void*)(A + off) : (const void*)&g_zero16;
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sa + (c & ~63) * 8), 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < TB::PER_THREAD; ++i) {
       const int c = tid + 256 * i;
+      const int row = c / TB::SLOTS, slot = c % TB::SLOTS;
+      const int gs = swz(row, slot);
       bool ok;
       size_t off;
-      if constexpr (BKI) {  // B_ROWK: Bt[n][k]
-        const int n = n0 + (c >> 3), k = k0 + (c & 7) * 8;
+      if constexpr (BKI) {  // B_ROWK: Bt[n][k], row = n
+        const int n = n0 + row, k = k0 + gs * 8;
         ok = n < p.N && k < p.K;
         off = (size_t)(ok ? n : 0) * p.ldb + (ok ? k : 0);
-      } else {
-        const int k = k0 + c / (BN / 8), n = n0 + (c % (BN / 8)) * 8;
+      } else {  // k-outer: row = k, chunk = 8 columns of n
+        const int k = k0 + row, n = n0 + gs * 8;
         const bool kn = k < p.K && n < p.N;
         if constexpr (BMD == B_ROWN) {
           ok = kn;
@@ -220,46 +201,23 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
           const uint32_t co = kk - tap * (uint32_t)p.conv_cout;
           ok = kn;
           off = (size_t)co * p.ldb + (size_t)(8 - tap) * p.N + (ok ? n : 0);
-        } else {  // B_IM2COL: row = output pixel k
+        } else {  // B_IM2COL: row = output pixel k, column n = (tap, ci)
           const uint32_t kk = kn ? (uint32_t)k : 0u;
-          const uint32_t b = fdiv(kk, aux.hw);
-          const uint32_t r = kk - b * (uint32_t)(p.conv.h * p.conv.w);
+          const uint32_t bb = fdiv(kk, aux.hw);
+          const uint32_t r = kk - bb * (uint32_t)(p.conv.h * p.conv.w);
           const int y = (int)fdiv(r, aux.w), x = (int)(r - (uint32_t)y * (uint32_t)p.conv.w);
+          const uint32_t nn = kn ? (uint32_t)n : 0u;
+          const uint32_t tap = fdiv(nn, aux.cin);
+          const uint32_t ci = nn - tap * (uint32_t)p.conv.cin;
+          const int ty = (int)((tap * 11u) >> 5), tx = (int)tap - 3 * ty;
           bool inb;
-          const uint32_t row = im2col_row(md, b, y, x, b_ty[i], b_tx[i], inb);
+          const uint32_t prow = im2col_row(md, bb, y, x, ty, tx, inb);
           ok = kn && inb;
-          off = (size_t)(ok ? row : 0u) * p.conv.ld_src + (ok ? (uint32_t)b_ci[i] : 0u);
+          off = (size_t)(ok ? prow : 0u) * p.conv.ld_src + (ok ? ci : 0u);
         }
       }
-      rb[i] = *(const uint4*)(B + off);
-      bmask |= (ok ? 1u : 0u) << i;
-    }
-  };
-
-  auto store_tile = [&](bf16_t* s, const uint4 (&ra)[TA::PER_THREAD], const uint4 (&rb)[TB::PER_THREAD],
-                        uint32_t amask, uint32_t bmask) {
-    const uint4 z = {0u, 0u, 0u, 0u};
-    bf16_t* sa = s;
-    bf16_t* sb = s + TA::ELEMS;
-#pragma unroll
-    for (int i = 0; i < TA::PER_THREAD; ++i) {
-      const int c = tid + 256 * i;
-      const uint4 v = ((amask >> i) & 1u) ? ra[i] : z;
-      if constexpr (AKI) {
-        *(uint4*)(sa + (c >> 3) * TA::LD + (c & 7) * 8) = v;
-      } else {
-        *(uint4*)(sa + (c / (BM / 8)) * TA::LD + (c % (BM / 8)) * 8) = v;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < TB::PER_THREAD; ++i) {
-      const int c = tid + 256 * i;
-      const uint4 v = ((bmask >> i) & 1u) ? rb[i] : z;
-      if constexpr (BKI) {
-        *(uint4*)(sb + (c >> 3) * TB::LD + (c & 7) * 8) = v;
-      } else {
-        *(uint4*)(sb + (c / (BN / 8)) * TB::LD + (c % (BN / 8)) * 8) = v;
-      }
+      const void* src = ok ? (const void*)(B + off) : (const void*)&g_zero16;
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sb + (c & ~63) * 8), 16, 0, 0);
     }
   };
 
@@ -278,13 +236,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
   const int tq = l16 >> 2, tp = l16 & 3;  // transpose-read address roles
 
   auto frag_kinner = [&](const bf16_t* s, int row, int kk) -> v8bf {
-    return *(const v8bf*)(s + row * (BK + PADK) + kk * 32 + g4 * 8);
+    return *(const v8bf*)(s + row * BK + swz(row, kk * 4 + g4) * 8);
   };
   auto frag_kouter = [&](const bf16_t* s, int ld, int colbase, int kk) -> v8bf {
+    // rows k = kk*32 + g4*8 + tq (+4): 4 bf16 at column colbase + 4*tp, swizzled chunk
     typedef __attribute__((address_space(3))) v4s lds_v4s;
-    const bf16_t* p0 = s + (kk * 32 + g4 * 8 + tq) * ld + colbase + tp * 4;
-    v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p0));
-    v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p0 + 4 * ld));
+    const int r0 = kk * 32 + g4 * 8 + tq, r1 = r0 + 4;
+    const int ch = (colbase >> 3) + (tp >> 1), sub = (tp & 1) * 4;
+    v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(s + r0 * ld + swz(r0, ch) * 8 + sub));
+    v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(s + r1 * ld + swz(r1, ch) * 8 + sub));
     v8s r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(v8bf, r);
   };
@@ -297,7 +257,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
       constexpr int RG = 256 / BM;
       const int col = tid % BM, rg = tid / BM;
 #pragma unroll 4
-      for (int r = rg * (BK / RG); r < (rg + 1) * (BK / RG); ++r) bsum += bf2f(sa[r * TA::LD + col]);
+      for (int r = rg * (BK / RG); r < (rg + 1) * (BK / RG); ++r)
+        bsum += bf2f(sa[r * TA::LD + swz(r, col >> 3) * 8 + (col & 7)]);
     }
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
@@ -321,28 +282,16 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
   };
 
   if (nkt > 0) {
-    // prologue: PF tiles in flight
-#pragma unroll
-    for (int u = 0; u < PF; ++u)
-      if (u < nkt) load_tile(kt_begin + u, ra_s[u], rb_s[u], am_s[u], bm_s[u]);
-    store_tile(smem, ra_s[0], rb_s[0], am_s[0], bm_s[0]);
-    __syncthreads();
-    // main loop, unrolled by PF so every register stage index is a compile-time constant:
-    // iteration i computes LDS buffer i&1, refills ring slot i%PF with tile i+PF and moves
-    // tile i+1 (slot (i+1)%PF) into the other LDS buffer.
-    for (int base = 0; base < nkt; base += PF) {
-#pragma unroll
-      for (int u = 0; u < PF; ++u) {
-        const int it = base + u;
-        if (it < nkt) {
-          if (it + PF < nkt) load_tile(kt_begin + it + PF, ra_s[u], rb_s[u], am_s[u], bm_s[u]);
-          compute(smem + (it & 1) * G::STAGE);
-          if (it + 1 < nkt)
-            store_tile(smem + ((it + 1) & 1) * G::STAGE, ra_s[(u + 1) % PF], rb_s[(u + 1) % PF], am_s[(u + 1) % PF],
-                       bm_s[(u + 1) % PF]);
-          __syncthreads();
-        }
-      }
+    stage(smem, kt_begin);
+    __syncthreads();  // (waits vmcnt(0): tile 0 landed)
+    for (int it = 0; it < nkt; ++it) {
+      if (it + 1 < nkt) stage(smem + ((it + 1) & 1) * G::STAGE, kt_begin + it + 1);
+      compute(smem + (it & 1) * G::STAGE);
+      // WAR: this wave's fragment reads of tile it are retired before the barrier, so the
+      // next iteration's DMA into this buffer cannot overtake them; RAW: vmcnt(0) + barrier
+      // makes tile it+1 visible to every wave
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __syncthreads();
     }
   }
 
@@ -376,7 +325,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
   }
   float* p_c_slab = (float*)p.c;
   constexpr int SLD = BN + 4;
-  static_assert(BM * SLD * 4 <= 2 * G::STAGE * 2, "epilogue staging must fit the LDS allocation");
+  static_assert(BM * SLD * 4 <= G::LDS_BYTES, "epilogue staging must fit the LDS allocation");
   float* sc = (float*)smem;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -484,7 +433,7 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const EncdiffGemmArg
 template <int BM, int BN, int AM, int BMD>
 hipError_t launch_t(const EncdiffGemmArgs& p, const GemmAux& aux, hipStream_t s) {
   using G = Gemm<BM, BN, AM, BMD>;
-  const size_t lds = 2 * G::STAGE * sizeof(bf16_t);
+  const size_t lds = G::LDS_BYTES;
   // dynamic LDS above 64 KiB must be opted in once per instantiation (thread-safe static init)
   static const hipError_t attr_ok = hipFuncSetAttribute(
       (const void*)gemm_kernel<BM, BN, AM, BMD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
