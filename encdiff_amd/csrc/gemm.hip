@@ -296,8 +296,27 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
   }
 
   if (do_bgrad) {
-    const int col = tid % BM;
-    if (m0 + col < p.M) atomicAdd(p.bias_grad + m0 + col, bsum);
+    // column sums of the k-outer A: rows 0..RG-1 of each column partial -> combine in LDS
+    // order, then ONE writer per column: a split-K slab (summed in order by the finalize),
+    // a plain += (single K range), or an atomic for the atomic output modes.
+    constexpr int RG = 256 / BM;
+    float* red = (float*)smem;  // staging buffers are free after the last barrier
+    const int col = tid % BM, rg = tid / BM;
+    red[rg * BM + col] = bsum;
+    __syncthreads();
+    if (rg == 0 && m0 + col < p.M) {
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < RG; ++r) t += red[r * BM + col];
+      const bool slab = p.split_k > 1 && p.c == (void*)p.workspace;
+      if (slab)
+        p.workspace[(long)p.split_k * p.M * p.N + (long)blockIdx.z * p.M + m0 + col] = t;
+      else if (p.c_mode == ENCDIFF_OUT_F32_ATOMIC || p.c_mode == ENCDIFF_OUT_F32_ATOMIC_CONVW || p.split_k > 1)
+        atomicAdd(p.bias_grad + m0 + col, t);
+      else
+        p.bias_grad[m0 + col] += t;
+    }
+    __syncthreads();
   }
 
   // ---- epilogue -------------------------------------------------------------
@@ -427,6 +446,21 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const EncdiffGemmArg
       else ((float*)p.c)[(long)row * p.ldc + col] = v;
     }
     __syncthreads();
+  }
+  if (p.bias_grad) {  // bias-gradient slabs [split][M] behind the C slabs, same ordered scheme
+    const float* bs = p.workspace + (long)p.split_k * total;
+    for (long t0 = (long)blockIdx.x * FIN_OPB; t0 < p.M; t0 += (long)gridDim.x * FIN_OPB) {
+      const long m = t0 + o;
+      float acc = 0.f;
+      if (m < p.M) {
+#pragma unroll 8
+        for (int z = zg; z < p.split_k; z += FIN_ZG) acc += bs[(long)z * p.M + m];
+      }
+      part[zg][o] = acc;
+      __syncthreads();
+      if (zg == 0 && m < p.M) p.bias_grad[m] += ((part[0][o] + part[1][o]) + part[2][o]) + part[3][o];
+      __syncthreads();
+    }
   }
 }
 

@@ -80,7 +80,7 @@ def plan(M, N, K, a_mode, b_mode, c_mode):
     hit = _tile_table().get(f"{a_mode},{b_mode},{c_mode},{M},{N},{K}")
     if hit is not None:
         tile, split = int(hit[0]), int(hit[1])
-        if split == 1 or c_mode in (L.OUT_F32_ATOMIC, L.OUT_F32_ATOMIC_CONVW) or split * M * N <= WS_FLOATS:
+        if split == 1 or c_mode in (L.OUT_F32_ATOMIC, L.OUT_F32_ATOMIC_CONVW) or split * M * (N + 1) <= WS_FLOATS:
             return tile, split
     atomic = c_mode in (L.OUT_F32_ATOMIC, L.OUT_F32_ATOMIC_CONVW)
     bm = 64 if M <= 64 else 128
@@ -99,7 +99,7 @@ def plan(M, N, K, a_mode, b_mode, c_mode):
         while nb * split < 256 and K // (split * 2) >= 256 and (split * 2) * M * N * 4 <= (8 << 20):
             split *= 2
     else:  # slab split-K (bf16 / f32 / f32-accumulate outputs)
-        while nb * split < 256 and K // (split * 2) >= 256 and (split * 2) * M * N <= WS_FLOATS:
+        while nb * split < 256 and K // (split * 2) >= 256 and (split * 2) * M * (N + 1) <= WS_FLOATS:
             split *= 2
     return tile, split
 
@@ -113,7 +113,8 @@ def gemm(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROW
         split_k = split_k or sp
     ws = None
     if split_k > 1 and c_mode in (L.OUT_BF16, L.OUT_F32, L.OUT_F32_ACCUM):
-        assert split_k * M * N <= WS_FLOATS, "split-K slabs exceed the workspace"
+        need = split_k * M * N + (split_k * M if bias_grad is not None else 0)
+        assert need <= WS_FLOATS, "split-K slabs exceed the workspace"
         ws = _workspace()
     args = L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=b_mode, c_mode=c_mode,
                       a=_p(a), lda=lda, b=_p(b), ldb=ldb, c=_p(c), ldc=ldc,

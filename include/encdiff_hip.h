@@ -95,7 +95,8 @@ typedef struct EncdiffGemmArgs {
   float* bias_grad;          /* OPA_ROWM only: += sum_k A[m][k] into bias_grad[m]  */
   int tile;                  /* 0 = auto, else 1:128x128 2:128x64 3:64x128 4:64x64 */
   int pad2_;
-  float* workspace;          /* split_k > 1 with a BF16/F32/F32_ACCUM c_mode: fp32 scratch of split_k*M*N;
+  float* workspace;          /* split_k > 1 with a BF16/F32/F32_ACCUM c_mode: fp32 scratch of split_k*M*N
+                                (+ split_k*M when bias_grad is set: per-split bias-gradient slabs);
                                 each split writes its own [M][N] slab, a finalize pass sums the
                                 slabs in order (reproducible) and applies alpha/bias/resid    */
 } EncdiffGemmArgs;

@@ -64,6 +64,21 @@ def test_linear(O, M, N, K):
     O.linear_wgrad(dy, x, dw, db)
     assert rel(dw, dy.float().t() @ x.float()) < 2e-3
     assert rel(db, dy.float().sum(0)) < 2e-3
+    # forced split-K: slab weight AND bias gradients accumulate (+=) reproducibly
+    import encdiff_amd._lib as L
+    for split in (1, 4):
+        if split * N * (K + 1) > O.WS_FLOATS:
+            continue
+        dw2, db2 = dw.clone(), db.clone()
+        outs = []
+        for _ in range(2):
+            a2, b2 = dw2.clone(), db2.clone()
+            O.gemm(N, K, M, dy, dy.stride(0), x, x.stride(0), a2, K, a_mode=L.OPA_ROWM, b_mode=L.OPB_ROWN,
+                   c_mode=L.OUT_F32_ACCUM, bias_grad=b2, split_k=split, tile=4)
+            outs.append((a2, b2))
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+        assert rel(outs[0][0] - dw2, dy.float().t() @ x.float()) < 2e-3
+        assert rel(outs[0][1] - db2, dy.float().sum(0)) < 2e-3
 
 
 @pytest.mark.parametrize("split", [2, 8])

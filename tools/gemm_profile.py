@@ -101,7 +101,7 @@ def main():
         if split is not None:
             a2.split_k = split
             a2.workspace = ws.data_ptr() if split > 1 else None
-            if split > 1 and a2.c_mode in (L.OUT_BF16, L.OUT_F32, L.OUT_F32_ACCUM) and split * a2.M * a2.N > ops.WS_FLOATS:
+            if split > 1 and a2.c_mode in (L.OUT_BF16, L.OUT_F32, L.OUT_F32_ACCUM) and split * a2.M * (a2.N + 1) > ops.WS_FLOATS:
                 return float("inf")
         for _ in range(2):
             rc = orig(C.byref(a2), stream)
