@@ -56,7 +56,7 @@ class LayerNormArgs(C.Structure):
                 ("x", vp), ("ldx", C.c_long), ("gamma", vp), ("beta", vp), ("y", vp), ("ldy", C.c_long),
                 ("stats", vp), ("dy", vp), ("lddy", C.c_long), ("dx", vp), ("lddx", C.c_long),
                 ("accumulate_dx", C.c_int), ("dgamma_part", vp), ("dbeta_part", vp), ("ld_part", C.c_long),
-                ("parts", C.c_int), ("pad_", C.c_int)]
+                ("parts", C.c_int), ("pad_", C.c_int), ("resid", vp), ("ld_resid", C.c_long)]
 
 
 class AttnArgs(C.Structure):
@@ -90,6 +90,7 @@ class PackJob(C.Structure):
 
 _PROTOS = {
     "encdiff_gemm": [C.POINTER(GemmArgs), vp],
+    "encdiff_gemm_pair": [C.POINTER(GemmArgs), C.POINTER(GemmArgs), vp],
     "encdiff_groupnorm_fwd": [C.POINTER(GroupNormArgs), vp],
     "encdiff_groupnorm_bwd": [C.POINTER(GroupNormArgs), vp],
     "encdiff_layernorm_fwd": [C.POINTER(LayerNormArgs), vp],

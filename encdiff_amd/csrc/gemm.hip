@@ -98,32 +98,52 @@ struct Gemm {
   static constexpr int TM = BM / 32;  // 16x16 MFMA tiles per wave along M
   static constexpr int TN = BN / 32;
   static constexpr int STAGE = TA::ELEMS + TB::ELEMS;  // elements per LDS stage
-  // two staging buffers, reused by the fp32 epilogue tile [BM][BN + 4]
-  static constexpr int LDS_BYTES = (2 * STAGE * 2 > BM * (BN + 4) * 4) ? 2 * STAGE * 2 : BM * (BN + 4) * 4;
+  // LDS ring depth.  Measured on the step's GEMMs: 3-4 stages (one or two workgroups per CU)
+  // lost 7% overall against 2 stages with up to five resident workgroups per CU hiding the
+  // load latency instead.
+  static constexpr int NSTAGE = 2;
+  static constexpr int LPS = TA::PER_THREAD + TB::PER_THREAD;  // LDS-DMA loads per thread per stage
+  // the staging ring, reused by the fp32 epilogue tile [BM][BN + 4]
+  static constexpr int LDS_BYTES =
+      (NSTAGE * STAGE * 2 > BM * (BN + 4) * 4) ? NSTAGE * STAGE * 2 : BM * (BN + 4) * 4;
 };
 
+// Wait until at most N of this thread's vector-memory loads are outstanding (LDS-DMA stages
+// still in flight behind the one about to be read).
+template <int N>
+ED_DEV void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int LPS>
+ED_DEV void vm_wait_stages(int ahead) {
+  if (ahead >= 2) vm_wait<2 * LPS>();
+  else if (ahead == 1) vm_wait<LPS>();
+  else vm_wait<0>();
+}
+
+// One output tile (bx, by) of split bz.  Shared by the single-GEMM kernel and the paired
+// kernel that runs two independent GEMMs (a layer's input- and weight-gradient) in one grid.
 template <int BM, int BN, int AM, int BMD>
-__global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, const GemmAux aux) {
+__device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAux& aux, const int bx, const int by,
+                                          const int bz, bf16_t* smem) {
   using G = Gemm<BM, BN, AM, BMD>;
   using TA = typename G::TA;
   using TB = typename G::TB;
   constexpr bool AKI = G::AKI, BKI = G::BKI;
   constexpr int TM = G::TM, TN = G::TN;
 
-  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wr = (wave >> 1) * (BM / 2);
   const int wc = (wave & 1) * (BN / 2);
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  const int m0 = bx * BM;
+  const int n0 = by * BN;
 
   // split-K range
   const int ktiles_total = (p.K + BK - 1) / BK;
   const int kt_per = (ktiles_total + p.split_k - 1) / p.split_k;
-  const int kt_begin = blockIdx.z * kt_per;
+  const int kt_begin = bz * kt_per;
   const int kt_end = min(ktiles_total, kt_begin + kt_per);
   const int nkt = kt_end - kt_begin;
 
@@ -228,7 +248,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
     for (int j = 0; j < TN; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
 
   // optional bias-gradient: column sums of the (k-outer) A operand over K
-  const bool do_bgrad = (AM == A_ROWM) && p.bias_grad != nullptr && blockIdx.y == 0;
+  const bool do_bgrad = (AM == A_ROWM) && p.bias_grad != nullptr && by == 0;
   float bsum = 0.f;
 
   const int l16 = lane & 15;
@@ -281,18 +301,29 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
     }
   };
 
+  // NSTAGE-deep LDS ring: tiles it+1 .. it+NSTAGE-2 stay in flight while tile it is
+  // multiplied, so the K loop is bound by MFMA / bandwidth rather than by one load latency
+  // per k-tile.  Per iteration: wait for tile it (vmcnt = loads issued after it), one
+  // barrier (tile it visible to all waves; every wave is done with tile it-1, whose slot is
+  // refilled next), issue tile it+NSTAGE-1, multiply tile it.
+  constexpr int D = G::NSTAGE;
+  static_assert(D - 2 <= 2, "vm_wait_stages covers up to two stages ahead");
   if (nkt > 0) {
-    stage(smem, kt_begin);
-    __syncthreads();  // (waits vmcnt(0): tile 0 landed)
+#pragma unroll
+    for (int st = 0; st < D - 1; ++st)
+      if (st < nkt) stage(smem + st * G::STAGE, kt_begin + st);
+    int rd = 0, wr = D - 1;  // ring slots of the tile read now / the tile issued next
     for (int it = 0; it < nkt; ++it) {
-      if (it + 1 < nkt) stage(smem + ((it + 1) & 1) * G::STAGE, kt_begin + it + 1);
-      compute(smem + (it & 1) * G::STAGE);
-      // WAR: this wave's fragment reads of tile it are retired before the barrier, so the
-      // next iteration's DMA into this buffer cannot overtake them; RAW: vmcnt(0) + barrier
-      // makes tile it+1 visible to every wave
+      vm_wait_stages<G::LPS>(min(D - 2, nkt - 1 - it));
+      asm volatile("s_barrier" ::: "memory");  // (asm: the compiler may not move LDS-DMA issue across it)
+      if (it + D - 1 < nkt) stage(smem + wr * G::STAGE, kt_begin + it + D - 1);
+      compute(smem + rd * G::STAGE);
+      // this wave's fragment reads of slot rd retire before it reaches the next barrier
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __syncthreads();
+      rd = rd + 1 == D ? 0 : rd + 1;
+      wr = wr + 1 == D ? 0 : wr + 1;
     }
+    __syncthreads();  // every wave is done with the ring before the epilogue reuses it
   }
 
   if (do_bgrad) {
@@ -310,7 +341,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
       for (int r = 0; r < RG; ++r) t += red[r * BM + col];
       const bool slab = p.split_k > 1 && p.c == (void*)p.workspace;
       if (slab)
-        p.workspace[(long)p.split_k * p.M * p.N + (long)blockIdx.z * p.M + m0 + col] = t;
+        p.workspace[(long)p.split_k * p.M * p.N + (long)bz * p.M + m0 + col] = t;
       else if (p.c_mode == ENCDIFF_OUT_F32_ATOMIC || p.c_mode == ENCDIFF_OUT_F32_ATOMIC_CONVW || p.split_k > 1)
         atomicAdd(p.bias_grad + m0 + col, t);
       else
@@ -322,7 +353,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
   // ---- epilogue -------------------------------------------------------------
   // Stage the fp32 tile through LDS (the staging buffers are free after the last barrier),
   // then write whole 16-byte row segments (bf16/fp32 outputs) or lane-contiguous fp32 atomics.
-  const bool add_bias = p.bias != nullptr && blockIdx.z == 0;
+  const bool add_bias = p.bias != nullptr && bz == 0;
   const bf16_t* R = (const bf16_t*)p.resid;
   if (p.c_mode == ENCDIFF_OUT_F32_ATOMIC_CONVW) {  // reference-layout scatter (rare path)
 #pragma unroll
@@ -364,7 +395,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
     return;
   }
   if (p.split_k > 1 && p.c_mode == ENCDIFF_OUT_F32)  // split-K slab of this z (workspace path)
-    p_c_slab = (float*)p.c + (long)blockIdx.z * p.M * p.N;
+    p_c_slab = (float*)p.c + (long)bz * p.M * p.N;
   const bool vec = (p.N % 8 == 0) && (p.ldc % 8 == 0) && (((uintptr_t)p.c & 15) == 0) &&
                    (!add_bias || (((uintptr_t)p.bias & 15) == 0)) &&
                    (!R || ((p.ld_resid % 8 == 0) && (((uintptr_t)R & 15) == 0)));
@@ -415,17 +446,45 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
   }
 }
 
+template <int BM, int BN, int AM, int BMD>
+__global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, const GemmAux aux) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  gemm_tile<BM, BN, AM, BMD>(p, aux, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+}
+
+// Two independent GEMMs in one 1-D grid: blocks [0, n1) run problem 1 (64 x 64 tiles),
+// the rest problem 2 (tile BM2 x BN2).  A layer's weight gradient (problem 1: deep split-K,
+// the longer-running blocks, dispatched first) and its input gradient (problem 2) then
+// share the machine instead of running back to back, each too small to fill 256 CUs, and
+// one launch boundary disappears.
+template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2>
+__global__ __launch_bounds__(256) void gemm2_kernel(const EncdiffGemmArgs p1, const GemmAux aux1,
+                                                    const EncdiffGemmArgs p2, const GemmAux aux2, int gx1,
+                                                    int gy1, int gx2, int gy2) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
+  const int n1 = gx1 * gy1 * p1.split_k;
+  int i = blockIdx.x;
+  if (i < n1) {
+    const int bx = i % gx1, t = i / gx1;
+    gemm_tile<64, 64, AM1, BMD1>(p1, aux1, bx, t % gy1, t / gy1, smem);
+  } else {
+    i -= n1;
+    const int bx = i % gx2, t = i / gx2;
+    gemm_tile<BM2, BN2, AM2, BMD2>(p2, aux2, bx, t % gy2, t / gy2, smem);
+  }
+}
+
 // split-K finalize: C = alpha * sum_z slab[z] (+bias)(+resid).  A workgroup owns 64
 // consecutive outputs; its 4 wave-rows each sum every 4th slab (8 loads in flight per
 // lane), then the 4 partials are added in a fixed order: bitwise reproducible, no atomics,
 // and a deep split (e.g. 128 slabs of a 64x64 weight gradient) stays bandwidth-bound.
 constexpr int FIN_ZG = 4, FIN_OPB = 64;
-__global__ __launch_bounds__(256) void gemm_finalize_kernel(const EncdiffGemmArgs p) {
+__device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const int bid, const int nblk) {
   __shared__ float part[FIN_ZG][FIN_OPB];
   const long total = (long)p.M * p.N;
   const bf16_t* R = (const bf16_t*)p.resid;
   const int o = threadIdx.x % FIN_OPB, zg = threadIdx.x / FIN_OPB;
-  for (long t0 = (long)blockIdx.x * FIN_OPB; t0 < total; t0 += (long)gridDim.x * FIN_OPB) {
+  for (long t0 = (long)bid * FIN_OPB; t0 < total; t0 += (long)nblk * FIN_OPB) {
     const long i = t0 + o;
     float acc = 0.f;
     if (i < total) {
@@ -449,7 +508,7 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const EncdiffGemmArg
   }
   if (p.bias_grad) {  // bias-gradient slabs [split][M] behind the C slabs, same ordered scheme
     const float* bs = p.workspace + (long)p.split_k * total;
-    for (long t0 = (long)blockIdx.x * FIN_OPB; t0 < p.M; t0 += (long)gridDim.x * FIN_OPB) {
+    for (long t0 = (long)bid * FIN_OPB; t0 < p.M; t0 += (long)nblk * FIN_OPB) {
       const long m = t0 + o;
       float acc = 0.f;
       if (m < p.M) {
@@ -462,6 +521,17 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const EncdiffGemmArg
       __syncthreads();
     }
   }
+}
+
+__global__ __launch_bounds__(256) void gemm_finalize_kernel(const EncdiffGemmArgs p) {
+  gemm_finalize(p, blockIdx.x, gridDim.x);
+}
+
+// finalize of two split-K GEMMs in one launch (blocks [0, g1) for p1, the rest for p2)
+__global__ __launch_bounds__(256) void gemm_finalize2_kernel(const EncdiffGemmArgs p1, const EncdiffGemmArgs p2,
+                                                             int g1) {
+  if ((int)blockIdx.x < g1) gemm_finalize(p1, blockIdx.x, g1);
+  else gemm_finalize(p2, blockIdx.x - g1, gridDim.x - g1);
 }
 
 template <int BM, int BN, int AM, int BMD>
@@ -507,9 +577,16 @@ int pick_tile(const EncdiffGemmArgs& p) {
   return 4;
 }
 
-}  // namespace
+// Validated launch plan of one GEMM: the arguments the tile kernel sees (split-K slabs
+// redirected into the workspace), the user's arguments for the finalize pass, aux constants.
+struct GemmPlan {
+  EncdiffGemmArgs p, user;
+  GemmAux aux;
+  int tile;
+  bool ws_path;
+};
 
-extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
+int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
   if (!pa) return ENCDIFF_ERR_ARG;
   EncdiffGemmArgs p = *pa;
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return ENCDIFF_ERR_SHAPE;
@@ -529,38 +606,113 @@ extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
   if (im2col && p.conv.resample == ENCDIFF_RESAMPLE_DOWN2) return ENCDIFF_ERR_UNSUPPORTED;
   if (p.K >= (1 << 24)) return ENCDIFF_ERR_SHAPE;
   if (p.bias_grad && p.a_mode != ENCDIFF_OPA_ROWM) return ENCDIFF_ERR_ARG;
-  const int tile = p.tile ? p.tile : pick_tile(p);
-  hipStream_t s = (hipStream_t)stream;
-  hipError_t e;
-  const int am = p.a_mode, bm = p.b_mode;
-  const EncdiffGemmArgs user = p;
+  g.tile = p.tile ? p.tile : pick_tile(p);
+  g.user = p;
+  g.ws_path = ws_path;
   if (ws_path) {  // per-split fp32 slabs (plain stores); epilogue in the finalize pass
     p.c = p.workspace; p.ldc = p.N; p.c_mode = ENCDIFF_OUT_F32; p.alpha = 1.f;
     p.bias = nullptr; p.resid = nullptr;
   }
-  GemmAux aux;
-  aux.cin = make_fdiv(p.conv.cin);
-  aux.cout = make_fdiv(p.conv_cout);
-  aux.hw = make_fdiv(p.conv.h * p.conv.w);
-  aux.w = make_fdiv(p.conv.w);
-  if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_ROWK, B_ROWK>(p, aux, tile, s);
-  else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_IM2COL, B_ROWK>(p, aux, tile, s);
-  else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWK, B_ROWN>(p, aux, tile, s);
+  g.p = p;
+  g.aux.cin = make_fdiv(p.conv.cin);
+  g.aux.cout = make_fdiv(p.conv_cout);
+  g.aux.hw = make_fdiv(p.conv.h * p.conv.w);
+  g.aux.w = make_fdiv(p.conv.w);
+  return ENCDIFF_OK;
+}
+
+int fin_blocks(const EncdiffGemmArgs& u) {
+  long total = (long)u.M * u.N;
+  long g = (total + FIN_OPB - 1) / FIN_OPB;
+  return (int)(g > 8192 ? 8192 : g);
+}
+
+int launch_one(const GemmPlan& g, hipStream_t s) {
+  const int am = g.p.a_mode, bm = g.p.b_mode;
+  hipError_t e;
+  if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_ROWK, B_ROWK>(g.p, g.aux, g.tile, s);
+  else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_IM2COL, B_ROWK>(g.p, g.aux, g.tile, s);
+  else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWK, B_ROWN>(g.p, g.aux, g.tile, s);
   else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_CONV_DGRAD)
-    e = launch_modes<A_IM2COL, B_CONVD>(p, aux, tile, s);
-  else if (am == ENCDIFF_OPA_ROWM && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWM, B_ROWN>(p, aux, tile, s);
-  else if (am == ENCDIFF_OPA_ROWM && bm == ENCDIFF_OPB_IM2COL) e = launch_modes<A_ROWM, B_IM2COL>(p, aux, tile, s);
+    e = launch_modes<A_IM2COL, B_CONVD>(g.p, g.aux, g.tile, s);
+  else if (am == ENCDIFF_OPA_ROWM && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWM, B_ROWN>(g.p, g.aux, g.tile, s);
+  else if (am == ENCDIFF_OPA_ROWM && bm == ENCDIFF_OPB_IM2COL) e = launch_modes<A_ROWM, B_IM2COL>(g.p, g.aux, g.tile, s);
   else return ENCDIFF_ERR_UNSUPPORTED;
   if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
-  if (ws_path) {
-    long total = (long)user.M * user.N;
-    long g = (total + FIN_OPB - 1) / FIN_OPB;
-    if (g > 8192) g = 8192;
-    hipLaunchKernelGGL(gemm_finalize_kernel, dim3((unsigned)g), dim3(256), 0, s, user);
+  if (g.ws_path) {
+    hipLaunchKernelGGL(gemm_finalize_kernel, dim3((unsigned)fin_blocks(g.user)), dim3(256), 0, s, g.user);
     e = hipGetLastError();
     if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
   }
   return ENCDIFF_OK;
+}
+
+template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2>
+hipError_t launch_pair_t(const GemmPlan& g1, const GemmPlan& g2, hipStream_t s) {
+  using G1 = Gemm<64, 64, AM1, BMD1>;
+  using G2 = Gemm<BM2, BN2, AM2, BMD2>;
+  constexpr size_t lds = G1::LDS_BYTES > G2::LDS_BYTES ? G1::LDS_BYTES : G2::LDS_BYTES;
+  static const hipError_t attr_ok = hipFuncSetAttribute(
+      (const void*)gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr_ok != hipSuccess) return attr_ok;
+  const int gx1 = (g1.p.M + 63) / 64, gy1 = (g1.p.N + 63) / 64;
+  const int gx2 = (g2.p.M + BM2 - 1) / BM2, gy2 = (g2.p.N + BN2 - 1) / BN2;
+  const long nb = (long)gx1 * gy1 * g1.p.split_k + (long)gx2 * gy2 * g2.p.split_k;
+  hipLaunchKernelGGL((gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2>), dim3((unsigned)nb), dim3(256), lds, s, g1.p,
+                     g1.aux, g2.p, g2.aux, gx1, gy1, gx2, gy2);
+  return hipGetLastError();
+}
+
+template <int AM1, int BMD1, int AM2, int BMD2>
+hipError_t launch_pair_tiles(const GemmPlan& g1, const GemmPlan& g2, hipStream_t s) {
+  switch (g2.tile) {
+    case 1: return launch_pair_t<AM1, BMD1, 128, 128, AM2, BMD2>(g1, g2, s);
+    case 2: return launch_pair_t<AM1, BMD1, 128, 64, AM2, BMD2>(g1, g2, s);
+    case 3: return launch_pair_t<AM1, BMD1, 64, 128, AM2, BMD2>(g1, g2, s);
+    default: return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2>(g1, g2, s);
+  }
+}
+
+}  // namespace
+
+extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
+  GemmPlan g;
+  const int rc = prepare(pa, g);
+  if (rc != ENCDIFF_OK) return rc;
+  return launch_one(g, (hipStream_t)stream);
+}
+
+extern "C" int encdiff_gemm_pair(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad, void* stream) {
+  GemmPlan g1, g2;
+  int rc = prepare(wgrad, g1);
+  if (rc != ENCDIFF_OK) return rc;
+  rc = prepare(dgrad, g2);
+  if (rc != ENCDIFF_OK) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const int a1 = g1.p.a_mode, b1 = g1.p.b_mode, a2 = g2.p.a_mode, b2 = g2.p.b_mode;
+  const bool lin = a1 == ENCDIFF_OPA_ROWM && b1 == ENCDIFF_OPB_ROWN && a2 == ENCDIFF_OPA_ROWK && b2 == ENCDIFF_OPB_ROWN;
+  const bool conv = a1 == ENCDIFF_OPA_ROWM && b1 == ENCDIFF_OPB_IM2COL && a2 == ENCDIFF_OPA_IM2COL &&
+                    b2 == ENCDIFF_OPB_CONV_DGRAD;
+  // pairs the fused kernel does not cover run back to back (same results)
+  if ((!lin && !conv) || g1.tile != 4) {
+    rc = launch_one(g1, s);
+    return rc != ENCDIFF_OK ? rc : launch_one(g2, s);
+  }
+  // both split-K problems need disjoint slabs
+  if (g1.ws_path && g2.ws_path && g1.p.workspace == g2.p.workspace) return ENCDIFF_ERR_ARG;
+  hipError_t e = lin ? launch_pair_tiles<A_ROWM, B_ROWN, A_ROWK, B_ROWN>(g1, g2, s)
+                     : launch_pair_tiles<A_ROWM, B_IM2COL, A_IM2COL, B_CONVD>(g1, g2, s);
+  if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+  if (g1.ws_path && g2.ws_path) {
+    const int f1 = fin_blocks(g1.user), f2 = fin_blocks(g2.user);
+    hipLaunchKernelGGL(gemm_finalize2_kernel, dim3((unsigned)(f1 + f2)), dim3(256), 0, s, g1.user, g2.user, f1);
+  } else if (g1.ws_path) {
+    hipLaunchKernelGGL(gemm_finalize_kernel, dim3((unsigned)fin_blocks(g1.user)), dim3(256), 0, s, g1.user);
+  } else if (g2.ws_path) {
+    hipLaunchKernelGGL(gemm_finalize_kernel, dim3((unsigned)fin_blocks(g2.user)), dim3(256), 0, s, g2.user);
+  }
+  e = hipGetLastError();
+  return e != hipSuccess ? ENCDIFF_ERR_LAUNCH - (int)e : ENCDIFF_OK;
 }
 
 extern "C" int encdiff_version(void) { return 1; }

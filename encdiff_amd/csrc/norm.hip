@@ -356,11 +356,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const EncdiffLayerNormArgs 
     s1 *= (1.f / C); s2 *= (1.f / C);
     bf16_t* dxp = (bf16_t*)p.dx + (long)row * p.lddx + lr * 8;
     float o8[8];
-    if (p.accumulate_dx) unpack8(*(const uint4*)dxp, o8);
+    // residual-branch gradient: dx itself (in place) or a separate tensor (out of place, so a
+    // weight gradient still reading that tensor on another stream is not overwritten)
+    const bf16_t* rp = p.resid ? (const bf16_t*)p.resid + (long)row * p.ld_resid + lr * 8
+                               : (p.accumulate_dx ? dxp : nullptr);
+    if (rp) unpack8(*(const uint4*)rp, o8);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float r = rstd * (d[i] * ga[i] - s1 - xh[i] * s2);
-      o8[i] = p.accumulate_dx ? o8[i] + r : r;
+      o8[i] = rp ? o8[i] + r : r;
     }
     *(uint4*)dxp = pack8(o8);
   }

@@ -57,10 +57,13 @@ _TILE_SHAPES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64)}
 
 
 def _workspace():
+    """Split-K slab scratch, one per (device, stream): GEMMs enqueued on different streams
+    (the executor's weight-gradient side stream) may run concurrently."""
     dev = torch.cuda.current_device()
-    ws = _WS.get(dev)
+    key = (dev, torch.cuda.current_stream().cuda_stream)
+    ws = _WS.get(key)
     if ws is None:
-        ws = _WS[dev] = torch.zeros(WS_FLOATS, device=f"cuda:{dev}", dtype=torch.float32)
+        ws = _WS[key] = torch.zeros(WS_FLOATS, device=f"cuda:{dev}", dtype=torch.float32)
     return ws
 
 
@@ -104,25 +107,60 @@ def plan(M, N, K, a_mode, b_mode, c_mode):
     return tile, split
 
 
-def gemm(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK, c_mode=L.OUT_BF16,
-         conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=None, bias=None,
-         resid=None, ld_resid=0, bias_grad=None, tile=0):
+def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK, c_mode=L.OUT_BF16,
+              conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=None, bias=None,
+              resid=None, ld_resid=0, bias_grad=None, tile=0, ws_offset=0):
+    """EncdiffGemmArgs with the measured (tile, split) plan; split-K slabs start `ws_offset`
+    floats into this stream's workspace."""
     if split_k is None or tile == 0:
         t, sp = plan(M, N, K, a_mode, b_mode, c_mode)
         tile = tile or t
         split_k = split_k or sp
     ws = None
     if split_k > 1 and c_mode in (L.OUT_BF16, L.OUT_F32, L.OUT_F32_ACCUM):
-        need = split_k * M * N + (split_k * M if bias_grad is not None else 0)
+        need = ws_offset + split_k * M * N + (split_k * M if bias_grad is not None else 0)
         assert need <= WS_FLOATS, "split-K slabs exceed the workspace"
         ws = _workspace()
-    args = L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=b_mode, c_mode=c_mode,
+    return L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=b_mode, c_mode=c_mode,
                       a=_p(a), lda=lda, b=_p(b), ldb=ldb, c=_p(c), ldc=ldc,
                       conv=conv if conv is not None else L.ConvGeom(),
                       conv_cout=conv_cout, convw_cin=convw_cin, alpha=alpha, split_k=split_k,
                       bias=_p(bias), resid=_p(resid), ld_resid=ld_resid, bias_grad=_p(bias_grad), tile=tile,
-                      workspace=_p(ws))
+                      workspace=None if ws is None else ws.data_ptr() + 4 * ws_offset)
+
+
+def ws_floats(args) -> int:
+    """Workspace floats a GEMM's split-K slabs (+ bias-gradient slabs) occupy."""
+    if args.split_k <= 1 or args.c_mode not in (L.OUT_BF16, L.OUT_F32, L.OUT_F32_ACCUM):
+        return 0
+    return args.split_k * args.M * args.N + (args.split_k * args.M if args.bias_grad else 0)
+
+
+def gemm(M, N, K, a, lda, b, ldb, c, ldc, **kw):
+    args = gemm_args(M, N, K, a, lda, b, ldb, c, ldc, **kw)
     check(lib.encdiff_gemm(C.byref(args), _s()), "encdiff_gemm")
+
+
+PAIR = True  # fuse a layer's weight- and input-gradient GEMMs into one launch (encdiff_gemm_pair)
+
+
+def gemm_pair(wgrad_args, dgrad_fn):
+    """Launch a weight-gradient GEMM and an input-gradient GEMM together.  `dgrad_fn(ws_offset)`
+    returns the input-gradient GemmArgs with its split-K slabs placed after the weight
+    gradient's, so the two never share workspace."""
+    off = ws_floats(wgrad_args)
+    d = dgrad_fn(0)
+    if off and ws_floats(d):
+        if off + ws_floats(d) > WS_FLOATS:  # both sets of slabs do not fit: run back to back
+            check(lib.encdiff_gemm(C.byref(wgrad_args), _s()), "encdiff_gemm")
+            check(lib.encdiff_gemm(C.byref(d), _s()), "encdiff_gemm")
+            return
+        d = dgrad_fn(off)
+    if not PAIR:
+        check(lib.encdiff_gemm(C.byref(wgrad_args), _s()), "encdiff_gemm")
+        check(lib.encdiff_gemm(C.byref(d), _s()), "encdiff_gemm")
+        return
+    check(lib.encdiff_gemm_pair(C.byref(wgrad_args), C.byref(d), _s()), "encdiff_gemm_pair")
 
 
 # ------------------------------------------------------------------ linear layers
@@ -142,13 +180,30 @@ def linear_dgrad(dy, w, dx, resid=None):
          resid=resid, ld_resid=_ld(resid) if resid is not None else 0)
 
 
-def linear_wgrad(dy, x, dw, db=None):
-    """dw[N][K] += dy[M][N]^T x[M][K] (split-K slabs summed in order: reproducible);
-    db[N] += sum_m dy[m][n] (fp32 atomics)."""
+def linear_dgrad_args(dy, w, dx, resid=None, ws_offset=0):
+    M, N = dy.shape
+    K = w.shape[1]
+    return gemm_args(M, K, N, dy, _ld(dy), w, _ld(w), dx, _ld(dx), b_mode=L.OPB_ROWN,
+                     resid=resid, ld_resid=_ld(resid) if resid is not None else 0, ws_offset=ws_offset)
+
+
+def linear_wgrad_args(dy, x, dw, db=None):
     M, N = dy.shape
     K = x.shape[1]
-    gemm(N, K, M, dy, _ld(dy), x, _ld(x), dw, K, a_mode=L.OPA_ROWM, b_mode=L.OPB_ROWN,
-         c_mode=L.OUT_F32_ACCUM, bias_grad=db)
+    return gemm_args(N, K, M, dy, _ld(dy), x, _ld(x), dw, K, a_mode=L.OPA_ROWM, b_mode=L.OPB_ROWN,
+                     c_mode=L.OUT_F32_ACCUM, bias_grad=db)
+
+
+def linear_wgrad(dy, x, dw, db=None):
+    """dw[N][K] += dy[M][N]^T x[M][K] (split-K slabs summed in order: reproducible);
+    db[N] += sum_m dy[m][n]."""
+    args = linear_wgrad_args(dy, x, dw, db)
+    check(lib.encdiff_gemm(C.byref(args), _s()), "encdiff_gemm")
+
+
+def linear_bwd(dy, w, x, dx, dw, db=None, resid=None):
+    """Backward of one linear layer: dw += dy^T x (+ db), dx = dy w (+ resid), one launch."""
+    gemm_pair(linear_wgrad_args(dy, x, dw, db), lambda off: linear_dgrad_args(dy, w, dx, resid, off))
 
 
 # ------------------------------------------------------------------ 3x3 convolutions
@@ -177,12 +232,33 @@ def conv3x3_wgrad(dy, x, g: Geom, cin, dw_ref, db=None, resample=L.RESAMPLE_NONE
          c_mode=L.OUT_F32_ATOMIC_CONVW, conv=_conv_geom(g, cin, resample, x), convw_cin=cin, bias_grad=db)
 
 
+def conv3x3_wgrad_cl_args(dy, x, g: Geom, cin, dw_cl, db=None, resample=L.RESAMPLE_NONE):
+    cout = dy.shape[1]
+    return gemm_args(cout, 9 * cin, g.pixels, dy, _ld(dy), x, _ld(x), dw_cl, _ld(dw_cl), a_mode=L.OPA_ROWM,
+                     b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32_ACCUM, conv=_conv_geom(g, cin, resample, x),
+                     bias_grad=db)
+
+
 def conv3x3_wgrad_cl(dy, x, g: Geom, cin, dw_cl, db=None, resample=L.RESAMPLE_NONE):
     """dw_cl[cout][9*cin] (fp32, channels-last [co][kh][kw][ci]) += dy^T im2col(resample(x))
     (split-K slabs summed in order: reproducible)."""
-    cout = dy.shape[1]
-    gemm(cout, 9 * cin, g.pixels, dy, _ld(dy), x, _ld(x), dw_cl, _ld(dw_cl), a_mode=L.OPA_ROWM,
-         b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32_ACCUM, conv=_conv_geom(g, cin, resample, x), bias_grad=db)
+    args = conv3x3_wgrad_cl_args(dy, x, g, cin, dw_cl, db, resample)
+    check(lib.encdiff_gemm(C.byref(args), _s()), "encdiff_gemm")
+
+
+def conv3x3_dgrad_args(dy, g: Geom, wf, dx, resid=None, ws_offset=0):
+    cout = wf.shape[0]
+    cin = wf.shape[1] // 9
+    return gemm_args(g.pixels, cin, 9 * cout, dy, _ld(dy), wf, _ld(wf), dx, _ld(dx), a_mode=L.OPA_IM2COL,
+                     b_mode=L.OPB_CONV_DGRAD, conv=_conv_geom(g, cout, L.RESAMPLE_NONE, dy), conv_cout=cout,
+                     resid=resid, ld_resid=_ld(resid) if resid is not None else 0, ws_offset=ws_offset)
+
+
+def conv3x3_bwd_cl(dy, g: Geom, wf, x, cin, dw_cl, dx, db=None, resample=L.RESAMPLE_NONE):
+    """Backward of one 3x3 conv: dw_cl += dy^T im2col(resample(x)) (+ db) and
+    dx = conv3x3^T(dy) at the conv resolution, one launch."""
+    gemm_pair(conv3x3_wgrad_cl_args(dy, x, g, cin, dw_cl, db, resample),
+              lambda off: conv3x3_dgrad_args(dy, g, wf, dx, None, off))
 
 
 # ------------------------------------------------------------------ normalisation
@@ -219,13 +295,15 @@ def layernorm_fwd(x, gamma, beta, y, stats, eps=1e-5):
     check(lib.encdiff_layernorm_fwd(C.byref(a), _s()), "encdiff_layernorm_fwd")
 
 
-def layernorm_bwd(x, gamma, stats, dy, dx, dgamma_part, dbeta_part, accumulate=False, ld_part=None):
+def layernorm_bwd(x, gamma, stats, dy, dx, dgamma_part, dbeta_part, accumulate=False, ld_part=None, resid=None):
+    """dx = LN_bwd(dy) (+ dx if accumulate) (+ resid: the residual-branch gradient, out of place)."""
     rows, c = x.shape
     parts = layernorm_parts(rows, c)
     ld_part = c if ld_part is None else ld_part
     a = L.LayerNormArgs(rows=rows, c=c, eps=0.0, x=_p(x), ldx=_ld(x), gamma=_p(gamma), stats=_p(stats),
                         dy=_p(dy), lddy=_ld(dy), dx=_p(dx), lddx=_ld(dx), accumulate_dx=int(accumulate),
-                        dgamma_part=_p(dgamma_part), dbeta_part=_p(dbeta_part), ld_part=ld_part, parts=parts)
+                        dgamma_part=_p(dgamma_part), dbeta_part=_p(dbeta_part), ld_part=ld_part, parts=parts,
+                        resid=_p(resid), ld_resid=_ld(resid) if resid is not None else 0)
     check(lib.encdiff_layernorm_bwd(C.byref(a), _s()), "encdiff_layernorm_bwd")
 
 

@@ -5,8 +5,8 @@ ResBlock._forward (:255-275), SpatialTransformer / BasicTransformerBlock /
 CrossAttention / GEGLU (attention.py:37-261) as a static schedule of C-ABI kernel
 launches over preallocated NHWC bf16 activations.  No torch autograd is used
 inside: the backward is written out layer by layer, weight gradients land in the
-fp32 arena (atomics for split-K GEMMs, one partial-sum reduction for all norm
-affine parameters), and only the gradient w.r.t. the context (concept tokens) is
+fp32 arena (split-K slabs summed in a fixed order, one partial-sum reduction for all
+norm affine parameters), and only the gradient w.r.t. the context (concept tokens) is
 handed back to torch for the as-is concept encoder.
 
 Fusions relative to the reference op graph:
@@ -15,7 +15,8 @@ Fusions relative to the reference op graph:
   * bias, residual adds and the skip path inside GEMM epilogues,
   * all 28 emb_layers projections as ONE GEMM, all 16 cross-attention K/V
     projections of the 20 concept tokens as ONE GEMM (fwd, dgrad and wgrad),
-  * q/k/v of self-attention as one [3C] GEMM, heads read in place ('b n (h d)').
+  * q/k/v of self-attention as one [3C] GEMM, heads read in place ('b n (h d)'),
+  * each layer's weight- and input-gradient GEMMs as ONE launch (encdiff_gemm_pair).
 """
 from __future__ import annotations
 
@@ -329,8 +330,7 @@ class UNetExecutor:
                 continue
             M = B * t_.h * t_.h
             c = t_.c
-            self.st_scratch[key] = dict(d_t=t(M, c), d_a=t(M, 4 * c), d_f=t(M, 8 * c), d_n=t(M, c), d_o=t(M, c),
-                                        d_qkv=t(M, 3 * c), d_q2=t(M, c), d_g=t(M, c))
+            self.st_scratch[key] = dict(d_a=t(M, 4 * c), d_n=t(M, c), d_o=t(M, c), d_g=t(M, c))
         self.res_scratch = {}
 
     def _res_bufs(self, r: ResSpec, B):
@@ -350,10 +350,14 @@ class UNetExecutor:
         t = self._t
         M = B * s.h * s.h
         c = s.c
+        # gradients the weight-gradient GEMMs read get a buffer of their own (written once per
+        # step; LayerNorm backward adds its residual branch out of place)
         return dict(gn=t(M, c), stg=t(B, 64, F32), t0=t(M, c), n1=t(M, c), s1=t(M, 2, F32), qkv=t(M, 3 * c),
                     o1=t(M, c), lse1=t(B * s.heads, s.h * s.h, F32), t1=t(M, c), n2=t(M, c), s2=t(M, 2, F32),
                     q2=t(M, c), o2=t(M, c), lse2=t(B * s.heads, s.h * s.h, F32), t2=t(M, c), n3=t(M, c),
-                    s3=t(M, 2, F32), f=t(M, 8 * c), a=t(M, 4 * c), t3=t(M, c), out=t(M, c), d_in=t(M, c))
+                    s3=t(M, 2, F32), f=t(M, 8 * c), a=t(M, 4 * c), t3=t(M, c), out=t(M, c), d_in=t(M, c),
+                    d_t3=t(M, c), d_t2=t(M, c), d_t1=t(M, c), d_t0=t(M, c), d_f=t(M, 8 * c), d_q2=t(M, c),
+                    d_qkv=t(M, 3 * c))
 
     # ---------------------------------------------------------------- forward
     def forward(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor) -> torch.Tensor:
@@ -538,21 +542,29 @@ class UNetExecutor:
                                 self.G("input_blocks.0.0.weight"), self.G("input_blocks.0.0.bias"))
         # batched emb_layers backward -> time MLP
         ops.ew(L.EW_F32_TO_BF16, self.dE, self.dE16)
-        ops.linear_dgrad(self.dE16, self.W("emb_all"), self.d_emb_s)
-        ops.linear_wgrad(self.dE16, self.emb_s, self.emb_w_grad, self.emb_bias_grad)
+        ops.linear_bwd(self.dE16, self.W("emb_all"), self.emb_s, self.d_emb_s, self.emb_w_grad, self.emb_bias_grad)
         ops.ew(L.EW_SILU_BWD, self.emb, self.d_emb, x2=self.d_emb_s)
-        ops.linear_wgrad(self.d_emb, self.ta1, self.G("time_embed.2.weight"), self.G("time_embed.2.bias"))
-        ops.linear_dgrad(self.d_emb, self.W("time_embed.2.weight"), self.d_ta1)
+        ops.linear_bwd(self.d_emb, self.W("time_embed.2.weight"), self.ta1, self.d_ta1, self.G("time_embed.2.weight"),
+                       self.G("time_embed.2.bias"))
         ops.ew(L.EW_SILU_BWD, self.th1, self.d_th1, x2=self.d_ta1)
         ops.linear_wgrad(self.d_th1, self.temb0, self.G("time_embed.0.weight"), self.G("time_embed.0.bias"))
-        # batched cross-attention K/V backward -> context gradient
-        ops.linear_wgrad(self.dKV, self.ctx16, self.kv_w_grad)
+        # batched cross-attention K/V backward -> context gradient (fp32 output: separate GEMM)
         ops.gemm(B * self.lu, self.cd, sp.kv_total, self.dKV, self.dKV.stride(0), self.W("kv_all"), self.cd,
                  self.d_ctx, self.cd, b_mode=L.OPB_ROWN, c_mode=L.OUT_F32)
+        ops.linear_wgrad(self.dKV, self.ctx16, self.kv_w_grad)
         # fold all norm affine partial sums into the arena
         self.gn.reduce()
         self.ln.reduce()
         return self.d_ctx
+
+    def conv_bwd(self, dy, g, cin, name, x, dx, db, resample=0):
+        """Backward of a 3x3 conv (weight `name`): weight and input gradient in one launch."""
+        if name in self.arena.cl:
+            ops.conv3x3_bwd_cl(dy, g, self.W(name), x, cin, self.arena.raw(self.arena.grad, name), dx, db,
+                               resample=resample)
+        else:
+            ops.conv3x3_dgrad(dy, g, self.W(name), dx)
+            self.conv_wgrad(dy, x, g, cin, name, db, resample=resample)
 
     def _layer_bwd(self, layer, dout, dx, acc):
         if isinstance(layer, ResSpec):
@@ -566,9 +578,9 @@ class UNetExecutor:
         x = S["x"]
         gi, go = Geom(B, r.hin, r.hin), Geom(B, r.hout, r.hout)
         pre = r.prefix
-        # conv2
-        ops.conv3x3_dgrad(dout, go, self.W(pre + "out_layers.3.weight"), S["d_a2"])
-        self.conv_wgrad(dout, S["a2"], go, r.cout, pre + "out_layers.3.weight", self.G(pre + "out_layers.3.bias"))
+        # conv2: input + weight gradient in one launch
+        self.conv_bwd(dout, go, r.cout, pre + "out_layers.3.weight", S["a2"], S["d_a2"],
+                      self.G(pre + "out_layers.3.bias"))
         # GN2 + FiLM + SiLU
         dg, db = self.gn.parts(pre + "out_layers.0.weight", r.cout)
         ops.groupnorm_bwd(S["h1"], go, self.P(pre + "out_layers.0.weight"), self.P(pre + "out_layers.0.bias"),
@@ -580,23 +592,19 @@ class UNetExecutor:
             a1, rs = S["a1r"], L.RESAMPLE_NONE
         else:
             a1, rs = S["a1"], r.updown
-        self.conv_wgrad(S["d_h1"], a1, go, r.cin, pre + "in_layers.2.weight", self.G(pre + "in_layers.2.bias"),
-                        resample=rs)
         dg, db = self.gn.parts(pre + "in_layers.0.weight", r.cin)
+        d_a1 = S["d_a1"]
+        self.conv_bwd(S["d_h1"], go, r.cin, pre + "in_layers.2.weight", a1, S["d_a1r"] if r.updown else d_a1,
+                      self.G(pre + "in_layers.2.bias"), resample=rs)
         if r.updown:
-            ops.conv3x3_dgrad(S["d_h1"], go, self.W(pre + "in_layers.2.weight"), S["d_a1r"])
-            d_a1 = S["d_a1"]
             ops.resample_bwd(S["d_a1r"], d_a1, gi, r.updown)
-        else:
-            d_a1 = S["d_a1"]
-            ops.conv3x3_dgrad(S["d_h1"], go, self.W(pre + "in_layers.2.weight"), d_a1)
         ops.groupnorm_bwd(x, gi, self.P(pre + "in_layers.0.weight"), self.P(pre + "in_layers.0.bias"), S["st1"],
                           GN_EPS, True, d_a1, dx, dg, db, accumulate=acc, ld_part=self.gn.ld)
         # skip path
         if r.cin != r.cout:
-            ops.linear_dgrad(dout, self.W(pre + "skip_connection.weight"), dx, resid=dx)
-            ops.linear_wgrad(dout, x, self.G(pre + "skip_connection.weight").view(r.cout, r.cin),
-                             self.G(pre + "skip_connection.bias"))
+            ops.linear_bwd(dout, self.W(pre + "skip_connection.weight"), x, dx,
+                           self.G(pre + "skip_connection.weight").view(r.cout, r.cin),
+                           self.G(pre + "skip_connection.bias"), resid=dx)
         elif r.updown:
             ops.resample_bwd(dout, dx, gi, r.updown, accumulate=True)
         else:
@@ -610,49 +618,51 @@ class UNetExecutor:
         tb = s.prefix + "transformer_blocks.0."
         ntok = s.h * s.h
         X = self.st_scratch[(s.h, c)]
-        d_t, d_a, d_f, d_n, d_o = X["d_t"], X["d_a"], X["d_f"], X["d_n"], X["d_o"]
+        d_a, d_n, d_o = X["d_a"], X["d_n"], X["d_o"]
         # residual x_in
         ops.ew(L.EW_COPY, dout, dx, accumulate=acc)
         # proj_out
-        ops.linear_dgrad(dout, self.W(s.prefix + "proj_out.weight"), d_t)
-        ops.linear_wgrad(dout, S["t3"], self.G(s.prefix + "proj_out.weight").view(c, c), self.G(s.prefix + "proj_out.bias"))
-        # FF: d_t == d(t3)
-        ops.linear_dgrad(d_t, self.W(tb + "ff.net.2.weight"), d_a)
-        ops.linear_wgrad(d_t, S["a"], self.G(tb + "ff.net.2.weight"), self.G(tb + "ff.net.2.bias"))
-        ops.geglu_bwd(S["f"], d_a, d_f)
-        ops.linear_dgrad(d_f, self.W(tb + "ff.net.0.proj.weight"), d_n)
-        ops.linear_wgrad(d_f, S["n3"], self.G(tb + "ff.net.0.proj.weight"), self.G(tb + "ff.net.0.proj.bias"))
+        d_t3 = S["d_t3"]
+        ops.linear_bwd(dout, self.W(s.prefix + "proj_out.weight"), S["t3"], d_t3,
+                       self.G(s.prefix + "proj_out.weight").view(c, c), self.G(s.prefix + "proj_out.bias"))
+        # FF
+        ops.linear_bwd(d_t3, self.W(tb + "ff.net.2.weight"), S["a"], d_a, self.G(tb + "ff.net.2.weight"),
+                       self.G(tb + "ff.net.2.bias"))
+        ops.geglu_bwd(S["f"], d_a, S["d_f"])
+        ops.linear_bwd(S["d_f"], self.W(tb + "ff.net.0.proj.weight"), S["n3"], d_n,
+                       self.G(tb + "ff.net.0.proj.weight"), self.G(tb + "ff.net.0.proj.bias"))
         dg, db = self.ln.parts(tb + "norm3.weight", c)
-        ops.layernorm_bwd(S["t2"], self.P(tb + "norm3.weight"), S["s3"], d_n, d_t, dg, db, accumulate=True,
-                          ld_part=self.ln.ld)
-        # cross-attention: d_t == d(t2)
-        ops.linear_dgrad(d_t, self.W(tb + "attn2.to_out.0.weight"), d_o)
-        ops.linear_wgrad(d_t, S["o2"], self.G(tb + "attn2.to_out.0.weight"), self.G(tb + "attn2.to_out.0.bias"))
+        d_t2 = S["d_t2"]  # d(t2) = d(t3) (residual) + norm3 backward
+        ops.layernorm_bwd(S["t2"], self.P(tb + "norm3.weight"), S["s3"], d_n, d_t2, dg, db, ld_part=self.ln.ld,
+                          resid=d_t3)
+        # cross-attention
+        ops.linear_bwd(d_t2, self.W(tb + "attn2.to_out.0.weight"), S["o2"], d_o,
+                       self.G(tb + "attn2.to_out.0.weight"), self.G(tb + "attn2.to_out.0.bias"))
         k2 = self.KV[:, s.kv_off:s.kv_off + c]
         v2 = self.KV[:, s.kv_off + c:s.kv_off + 2 * c]
         dk2 = self.dKV[:, s.kv_off:s.kv_off + c]
         dv2 = self.dKV[:, s.kv_off + c:s.kv_off + 2 * c]
-        ops.attention_bwd(S["q2"], k2, v2, S["o2"], S["lse2"], d_o, X["d_q2"], dk2, dv2, B, s.heads, ntok, self.lu,
+        ops.attention_bwd(S["q2"], k2, v2, S["o2"], S["lse2"], d_o, S["d_q2"], dk2, dv2, B, s.heads, ntok, self.lu,
                           s.dh)
-        ops.linear_dgrad(X["d_q2"], self.W(tb + "attn2.to_q.weight"), d_n)
-        ops.linear_wgrad(X["d_q2"], S["n2"], self.G(tb + "attn2.to_q.weight"))
+        ops.linear_bwd(S["d_q2"], self.W(tb + "attn2.to_q.weight"), S["n2"], d_n, self.G(tb + "attn2.to_q.weight"))
         dg, db = self.ln.parts(tb + "norm2.weight", c)
-        ops.layernorm_bwd(S["t1"], self.P(tb + "norm2.weight"), S["s2"], d_n, d_t, dg, db, accumulate=True,
-                          ld_part=self.ln.ld)
-        # self-attention: d_t == d(t1)
-        ops.linear_dgrad(d_t, self.W(tb + "attn1.to_out.0.weight"), d_o)
-        ops.linear_wgrad(d_t, S["o1"], self.G(tb + "attn1.to_out.0.weight"), self.G(tb + "attn1.to_out.0.bias"))
-        qkv, dqkv = S["qkv"], X["d_qkv"]
+        d_t1 = S["d_t1"]
+        ops.layernorm_bwd(S["t1"], self.P(tb + "norm2.weight"), S["s2"], d_n, d_t1, dg, db, ld_part=self.ln.ld,
+                          resid=d_t2)
+        # self-attention
+        ops.linear_bwd(d_t1, self.W(tb + "attn1.to_out.0.weight"), S["o1"], d_o,
+                       self.G(tb + "attn1.to_out.0.weight"), self.G(tb + "attn1.to_out.0.bias"))
+        qkv, dqkv = S["qkv"], S["d_qkv"]
         ops.attention_bwd(qkv[:, :c], qkv[:, c:2 * c], qkv[:, 2 * c:], S["o1"], S["lse1"], d_o, dqkv[:, :c],
                           dqkv[:, c:2 * c], dqkv[:, 2 * c:], B, s.heads, ntok, ntok, s.dh)
-        ops.linear_dgrad(dqkv, self.W(s.prefix + "qkv"), d_n)
-        ops.linear_wgrad(dqkv, S["n1"], self.qkv_grad[s.prefix])
+        ops.linear_bwd(dqkv, self.W(s.prefix + "qkv"), S["n1"], d_n, self.qkv_grad[s.prefix])
         dg, db = self.ln.parts(tb + "norm1.weight", c)
-        ops.layernorm_bwd(S["t0"], self.P(tb + "norm1.weight"), S["s1"], d_n, d_t, dg, db, accumulate=True,
-                          ld_part=self.ln.ld)
-        # proj_in: d_t == d(t0)
-        ops.linear_dgrad(d_t, self.W(s.prefix + "proj_in.weight"), X["d_g"])
-        ops.linear_wgrad(d_t, S["gn"], self.G(s.prefix + "proj_in.weight").view(c, c), self.G(s.prefix + "proj_in.bias"))
+        d_t0 = S["d_t0"]
+        ops.layernorm_bwd(S["t0"], self.P(tb + "norm1.weight"), S["s1"], d_n, d_t0, dg, db, ld_part=self.ln.ld,
+                          resid=d_t1)
+        # proj_in
+        ops.linear_bwd(d_t0, self.W(s.prefix + "proj_in.weight"), S["gn"], X["d_g"],
+                       self.G(s.prefix + "proj_in.weight").view(c, c), self.G(s.prefix + "proj_in.bias"))
         dg, db = self.gn.parts(s.prefix + "norm.weight", c)
         ops.groupnorm_bwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["stg"], ST_GN_EPS,
                           False, X["d_g"], dx, dg, db, accumulate=True, ld_part=self.gn.ld)

@@ -103,6 +103,14 @@ typedef struct EncdiffGemmArgs {
 
 int encdiff_gemm(const EncdiffGemmArgs* args, void* stream);
 
+/* Two independent GEMMs of one layer's backward in ONE launch: the weight gradient
+ * (a_mode OPA_ROWM) and the input gradient (linear: OPA_ROWK x OPB_ROWN; 3x3 conv:
+ * OPA_IM2COL x OPB_CONV_DGRAD), their split-K finalizes in one more.  Results are
+ * identical to two encdiff_gemm calls; pairs outside these forms run as two calls.  When
+ * both use split-K their workspaces must be distinct.  Replaces the autograd backward of
+ * one nn.Linear / nn.Conv2d (openaimodel_enc.py:230,237-241; attention.py:159-167,43,58). */
+int encdiff_gemm_pair(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad, void* stream);
+
 /* ---------------------------------------------------------------- GroupNorm
  * y = act( GN(x) * (1 + scale[b,c]) + shift[b,c] )
  * Replaces GroupNorm32 + SiLU (+ FiLM) of ResBlock in/out_layers and UNet.out
@@ -151,6 +159,8 @@ typedef struct EncdiffLayerNormArgs {
   long ld_part;
   int parts;                 /* number of partial rows (grid size of the backward) */
   int pad_;
+  const void* resid; long ld_resid; /* backward: optional bf16 residual-branch gradient:
+                                        dx = resid + LN_bwd (out of place; may alias dx) */
 } EncdiffLayerNormArgs;
 
 int encdiff_layernorm_fwd(const EncdiffLayerNormArgs* args, void* stream);

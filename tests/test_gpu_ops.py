@@ -459,3 +459,46 @@ def test_encoder_warp(O, B):
     assert rel(u.grad, u2.grad) < 1e-5
     for (n, p), (_, pr) in zip(enc.net.named_parameters(), ref.net.named_parameters()):
         assert rel(p.grad, pr.grad) < 1e-4, n
+
+
+@pytest.mark.parametrize("kind,M,C,K", [("lin", 32768, 64, 64), ("lin", 2048, 256, 256), ("lin", 8192, 128, 512),
+                                         ("conv", 16, 64, 64), ("conv", 8, 256, 256), ("conv", 4, 256, 512)])
+def test_gemm_pair_matches_two_launches(O, kind, M, C, K):
+    """encdiff_gemm_pair (weight + input gradient of one layer in ONE launch) is bitwise
+    identical to the two separate GEMMs, whatever tiles / split-K the plan picks."""
+    import encdiff_amd._lib as L
+    from encdiff_amd.ops import Geom
+    torch.manual_seed(3)
+    outs = []
+    if kind == "lin":
+        dy, x, w = bf(M, C), bf(M, K), bf(C, K, scale=K ** -0.5)
+        for pair in (False, True):
+            dw = torch.ones(C, K, device=dev)
+            db = torch.ones(C, device=dev)
+            dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+            if pair:
+                O.linear_bwd(dy, w, x, dx, dw, db)
+            else:
+                O.linear_wgrad(dy, x, dw, db)
+                O.linear_dgrad(dy, w, dx)
+            outs.append((dw, db, dx))
+        assert rel(outs[1][0] - 1, dy.float().t() @ x.float()) < 2e-3
+        assert rel(outs[1][2], dy.float() @ w.float()) < 1e-2
+    else:
+        g = Geom(128, M, M)
+        cin, cout = K, C
+        dy, x, wf = bf(g.pixels, cout), bf(g.pixels, cin), bf(cout, 9 * cin, scale=(9 * cin) ** -0.5)
+        for pair in (False, True):
+            dw = torch.zeros(cout, 9 * cin, device=dev)
+            db = torch.zeros(cout, device=dev)
+            dx = torch.empty(g.pixels, cin, device=dev, dtype=torch.bfloat16)
+            if pair:
+                O.conv3x3_bwd_cl(dy, g, wf, x, cin, dw, dx, db)
+            else:
+                O.conv3x3_wgrad_cl(dy, x, g, cin, dw, db)
+                O.conv3x3_dgrad(dy, g, wf, dx)
+            outs.append((dw, db, dx))
+        ref_dx = F.conv_transpose2d(nhwc(dy, g), wf.float().view(cout, 3, 3, cin).permute(0, 3, 1, 2), padding=1)
+        assert rel(nhwc(outs[1][2], g), ref_dx) < 1e-2
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
