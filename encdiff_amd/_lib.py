@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("ENCDIFF_LIB", os.path.join(HERE, "libencdiff_hip.so")
 OPA_ROWK, OPA_IM2COL, OPA_ROWM = 0, 1, 2
 OPB_ROWK, OPB_ROWN, OPB_CONV_DGRAD, OPB_IM2COL = 0, 1, 2, 3
 OUT_BF16, OUT_F32, OUT_F32_ATOMIC, OUT_F32_ATOMIC_CONVW, OUT_F32_ACCUM = 0, 1, 2, 3, 4
-RESAMPLE_NONE, RESAMPLE_DOWN2, RESAMPLE_UP2, RESAMPLE_STRIDE2 = 0, 1, 2, 3
+RESAMPLE_NONE, RESAMPLE_DOWN2, RESAMPLE_UP2, RESAMPLE_STRIDE2, RESAMPLE_K4S2, RESAMPLE_K4S2_T = 0, 1, 2, 3, 4, 5
 (EW_COPY, EW_SILU, EW_SILU_BWD, EW_GEGLU, EW_GEGLU_BWD, EW_ADD, EW_RESAMPLE, EW_RESAMPLE_BWD,
  EW_F32_TO_BF16, EW_BF16_TO_F32) = range(10)
 
@@ -83,6 +83,14 @@ class SmallConvArgs(C.Structure):
                 ("dx", vp), ("lddx", C.c_long), ("dweight", vp), ("dbias", vp)]
 
 
+class BatchNormArgs(C.Structure):
+    _fields_ = [("rows", C.c_int), ("c", C.c_int), ("eps", C.c_float), ("momentum", C.c_float),
+                ("relu", C.c_int), ("pad_", C.c_int), ("x", vp), ("ldx", C.c_long), ("gamma", vp), ("beta", vp),
+                ("y", vp), ("ldy", C.c_long), ("mean", vp), ("rstd", vp), ("running_mean", vp), ("running_var", vp),
+                ("partials", vp), ("counter", vp), ("dy", vp), ("lddy", C.c_long), ("dx", vp), ("lddx", C.c_long),
+                ("dgamma", vp), ("dbeta", vp)]
+
+
 class PackJob(C.Structure):
     _fields_ = [("src_off", C.c_longlong), ("dst_off", C.c_longlong), ("rows", C.c_int), ("cols", C.c_int),
                 ("kind", C.c_int), ("cin", C.c_int)]
@@ -113,6 +121,10 @@ _PROTOS = {
                                  vp, vp],
     "encdiff_gather_images_u8": [vp, C.c_longlong, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, C.c_int,
                                  vp, vp],
+    "encdiff_batchnorm_partials_floats": [C.c_int, C.c_int],
+    "encdiff_batchnorm_fwd": [C.POINTER(BatchNormArgs), vp],
+    "encdiff_batchnorm_bwd": [C.POINTER(BatchNormArgs), vp],
+    "encdiff_nchw_to_rows": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_long, vp],
     "encdiff_version": [],
 }
 

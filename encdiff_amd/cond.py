@@ -1,0 +1,252 @@
+"""HIP executor of the concept encoder's convolution trunk.
+
+Encoder4.encoder (openaimodel_enc.py:1002-1012) is
+
+    Conv2d(3, d, 4, 2, 1)  BN ReLU      64x64 -> 32x32
+    Conv2d(d, d, 4, 2, 1)  BN ReLU            -> 16x16
+    Conv2d(d, d, 4, 2, 1)  BN                 ->  8x8
+    Conv2d(d, d, 4, 2, 1)  BN ReLU            ->  4x4
+    EncResBlock(bn)  BN ReLU  EncResBlock(bn)       (x + conv1x1(ReLU(BN(conv3x3(ReLU(x))))))
+    View(-1, d*16)  Linear(d*16, latent_unit)
+
+trained with batch statistics.  The reference runs it in fp32 through cuDNN/MIOpen
+(~60 launches, ~1.9 ms per fwd+bwd at B=128 on the MI355X).  Here the convolutions are
+the UNet's implicit-im2col MFMA GEMMs (Conv2d(k4,s2,p1) is an im2col mode; its input
+gradient the transposed mode; each layer's input and weight gradients one paired launch),
+BatchNorm+ReLU are two launches each way (deterministic last-workgroup folds), and
+activations are NHWC bf16.  Both EncResBlock inputs are ReLU outputs, so their leading
+ReLU is the identity and its gradient mask equals the preceding BN-ReLU's (mask^2 = mask).
+The trunk hands its output to the reference modules as the fp32 NCHW-flattened
+(B, d*16) tensor, so `Linear(d*16, latent_unit)` and the warp MLPs follow unchanged.
+
+Weight gradients are written into the fp32 parameter arena (the modules' .grad views);
+only d(input image) is not computed (the image carries no gradient).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List
+
+import torch
+
+from . import _lib as L
+from . import ops
+from .arena import PackTable
+from .ops import Geom
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+class _Conv:
+    def __init__(self, name: str, mod: torch.nn.Conv2d, hout: int, k4: bool):
+        self.name, self.mod, self.hout, self.k4 = name, mod, hout, k4
+        self.cout, self.cin = mod.weight.shape[0], mod.weight.shape[1]
+
+
+class Encoder4TrunkExecutor:
+    """Binds Encoder4.encoder (all but View + Linear) to the parameter arena."""
+
+    def __init__(self, enc, arena, prefix: str):
+        seq = enc.encoder
+        self.enc = enc
+        self.arena = arena
+        self.prefix = prefix
+        self.dev = arena.device
+        mods = list(seq)
+        conv_idx = [0, 3, 6, 8]
+        bn_idx = [1, 4, 7, 9]
+        relu_after = [True, True, False, True]
+        self.d = mods[0].weight.shape[0]
+        self.cin_img = mods[0].weight.shape[1]
+        assert mods[0].kernel_size == (4, 4) and self.cin_img <= 8, "Encoder4 trunk layout"
+        hs = [32, 16, 8, 4]
+        self.convs = [_Conv(f"encoder.{i}", mods[i], h, True) for i, h in zip(conv_idx, hs)]
+        self.bns = [(f"encoder.{i}", mods[i], r) for i, r in zip(bn_idx, relu_after)]
+        self.res = []
+        for ri, bi in ((11, 12), (14, None)):
+            rb = mods[ri]
+            c3, bnm, c1 = rb.convs[1], rb.convs[2], rb.convs[4]
+            self.res.append(dict(prefix=f"encoder.{ri}.convs.", conv3=c3, bn=bnm, conv1=c1,
+                                 post_bn=(f"encoder.{bi}", mods[bi]) if bi is not None else None))
+        self.flat = mods[16]
+        pk = PackTable(arena)
+        a = arena
+        c0 = self.convs[0]
+        # first conv: [d][3][4][4] -> [d][16 taps][8] (channels padded with zeros)
+        pk.add("c0", a.offsets[self.pn(c0.name + ".weight")][0], self.d, 16 * 8, kind=2, cin=self.cin_img)
+        for c in self.convs[1:]:
+            pk.add(c.name, a.offsets[self.pn(c.name + ".weight")][0], c.cout, 16 * c.cin)
+        for r in self.res:
+            p = r["prefix"]
+            pk.add(p + "1", a.offsets[self.pn(p + "1.weight")][0], self.d, 9 * self.d)
+            pk.add(p + "4", a.offsets[self.pn(p + "4.weight")][0], self.d, self.d)
+        pk.finalize()
+        pk.repack()
+        self.pack = pk
+        self._bufs: Dict[int, dict] = {}
+
+    # ------------------------------------------------------------ helpers
+    def pn(self, local: str) -> str:
+        return self.prefix + local
+
+    def P(self, local):
+        return self.arena.f32(self.pn(local))
+
+    def G(self, local):
+        return self.arena.grad_of(self.pn(local))
+
+    def Graw(self, local):
+        return self.arena.raw(self.arena.grad, self.pn(local))
+
+    @staticmethod
+    def channels_last_names(enc, prefix: str) -> List[str]:
+        """Conv weights the arena stores [co][kh][kw][ci] (the GEMM B layout)."""
+        out = [prefix + f"encoder.{i}.weight" for i in (3, 6, 8)]
+        out += [prefix + f"encoder.{ri}.convs.1.weight" for ri in (11, 14)]
+        return out
+
+    def _bn_state(self, B, key, rows, c):
+        bufs = self._bufs[B]
+        st = bufs.get("bn:" + key)
+        if st is None:
+            n = L.lib.encdiff_batchnorm_partials_floats(rows, c)
+            st = bufs["bn:" + key] = dict(mean=torch.empty(c, device=self.dev), rstd=torch.empty(c, device=self.dev),
+                                          part=torch.empty(n, device=self.dev),
+                                          counter=torch.zeros(1, device=self.dev, dtype=torch.int32))
+        return st
+
+    def _bind(self, B):
+        if B in self._bufs:
+            return self._bufs[B]
+        t = lambda rows, c, dt=BF16: torch.empty(rows, c, device=self.dev, dtype=dt)  # noqa: E731
+        d = self.d
+        b = dict(x0=t(B * 64 * 64, 8))
+        for i, c in enumerate(self.convs):
+            n = B * c.hout * c.hout
+            b[f"c{i}"], b[f"a{i}"], b[f"dc{i}"], b[f"da{i}"] = t(n, d), t(n, d), t(n, d), t(n, d)
+        n4 = B * 16
+        for j in range(2):
+            for k in ("t", "u", "r", "h", "dt", "du", "dr", "dh"):
+                b[f"{k}{j}"] = t(n4, d)
+        b["dw0"] = t(d, 16 * 8, F32)
+        b["flat"] = torch.empty(B, 16 * d, device=self.dev, dtype=F32)
+        self._bufs[B] = b
+        return b
+
+    def _bn_fwd(self, B, key, mod, x, y, relu):
+        st = self._bn_state(B, key, x.shape[0], x.shape[1])
+        a = L.BatchNormArgs(rows=x.shape[0], c=x.shape[1], eps=mod.eps, momentum=mod.momentum, relu=int(relu),
+                            x=x.data_ptr(), ldx=x.stride(0), gamma=self.P(key + ".weight").data_ptr(),
+                            beta=self.P(key + ".bias").data_ptr(), y=y.data_ptr(), ldy=y.stride(0),
+                            mean=st["mean"].data_ptr(), rstd=st["rstd"].data_ptr(),
+                            running_mean=mod.running_mean.data_ptr() if mod.training else None,
+                            running_var=mod.running_var.data_ptr() if mod.training else None,
+                            partials=st["part"].data_ptr(), counter=st["counter"].data_ptr())
+        L.check(L.lib.encdiff_batchnorm_fwd(C.byref(a), ops._s()), "encdiff_batchnorm_fwd")
+
+    def _bn_bwd(self, B, key, mod, x, dy, dx, relu):
+        st = self._bn_state(B, key, x.shape[0], x.shape[1])
+        a = L.BatchNormArgs(rows=x.shape[0], c=x.shape[1], eps=mod.eps, momentum=mod.momentum, relu=int(relu),
+                            x=x.data_ptr(), ldx=x.stride(0), gamma=self.P(key + ".weight").data_ptr(),
+                            beta=self.P(key + ".bias").data_ptr(), mean=st["mean"].data_ptr(),
+                            rstd=st["rstd"].data_ptr(), partials=st["part"].data_ptr(),
+                            counter=st["counter"].data_ptr(), dy=dy.data_ptr(), lddy=dy.stride(0),
+                            dx=dx.data_ptr(), lddx=dx.stride(0), dgamma=self.G(key + ".weight").data_ptr(),
+                            dbeta=self.G(key + ".bias").data_ptr())
+        L.check(L.lib.encdiff_batchnorm_bwd(C.byref(a), ops._s()), "encdiff_batchnorm_bwd")
+
+    # ------------------------------------------------------------ forward
+    def forward(self, img: torch.Tensor) -> torch.Tensor:
+        """img fp32 NCHW (B, 3, 64, 64) -> trunk output fp32 (B, d*16) in NCHW-flatten order."""
+        assert img.is_cuda and img.dtype == F32 and img.shape[1:] == (self.cin_img, 64, 64), \
+            "HIP Encoder4 trunk: fp32 (B, 3, 64, 64) device input"
+        B = img.shape[0]
+        b = self._bind(B)
+        img = img.contiguous()
+        L.check(L.lib.encdiff_nchw_to_rows(img.data_ptr(), B, self.cin_img, 64 * 64, 8, b["x0"].data_ptr(), 8,
+                                           ops._s()), "encdiff_nchw_to_rows")
+        x, cin = b["x0"], 8
+        for i, c in enumerate(self.convs):
+            g = Geom(B, c.hout, c.hout)
+            w = self.pack.view("c0" if i == 0 else c.name)
+            ops.conv4x4s2_fwd(x, g, cin, w, b[f"c{i}"], bias=self.P(c.name + ".bias"))
+            key, mod, relu = self.bns[i]
+            self._bn_fwd(B, key, mod, b[f"c{i}"], b[f"a{i}"], relu)
+            x, cin = b[f"a{i}"], c.cout
+        g4 = Geom(B, 4, 4)
+        h = x
+        for j, r in enumerate(self.res):
+            p = r["prefix"]
+            b[f"in{j}"] = h
+            ops.conv3x3_fwd(h, g4, self.d, self.pack.view(p + "1"), b[f"t{j}"], bias=self.P(p + "1.bias"))
+            self._bn_fwd(B, p + "2", r["bn"], b[f"t{j}"], b[f"u{j}"], True)
+            ops.linear_fwd(b[f"u{j}"], self.pack.view(p + "4"), b[f"r{j}"], bias=self.P(p + "4.bias"), resid=h)
+            h = b[f"r{j}"]
+            if r["post_bn"] is not None:
+                key, mod = r["post_bn"]
+                self._bn_fwd(B, key, mod, h, b[f"h{j}"], True)
+                h = b[f"h{j}"]
+        flat = b["flat"]
+        flat.view(B, self.d, 4, 4).copy_(h.view(B, 4, 4, self.d).permute(0, 3, 1, 2))
+        return flat
+
+    # ------------------------------------------------------------ backward
+    def backward(self, d_flat: torch.Tensor):
+        """d_flat fp32 (B, d*16), NCHW-flatten order -> weight / BN gradients (+=) in the arena."""
+        B = d_flat.shape[0]
+        b = self._bufs[B]
+        d = self.d
+        g4 = Geom(B, 4, 4)
+        dh = b["dr1"]
+        dh.view(B, 4, 4, d).copy_(d_flat.view(B, d, 4, 4).permute(0, 2, 3, 1))
+        for j in (1, 0):
+            r = self.res[j]
+            p = r["prefix"]
+            if r["post_bn"] is not None:  # h_j = ReLU(BN(r_j))
+                key, mod = r["post_bn"]
+                self._bn_bwd(B, key, mod, b[f"r{j}"], dh, b[f"dr{j}"], True)
+                dh = b[f"dr{j}"]
+            # r = in + conv1x1(u): dgrad + wgrad of the 1x1 in one launch
+            ops.linear_bwd(dh, self.pack.view(p + "4"), b[f"u{j}"], b[f"du{j}"],
+                           self.G(p + "4.weight").view(d, d), self.G(p + "4.bias"))
+            self._bn_bwd(B, p + "2", r["bn"], b[f"t{j}"], b[f"du{j}"], b[f"dt{j}"], True)
+            # in-gradient = dh (residual) + conv3x3^T(dt): the residual rides the dgrad epilogue
+            ops.conv3x3_bwd_cl(b[f"dt{j}"], g4, self.pack.view(p + "1"), b[f"in{j}"], d,
+                               self.Graw(p + "1.weight"), b[f"dh{j}"], self.G(p + "1.bias"), resid=dh)
+            dh = b[f"dh{j}"]
+        for i in (3, 2, 1, 0):
+            c = self.convs[i]
+            key, mod, relu = self.bns[i]
+            self._bn_bwd(B, key, mod, b[f"c{i}"], dh, b[f"dc{i}"], relu)
+            dy = b[f"dc{i}"]
+            g = Geom(B, c.hout, c.hout)
+            if i == 0:  # the image has no gradient: weight gradient only (channel-padded, then folded)
+                x = b["x0"]
+                ops.gemm(c.cout, 16 * 8, g.pixels, dy, dy.stride(0), x, x.stride(0), b["dw0"], 16 * 8,
+                         a_mode=L.OPA_ROWM, b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32,
+                         conv=L.ConvGeom(batch=B, h=c.hout, w=c.hout, cin=8, resample=L.RESAMPLE_K4S2, ld_src=8),
+                         bias_grad=self.G(c.name + ".bias"))
+                gw = self.G(c.name + ".weight").view(c.cout, self.cin_img, 16)
+                gw.add_(b["dw0"].view(c.cout, 16, 8)[:, :, :self.cin_img].permute(0, 2, 1))
+                break
+            x = b[f"a{i - 1}"]
+            ops.conv4x4s2_bwd_cl(dy, g, self.pack.view(c.name), x, c.cin, self.Graw(c.name + ".weight"),
+                                 b[f"da{i - 1}"], self.G(c.name + ".bias"))
+            dh = b[f"da{i - 1}"]
+
+
+class TrunkFn(torch.autograd.Function):
+    """Encoder4 trunk on HIP: image -> (B, d*16) fp32.  The parameters' gradients go straight
+    to the arena (their .grad views); `anchor` (a trunk parameter) only makes the output
+    require grad so the backward runs; the image gets no gradient."""
+
+    @staticmethod
+    def forward(ctx, img, anchor, ex):
+        ctx.ex = ex
+        return ex.forward(img)
+
+    @staticmethod
+    def backward(ctx, d_flat):
+        ctx.ex.backward(d_flat.contiguous())
+        return None, None, None

@@ -1,0 +1,298 @@
+// bn.hip -- training-mode BatchNorm2d (+ReLU) over NHWC bf16 activations for the concept
+// encoder Encoder4 (openaimodel_enc.py:1002-1012: Conv2d(k4,s2,p1) + BatchNorm2d (+ReLU)
+// trunk, EncResBlock(bn=True) at :969-989), and the image repack feeding its first conv.
+//
+// Statistics are over all N*H*W pixels of a channel (BatchNorm2d.train(), biased variance
+// for the normalisation, unbiased for running_var, momentum 0.1).  Each reduction is one
+// launch: workgroups reduce a contiguous pixel range into per-workgroup partials, and the
+// LAST workgroup to finish (device-scope counter) folds the partials in a fixed order, in
+// fp64 -- deterministic, no atomics on data -- and resets the counter for the next launch
+// (graph-replay safe).  The elementwise apply is a second launch.
+#include "common.h"
+
+namespace {
+
+constexpr int BN_T = 256;
+constexpr int BN_MAXBLK = 128;  // workgroups of a reduction (pixel ranges)
+
+ED_DEV __host__ inline int bn_blocks(int rows) {
+  const int b = (rows + 127) / 128;
+  return b < BN_MAXBLK ? b : BN_MAXBLK;
+}
+
+struct BnLayout {  // thread -> (8-channel vector, pixel lane)
+  int nv, lanes, v, pl;
+  ED_DEV BnLayout(int c) {
+    nv = c >> 3;
+    lanes = BN_T / nv;
+    v = threadIdx.x % nv;
+    pl = threadIdx.x / nv;
+  }
+};
+
+ED_DEV void ld8f(const float* p, float* v) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = p[i];
+}
+
+// per-workgroup partial [blk][NQ][c] from q[NQ][8] of every thread: LDS rows summed in order
+template <int NQ>
+ED_DEV void bn_block_partial(const float (&q)[NQ][8], const BnLayout& L, int c, float* part_out) {
+  __shared__ float red[BN_T * 8 * NQ];
+  if (L.pl < L.lanes) {
+#pragma unroll
+    for (int k = 0; k < NQ; ++k)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) red[(k * L.lanes + L.pl) * c + L.v * 8 + i] = q[k][i];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < NQ * c; e += BN_T) {
+    const int k = e / c, ch = e - k * c;
+    float a = 0.f;
+    for (int r = 0; r < L.lanes; ++r) a += red[(k * L.lanes + r) * c + ch];
+    part_out[(long)k * c + ch] = a;
+  }
+}
+
+// fold the per-workgroup partials [nblk][2][c] in a fixed order (fp64): thread t sums
+// channel t % c over blocks t / c, t / c + S, ... (S = 256 / c), then the S partial sums
+// of a channel are added in order through LDS.  Result out[2][c].
+ED_DEV void bn_fold(const float* part, int nblk, int c, double* out) {
+  __shared__ double fold[2][BN_T];
+  const int S = BN_T / c, ch = threadIdx.x % c, j = threadIdx.x / c;
+  double s0 = 0.0, s1 = 0.0;
+  if (j < S) {
+#pragma unroll 4
+    for (int b = j; b < nblk; b += S) {
+      s0 += part[(long)b * 2 * c + ch];
+      s1 += part[(long)b * 2 * c + c + ch];
+    }
+  }
+  fold[0][threadIdx.x] = s0;
+  fold[1][threadIdx.x] = s1;
+  __syncthreads();
+  if (threadIdx.x < c) {
+    double a0 = 0.0, a1 = 0.0;
+    for (int k = 0; k < S; ++k) { a0 += fold[0][k * c + threadIdx.x]; a1 += fold[1][k * c + threadIdx.x]; }
+    out[threadIdx.x] = a0;
+    out[c + threadIdx.x] = a1;
+  }
+  __syncthreads();
+}
+
+// true in exactly one workgroup: the last to arrive (after its partials are visible)
+ED_DEV bool bn_last_block(unsigned int* counter) {
+  __shared__ bool last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(counter, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (last) __threadfence();
+  return last;
+}
+
+__global__ __launch_bounds__(BN_T) void bn_stats_kernel(const EncdiffBatchNormArgs p) {
+  const BnLayout L(p.c);
+  const bf16_t* X = (const bf16_t*)p.x;
+  const int per = (p.rows + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * per, r1 = min(p.rows, r0 + per);
+  float q[2][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q[0][i] = q[1][i] = 0.f;
+  if (L.pl < L.lanes) {
+    for (int r = r0 + L.pl; r < r1; r += L.lanes) {
+      float x[8];
+      unpack8(*(const uint4*)(X + (long)r * p.ldx + L.v * 8), x);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { q[0][i] += x[i]; q[1][i] += x[i] * x[i]; }
+    }
+  }
+  float* part = p.partials + (long)blockIdx.x * 2 * p.c;
+  bn_block_partial<2>(q, L, p.c, part);
+  if (!bn_last_block(p.counter)) return;
+  __shared__ double tot[2 * BN_T];
+  bn_fold(p.partials, gridDim.x, p.c, tot);
+  const double n = (double)p.rows;
+  for (int ch = threadIdx.x; ch < p.c; ch += BN_T) {
+    const double s = tot[ch], ss = tot[p.c + ch];
+    const double mean = s / n;
+    double var = ss / n - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    p.mean[ch] = (float)mean;
+    p.rstd[ch] = (float)(1.0 / sqrt(var + (double)p.eps));
+    if (p.running_mean) {
+      const float m = p.momentum;
+      p.running_mean[ch] = (1.f - m) * p.running_mean[ch] + m * (float)mean;
+      p.running_var[ch] = (1.f - m) * p.running_var[ch] + m * (float)(var * n / (n > 1.0 ? n - 1.0 : 1.0));
+    }
+  }
+  if (threadIdx.x == 0) *p.counter = 0u;
+}
+
+__global__ __launch_bounds__(BN_T) void bn_apply_kernel(const EncdiffBatchNormArgs p) {
+  const int nv = p.c >> 3;
+  const long total = (long)p.rows * nv;
+  for (long e = (long)blockIdx.x * BN_T + threadIdx.x; e < total; e += (long)gridDim.x * BN_T) {
+    const long r = e / nv;
+    const int cb = (int)(e - r * nv) * 8;
+    float x[8], m[8], rs[8], g[8], b[8];
+    unpack8(*(const uint4*)((const bf16_t*)p.x + r * p.ldx + cb), x);
+    ld8f(p.mean + cb, m);
+    ld8f(p.rstd + cb, rs);
+    ld8f(p.gamma + cb, g);
+    ld8f(p.beta + cb, b);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float z = (x[i] - m[i]) * rs[i] * g[i] + b[i];
+      x[i] = p.relu ? fmaxf(z, 0.f) : z;
+    }
+    *(uint4*)((bf16_t*)p.y + r * p.ldy + cb) = pack8(x);
+  }
+}
+
+// backward reduction: g = dy * relu'(z) (z recomputed from x and the saved statistics);
+// sums of g and g * xhat per channel -> dbeta, dgamma (+=) and the apply constants
+__global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const EncdiffBatchNormArgs p) {
+  const BnLayout L(p.c);
+  const bf16_t* X = (const bf16_t*)p.x;
+  const bf16_t* DY = (const bf16_t*)p.dy;
+  const int per = (p.rows + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * per, r1 = min(p.rows, r0 + per);
+  float q[2][8], m[8], rs[8], ga[8], be[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q[0][i] = q[1][i] = 0.f;
+  if (L.pl < L.lanes) {
+    const int cb = L.v * 8;
+    ld8f(p.mean + cb, m);
+    ld8f(p.rstd + cb, rs);
+    ld8f(p.gamma + cb, ga);
+    ld8f(p.beta + cb, be);
+    for (int r = r0 + L.pl; r < r1; r += L.lanes) {
+      float x[8], d[8];
+      unpack8(*(const uint4*)(X + (long)r * p.ldx + cb), x);
+      unpack8(*(const uint4*)(DY + (long)r * p.lddy + cb), d);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xh = (x[i] - m[i]) * rs[i];
+        const float g = (p.relu && xh * ga[i] + be[i] <= 0.f) ? 0.f : d[i];
+        q[0][i] += g;
+        q[1][i] += g * xh;
+      }
+    }
+  }
+  float* part = p.partials + (long)blockIdx.x * 2 * p.c;
+  bn_block_partial<2>(q, L, p.c, part);
+  if (!bn_last_block(p.counter)) return;
+  float* coef = p.partials + (long)gridDim.x * 2 * p.c;  // [2][c]: mean(g), mean(g * xhat)
+  __shared__ double tot[2 * BN_T];
+  bn_fold(p.partials, gridDim.x, p.c, tot);
+  for (int ch = threadIdx.x; ch < p.c; ch += BN_T) {
+    const double s = tot[ch], sx = tot[p.c + ch];
+    p.dbeta[ch] += (float)s;
+    p.dgamma[ch] += (float)sx;
+    coef[ch] = (float)(s / p.rows);
+    coef[p.c + ch] = (float)(sx / p.rows);
+  }
+  if (threadIdx.x == 0) *p.counter = 0u;
+}
+
+// dx = gamma * rstd * (g - mean(g) - xhat * mean(g * xhat))
+__global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const EncdiffBatchNormArgs p, int nblk_reduce) {
+  const int nv = p.c >> 3;
+  const long total = (long)p.rows * nv;
+  const float* coef = p.partials + (long)nblk_reduce * 2 * p.c;
+  for (long e = (long)blockIdx.x * BN_T + threadIdx.x; e < total; e += (long)gridDim.x * BN_T) {
+    const long r = e / nv;
+    const int cb = (int)(e - r * nv) * 8;
+    float x[8], d[8], m[8], rs[8], ga[8], be[8], c0[8], c1[8];
+    unpack8(*(const uint4*)((const bf16_t*)p.x + r * p.ldx + cb), x);
+    unpack8(*(const uint4*)((const bf16_t*)p.dy + r * p.lddy + cb), d);
+    ld8f(p.mean + cb, m);
+    ld8f(p.rstd + cb, rs);
+    ld8f(p.gamma + cb, ga);
+    ld8f(p.beta + cb, be);
+    ld8f(coef + cb, c0);
+    ld8f(coef + p.c + cb, c1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float xh = (x[i] - m[i]) * rs[i];
+      const float g = (p.relu && xh * ga[i] + be[i] <= 0.f) ? 0.f : d[i];
+      x[i] = ga[i] * rs[i] * (g - c0[i] - xh * c1[i]);
+    }
+    *(uint4*)((bf16_t*)p.dx + r * p.lddx + cb) = pack8(x);
+  }
+}
+
+// fp32 NCHW [B][C][H][W] -> bf16 [B*H*W][ld] with channels [C, cpad) zero
+__global__ __launch_bounds__(256) void nchw_to_rows_kernel(const float* __restrict__ x, int B, int C, int HW,
+                                                           int cpad, bf16_t* __restrict__ y, long ld) {
+  const long total = (long)B * HW;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const long b = i / HW, px = i - b * HW;
+    for (int c0 = 0; c0 < cpad; c0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = (c0 + k < C) ? x[(b * C + c0 + k) * HW + px] : 0.f;
+      *(uint4*)(y + i * ld + c0) = pack8(v);
+    }
+  }
+}
+
+int bn_check(const EncdiffBatchNormArgs* a) {
+  if (!a || !a->x || !a->mean || !a->rstd || !a->gamma || !a->beta || !a->partials || !a->counter)
+    return ENCDIFF_ERR_ARG;
+  // 8-channel vectors must tile the 256 threads; the fold needs c <= 256
+  if (a->rows <= 0 || a->c <= 0 || a->c % 8 || a->c > 256 || BN_T % (a->c / 8) || BN_T % a->c)
+    return ENCDIFF_ERR_SHAPE;
+  if (a->ldx % 8) return ENCDIFF_ERR_SHAPE;
+  return ENCDIFF_OK;
+}
+
+int apply_grid(const EncdiffBatchNormArgs* a) {
+  long g = ((long)a->rows * (a->c / 8) + BN_T - 1) / BN_T;
+  return (int)(g > 4096 ? 4096 : g);
+}
+
+}  // namespace
+
+extern "C" int encdiff_batchnorm_partials_floats(int rows, int c) {
+  return bn_blocks(rows) * 2 * c + 2 * c;
+}
+
+extern "C" int encdiff_batchnorm_fwd(const EncdiffBatchNormArgs* a, void* stream) {
+  const int rc = bn_check(a);
+  if (rc) return rc;
+  if (!a->y || a->ldy % 8) return ENCDIFF_ERR_ARG;
+  if (a->running_mean && !a->running_var) return ENCDIFF_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int nblk = bn_blocks(a->rows);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(nblk), dim3(BN_T), 0, s, *a);
+  ED_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(a)), dim3(BN_T), 0, s, *a);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_batchnorm_bwd(const EncdiffBatchNormArgs* a, void* stream) {
+  const int rc = bn_check(a);
+  if (rc) return rc;
+  if (!a->dy || !a->dx || !a->dgamma || !a->dbeta || a->lddy % 8 || a->lddx % 8) return ENCDIFF_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int nblk = bn_blocks(a->rows);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(BN_T), 0, s, *a);
+  ED_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(apply_grid(a)), dim3(BN_T), 0, s, *a, nblk);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_nchw_to_rows(const float* x, int batch, int c, int hw, int cpad, void* y, long ldy,
+                                    void* stream) {
+  if (!x || !y || batch <= 0 || c <= 0 || hw <= 0 || cpad < c || cpad % 8 || ldy < cpad || ldy % 8)
+    return ENCDIFF_ERR_ARG;
+  long g = ((long)batch * hw + 255) / 256;
+  hipLaunchKernelGGL(nchw_to_rows_kernel, dim3((unsigned)(g > 4096 ? 4096 : g)), dim3(256), 0, (hipStream_t)stream,
+                     x, batch, c, hw, cpad, (bf16_t*)y, ldy);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}

@@ -443,6 +443,13 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src
     if (j.kind == 1) {  // conv [co][ci][3][3] -> [co][tap][ci]; c = tap*cin + ci
       const int tap = c / j.cin, ci = c - tap * j.cin;
       s = (long)r * j.cols + ci * 9 + tap;
+    } else if (j.kind == 2) {  // conv [co][cin][taps] -> [co][tap][8], channels cin..7 zero
+      const int taps = j.cols >> 3, tap = c >> 3, ci = c & 7;
+      if (ci >= j.cin) {
+        dst[j.dst_off + i] = 0;
+        continue;
+      }
+      s = (long)r * j.cin * taps + ci * taps + tap;
     } else {
       s = i;
     }

@@ -67,24 +67,38 @@ struct GemmAux {
 // 3x3 tap (ty, tx) is  ys = sy*y + ty + oy  (limits lh x lw), then >> sh (nearest-up
 // source), row = (b*hs + ys)*ws + xs.  Padding gives ok = false and row 0: the load is
 // still issued (and masked when written to LDS), so no branch or early wait is needed.
+//   K4S2   (Encoder4 Conv2d(k4, s2, p1), openaimodel_enc.py:1002-1009): 4x4 taps at
+//          (2y + ty - 1, 2x + tx - 1) of the (2h, 2w) source;
+//   K4S2_T (its input gradient): 4x4 taps t' = 15 - t at (y + ty' - 2, x + tx' - 2) of the
+//          full-resolution grid, valid only at even coordinates, source pixel = coordinate / 2.
 struct Im2colMode {
-  int sy, oy, lh, lw, sh, hs, ws;
+  int sy, oy, lh, lw, sh, hs, ws, par, k4;
   ED_DEV Im2colMode(const EncdiffConvGeom& g) {
     const bool s2 = g.resample == ENCDIFF_RESAMPLE_STRIDE2;  // VQ Downsample: pad (0,1,0,1), k3 s2 p0
     const bool up = g.resample == ENCDIFF_RESAMPLE_UP2;      // nearest x2 (openaimodel_enc.py:116)
-    sy = s2 ? 2 : 1;
-    oy = s2 ? 0 : -1;
-    lh = s2 ? 2 * g.h : g.h;
-    lw = s2 ? 2 * g.w : g.w;
-    sh = up ? 1 : 0;
+    const bool f4 = g.resample == ENCDIFF_RESAMPLE_K4S2;
+    const bool t4 = g.resample == ENCDIFF_RESAMPLE_K4S2_T;
+    sy = (s2 || f4) ? 2 : 1;
+    oy = s2 ? 0 : (t4 ? -2 : -1);
+    lh = (s2 || f4) ? 2 * g.h : g.h;
+    lw = (s2 || f4) ? 2 * g.w : g.w;
+    sh = (up || t4) ? 1 : 0;
     hs = lh >> sh;
     ws = lw >> sh;
+    par = t4 ? 1 : 0;
+    k4 = (f4 || t4) ? 1 : 0;
   }
 };
 
+// tap index -> (ty, tx): 3x3 (tap / 3 via a multiply) or 4x4 taps
+ED_DEV void tap_yx(const Im2colMode& md, uint32_t tap, int& ty, int& tx) {
+  ty = md.k4 ? (int)(tap >> 2) : (int)((tap * 11u) >> 5);
+  tx = (int)tap - (md.k4 ? 4 : 3) * ty;
+}
+
 ED_DEV uint32_t im2col_row(const Im2colMode& md, uint32_t b, int y, int x, int ty, int tx, bool& ok) {
   const int ys = md.sy * y + ty + md.oy, xs = md.sy * x + tx + md.oy;
-  ok = (unsigned)ys < (unsigned)md.lh && (unsigned)xs < (unsigned)md.lw;
+  ok = (unsigned)ys < (unsigned)md.lh && (unsigned)xs < (unsigned)md.lw && ((ys | xs) & md.par) == 0;
   const uint32_t row = (b * (uint32_t)md.hs + (uint32_t)(ys >> md.sh)) * (uint32_t)md.ws + (uint32_t)(xs >> md.sh);
   return ok ? row : 0u;
 }
@@ -184,7 +198,8 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
           const uint32_t kk = k < p.K ? (uint32_t)k : 0u;
           const uint32_t tap = fdiv(kk, aux.cin);
           const uint32_t ch = kk - tap * (uint32_t)p.conv.cin;
-          const int ty = (int)((tap * 11u) >> 5), tx = (int)tap - 3 * ty;
+          int ty, tx;
+          tap_yx(md, tap, ty, tx);
           bool inb;
           const uint32_t prow = im2col_row(md, bb, y, x, ty, tx, inb);
           ok = min && k < p.K && inb;
@@ -220,7 +235,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
           const uint32_t tap = fdiv(kk, aux.cout);
           const uint32_t co = kk - tap * (uint32_t)p.conv_cout;
           ok = kn;
-          off = (size_t)co * p.ldb + (size_t)(8 - tap) * p.N + (ok ? n : 0);
+          off = (size_t)co * p.ldb + (size_t)((md.k4 ? 15 : 8) - tap) * p.N + (ok ? n : 0);
         } else {  // B_IM2COL: row = output pixel k, column n = (tap, ci)
           const uint32_t kk = kn ? (uint32_t)k : 0u;
           const uint32_t bb = fdiv(kk, aux.hw);
@@ -229,7 +244,8 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
           const uint32_t nn = kn ? (uint32_t)n : 0u;
           const uint32_t tap = fdiv(nn, aux.cin);
           const uint32_t ci = nn - tap * (uint32_t)p.conv.cin;
-          const int ty = (int)((tap * 11u) >> 5), tx = (int)tap - 3 * ty;
+          int ty, tx;
+          tap_yx(md, tap, ty, tx);
           bool inb;
           const uint32_t prow = im2col_row(md, bb, y, x, ty, tx, inb);
           ok = kn && inb;

@@ -440,6 +440,10 @@ class LatentDiffusion(DDPM):
         order = self.hip_trainables()
         ema_names = ["model.diffusion_model." + n for n, _ in unet.named_parameters()]
         cl = ["model.diffusion_model." + n for n in unet._spec.conv_weights()]
+        cs = self.cond_stage_model
+        if self.cond_stage_trainable and type(cs).__name__ == "Encoder4":
+            from encdiff_amd.cond import Encoder4TrunkExecutor   # trunk convs channels-last (§8(f) row 2)
+            cl += Encoder4TrunkExecutor.channels_last_names(cs, "cond_stage_model.")
         arena = ParamArena(order, self.device, ema_names=ema_names, channels_last=cl)
 
         # the UNet executor addresses its parameters by their UNet-local names
@@ -468,7 +472,8 @@ class LatentDiffusion(DDPM):
         unet = self.model.diffusion_model
         params = [p for _, p in self.hip_trainables()]
         opt = FusedArenaAdamW(params, arena, lr=lr, ema=self.model_ema if self.use_ema else None,
-                              repack=lambda: (unet.executor().pack.repack(), unet.mark_repacked()))
+                              repack=lambda: (unet.executor().pack.repack(), unet.mark_repacked(),
+                                            getattr(self.cond_stage_model, "repack_hip", lambda: None)()))
         self._optimizer = opt
         if self.use_scheduler:
             sched = instantiate_from_config(self.scheduler_config)

@@ -253,6 +253,7 @@ class Encoder4(nn.Module):
         self.net = nn.ModuleList([nn.Sequential(nn.Linear(1, 64), nn.ELU(True), nn.Linear(64, 128), nn.ELU(True),
                                                 nn.Linear(128, context_dim)) for _ in range(latent_unit)])
         self._warp_bind = None
+        self._trunk = None
 
     def bind_arena(self, arena, prefix: str):
         """Run warp() on the HIP kernels (encdiff_encoder_warp_*): the per-unit MLP
@@ -272,6 +273,30 @@ class Encoder4(nn.Module):
             if i > 0 and offs[0] != base + i * stride:
                 raise ValueError("Encoder4.net units do not have a constant arena stride")
         self._warp_bind = (arena, base, stride or sum(sizes))
+        # convolution trunk on HIP when its conv weights sit channels-last in the arena
+        from encdiff_amd.cond import Encoder4TrunkExecutor
+        self._trunk = None
+        if all(n in arena.cl for n in Encoder4TrunkExecutor.channels_last_names(self, prefix)):
+            self._trunk = Encoder4TrunkExecutor(self, arena, prefix)
+            self._trunk_version = arena.master._version
+
+    def repack_hip(self):
+        """Refresh the trunk's bf16 weights from the arena (after an optimizer step)."""
+        if getattr(self, "_trunk", None) is not None:
+            self._trunk.pack.repack()
+            self._trunk_version = self._trunk.arena.master._version
+
+    def _encode(self, x):
+        """Trunk + Linear: on HIP in training mode (batch-statistics BatchNorm), else the
+        reference modules (eval mode uses the running statistics)."""
+        ex = getattr(self, "_trunk", None)
+        if ex is None or not self.training or not x.is_cuda:
+            return self.encoder(x)
+        from encdiff_amd.cond import TrunkFn
+        if ex.arena.master._version != self._trunk_version:  # parameters modified in place
+            self.repack_hip()
+        flat = TrunkFn.apply(x, self.encoder[0].weight, ex)
+        return self.encoder[-1](flat)
 
     def warp(self, u):
         if self._warp_bind is not None:
@@ -279,7 +304,7 @@ class Encoder4(nn.Module):
         return torch.cat([self.net[i](u[:, i][:, None]) for i in range(self.latent_unit)], dim=1)
 
     def forward(self, x):
-        return self.warp(self.encoder(x))
+        return self.warp(self._encode(x))
 
     def encoding(self, x):
-        return self.encoder(x)
+        return self._encode(x)

@@ -254,11 +254,39 @@ def conv3x3_dgrad_args(dy, g: Geom, wf, dx, resid=None, ws_offset=0):
                      resid=resid, ld_resid=_ld(resid) if resid is not None else 0, ws_offset=ws_offset)
 
 
-def conv3x3_bwd_cl(dy, g: Geom, wf, x, cin, dw_cl, dx, db=None, resample=L.RESAMPLE_NONE):
+def conv3x3_bwd_cl(dy, g: Geom, wf, x, cin, dw_cl, dx, db=None, resample=L.RESAMPLE_NONE, resid=None):
     """Backward of one 3x3 conv: dw_cl += dy^T im2col(resample(x)) (+ db) and
-    dx = conv3x3^T(dy) at the conv resolution, one launch."""
+    dx = conv3x3^T(dy) (+ resid) at the conv resolution, one launch."""
     gemm_pair(conv3x3_wgrad_cl_args(dy, x, g, cin, dw_cl, db, resample),
-              lambda off: conv3x3_dgrad_args(dy, g, wf, dx, None, off))
+              lambda off: conv3x3_dgrad_args(dy, g, wf, dx, resid, off))
+
+
+# ------------------------------------------------------------------ 4x4 stride-2 convolutions
+def conv4x4s2_fwd(x, g_out: Geom, cin, wf, out, bias=None):
+    """Conv2d(k4, s2, p1) (Encoder4, openaimodel_enc.py:1002-1009): x at (2h, 2w), out at
+    g_out = (h, w); wf packed [cout][16*cin] ([co][kh][kw][ci])."""
+    cout = wf.shape[0]
+    gemm(g_out.pixels, cout, 16 * cin, x, _ld(x), wf, _ld(wf), out, _ld(out), a_mode=L.OPA_IM2COL,
+         conv=L.ConvGeom(batch=g_out.batch, h=g_out.h, w=g_out.w, cin=cin, resample=L.RESAMPLE_K4S2,
+                         ld_src=_ld(x)), bias=bias)
+
+
+def conv4x4s2_bwd_cl(dy, g_out: Geom, wf, x, cin, dw_cl, dx, db=None):
+    """Backward of Conv2d(k4, s2, p1): dw_cl[cout][16*cin] += dy^T im2col(x) (+ db) and
+    dx (2h, 2w) = transposed conv of dy, one paired launch."""
+    cout = wf.shape[0]
+    gin = Geom(g_out.batch, 2 * g_out.h, 2 * g_out.w)
+    wargs = gemm_args(cout, 16 * cin, g_out.pixels, dy, _ld(dy), x, _ld(x), dw_cl, _ld(dw_cl), a_mode=L.OPA_ROWM,
+                      b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32_ACCUM,
+                      conv=L.ConvGeom(batch=g_out.batch, h=g_out.h, w=g_out.w, cin=cin, resample=L.RESAMPLE_K4S2,
+                                      ld_src=_ld(x)), bias_grad=db)
+
+    def dargs(off):
+        return gemm_args(gin.pixels, cin, 16 * cout, dy, _ld(dy), wf, _ld(wf), dx, _ld(dx), a_mode=L.OPA_IM2COL,
+                         b_mode=L.OPB_CONV_DGRAD, conv=L.ConvGeom(batch=gin.batch, h=gin.h, w=gin.w, cin=cout,
+                                                                  resample=L.RESAMPLE_K4S2_T, ld_src=_ld(dy)),
+                         conv_cout=cout, ws_offset=off)
+    gemm_pair(wargs, dargs)
 
 
 # ------------------------------------------------------------------ normalisation

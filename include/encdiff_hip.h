@@ -49,7 +49,8 @@ enum {
 enum {
   ENCDIFF_OPB_ROWK = 0,       /* B[k][n] at b + n*ldb + k (weights [out][in])               */
   ENCDIFF_OPB_ROWN = 1,       /* B[k][n] at b + k*ldb + n                                    */
-  ENCDIFF_OPB_CONV_DGRAD = 2, /* B[(tap,co)][ci] = Wf[co][8-tap][ci], Wf packed [co][9][cin] */
+  ENCDIFF_OPB_CONV_DGRAD = 2, /* B[(tap,co)][ci] = Wf[co][T-1-tap][ci], Wf packed [co][T][cin], T = 9
+                                 (16 with resample K4S2_T)                                     */
   ENCDIFF_OPB_IM2COL = 3      /* B[pixel][tap*cin + c] = im2col3x3(src) (conv wgrad)          */
 };
 enum {
@@ -66,8 +67,12 @@ enum {
   ENCDIFF_RESAMPLE_NONE = 0,
   ENCDIFF_RESAMPLE_DOWN2 = 1, /* source is (2h,2w); AvgPool2d(2) on the fly  (openaimodel_enc.py:156) */
   ENCDIFF_RESAMPLE_UP2 = 2,   /* source is (h/2,w/2); nearest x2 on the fly (openaimodel_enc.py:116) */
-  ENCDIFF_RESAMPLE_STRIDE2 = 3 /* source is (2h,2w); 3x3 taps at (2y+ky, 2x+kx), zero pad right/bottom
+  ENCDIFF_RESAMPLE_STRIDE2 = 3, /* source is (2h,2w); 3x3 taps at (2y+ky, 2x+kx), zero pad right/bottom
                                   only: F.pad(x,(0,1,0,1)) + Conv2d(k3, s2, p0) (model.py Downsample) */
+  ENCDIFF_RESAMPLE_K4S2 = 4,   /* source is (2h,2w); 4x4 taps (K = 16*cin) at (2y+ky-1, 2x+kx-1):
+                                  Conv2d(k4, s2, p1) of Encoder4 (openaimodel_enc.py:1002-1009)   */
+  ENCDIFF_RESAMPLE_K4S2_T = 5  /* input gradient of K4S2: source dY is (h/2,w/2); with
+                                  OPB_CONV_DGRAD (16 taps, flipped) computes dX at (h,w)          */
 };
 
 typedef struct EncdiffConvGeom {
@@ -286,7 +291,9 @@ int encdiff_adamw_ema(float* p, const float* g, float* m, float* v, float* ema, 
 
 /* Pack fp32 master weights into bf16 compute layouts.  Each job copies `rows x cols`
  * elements: dst[r*dst_ld + c] = src[src_index(r, c)], kind 0: src[r*cols + c]
- * (identity), kind 1: conv [co][ci][3][3] -> [co][tap][ci] (r=co, c=tap*cin+ci). */
+ * (identity), kind 1: conv [co][ci][3][3] -> [co][tap][ci] (r=co, c=tap*cin+ci), kind 2:
+ * conv [co][cin][taps] -> [co][tap][8] with channels cin..7 zero (cols = 8*taps; the
+ * first Encoder4 conv, image channels padded to 8). */
 typedef struct EncdiffPackJob {
   long long src_off, dst_off;
   int rows, cols, kind, cin;
@@ -325,6 +332,42 @@ int encdiff_encoder_warp_fwd(const float* u, long ldu, int batch, int units, con
 int encdiff_encoder_warp_bwd(const float* u, long ldu, int batch, int units, const float* params,
                              long unit_stride, int context_dim, const float* dout, long lddo, float* du,
                              long lddu, float* grads, void* stream);
+
+/* Encoder4 convolution trunk (openaimodel_enc.py:1002-1012, EncResBlock :969-989) runs on
+ * encdiff_gemm (Conv2d(k4,s2,p1): RESAMPLE_K4S2 / K4S2_T im2col modes; 3x3 and 1x1 convs)
+ * and these training-mode BatchNorm2d kernels over NHWC bf16 rows (nn.BatchNorm2d.train():
+ * batch statistics over N*H*W, biased variance to normalise, running stats updated with
+ * `momentum` and the unbiased variance).
+ *   fwd: y = act((x - mean) * rstd * gamma + beta), act = ReLU if relu; writes mean/rstd.
+ *   bwd: g = dy * act'(z) (z recomputed), dgamma += sum g*xhat, dbeta += sum g,
+ *        dx = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)).
+ * Each reduction is one launch whose last workgroup folds per-workgroup partials in a
+ * fixed order (fp64): deterministic.  `partials` holds
+ * encdiff_batchnorm_partials_floats(rows, c) floats; `counter` is a zero-initialised
+ * device uint32 the kernels leave at zero.  c % 8 == 0, 256 % c == 0. */
+typedef struct EncdiffBatchNormArgs {
+  int rows, c;
+  float eps, momentum;
+  int relu, pad_;
+  const void* x; long ldx;          /* bf16 [rows][c] (pre-BN activations)           */
+  const float* gamma; const float* beta;
+  void* y; long ldy;                /* fwd: bf16 out                                 */
+  float* mean; float* rstd;         /* [c]: written by fwd, read by bwd              */
+  float* running_mean; float* running_var;  /* optional (fwd)                        */
+  float* partials;                  /* scratch                                       */
+  unsigned int* counter;
+  const void* dy; long lddy;        /* bwd: gradient of the (activated) output       */
+  void* dx; long lddx;              /* bwd: bf16 out                                 */
+  float* dgamma; float* dbeta;      /* bwd: fp32 +=                                  */
+} EncdiffBatchNormArgs;
+
+int encdiff_batchnorm_partials_floats(int rows, int c);
+int encdiff_batchnorm_fwd(const EncdiffBatchNormArgs* args, void* stream);
+int encdiff_batchnorm_bwd(const EncdiffBatchNormArgs* args, void* stream);
+
+/* fp32 NCHW [batch][c][hw] -> bf16 rows [batch*hw][ldy], channels c..cpad-1 zero
+ * (the image as the first Encoder4 conv's im2col source, channels padded to 8). */
+int encdiff_nchw_to_rows(const float* x, int batch, int c, int hw, int cpad, void* y, long ldy, void* stream);
 
 /* Library/device information (for tests): returns the number of exported kernels. */
 int encdiff_version(void);

@@ -31,7 +31,7 @@ def test_header_exports_match_library():
 STRUCTS = {
     "EncdiffConvGeom": "ConvGeom", "EncdiffGemmArgs": "GemmArgs", "EncdiffGroupNormArgs": "GroupNormArgs",
     "EncdiffLayerNormArgs": "LayerNormArgs", "EncdiffAttnArgs": "AttnArgs", "EncdiffEwArgs": "EwArgs",
-    "EncdiffSmallConvArgs": "SmallConvArgs", "EncdiffPackJob": "PackJob",
+    "EncdiffSmallConvArgs": "SmallConvArgs", "EncdiffPackJob": "PackJob", "EncdiffBatchNormArgs": "BatchNormArgs",
 }
 
 

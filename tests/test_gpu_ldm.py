@@ -87,11 +87,13 @@ def test_training_gradients_match_oracle(ldm):
         r = rel(unet[n].grad, P[n].grad)
         print(n, r)
         assert r < 5e-2, n
+    # Encoder4's trunk runs in bf16 with ReLU masks: near-zero pre-activations flip (see
+    # test_encoder4_trunk_hip), hence the looser bound on its first conv
     cond = dict(ldm.cond_stage_model.named_parameters())
-    for n in ["encoder.0.weight", "encoder.16.weight", "net.3.4.weight"]:
+    for n, tol in [("encoder.0.weight", 0.2), ("encoder.16.weight", 5e-2), ("net.3.4.weight", 5e-2)]:
         r = rel(cond[n].grad, E[n].grad)
         print("cond", n, r)
-        assert r < 5e-2, n
+        assert r < tol, n
 
 
 @pytest.mark.parametrize("graph", [False, True])
@@ -133,3 +135,62 @@ def test_vq_encoder_hip():
         fs._hip_encoder = None
         ref2 = fs.encode(x)
     assert ((out2 - ref2).norm() / ref2.norm()).item() < 2e-2
+
+
+def test_encoder4_trunk_hip():
+    """HIP Encoder4 convolution trunk (bf16 NHWC GEMMs + BatchNorm kernels) vs the as-is fp32
+    torch modules on the same weights, training mode: output u rel-L2 < 3e-2, trunk parameter
+    gradients within the ReLU-mask bound below, BN running statistics updated alike."""
+    import copy
+    import encdiff_amd  # noqa: F401
+    from encdiff_amd.configs import model_config
+    from encdiff_amd.ldm.util import instantiate_from_config
+    torch.manual_seed(1)
+    ldm = instantiate_from_config(model_config("shapes3d")).cuda()
+    ldm.train()
+    ref = copy.deepcopy(ldm.cond_stage_model)
+    ldm.setup_hip_training()
+    enc = ldm.cond_stage_model
+    assert enc._trunk is not None, "trunk not bound to the arena"
+    x = torch.rand(16, 3, 64, 64, device="cuda") * 2 - 1
+    proj = torch.randn(16, enc.latent_unit, device="cuda")
+    ldm._arena.zero_grad()
+    u = enc.encoding(x)
+    (u * proj).sum().backward()
+    u_ref = ref.encoding(x)
+    (u_ref * proj).sum().backward()
+    r = rel(u.detach(), u_ref.detach())
+    print("u rel-L2", r)
+    assert r < 3e-2
+    # ReLU masks are evaluated on bf16 activations: the ~1% of near-zero pre-activations whose
+    # sign differs from the fp32 reference each pass a full upstream gradient, which shows as
+    # ~10% rel-L2 on random-init gradients (the kernels themselves are pinned to 1e-2 in
+    # test_gpu_ops.py).  Gradients must agree to 0.2 rel-L2 and cos > 0.98; conv biases that
+    # feed a BatchNorm have zero true gradient: their bf16 residue is measured against the
+    # following BN's beta gradient (same scale).
+    got = dict(enc.named_parameters())
+    pre_bn_bias = {"encoder.0.bias": "encoder.1.bias", "encoder.3.bias": "encoder.4.bias",
+                   "encoder.6.bias": "encoder.7.bias", "encoder.8.bias": "encoder.9.bias",
+                   "encoder.11.convs.1.bias": "encoder.11.convs.2.bias", "encoder.11.convs.4.bias": "encoder.12.bias",
+                   "encoder.14.convs.1.bias": "encoder.14.convs.2.bias"}
+    for n, p in ref.named_parameters():
+        if not n.startswith("encoder."):
+            continue
+        g, gr = got[n].grad.double().flatten(), p.grad.double().flatten()
+        if n in pre_bn_bias:
+            scale = got[pre_bn_bias[n]].grad.double().norm()
+            print(n, "residue", (g.norm() / scale).item())
+            assert g.norm() < 0.1 * scale, n
+            continue
+        e, cos = rel(g, gr), torch.nn.functional.cosine_similarity(g, gr, dim=0).item()
+        print(n, e, cos)
+        assert e < 0.2 and cos > 0.98, n
+    for (n, b), (_, b_ref) in zip(enc.named_buffers(), ref.named_buffers()):
+        if "running" in n:
+            assert rel(b, b_ref) < 2e-2, n
+    # two identical steps give bitwise identical gradients (deterministic BN folds)
+    g1 = ldm._arena.grad.clone()
+    ldm._arena.zero_grad()
+    u = enc.encoding(x)
+    (u * proj).sum().backward()
+    assert torch.equal(g1, ldm._arena.grad)

@@ -502,3 +502,81 @@ def test_gemm_pair_matches_two_launches(O, kind, M, C, K):
         assert rel(nhwc(outs[1][2], g), ref_dx) < 1e-2
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("H,C,relu", [(32, 128, True), (8, 128, False), (4, 128, True), (16, 64, True)])
+def test_batchnorm_train_fwd_bwd(O, H, C, relu):
+    """BatchNorm2d.train() (+ReLU) on NHWC bf16 rows vs torch fp32 on the same bf16 input; the
+    ReLU mask is evaluated on identical inputs, so the backward is pinned tightly too."""
+    import ctypes
+    import encdiff_amd._lib as L
+    torch.manual_seed(5)
+    B = 16
+    rows = B * H * H
+    x = (torch.randn(rows, C, device=dev) * 2 + 0.5).to(torch.bfloat16)
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev) * 0.2
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    y = torch.empty_like(x)
+    mean, rstd = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    part = torch.empty(L.lib.encdiff_batchnorm_partials_floats(rows, C), device=dev)
+    cnt = torch.zeros(1, device=dev, dtype=torch.int32)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    a = L.BatchNormArgs(rows=rows, c=C, eps=1e-5, momentum=0.1, relu=int(relu), x=x.data_ptr(), ldx=C,
+                        gamma=gamma.data_ptr(), beta=beta.data_ptr(), y=y.data_ptr(), ldy=C, mean=mean.data_ptr(),
+                        rstd=rstd.data_ptr(), running_mean=rm.data_ptr(), running_var=rv.data_ptr(),
+                        partials=part.data_ptr(), counter=cnt.data_ptr())
+    L.check(L.lib.encdiff_batchnorm_fwd(ctypes.byref(a), s), "bn fwd")
+    bn = torch.nn.BatchNorm2d(C).to(dev)
+    with torch.no_grad():
+        bn.weight.copy_(gamma)
+        bn.bias.copy_(beta)
+    xr = nhwc(x, Geom_(B, H)).requires_grad_(True)
+    ref = bn(xr)
+    ref = torch.relu(ref) if relu else ref
+    assert rel(nhwc(y, Geom_(B, H)), ref) < 1e-2
+    assert rel(rm, bn.running_mean) < 1e-4 and rel(rv, bn.running_var) < 1e-4
+    assert int(cnt.item()) == 0
+    dy = bf(rows, C)
+    ref.backward(nhwc(dy, Geom_(B, H)))
+    dx = torch.empty_like(x)
+    dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    a.dy, a.lddy, a.dx, a.lddx, a.dgamma, a.dbeta = dy.data_ptr(), C, dx.data_ptr(), C, dg.data_ptr(), db.data_ptr()
+    L.check(L.lib.encdiff_batchnorm_bwd(ctypes.byref(a), s), "bn bwd")
+    assert rel(nhwc(dx, Geom_(B, H)), xr.grad) < 2e-2
+    assert rel(dg, bn.weight.grad) < 2e-3 and rel(db, bn.bias.grad) < 2e-3
+
+
+def Geom_(B, H):
+    from encdiff_amd.ops import Geom
+    return Geom(B, H, H)
+
+
+@pytest.mark.parametrize("Hout,cin,cout", [(32, 8, 128), (16, 128, 128), (4, 128, 128)])
+def test_conv4x4s2(O, Hout, cin, cout):
+    """Conv2d(k4, s2, p1) forward, input gradient (transposed im2col mode) and weight gradient
+    vs torch fp32 on the same bf16 operands."""
+    torch.manual_seed(6)
+    B = 8
+    g = Geom_(B, Hout)
+    gi = Geom_(B, 2 * Hout)
+    x = bf(gi.pixels, cin)
+    w = torch.randn(cout, cin, 4, 4, device=dev) * (16 * cin) ** -0.5
+    wf = w.permute(0, 2, 3, 1).reshape(cout, 16 * cin).to(torch.bfloat16).contiguous()
+    wr = wf.float().view(cout, 4, 4, cin).permute(0, 3, 1, 2)
+    bias = torch.randn(cout, device=dev)
+    out = torch.empty(g.pixels, cout, device=dev, dtype=torch.bfloat16)
+    O.conv4x4s2_fwd(x, g, cin, wf, out, bias=bias)
+    ref = F.conv2d(nhwc(x, gi), wr, bias, stride=2, padding=1)
+    assert rel(nhwc(out, g), ref) < 1e-2
+    dy = bf(g.pixels, cout)
+    dw = torch.zeros(cout, 16 * cin, device=dev)
+    db = torch.zeros(cout, device=dev)
+    dx = torch.empty(gi.pixels, cin, device=dev, dtype=torch.bfloat16)
+    O.conv4x4s2_bwd_cl(dy, g, wf, x, cin, dw, dx, db)
+    xr = nhwc(x, gi).requires_grad_(True)
+    wrr = wr.clone().requires_grad_(True)
+    F.conv2d(xr, wrr, None, stride=2, padding=1).backward(nhwc(dy, g))
+    assert rel(nhwc(dx, gi), xr.grad) < 1e-2
+    assert rel(dw.view(cout, 4, 4, cin).permute(0, 3, 1, 2), wrr.grad) < 2e-3
+    assert rel(db, dy.float().sum(0)) < 2e-3
