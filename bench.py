@@ -74,27 +74,58 @@ def build_ldm():
     return instantiate_from_config(cfg).cuda(), cfg
 
 
-def record_gemms(tr):
-    """Arguments of every encdiff_gemm launch of one eager training step (the UNet's conv
-    and linear forward / dgrad / wgrad GEMMs), in launch order."""
+def _copy_args(argp):
     import ctypes as C
     from encdiff_amd import _lib as L
-    calls = []
-    orig = L.lib.encdiff_gemm
+    if not argp:
+        return None
+    a = L.GemmArgs()
+    C.memmove(C.byref(a), argp, C.sizeof(L.GemmArgs))
+    return a
 
-    class Rec:
-        def __call__(self, argp, stream):
-            a = L.GemmArgs()
-            C.memmove(C.byref(a), argp, C.sizeof(L.GemmArgs))
-            calls.append(a)
-            return orig(argp, stream)
-    L.lib.encdiff_gemm = Rec()
+
+def record_gemms(tr):
+    """Every GEMM-family launch of one eager training step, in order: single GEMMs
+    (encdiff_gemm), paired weight/input-gradient GEMMs with a deferred finalize riding along
+    (encdiff_gemm_pair_ex, encdiff_gemm_pair) and explicit finalizes (encdiff_gemm_finalize).
+    Returns [(kind, args...)]; `gemm_problems` lists the GEMM problems inside."""
+    from encdiff_amd import _lib as L
+    calls = []
+    names = ("encdiff_gemm", "encdiff_gemm_pair", "encdiff_gemm_pair_ex", "encdiff_gemm_finalize")
+    orig = {n: getattr(L.lib, n) for n in names}
+
+    def rec(name):
+        def f(*a):
+            stream = a[-1]
+            if name == "encdiff_gemm":
+                calls.append(("gemm", _copy_args(a[0])))
+            elif name == "encdiff_gemm_pair":
+                calls.append(("pair_ex", _copy_args(a[0]), _copy_args(a[1]), None, 0))
+            elif name == "encdiff_gemm_pair_ex":
+                calls.append(("pair_ex", _copy_args(a[0]), _copy_args(a[1]), _copy_args(a[2]), a[3]))
+            else:
+                calls.append(("finalize", _copy_args(a[0])))
+            return orig[name](*a[:-1], stream)
+        return f
+    for n in names:
+        setattr(L.lib, n, rec(n))
     try:
         tr.step_eager()
     finally:
-        L.lib.encdiff_gemm = orig
+        for n in names:
+            setattr(L.lib, n, orig[n])
     torch.cuda.synchronize()
     return calls
+
+
+def gemm_problems(calls):
+    out = []
+    for c in calls:
+        if c[0] == "gemm":
+            out.append(c[1])
+        elif c[0] == "pair_ex":
+            out += [c[1], c[2]]
+    return out
 
 
 def gemm_alg_bytes(a):
@@ -102,7 +133,8 @@ def gemm_alg_bytes(a):
     operand is its source image, not the 9x-expanded matrix), the output written once."""
     def src():
         pix = a.conv.batch * a.conv.h * a.conv.w
-        pix = pix * 4 if a.conv.resample == 1 else (pix // 4 if a.conv.resample == 2 else pix)
+        # DOWN2 / STRIDE2 / K4S2 read a (2h, 2w) source, UP2 / K4S2_T an (h/2, w/2) one
+        pix = pix * 4 if a.conv.resample in (1, 3, 4) else (pix // 4 if a.conv.resample in (2, 5) else pix)
         return 2.0 * pix * a.conv.cin
     abytes = src() if a.a_mode == 1 else 2.0 * a.M * a.K
     bbytes = src() if a.b_mode == 3 else 2.0 * a.N * a.K
@@ -113,9 +145,15 @@ def replay_gemms(calls, reps=1):
     import ctypes as C
     from encdiff_amd import _lib as L
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ref = lambda a: C.byref(a) if a is not None else None  # noqa: E731
     for _ in range(reps):
-        for a in calls:
-            L.check(L.lib.encdiff_gemm(C.byref(a), stream), "encdiff_gemm")
+        for c in calls:
+            if c[0] == "gemm":
+                L.check(L.lib.encdiff_gemm(ref(c[1]), stream), "encdiff_gemm")
+            elif c[0] == "pair_ex":
+                L.check(L.lib.encdiff_gemm_pair_ex(ref(c[1]), ref(c[2]), ref(c[3]), c[4], stream), "pair_ex")
+            else:
+                L.check(L.lib.encdiff_gemm_finalize(ref(c[1]), stream), "finalize")
 
 
 def kernel_roofline(tr, reps=10):
@@ -125,7 +163,8 @@ def kernel_roofline(tr, reps=10):
     between HIP events on the replay stream: achieved = algorithmic flops (sum 2*M*N*K)
     / GPU time, per launch averages reported beside it."""
     calls = record_gemms(tr)
-    flops = sum(2.0 * a.M * a.N * a.K for a in calls)
+    probs = gemm_problems(calls)
+    flops = sum(2.0 * a.M * a.N * a.K for a in probs)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
@@ -142,13 +181,14 @@ def kernel_roofline(tr, reps=10):
         e1.record(s)
         s.synchronize()
     t_set = e0.elapsed_time(e1) / 1e3 / reps
-    out = {"kernel": f"gemm_kernel<*> family: {len(calls)} UNet conv/linear GEMM launches per step "
-                     "(fwd+dgrad+wgrad, incl. split-K finalize)",
+    out = {"kernel": f"GEMM family (gemm_kernel / paired gemm2_kernel + split-K finalizes): {len(probs)} "
+                     f"conv/linear GEMM problems of the step (UNet, VQ encoder, Encoder4; fwd+dgrad+wgrad) "
+                     f"in {len(calls)} calls",
            "bound": "mfma", "achieved": flops / t_set / 1e12, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
            "frac": flops / t_set / 1e12 / PEAK_BF16_TFLOPS, "traffic": None,
            "avg_us": t_set / len(calls) * 1e6, "flops_per_launch": flops / len(calls),
            "launches_per_step": len(calls), "gemm_ms_per_step": t_set * 1e3,
-           "alg_bytes_per_launch": sum(gemm_alg_bytes(a) for a in calls) / len(calls)}
+           "alg_bytes_per_launch": sum(gemm_alg_bytes(a) for a in probs) / len(calls)}
     prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "gemm_traffic.json")
     if os.path.exists(prof):  # HBM bytes per launch from the committed rocprofv3 PMC passes
         with open(prof) as f:

@@ -99,6 +99,8 @@ class PackJob(C.Structure):
 _PROTOS = {
     "encdiff_gemm": [C.POINTER(GemmArgs), vp],
     "encdiff_gemm_pair": [C.POINTER(GemmArgs), C.POINTER(GemmArgs), vp],
+    "encdiff_gemm_pair_ex": [C.POINTER(GemmArgs), C.POINTER(GemmArgs), C.POINTER(GemmArgs), C.c_int, vp],
+    "encdiff_gemm_finalize": [C.POINTER(GemmArgs), vp],
     "encdiff_groupnorm_fwd": [C.POINTER(GroupNormArgs), vp],
     "encdiff_groupnorm_bwd": [C.POINTER(GroupNormArgs), vp],
     "encdiff_layernorm_fwd": [C.POINTER(LayerNormArgs), vp],

@@ -229,6 +229,7 @@ class Encoder4TrunkExecutor:
                          bias_grad=self.G(c.name + ".bias"))
                 gw = self.G(c.name + ".weight").view(c.cout, self.cin_img, 16)
                 gw.add_(b["dw0"].view(c.cout, 16, 8)[:, :, :self.cin_img].permute(0, 2, 1))
+                ops.flush()
                 break
             x = b[f"a{i - 1}"]
             ops.conv4x4s2_bwd_cl(dy, g, self.pack.view(c.name), x, c.cin, self.Graw(c.name + ".weight"),

@@ -468,25 +468,32 @@ __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, cons
   gemm_tile<BM, BN, AM, BMD>(p, aux, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
+__device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const int bid, const int nblk);
+
 // Two independent GEMMs in one 1-D grid: blocks [0, n1) run problem 1 (64 x 64 tiles),
-// the rest problem 2 (tile BM2 x BN2).  A layer's weight gradient (problem 1: deep split-K,
-// the longer-running blocks, dispatched first) and its input gradient (problem 2) then
-// share the machine instead of running back to back, each too small to fill 256 CUs, and
-// one launch boundary disappears.
+// the next n2 problem 2 (tile BM2 x BN2), the last nf the split-K finalize of an EARLIER
+// launch's weight gradient (pf), deferred into this launch.  A layer's weight gradient
+// (problem 1: deep split-K, the longer-running blocks, dispatched first) and its input
+// gradient (problem 2) share the machine instead of running back to back, each too small
+// to fill 256 CUs; the previous layer's weight-gradient finalize rides along, so neither
+// needs a launch of its own.
 template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2>
 __global__ __launch_bounds__(256) void gemm2_kernel(const EncdiffGemmArgs p1, const GemmAux aux1,
                                                     const EncdiffGemmArgs p2, const GemmAux aux2, int gx1,
-                                                    int gy1, int gx2, int gy2) {
+                                                    int gy1, int gx2, int gy2, const EncdiffGemmArgs pf, int nf) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
   const int n1 = gx1 * gy1 * p1.split_k;
+  const int n2 = gx2 * gy2 * p2.split_k;
   int i = blockIdx.x;
   if (i < n1) {
     const int bx = i % gx1, t = i / gx1;
     gemm_tile<64, 64, AM1, BMD1>(p1, aux1, bx, t % gy1, t / gy1, smem);
-  } else {
+  } else if (i < n1 + n2) {
     i -= n1;
     const int bx = i % gx2, t = i / gx2;
     gemm_tile<BM2, BN2, AM2, BMD2>(p2, aux2, bx, t % gy2, t / gy2, smem);
+  } else {
+    gemm_finalize(pf, i - n1 - n2, nf);
   }
 }
 
@@ -664,7 +671,7 @@ int launch_one(const GemmPlan& g, hipStream_t s) {
 }
 
 template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2>
-hipError_t launch_pair_t(const GemmPlan& g1, const GemmPlan& g2, hipStream_t s) {
+hipError_t launch_pair_t(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
   using G1 = Gemm<64, 64, AM1, BMD1>;
   using G2 = Gemm<BM2, BN2, AM2, BMD2>;
   constexpr size_t lds = G1::LDS_BYTES > G2::LDS_BYTES ? G1::LDS_BYTES : G2::LDS_BYTES;
@@ -673,20 +680,26 @@ hipError_t launch_pair_t(const GemmPlan& g1, const GemmPlan& g2, hipStream_t s) 
   if (attr_ok != hipSuccess) return attr_ok;
   const int gx1 = (g1.p.M + 63) / 64, gy1 = (g1.p.N + 63) / 64;
   const int gx2 = (g2.p.M + BM2 - 1) / BM2, gy2 = (g2.p.N + BN2 - 1) / BN2;
-  const long nb = (long)gx1 * gy1 * g1.p.split_k + (long)gx2 * gy2 * g2.p.split_k;
+  const long nb = (long)gx1 * gy1 * g1.p.split_k + (long)gx2 * gy2 * g2.p.split_k + nf;
   hipLaunchKernelGGL((gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2>), dim3((unsigned)nb), dim3(256), lds, s, g1.p,
-                     g1.aux, g2.p, g2.aux, gx1, gy1, gx2, gy2);
+                     g1.aux, g2.p, g2.aux, gx1, gy1, gx2, gy2, pf, nf);
   return hipGetLastError();
 }
 
 template <int AM1, int BMD1, int AM2, int BMD2>
-hipError_t launch_pair_tiles(const GemmPlan& g1, const GemmPlan& g2, hipStream_t s) {
+hipError_t launch_pair_tiles(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf,
+                             hipStream_t s) {
   switch (g2.tile) {
-    case 1: return launch_pair_t<AM1, BMD1, 128, 128, AM2, BMD2>(g1, g2, s);
-    case 2: return launch_pair_t<AM1, BMD1, 128, 64, AM2, BMD2>(g1, g2, s);
-    case 3: return launch_pair_t<AM1, BMD1, 64, 128, AM2, BMD2>(g1, g2, s);
-    default: return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2>(g1, g2, s);
+    case 1: return launch_pair_t<AM1, BMD1, 128, 128, AM2, BMD2>(g1, g2, pf, nf, s);
+    case 2: return launch_pair_t<AM1, BMD1, 128, 64, AM2, BMD2>(g1, g2, pf, nf, s);
+    case 3: return launch_pair_t<AM1, BMD1, 64, 128, AM2, BMD2>(g1, g2, pf, nf, s);
+    default: return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2>(g1, g2, pf, nf, s);
   }
+}
+
+hipError_t launch_finalize(const EncdiffGemmArgs& u, hipStream_t s) {
+  hipLaunchKernelGGL(gemm_finalize_kernel, dim3((unsigned)fin_blocks(u)), dim3(256), 0, s, u);
+  return hipGetLastError();
 }
 
 }  // namespace
@@ -698,36 +711,63 @@ extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
   return launch_one(g, (hipStream_t)stream);
 }
 
-extern "C" int encdiff_gemm_pair(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad, void* stream) {
-  GemmPlan g1, g2;
+extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad,
+                                    const EncdiffGemmArgs* prev_wgrad, int defer, void* stream) {
+  GemmPlan g1, g2, gp;
   int rc = prepare(wgrad, g1);
   if (rc != ENCDIFF_OK) return rc;
   rc = prepare(dgrad, g2);
   if (rc != ENCDIFF_OK) return rc;
+  bool have_prev = false;
+  if (prev_wgrad) {
+    rc = prepare(prev_wgrad, gp);
+    if (rc != ENCDIFF_OK) return rc;
+    have_prev = gp.ws_path;
+  }
   hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
   const int a1 = g1.p.a_mode, b1 = g1.p.b_mode, a2 = g2.p.a_mode, b2 = g2.p.b_mode;
   const bool lin = a1 == ENCDIFF_OPA_ROWM && b1 == ENCDIFF_OPB_ROWN && a2 == ENCDIFF_OPA_ROWK && b2 == ENCDIFF_OPB_ROWN;
   const bool conv = a1 == ENCDIFF_OPA_ROWM && b1 == ENCDIFF_OPB_IM2COL && a2 == ENCDIFF_OPA_IM2COL &&
                     b2 == ENCDIFF_OPB_CONV_DGRAD;
-  // pairs the fused kernel does not cover run back to back (same results)
-  if ((!lin && !conv) || g1.tile != 4) {
-    rc = launch_one(g1, s);
-    return rc != ENCDIFF_OK ? rc : launch_one(g2, s);
-  }
   // both split-K problems need disjoint slabs
   if (g1.ws_path && g2.ws_path && g1.p.workspace == g2.p.workspace) return ENCDIFF_ERR_ARG;
-  hipError_t e = lin ? launch_pair_tiles<A_ROWM, B_ROWN, A_ROWK, B_ROWN>(g1, g2, s)
-                     : launch_pair_tiles<A_ROWM, B_IM2COL, A_IM2COL, B_CONVD>(g1, g2, s);
+  const bool defer1 = defer && g1.ws_path;
+  if ((!lin && !conv) || g1.tile != 4) {  // pairs the fused kernel does not cover: back to back
+    if (have_prev && (e = launch_finalize(gp.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+    GemmPlan w = g1;
+    w.ws_path = g1.ws_path && !defer1;
+    rc = launch_one(w, s);
+    return rc != ENCDIFF_OK ? rc : launch_one(g2, s);
+  }
+  const EncdiffGemmArgs pf = have_prev ? gp.user : g1.user;
+  const int nf = have_prev ? fin_blocks(gp.user) : 0;
+  e = lin ? launch_pair_tiles<A_ROWM, B_ROWN, A_ROWK, B_ROWN>(g1, g2, pf, nf, s)
+          : launch_pair_tiles<A_ROWM, B_IM2COL, A_IM2COL, B_CONVD>(g1, g2, pf, nf, s);
   if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
-  if (g1.ws_path && g2.ws_path) {
-    const int f1 = fin_blocks(g1.user), f2 = fin_blocks(g2.user);
-    hipLaunchKernelGGL(gemm_finalize2_kernel, dim3((unsigned)(f1 + f2)), dim3(256), 0, s, g1.user, g2.user, f1);
-  } else if (g1.ws_path) {
-    hipLaunchKernelGGL(gemm_finalize_kernel, dim3((unsigned)fin_blocks(g1.user)), dim3(256), 0, s, g1.user);
+  const bool f1 = g1.ws_path && !defer1;
+  if (f1 && g2.ws_path) {
+    const int n1 = fin_blocks(g1.user), n2 = fin_blocks(g2.user);
+    hipLaunchKernelGGL(gemm_finalize2_kernel, dim3((unsigned)(n1 + n2)), dim3(256), 0, s, g1.user, g2.user, n1);
+  } else if (f1) {
+    launch_finalize(g1.user, s);
   } else if (g2.ws_path) {
-    hipLaunchKernelGGL(gemm_finalize_kernel, dim3((unsigned)fin_blocks(g2.user)), dim3(256), 0, s, g2.user);
+    launch_finalize(g2.user, s);
   }
   e = hipGetLastError();
+  return e != hipSuccess ? ENCDIFF_ERR_LAUNCH - (int)e : ENCDIFF_OK;
+}
+
+extern "C" int encdiff_gemm_pair(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad, void* stream) {
+  return encdiff_gemm_pair_ex(wgrad, dgrad, nullptr, 0, stream);
+}
+
+extern "C" int encdiff_gemm_finalize(const EncdiffGemmArgs* args, void* stream) {
+  GemmPlan g;
+  const int rc = prepare(args, g);
+  if (rc != ENCDIFF_OK) return rc;
+  if (!g.ws_path) return ENCDIFF_OK;
+  const hipError_t e = launch_finalize(g.user, (hipStream_t)stream);
   return e != hipSuccess ? ENCDIFF_ERR_LAUNCH - (int)e : ENCDIFF_OK;
 }
 

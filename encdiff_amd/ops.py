@@ -51,7 +51,8 @@ def _conv_geom(g: Geom, cin: int, resample: int, src: torch.Tensor) -> L.ConvGeo
 
 
 _WS = {}
-WS_FLOATS = 8 * 1024 * 1024          # fp32 split-K scratch (zero-initialised, self-cleaning)
+WS_FLOATS = 16 * 1024 * 1024         # fp32 split-K scratch per stream (two halves, see gemm_pair)
+WS_HALF = WS_FLOATS // 2
 _TILES = None
 _TILE_SHAPES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64)}
 
@@ -136,31 +137,61 @@ def ws_floats(args) -> int:
     return args.split_k * args.M * args.N + (args.split_k * args.M if args.bias_grad else 0)
 
 
+_PENDING = {}  # stream -> GemmArgs of a weight gradient whose split-K finalize is deferred
+_HALF = {}     # stream -> workspace half used by the last paired launch
+
+
+def flush():
+    """Run the deferred weight-gradient finalize of the current stream, if any (the end of a
+    backward, or before a GEMM that needs the workspace)."""
+    key = torch.cuda.current_stream().cuda_stream
+    pend = _PENDING.pop(key, None)
+    if pend is not None:
+        check(lib.encdiff_gemm_finalize(C.byref(pend), _s()), "encdiff_gemm_finalize")
+
+
 def gemm(M, N, K, a, lda, b, ldb, c, ldc, **kw):
     args = gemm_args(M, N, K, a, lda, b, ldb, c, ldc, **kw)
+    if ws_floats(args):
+        flush()  # its slabs start at offset 0: the deferred slabs must be consumed first
     check(lib.encdiff_gemm(C.byref(args), _s()), "encdiff_gemm")
 
 
-PAIR = True  # fuse a layer's weight- and input-gradient GEMMs into one launch (encdiff_gemm_pair)
+PAIR = True  # fuse a layer's weight- and input-gradient GEMMs into one launch (encdiff_gemm_pair_ex)
 
 
-def gemm_pair(wgrad_args, dgrad_fn):
-    """Launch a weight-gradient GEMM and an input-gradient GEMM together.  `dgrad_fn(ws_offset)`
-    returns the input-gradient GemmArgs with its split-K slabs placed after the weight
-    gradient's, so the two never share workspace."""
-    off = ws_floats(wgrad_args)
-    d = dgrad_fn(0)
-    if off and ws_floats(d):
-        if off + ws_floats(d) > WS_FLOATS:  # both sets of slabs do not fit: run back to back
-            check(lib.encdiff_gemm(C.byref(wgrad_args), _s()), "encdiff_gemm")
-            check(lib.encdiff_gemm(C.byref(d), _s()), "encdiff_gemm")
-            return
-        d = dgrad_fn(off)
+def gemm_pair(wgrad_fn, dgrad_fn):
+    """Launch a layer's weight-gradient and input-gradient GEMMs together (`wgrad_fn(off)`,
+    `dgrad_fn(off)` build their GemmArgs with split-K slabs at workspace offset `off`).
+    Consecutive pairs alternate between the two workspace halves: the weight gradient's
+    finalize is deferred into the NEXT pair's launch (its slabs stay intact in the other
+    half), so a backward of N layers needs no finalize launches for weight gradients but the
+    last (`flush`)."""
+    key = torch.cuda.current_stream().cuda_stream
     if not PAIR:
-        check(lib.encdiff_gemm(C.byref(wgrad_args), _s()), "encdiff_gemm")
+        flush()
+        w = wgrad_fn(0)
+        d = dgrad_fn(ws_floats(w))
+        check(lib.encdiff_gemm(C.byref(w), _s()), "encdiff_gemm")
         check(lib.encdiff_gemm(C.byref(d), _s()), "encdiff_gemm")
         return
-    check(lib.encdiff_gemm_pair(C.byref(wgrad_args), C.byref(d), _s()), "encdiff_gemm_pair")
+    w = wgrad_fn(0)
+    nw = ws_floats(w)
+    if nw + ws_floats(dgrad_fn(0)) > WS_HALF:  # does not fit a half: plain pair, whole workspace
+        flush()
+        d = dgrad_fn(nw)
+        check(lib.encdiff_gemm_pair(C.byref(w), C.byref(d), _s()), "encdiff_gemm_pair")
+        return
+    h = 1 - _HALF.get(key, 1)
+    if h:
+        w = wgrad_fn(h * WS_HALF)
+    d = dgrad_fn(h * WS_HALF + nw)
+    prev = _PENDING.pop(key, None)
+    check(lib.encdiff_gemm_pair_ex(C.byref(w), C.byref(d), C.byref(prev) if prev is not None else None, 1, _s()),
+          "encdiff_gemm_pair_ex")
+    if nw:
+        _PENDING[key] = w
+    _HALF[key] = h
 
 
 # ------------------------------------------------------------------ linear layers
@@ -187,23 +218,25 @@ def linear_dgrad_args(dy, w, dx, resid=None, ws_offset=0):
                      resid=resid, ld_resid=_ld(resid) if resid is not None else 0, ws_offset=ws_offset)
 
 
-def linear_wgrad_args(dy, x, dw, db=None):
+def linear_wgrad_args(dy, x, dw, db=None, ws_offset=0):
     M, N = dy.shape
     K = x.shape[1]
     return gemm_args(N, K, M, dy, _ld(dy), x, _ld(x), dw, K, a_mode=L.OPA_ROWM, b_mode=L.OPB_ROWN,
-                     c_mode=L.OUT_F32_ACCUM, bias_grad=db)
+                     c_mode=L.OUT_F32_ACCUM, bias_grad=db, ws_offset=ws_offset)
 
 
 def linear_wgrad(dy, x, dw, db=None):
     """dw[N][K] += dy[M][N]^T x[M][K] (split-K slabs summed in order: reproducible);
     db[N] += sum_m dy[m][n]."""
     args = linear_wgrad_args(dy, x, dw, db)
+    if ws_floats(args):
+        flush()
     check(lib.encdiff_gemm(C.byref(args), _s()), "encdiff_gemm")
 
 
 def linear_bwd(dy, w, x, dx, dw, db=None, resid=None):
     """Backward of one linear layer: dw += dy^T x (+ db), dx = dy w (+ resid), one launch."""
-    gemm_pair(linear_wgrad_args(dy, x, dw, db), lambda off: linear_dgrad_args(dy, w, dx, resid, off))
+    gemm_pair(lambda off: linear_wgrad_args(dy, x, dw, db, off), lambda off: linear_dgrad_args(dy, w, dx, resid, off))
 
 
 # ------------------------------------------------------------------ 3x3 convolutions
@@ -232,17 +265,19 @@ def conv3x3_wgrad(dy, x, g: Geom, cin, dw_ref, db=None, resample=L.RESAMPLE_NONE
          c_mode=L.OUT_F32_ATOMIC_CONVW, conv=_conv_geom(g, cin, resample, x), convw_cin=cin, bias_grad=db)
 
 
-def conv3x3_wgrad_cl_args(dy, x, g: Geom, cin, dw_cl, db=None, resample=L.RESAMPLE_NONE):
+def conv3x3_wgrad_cl_args(dy, x, g: Geom, cin, dw_cl, db=None, resample=L.RESAMPLE_NONE, ws_offset=0):
     cout = dy.shape[1]
     return gemm_args(cout, 9 * cin, g.pixels, dy, _ld(dy), x, _ld(x), dw_cl, _ld(dw_cl), a_mode=L.OPA_ROWM,
                      b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32_ACCUM, conv=_conv_geom(g, cin, resample, x),
-                     bias_grad=db)
+                     bias_grad=db, ws_offset=ws_offset)
 
 
 def conv3x3_wgrad_cl(dy, x, g: Geom, cin, dw_cl, db=None, resample=L.RESAMPLE_NONE):
     """dw_cl[cout][9*cin] (fp32, channels-last [co][kh][kw][ci]) += dy^T im2col(resample(x))
     (split-K slabs summed in order: reproducible)."""
     args = conv3x3_wgrad_cl_args(dy, x, g, cin, dw_cl, db, resample)
+    if ws_floats(args):
+        flush()
     check(lib.encdiff_gemm(C.byref(args), _s()), "encdiff_gemm")
 
 
@@ -257,7 +292,7 @@ def conv3x3_dgrad_args(dy, g: Geom, wf, dx, resid=None, ws_offset=0):
 def conv3x3_bwd_cl(dy, g: Geom, wf, x, cin, dw_cl, dx, db=None, resample=L.RESAMPLE_NONE, resid=None):
     """Backward of one 3x3 conv: dw_cl += dy^T im2col(resample(x)) (+ db) and
     dx = conv3x3^T(dy) (+ resid) at the conv resolution, one launch."""
-    gemm_pair(conv3x3_wgrad_cl_args(dy, x, g, cin, dw_cl, db, resample),
+    gemm_pair(lambda off: conv3x3_wgrad_cl_args(dy, x, g, cin, dw_cl, db, resample, off),
               lambda off: conv3x3_dgrad_args(dy, g, wf, dx, resid, off))
 
 
@@ -276,10 +311,11 @@ def conv4x4s2_bwd_cl(dy, g_out: Geom, wf, x, cin, dw_cl, dx, db=None):
     dx (2h, 2w) = transposed conv of dy, one paired launch."""
     cout = wf.shape[0]
     gin = Geom(g_out.batch, 2 * g_out.h, 2 * g_out.w)
-    wargs = gemm_args(cout, 16 * cin, g_out.pixels, dy, _ld(dy), x, _ld(x), dw_cl, _ld(dw_cl), a_mode=L.OPA_ROWM,
-                      b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32_ACCUM,
-                      conv=L.ConvGeom(batch=g_out.batch, h=g_out.h, w=g_out.w, cin=cin, resample=L.RESAMPLE_K4S2,
-                                      ld_src=_ld(x)), bias_grad=db)
+    def wargs(off):
+        return gemm_args(cout, 16 * cin, g_out.pixels, dy, _ld(dy), x, _ld(x), dw_cl, _ld(dw_cl),
+                         a_mode=L.OPA_ROWM, b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32_ACCUM,
+                         conv=L.ConvGeom(batch=g_out.batch, h=g_out.h, w=g_out.w, cin=cin,
+                                         resample=L.RESAMPLE_K4S2, ld_src=_ld(x)), bias_grad=db, ws_offset=off)
 
     def dargs(off):
         return gemm_args(gin.pixels, cin, 16 * cout, dy, _ld(dy), wf, _ld(wf), dx, _ld(dx), a_mode=L.OPA_IM2COL,

@@ -552,6 +552,7 @@ class UNetExecutor:
         ops.gemm(B * self.lu, self.cd, sp.kv_total, self.dKV, self.dKV.stride(0), self.W("kv_all"), self.cd,
                  self.d_ctx, self.cd, b_mode=L.OPB_ROWN, c_mode=L.OUT_F32)
         ops.linear_wgrad(self.dKV, self.ctx16, self.kv_w_grad)
+        ops.flush()  # the last deferred weight-gradient finalize
         # fold all norm affine partial sums into the arena
         self.gn.reduce()
         self.ln.reduce()

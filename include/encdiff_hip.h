@@ -116,6 +116,17 @@ int encdiff_gemm(const EncdiffGemmArgs* args, void* stream);
  * one nn.Linear / nn.Conv2d (openaimodel_enc.py:230,237-241; attention.py:159-167,43,58). */
 int encdiff_gemm_pair(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad, void* stream);
 
+/* encdiff_gemm_pair with deferred weight-gradient finalizes.  defer != 0: when `wgrad` uses
+ * split-K slabs its finalize (C += ordered slab sum, + bias gradient) is NOT launched; the
+ * caller hands `wgrad` to a later call as `prev_wgrad`, whose launch then runs that finalize
+ * in extra workgroups (or to encdiff_gemm_finalize).  Its slabs must stay untouched until
+ * then (the next pair uses a different workspace region).  Results are identical. */
+int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad,
+                         const EncdiffGemmArgs* prev_wgrad, int defer, void* stream);
+
+/* The split-K finalize of a GEMM launched with a deferred finalize (no-op without slabs). */
+int encdiff_gemm_finalize(const EncdiffGemmArgs* args, void* stream);
+
 /* ---------------------------------------------------------------- GroupNorm
  * y = act( GN(x) * (1 + scale[b,c]) + shift[b,c] )
  * Replaces GroupNorm32 + SiLU (+ FiLM) of ResBlock in/out_layers and UNet.out

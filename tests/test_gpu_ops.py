@@ -478,6 +478,7 @@ def test_gemm_pair_matches_two_launches(O, kind, M, C, K):
             dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
             if pair:
                 O.linear_bwd(dy, w, x, dx, dw, db)
+                O.flush()  # the weight-gradient finalize is deferred into the next pair / flush
             else:
                 O.linear_wgrad(dy, x, dw, db)
                 O.linear_dgrad(dy, w, dx)
@@ -494,6 +495,7 @@ def test_gemm_pair_matches_two_launches(O, kind, M, C, K):
             dx = torch.empty(g.pixels, cin, device=dev, dtype=torch.bfloat16)
             if pair:
                 O.conv3x3_bwd_cl(dy, g, wf, x, cin, dw, dx, db)
+                O.flush()
             else:
                 O.conv3x3_wgrad_cl(dy, x, g, cin, dw, db)
                 O.conv3x3_dgrad(dy, g, wf, dx)
@@ -574,9 +576,38 @@ def test_conv4x4s2(O, Hout, cin, cout):
     db = torch.zeros(cout, device=dev)
     dx = torch.empty(gi.pixels, cin, device=dev, dtype=torch.bfloat16)
     O.conv4x4s2_bwd_cl(dy, g, wf, x, cin, dw, dx, db)
+    O.flush()
     xr = nhwc(x, gi).requires_grad_(True)
     wrr = wr.clone().requires_grad_(True)
     F.conv2d(xr, wrr, None, stride=2, padding=1).backward(nhwc(dy, g))
     assert rel(nhwc(dx, gi), xr.grad) < 1e-2
     assert rel(dw.view(cout, 4, 4, cin).permute(0, 3, 1, 2), wrr.grad) < 2e-3
     assert rel(db, dy.float().sum(0)) < 2e-3
+
+
+def test_gemm_pair_chain_deferred_finalize(O):
+    """A chain of paired backward launches: each weight gradient's split-K finalize runs inside
+    the NEXT pair's launch (ping-pong workspace halves), the last one at flush().  Bitwise equal
+    to unpaired launches."""
+    torch.manual_seed(4)
+    shapes = [(32768, 64, 64), (8192, 128, 512), (2048, 256, 256), (32768, 192, 64), (512, 256, 1024)]
+    ins = [(bf(M, C), bf(M, K), bf(C, K, scale=K ** -0.5)) for M, C, K in shapes]
+    res = []
+    for pair in (False, True):
+        O.PAIR = pair
+        try:
+            outs = []
+            for (dy, x, w), (M, C, K) in zip(ins, shapes):
+                dw = torch.zeros(C, K, device=dev)
+                db = torch.zeros(C, device=dev)
+                dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+                O.linear_bwd(dy, w, x, dx, dw, db)
+                outs += [dw, db, dx]
+            O.flush()
+        finally:
+            O.PAIR = True
+        res.append(outs)
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    for (dy, x, w), k in zip(ins, range(0, 15, 3)):
+        assert rel(res[1][k], dy.float().t() @ x.float()) < 2e-3

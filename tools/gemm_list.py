@@ -37,7 +37,7 @@ def main():
     tr = HipTrainer(ldm, args.batch, graph=False)
     tr.init_scale_factor()
     tr.step_eager()
-    calls = bench.record_gemms(tr)
+    calls = bench.gemm_problems(bench.record_gemms(tr))
     orig = L.lib.encdiff_gemm
     ev = lambda: torch.cuda.Event(enable_timing=True)
 
@@ -63,6 +63,8 @@ def main():
     def cat(a):
         return {(1, 0): "conv_fwd", (1, 2): "conv_dgrad", (2, 3): "conv_wgrad", (0, 0): "lin_fwd",
                 (0, 1): "lin_dgrad", (2, 1): "lin_wgrad"}.get((a.a_mode, a.b_mode), str((a.a_mode, a.b_mode)))
+
+    # time each problem on its own (its own split-K finalize included, never deferred)
 
     seen = {}
     groups = defaultdict(list)

@@ -50,10 +50,11 @@ def run(batch: int):
     bench.replay_gemms(calls)
     torch.cuda._sleep(1000)
     torch.cuda.synchronize()
-    alg = sum(bench.gemm_alg_bytes(a) for a in calls)
+    probs = bench.gemm_problems(calls)
+    alg = sum(bench.gemm_alg_bytes(a) for a in probs)
     with open(os.path.join(REPO, "gpurun_out", "gemm_traffic_calls.json"), "w") as f:
         json.dump({"launches": len(calls), "alg_bytes": alg,
-                   "flops": sum(2.0 * a.M * a.N * a.K for a in calls)}, f)
+                   "flops": sum(2.0 * a.M * a.N * a.K for a in probs)}, f)
     print(f"replayed {len(calls)} gemm launches")
 
 
