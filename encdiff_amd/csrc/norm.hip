@@ -7,6 +7,8 @@
 // The backward recomputes the forward from x and the saved statistics and emits
 // per-image partial sums for dgamma/dbeta (reduced once per step by
 // encdiff_reduce_partials) and the FiLM gradients d(scale), d(shift) per (b, c).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -59,17 +61,45 @@ ED_DEV void slice_reduce(float (&q)[NQ][8], const GnSlice& L, float* red, float*
   const bool pow2 = (L.nvc & (L.nvc - 1)) == 0;
   int rows;
   if (pow2) {
-    for (int off = L.nvc; off < 64; off <<= 1) {
+    // Butterfly reduce-scatter over the lanes sharing tv (lane bits >= log2(nvc)): at each of
+    // the first three levels a lane keeps half of its channel set and sends the other half
+    // (4, 2, 1 shuffles per k instead of 8), so after them it owns ONE channel's partial;
+    // further levels add single values.  ~9 shuffles per k instead of 40 (nvc = 2): the
+    // shuffles (ds_bpermute, LDS latency each) were the latency chain of the whole kernel.
+    int c = 0, hs = 4, off = L.nvc;
 #pragma unroll
-      for (int k = 0; k < NQ; ++k)
+    for (int lvl = 0; lvl < 3; ++lvl, hs >>= 1) {
+      if (off < 64) {
+        const bool hi = (lane & off) != 0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) q[k][i] += __shfl_xor(q[k][i], off, 64);
+        for (int k = 0; k < NQ; ++k) {
+          float send[4], recv[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (i < hs) send[i] = hi ? q[k][i] : q[k][i + hs];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (i < hs) recv[i] = __shfl_xor(send[i], off, 64);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (i < hs) q[k][i] = (hi ? q[k][i + hs] : q[k][i]) + recv[i];
+        }
+        c += hi ? hs : 0;
+        off <<= 1;
+      }
     }
-    if (lane < L.nvc) {
+    const int nval = 8 >> __builtin_ctz((unsigned)(off / L.nvc));  // 8 >> (butterfly levels done)
+    for (; off < 64; off <<= 1) {
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) q[k][0] += __shfl_xor(q[k][0], off, 64);
+    }
+    // lanes whose remaining-level bits are zero hold the totals of channels c .. c+nval-1
+    // (nval = 1 after three butterfly levels; 2, 4, 8 when fewer levels exist)
+    const int owner_mask = 63 & ~(L.nvc * 8 - 1);
+    if ((lane & owner_mask) == 0) {
 #pragma unroll
       for (int k = 0; k < NQ; ++k)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) red[(wave * NQ + k) * L.cs + L.tv * 8 + i] = q[k][i];
+        for (int i = 0; i < nval; ++i) red[(wave * NQ + k) * L.cs + L.tv * 8 + c + i] = q[k][i];
     }
     rows = L.nvc >= 64 ? GN_THREADS / L.nvc : GN_THREADS / 64;
   } else {
@@ -380,12 +410,20 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const EncdiffLayerNormArgs 
 }
 
 // channel-slice width: the narrowest multiple of lcm(8, channels-per-group) dividing C whose
-// slice holds >= 4096 elements (so small images still fill a workgroup), else all of C.
+// slice holds >= gn_min_slice() elements (so small images still fill a workgroup), else all of C.
+int gn_min_slice() {
+  static const int v = [] {
+    const char* e = getenv("ENCDIFF_GN_MIN_SLICE");  // tuning knob (elements per workgroup)
+    return e ? atoi(e) : 8192;  // measured best of 1K..64K on the step's shapes (tools/kbench.py)
+  }();
+  return v;
+}
+
 int gn_slice(int C, int HW, int cpg) {
   int unit = 8;
   while (unit % cpg) unit += 8;
   for (int w = unit; w < C; w += unit)
-    if (C % w == 0 && (long)w * HW >= 4096) return w;
+    if (C % w == 0 && (long)w * HW >= gn_min_slice()) return w;
   return C;
 }
 
