@@ -51,7 +51,7 @@ def _conv_geom(g: Geom, cin: int, resample: int, src: torch.Tensor) -> L.ConvGeo
 
 
 _WS = {}
-WS_FLOATS = 16 * 1024 * 1024         # fp32 split-K scratch per stream (two halves, see gemm_pair)
+WS_FLOATS = 64 * 1024 * 1024         # fp32 split-K scratch per stream, 256 MB (two halves, see gemm_pair)
 WS_HALF = WS_FLOATS // 2
 _TILES = None
 _TILE_SHAPES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64)}
@@ -73,15 +73,21 @@ def _tile_table():
     if _TILES is None:
         import json
         import os
-        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_tiles.json")
+        path = os.environ.get("ENCDIFF_GEMM_TILES") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                    "gemm_tiles.json")
         _TILES = json.load(open(path)) if os.path.exists(path) else {}
     return _TILES
 
 
-def plan(M, N, K, a_mode, b_mode, c_mode):
+def plan_key(M, N, K, a_mode, b_mode, c_mode, resample=0):
+    key = f"{a_mode},{b_mode},{c_mode},{M},{N},{K}"
+    return key + (f",r{resample}" if resample else "")
+
+
+def plan(M, N, K, a_mode, b_mode, c_mode, resample=0):
     """(tile, split_k) for a GEMM: measured table (tools/gemm_profile.py --write-table) first,
     else a heuristic aiming at >= 256 workgroups with bounded split-K traffic."""
-    hit = _tile_table().get(f"{a_mode},{b_mode},{c_mode},{M},{N},{K}")
+    hit = _tile_table().get(plan_key(M, N, K, a_mode, b_mode, c_mode, resample))
     if hit is not None:
         tile, split = int(hit[0]), int(hit[1])
         if split == 1 or c_mode in (L.OUT_F32_ATOMIC, L.OUT_F32_ATOMIC_CONVW) or split * M * (N + 1) <= WS_FLOATS:
@@ -103,7 +109,7 @@ def plan(M, N, K, a_mode, b_mode, c_mode):
         while nb * split < 256 and K // (split * 2) >= 256 and (split * 2) * M * N * 4 <= (8 << 20):
             split *= 2
     else:  # slab split-K (bf16 / f32 / f32-accumulate outputs)
-        while nb * split < 256 and K // (split * 2) >= 256 and (split * 2) * M * (N + 1) <= WS_FLOATS:
+        while nb * split < 256 and K // (split * 2) >= 256 and (split * 2) * M * (N + 1) <= WS_HALF // 2:
             split *= 2
     return tile, split
 
@@ -114,7 +120,7 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
     """EncdiffGemmArgs with the measured (tile, split) plan; split-K slabs start `ws_offset`
     floats into this stream's workspace."""
     if split_k is None or tile == 0:
-        t, sp = plan(M, N, K, a_mode, b_mode, c_mode)
+        t, sp = plan(M, N, K, a_mode, b_mode, c_mode, conv.resample if conv is not None else 0)
         tile = tile or t
         split_k = split_k or sp
     ws = None

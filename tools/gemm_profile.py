@@ -71,24 +71,11 @@ def main():
     for i, n in enumerate(names):
         print(f"phase {n:22s} {e[i].elapsed_time(e[i + 1]):8.3f} ms")
 
-    # ---- record GEMMs ---------------------------------------------------------------
-    calls = []
+    # ---- record GEMMs (every problem of one training step, incl. the paired ones) ----
+    import bench
+    calls = bench.gemm_problems(bench.record_gemms(tr))
+    print(f"{len(calls)} GEMM problems per training step")
     orig = L.lib.encdiff_gemm
-
-    class Rec:
-        def __call__(self, argp, stream):
-            a = L.GemmArgs()
-            C.memmove(C.byref(a), argp, C.sizeof(L.GemmArgs))
-            calls.append(a)
-            return orig(argp, stream)
-    L.lib.encdiff_gemm = Rec()
-    try:
-        eps = ex.forward(xn, t, c.detach())
-        ex.backward(torch.sign(eps - noise) / eps.numel())
-        torch.cuda.synchronize()
-    finally:
-        L.lib.encdiff_gemm = orig
-    print(f"{len(calls)} GEMM launches per UNet fwd+bwd")
 
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
@@ -133,12 +120,26 @@ def main():
     flops = defaultdict(float)
     table = {}
     rows = []
+    done = {}
     for a in calls:
+        key = ops.plan_key(a.M, a.N, a.K, a.a_mode, a.b_mode, a.c_mode, a.conv.resample)
+        if key in done:  # same problem already swept: reuse
+            cur, best_tile, best_split, best_t = done[key]
+            k = cat(a)
+            tot_cur[k] += cur
+            tot_best[k] += best_t
+            flops[k] += 2.0 * a.M * a.N * a.K
+            continue
         cur = timeit(a, a.tile)
         best_t, best_tile, best_split = cur, a.tile, a.split_k
-        for tile in (1, 2, 3, 4):
+        # weight gradients run inside the paired kernel (64 x 64 tiles) with their slabs in
+        # one workspace half (deferred finalize): only splits that fit are candidates
+        wgrad = a.a_mode == L.OPA_ROWM
+        for tile in ((4,) if wgrad else (1, 2, 3, 4)):
             for split in (1, 2, 4, 8, 16, 32, 64, 128, 256):
                 if split > 1 and a.K // split < 64:
+                    continue
+                if wgrad and split > 1 and split * a.M * (a.N + 1) > ops.WS_HALF // 2:
                     continue
                 tt = timeit(a, tile, split)
                 if tt < best_t:
@@ -147,10 +148,12 @@ def main():
         tot_cur[k] += cur
         tot_best[k] += best_t
         flops[k] += 2.0 * a.M * a.N * a.K
-        key = f"{a.a_mode},{a.b_mode},{a.c_mode},{a.M},{a.N},{a.K}"
+        done[key] = (cur, best_tile, best_split, best_t)
         if key not in table or table[key][2] > best_t:
             table[key] = [best_tile, best_split, best_t]
         rows.append((k, a.M, a.N, a.K, a.split_k, a.tile, cur, f"{best_tile}/{best_split}", best_t))
+        print(f"[{len(rows)}/{len(calls)}] {k} {a.M}x{a.N}x{a.K} r{a.conv.resample}: {cur:.1f} -> "
+              f"{best_tile}/{best_split} {best_t:.1f} us", flush=True)
     for cat_name in sorted(tot_cur):
         sel = sorted([r for r in rows if r[0] == cat_name], key=lambda r: -r[6])[:8]
         for r in sel:
