@@ -120,7 +120,8 @@ _PROTOS = {
     "encdiff_reduce_partials": [vp, C.c_long, C.c_int, C.c_int, vp, vp, vp],
     "encdiff_encoder_warp_fwd": [vp, C.c_long, C.c_int, C.c_int, vp, C.c_long, C.c_int, vp, C.c_long, vp],
     "encdiff_encoder_warp_bwd": [vp, C.c_long, C.c_int, C.c_int, vp, C.c_long, C.c_int, vp, C.c_long, vp, C.c_long,
-                                 vp, vp],
+                                 vp, vp, vp],
+    "encdiff_encoder_warp_partials_floats": [C.c_int, C.c_int, C.c_long],
     "encdiff_gather_images_u8": [vp, C.c_longlong, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, C.c_int,
                                  vp, vp],
     "encdiff_batchnorm_partials_floats": [C.c_int, C.c_int],

@@ -4,16 +4,17 @@
 //   u_i (B scalars) -> Linear(1,64) -> ELU -> Linear(64,128) -> ELU -> Linear(128,16)
 // whose outputs are concatenated to (B, latent_unit*16).  The reference runs them as
 // 100 forward / ~300 backward tiny launches; here one workgroup per unit runs the whole
-// MLP in fp32 (VALU FMA, weights and 32-row activation chunks in LDS), forward in one
-// launch and backward (recomputing the activations) in one launch.  The backward adds
-// the weight gradients of unit i straight into the fp32 gradient arena (one workgroup
-// owns them: deterministic) and writes d u.
+// MLP in fp32 (VALU FMA, weights and WR-row activation chunks in LDS).  The grid is
+// (unit, batch chunk): every workgroup runs one unit's MLP on WR rows, so B = 128 fills
+// 160 workgroups instead of 20 serial loops.  The backward writes d u and each chunk's
+// weight-gradient partials to a caller-provided scratch; a second launch adds the chunks
+// in a fixed order into the fp32 gradient arena (deterministic, no atomics).
 #include "common.h"
 
 namespace {
 
 constexpr int WT = 256;   // threads
-constexpr int WR = 32;    // batch rows per chunk
+constexpr int WR = 16;    // batch rows per chunk (one workgroup each)
 constexpr int H1 = 64, H2 = 128;
 
 ED_DEV float elu_f(float z) { return z > 0.f ? z : expm1f(z); }
@@ -70,7 +71,8 @@ __global__ __launch_bounds__(WT) void warp_fwd_kernel(const float* __restrict__ 
   WarpSmem& s = *reinterpret_cast<WarpSmem*>(smem_raw);
   const int unit = blockIdx.x;
   load_unit(s, params + unit * unit_stride, D);
-  for (int r0 = 0; r0 < batch; r0 += WR) {
+  {
+    const int r0 = blockIdx.y * WR;
     const int nr = min(WR, batch - r0);
     warp_hidden(s, u, ldu, unit, r0, nr);
     for (int e = threadIdx.x; e < nr * D; e += WT) {
@@ -95,7 +97,7 @@ __global__ __launch_bounds__(WT) void warp_bwd_kernel(const float* __restrict__ 
                                                       const float* __restrict__ params, long unit_stride, int D,
                                                       const float* __restrict__ dout, long lddo,
                                                       float* __restrict__ du, long lddu,
-                                                      float* __restrict__ grads) {
+                                                      float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float smem_raw[];
   WarpBwdSmem& s = *reinterpret_cast<WarpBwdSmem*>(smem_raw);
   const int unit = blockIdx.x, tid = threadIdx.x;
@@ -108,7 +110,8 @@ __global__ __launch_bounds__(WT) void warp_bwd_kernel(const float* __restrict__ 
   for (int q = 0; q < H2 * H1 / WT; ++q) gW2[q] = 0.f;
 #pragma unroll
   for (int q = 0; q < 16 * H2 / WT; ++q) gW3[q] = 0.f;
-  for (int r0 = 0; r0 < batch; r0 += WR) {
+  {
+    const int r0 = blockIdx.y * WR;
     const int nr = min(WR, batch - r0);
     warp_hidden(s.f, u, ldu, unit, r0, nr);
     for (int e = tid; e < WR * D; e += WT) {
@@ -176,22 +179,35 @@ __global__ __launch_bounds__(WT) void warp_bwd_kernel(const float* __restrict__ 
     }
     __syncthreads();
   }
-  float* G = grads + unit * unit_stride;
+  // this chunk's partial gradients: part[(unit * chunks + chunk) * unit_stride + param]
+  float* G = part + ((long)unit * gridDim.y + blockIdx.y) * unit_stride;
   float* gW1p = G;
   float* gb1p = gW1p + H1;
   float* gW2p = gb1p + H1;
   float* gb2p = gW2p + H2 * H1;
   float* gW3p = gb2p + H2;
   float* gb3p = gW3p + D * H2;
-  if (tid < H1) { gW1p[tid] += gW1; gb1p[tid] += gb1; }
-  if (tid < H2) gb2p[tid] += gb2;
-  if (tid < D) gb3p[tid] += gb3;
+  if (tid < H1) { gW1p[tid] = gW1; gb1p[tid] = gb1; }
+  if (tid < H2) gb2p[tid] = gb2;
+  if (tid < D) gb3p[tid] = gb3;
 #pragma unroll
-  for (int q = 0; q < H2 * H1 / WT; ++q) gW2p[tid + WT * q] += gW2[q];
+  for (int q = 0; q < H2 * H1 / WT; ++q) gW2p[tid + WT * q] = gW2[q];
 #pragma unroll
   for (int q = 0; q < 16 * H2 / WT; ++q) {
     const int e = tid + WT * q;
-    if (e < D * H2) gW3p[e] += gW3[q];
+    if (e < D * H2) gW3p[e] = gW3[q];
+  }
+}
+
+// grads[unit * stride + i] += sum over chunks (in order) of part[(unit * chunks + c) * stride + i]
+__global__ __launch_bounds__(WT) void warp_grad_reduce_kernel(const float* __restrict__ part, int units, int chunks,
+                                                             long stride, long n_per_unit, float* __restrict__ grads) {
+  const long total = (long)units * n_per_unit;
+  for (long e = (long)blockIdx.x * WT + threadIdx.x; e < total; e += (long)gridDim.x * WT) {
+    const long unit = e / n_per_unit, i = e - unit * n_per_unit;
+    float a = 0.f;
+    for (int c = 0; c < chunks; ++c) a += part[(unit * chunks + c) * stride + i];
+    grads[unit * stride + i] += a;
   }
 }
 
@@ -205,23 +221,33 @@ extern "C" int encdiff_encoder_warp_fwd(const float* u, long ldu, int batch, int
   static const hipError_t attr = hipFuncSetAttribute((const void*)warp_fwd_kernel,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)attr;
-  hipLaunchKernelGGL(warp_fwd_kernel, dim3(units), dim3(WT), sizeof(WarpSmem), (hipStream_t)stream, u, ldu, batch,
-                     params, unit_stride, context_dim, out, ldo);
+  hipLaunchKernelGGL(warp_fwd_kernel, dim3(units, (batch + WR - 1) / WR), dim3(WT), sizeof(WarpSmem),
+                     (hipStream_t)stream, u, ldu, batch, params, unit_stride, context_dim, out, ldo);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
 
+extern "C" int encdiff_encoder_warp_partials_floats(int batch, int units, long unit_stride) {
+  return (int)((long)units * ((batch + WR - 1) / WR) * unit_stride);
+}
+
 extern "C" int encdiff_encoder_warp_bwd(const float* u, long ldu, int batch, int units, const float* params,
                                         long unit_stride, int context_dim, const float* dout, long lddo, float* du,
-                                        long lddu, float* grads, void* stream) {
-  if (!u || !params || !dout || !du || !grads || batch <= 0 || units <= 0) return ENCDIFF_ERR_ARG;
+                                        long lddu, float* grads, float* partials, void* stream) {
+  if (!u || !params || !dout || !du || !grads || !partials || batch <= 0 || units <= 0) return ENCDIFF_ERR_ARG;
   if (context_dim <= 0 || context_dim > 16) return ENCDIFF_ERR_UNSUPPORTED;
   if (unit_stride < 2 * H1 + H2 * H1 + H2 + context_dim * H2 + context_dim) return ENCDIFF_ERR_SHAPE;
   static const hipError_t attr = hipFuncSetAttribute((const void*)warp_bwd_kernel,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)attr;
-  hipLaunchKernelGGL(warp_bwd_kernel, dim3(units), dim3(WT), sizeof(WarpBwdSmem), (hipStream_t)stream, u, ldu,
-                     batch, params, unit_stride, context_dim, dout, lddo, du, lddu, grads);
+  const int chunks = (batch + WR - 1) / WR;
+  hipLaunchKernelGGL(warp_bwd_kernel, dim3(units, chunks), dim3(WT), sizeof(WarpBwdSmem), (hipStream_t)stream, u,
+                     ldu, batch, params, unit_stride, context_dim, dout, lddo, du, lddu, partials);
+  ED_CHECK_LAUNCH();
+  const long n_per_unit = 2 * H1 + H2 * H1 + H2 + (long)context_dim * H2 + context_dim;
+  long g = ((long)units * n_per_unit + WT - 1) / WT;
+  hipLaunchKernelGGL(warp_grad_reduce_kernel, dim3((unsigned)(g > 1024 ? 1024 : g)), dim3(WT), 0, (hipStream_t)stream,
+                     partials, units, chunks, unit_stride, n_per_unit, grads);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }

@@ -517,8 +517,18 @@ def encoder_warp_fwd(u, params, unit_stride, units, context_dim, out):
                                        _p(out), out.stride(0), _s()), "encdiff_encoder_warp_fwd")
 
 
+_WARP_SCRATCH = {}
+
+
 def encoder_warp_bwd(u, params, unit_stride, units, context_dim, dout, du, grads):
+    """Backward of the warp MLPs: du, and the weight gradients ADDED into `grads` (per-chunk
+    partials in a cached scratch, folded in order)."""
     assert dout.stride(1) == 1 and du.stride(1) == 1
+    n = lib.encdiff_encoder_warp_partials_floats(u.shape[0], units, unit_stride)
+    key = (u.device.index, n)
+    part = _WARP_SCRATCH.get(key)
+    if part is None:
+        part = _WARP_SCRATCH[key] = torch.empty(max(n, 1), device=u.device, dtype=torch.float32)
     check(lib.encdiff_encoder_warp_bwd(_p(u), u.stride(0), u.shape[0], units, _p(params), unit_stride, context_dim,
-                                       _p(dout), dout.stride(0), _p(du), du.stride(0), _p(grads), _s()),
+                                       _p(dout), dout.stride(0), _p(du), du.stride(0), _p(grads), _p(part), _s()),
           "encdiff_encoder_warp_bwd")

@@ -337,12 +337,15 @@ int encdiff_gather_images_u8(const void* pool, long long n_images, int h, int w,
  * params: unit i's tensors contiguous at params + i*unit_stride in nn.Sequential order
  * [W1 64][b1 64][W2 128x64][b2 128][W3 context_dim x 128][b3 context_dim] (the layout
  * of the parameter arena).  The backward ADDS the weight gradients into `grads` (same
- * layout) and writes du; one workgroup per unit, deterministic. context_dim <= 16. */
+ * layout) and writes du: one workgroup per (unit, 16-row batch chunk), chunk partials in
+ * `partials`, folded in a fixed order by a second launch (deterministic). context_dim <= 16. */
 int encdiff_encoder_warp_fwd(const float* u, long ldu, int batch, int units, const float* params,
                              long unit_stride, int context_dim, float* out, long ldo, void* stream);
 int encdiff_encoder_warp_bwd(const float* u, long ldu, int batch, int units, const float* params,
                              long unit_stride, int context_dim, const float* dout, long lddo, float* du,
-                             long lddu, float* grads, void* stream);
+                             long lddu, float* grads, float* partials, void* stream);
+/* fp32 scratch the backward needs for its per-batch-chunk weight-gradient partials. */
+int encdiff_encoder_warp_partials_floats(int batch, int units, long unit_stride);
 
 /* Encoder4 convolution trunk (openaimodel_enc.py:1002-1012, EncResBlock :969-989) runs on
  * encdiff_gemm (Conv2d(k4,s2,p1): RESAMPLE_K4S2 / K4S2_T im2col modes; 3x3 and 1x1 convs)
