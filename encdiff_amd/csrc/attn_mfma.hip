@@ -27,9 +27,13 @@ ED_DEV s4 pack4(float a, float b, float c, float d) {
 
 // stage rows [n][dh] of a head from a [rows][ld] tensor into LDS row-major [np][DP]
 // (and optionally transposed [DP][np]); zero padding for rows >= n and dims >= dh.
+// Transposed copies use a row stride of np + 8 elements (16 B of padding): the MFMA operand
+// reads take 16 consecutive rows per instruction, which an unpadded power-of-two stride
+// would put in the same LDS banks (16-way conflicts).
 template <int DH, int DP>
 ED_DEV void stage_rows(const bf16_t* __restrict__ src, long ld, int n, int np, bf16_t* rm, bf16_t* tr, int tid,
                        int nthr) {
+  const int tld = np + 8;
   constexpr int CH = DP / 8;  // 16-byte chunks per padded row
   for (int e = tid; e < np * CH; e += nthr) {
     const int r = e / CH, c8 = (e - r * CH) * 8;
@@ -39,28 +43,38 @@ ED_DEV void stage_rows(const bf16_t* __restrict__ src, long ld, int n, int np, b
     if (tr) {
       const bf16_t* h = (const bf16_t*)&v;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) tr[(c8 + k) * np + r] = h[k];
+      for (int k = 0; k < 8; ++k) tr[(c8 + k) * tld + r] = h[k];
     }
   }
 }
 
-template <int DH>
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+// Forward.  A wave task is a PAIR of 16-query tiles of one head: the K and V^T fragments
+// read from LDS serve both, and the two online-softmax chains are independent.  Keys are
+// consumed 32 at a time (two MFMA tiles) per softmax update, halving the max / rescale
+// work per score; scores live in the log2 domain (scale * log2 e folded, raw v_exp_f32 --
+// arguments are <= 0, underflow to 0 is the correct limit).  MASK: key count not a
+// multiple of 32 (keys past SK get -inf).
+ED_DEV float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+template <int DH, bool MASK>
 __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, int hpb) {
   constexpr int DP = DH < 16 ? 16 : DH;
   constexpr int KC = DP / 16;
   extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
   const int H = p.heads, SQ = p.sq, SK = p.sk;
-  const int SKP = (SK + 15) & ~15;
+  const int SKP = (SK + 31) & ~31, TK = SKP + 8;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const int bh0 = blockIdx.x * hpb;
   bf16_t* Ks = sm;                        // [hpb][SKP][DP]
-  bf16_t* Vt = sm + hpb * SKP * DP;       // [hpb][DP][SKP]
+  bf16_t* Vt = sm + hpb * SKP * DP;       // [hpb][DP][TK] (padded rows)
   for (int hl = 0; hl < hpb; ++hl) {
     const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
     stage_rows<DH, DP>((const bf16_t*)p.k + (long)b * SK * p.ldk + h * DH, p.ldk, SK, SKP, Ks + hl * SKP * DP,
                        nullptr, tid, 256);
-    // V transposed only
     constexpr int CH = DP / 8;
     for (int e = tid; e < SKP * CH; e += 256) {
       const int r = e / CH, c8 = (e - r * CH) * 8;
@@ -68,74 +82,111 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
       if (r < SK && c8 < DH) v = *(const uint4*)((const bf16_t*)p.v + ((long)b * SK + r) * p.ldv + h * DH + c8);
       const bf16_t* hv = (const bf16_t*)&v;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) Vt[hl * DP * SKP + (c8 + k) * SKP + r] = hv[k];
+      for (int k = 0; k < 8; ++k) Vt[hl * DP * TK + (c8 + k) * TK + r] = hv[k];
     }
   }
   __syncthreads();
-  const int qtiles = (SQ + 15) >> 4;
-  const float scale = p.scale;
-  for (int task = wave; task < hpb * qtiles; task += 4) {
-    const int hl = task / qtiles, qt = task - hl * qtiles;
+  const int qtiles = (SQ + 15) >> 4, npairs = (qtiles + 1) >> 1;
+  const float sl2 = p.scale * LOG2E;
+  for (int task = wave; task < hpb * npairs; task += 4) {
+    const int hl = task / npairs, qp = task - hl * npairs;
     const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
-    const int q = qt * 16 + l16;
-    const bool qv = q < SQ;
-    const bf16_t* qp = (const bf16_t*)p.q + ((long)b * SQ + q) * p.ldq + h * DH;
-    s4 qf[KC];
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      const int d0 = kc * 16 + 4 * g;
-      qf[kc] = (qv && d0 < DH) ? ld4(qp + d0) : (s4){0, 0, 0, 0};
-    }
     const bf16_t* kb = Ks + hl * SKP * DP;
-    const bf16_t* vb = Vt + hl * DP * SKP;
-    float m = -INFINITY, l = 0.f;
-    v4f o[KC];
+    const bf16_t* vb = Vt + hl * DP * TK;
+    s4 qf[2][KC];
+    int q[2];
 #pragma unroll
-    for (int dt = 0; dt < KC; ++dt) o[dt] = (v4f){0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < SKP / 16; ++kt) {
-      v4f s = {0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 2; ++u) {
+      q[u] = (2 * qp + u) * 16 + l16;
+      const bool qv = q[u] < SQ;
+      const bf16_t* qp_ = (const bf16_t*)p.q + ((long)b * SQ + q[u]) * p.ldq + h * DH;
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) s = mma(ld4(kb + (kt * 16 + l16) * DP + kc * 16 + 4 * g), qf[kc], s);
-      float sv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) sv[i] = (kt * 16 + 4 * g + i < SK) ? s[i] * scale : -INFINITY;
-      float tmax = fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3]));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mn = fmaxf(m, tmax);
-      const float alpha = __expf(m - mn);
-      m = mn;
-      l *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < KC; ++dt) o[dt] *= alpha;
-      float pv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { pv[i] = __expf(sv[i] - m); l += pv[i]; }
-      const s4 pf = pack4(pv[0], pv[1], pv[2], pv[3]);
-#pragma unroll
-      for (int dt = 0; dt < KC; ++dt) o[dt] = mma(ld4(vb + (dt * 16 + l16) * SKP + kt * 16 + 4 * g), pf, o[dt]);
-    }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    const float inv = 1.f / l;
-    if (qv) {
-      bf16_t* op = (bf16_t*)p.o + ((long)b * SQ + q) * p.ldo + h * DH;
-#pragma unroll
-      for (int dt = 0; dt < KC; ++dt) {
-        const int d0 = dt * 16 + 4 * g;
-        if (d0 < DH) {
-          uint2 w;
-          w.x = pack2(o[dt][0] * inv, o[dt][1] * inv);
-          w.y = pack2(o[dt][2] * inv, o[dt][3] * inv);
-          *(uint2*)(op + d0) = w;
-        }
+      for (int kc = 0; kc < KC; ++kc) {
+        const int d0 = kc * 16 + 4 * g;
+        qf[u][kc] = (qv && d0 < DH) ? ld4(qp_ + d0) : (s4){0, 0, 0, 0};
       }
-      if (g == 0 && p.lse) p.lse[(long)bh * SQ + q] = m + __logf(l);
+    }
+    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+    v4f o[2][KC];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int dt = 0; dt < KC; ++dt) o[u][dt] = (v4f){0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < SKP; k0 += 32) {
+      s4 kf[2][KC];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) kf[t][kc] = ld4(kb + (k0 + t * 16 + l16) * DP + kc * 16 + 4 * g);
+      s4 pf[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float sv[8];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          v4f sc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kc = 0; kc < KC; ++kc) sc = mma(kf[t][kc], qf[u][kc], sc);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            sv[4 * t + i] = (!MASK || k0 + t * 16 + 4 * g + i < SK) ? sc[i] * sl2 : -INFINITY;
+        }
+        float tmax = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
+                           fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float mn = fmaxf(m[u], tmax);
+        const float alpha = ex2(m[u] - mn);
+        m[u] = mn;
+        float ls = 0.f, pv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { pv[i] = ex2(sv[i] - mn); ls += pv[i]; }
+        l[u] = l[u] * alpha + ls;
+#pragma unroll
+        for (int dt = 0; dt < KC; ++dt) o[u][dt] *= alpha;
+        pf[u][0] = pack4(pv[0], pv[1], pv[2], pv[3]);
+        pf[u][1] = pack4(pv[4], pv[5], pv[6], pv[7]);
+      }
+#pragma unroll
+      for (int dt = 0; dt < KC; ++dt)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const s4 vf = ld4(vb + (dt * 16 + l16) * TK + k0 + t * 16 + 4 * g);
+          o[0][dt] = mma(vf, pf[0][t], o[0][dt]);
+          o[1][dt] = mma(vf, pf[1][t], o[1][dt]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float lu = l[u];
+      lu += __shfl_xor(lu, 16, 64);
+      lu += __shfl_xor(lu, 32, 64);
+      const float inv = 1.f / lu;
+      if (q[u] < SQ) {
+        bf16_t* op = (bf16_t*)p.o + ((long)b * SQ + q[u]) * p.ldo + h * DH;
+#pragma unroll
+        for (int dt = 0; dt < KC; ++dt) {
+          const int d0 = dt * 16 + 4 * g;
+          if (d0 < DH) {
+            uint2 w;
+            w.x = pack2(o[u][dt][0] * inv, o[u][dt][1] * inv);
+            w.y = pack2(o[u][dt][2] * inv, o[u][dt][3] * inv);
+            *(uint2*)(op + d0) = w;
+          }
+        }
+        if (g == 0 && p.lse) p.lse[(long)bh * SQ + q[u]] = (m[u] + __log2f(lu)) * LN2;  // natural-log LSE
+      }
     }
   }
 }
 
-template <int DH>
+// q-split of phase A: enough (key tile, query slice) tasks for the 4 waves
+ED_DEV __host__ inline int attn_qsplit(int ktiles, int hpb) {
+  const int t = ktiles * hpb;
+  return t >= 4 ? 1 : (t >= 2 ? 2 : 4);
+}
+
+template <int DH, bool MASK>
 __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, int hpb) {
   constexpr int DP = DH < 16 ? 16 : DH;
   constexpr int KC = DP / 16;
@@ -145,24 +196,30 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const int bh0 = blockIdx.x * hpb;
-  // per head: Q, dO [SQP][DP]; Qt, dOt [DP][SQP]; K, V [SKP][DP]; Kt [DP][SKP]; lse, D [SQP] fp32
-  const int QE = SQP * DP, KE = SKP * DP;
-  const int per_head = 4 * QE + 3 * KE;
+  // per head: Q, dO [SQP][DP]; Qt, dOt [DP][SQP + 8]; K, V [SKP][DP]; Kt [DP][SKP + 8]; lse2, D [SQP]
+  const int TQ = SQP + 8, TK = SKP + 8;
+  const int QE = SQP * DP, KE = SKP * DP, QT = DP * TQ;
+  const int oQt = QE, oG = QE + QT, oGt = 2 * QE + QT, oK = 2 * QE + 2 * QT, oV = oK + KE, oKt = oK + 2 * KE;
+  const int per_head = oKt + DP * TK;
   float* fls = (float*)(sm + hpb * per_head);
+  const int qtiles = SQP >> 4, ktiles = SKP >> 4;
+  const int QS = attn_qsplit(ktiles, hpb);
+  float* red = fls + hpb * 2 * SQP;  // phase-A partials [task][2][16*DP lanes-major] when QS > 1
   for (int hl = 0; hl < hpb; ++hl) {
     const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
     bf16_t* base = sm + hl * per_head;
-    stage_rows<DH, DP>((const bf16_t*)p.q + (long)b * SQ * p.ldq + h * DH, p.ldq, SQ, SQP, base, base + QE, tid, 256);
-    stage_rows<DH, DP>((const bf16_t*)p.d_o + (long)b * SQ * p.lddo + h * DH, p.lddo, SQ, SQP, base + 2 * QE,
-                       base + 3 * QE, tid, 256);
-    stage_rows<DH, DP>((const bf16_t*)p.k + (long)b * SK * p.ldk + h * DH, p.ldk, SK, SKP, base + 4 * QE,
-                       base + 4 * QE + 2 * KE, tid, 256);
-    stage_rows<DH, DP>((const bf16_t*)p.v + (long)b * SK * p.ldv + h * DH, p.ldv, SK, SKP, base + 4 * QE + KE,
-                       nullptr, tid, 256);
+    stage_rows<DH, DP>((const bf16_t*)p.q + (long)b * SQ * p.ldq + h * DH, p.ldq, SQ, SQP, base, base + oQt, tid,
+                       256);
+    stage_rows<DH, DP>((const bf16_t*)p.d_o + (long)b * SQ * p.lddo + h * DH, p.lddo, SQ, SQP, base + oG,
+                       base + oGt, tid, 256);
+    stage_rows<DH, DP>((const bf16_t*)p.k + (long)b * SK * p.ldk + h * DH, p.ldk, SK, SKP, base + oK, base + oKt,
+                       tid, 256);
+    stage_rows<DH, DP>((const bf16_t*)p.v + (long)b * SK * p.ldv + h * DH, p.ldv, SK, SKP, base + oV, nullptr,
+                       tid, 256);
     for (int q = tid; q < SQP; q += 256) {
       float lse = 0.f, D = 0.f;
       if (q < SQ) {
-        lse = p.lse[(long)bh * SQ + q];
+        lse = p.lse[(long)bh * SQ + q] * LOG2E;
         const bf16_t* op = (const bf16_t*)p.o + ((long)b * SQ + q) * p.ldo + h * DH;
         const bf16_t* gp = (const bf16_t*)p.d_o + ((long)b * SQ + q) * p.lddo + h * DH;
         for (int d = 0; d < DH; d += 8) {
@@ -178,15 +235,16 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
     }
   }
   __syncthreads();
-  const float scale = p.scale;
-  const int qtiles = SQP >> 4, ktiles = SKP >> 4;
-  // ---- phase A: dK, dV (waves own key tiles) --------------------------------------
-  for (int task = wave; task < hpb * ktiles; task += 4) {
-    const int hl = task / ktiles, kt = task - hl * ktiles;
+  const float scale = p.scale, sl2 = p.scale * LOG2E;
+  // ---- phase A: dK, dV (task = key tile x query slice; query tiles in pairs) ----------
+  const int ntA = hpb * ktiles * QS;
+  for (int task = wave; task < ntA; task += 4) {
+    const int hl = task / (ktiles * QS), rem = task - hl * ktiles * QS;
+    const int kt = rem / QS, qs = rem - kt * QS;
     const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
     const bf16_t* base = sm + hl * per_head;
-    const bf16_t *Qs = base, *Qt = base + QE, *Gs = base + 2 * QE, *Gt = base + 3 * QE;
-    const bf16_t *Ks = base + 4 * QE, *Vs = base + 4 * QE + KE;
+    const bf16_t *Qs = base, *Qt = base + oQt, *Gs = base + oG, *Gt = base + oGt;
+    const bf16_t *Ks = base + oK, *Vs = base + oV;
     const float* lse = fls + hl * 2 * SQP;
     const float* Dv = lse + SQP;
     const int key = kt * 16 + l16;
@@ -197,32 +255,50 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
       kf[kc] = ld4(Ks + key * DP + kc * 16 + 4 * g);
       vf[kc] = ld4(Vs + key * DP + kc * 16 + 4 * g);
     }
-    v4f dk[KC], dv[KC];
+    v4f dk[2][KC], dv[2][KC];
 #pragma unroll
-    for (int dt = 0; dt < KC; ++dt) { dk[dt] = (v4f){0.f, 0.f, 0.f, 0.f}; dv[dt] = dk[dt]; }
-    for (int qt = 0; qt < qtiles; ++qt) {
-      v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        s = mma(ld4(Qs + (qt * 16 + l16) * DP + kc * 16 + 4 * g), kf[kc], s);
-        dp = mma(ld4(Gs + (qt * 16 + l16) * DP + kc * 16 + 4 * g), vf[kc], dp);
-      }
-      float pv[4], ds[4];
+      for (int dt = 0; dt < KC; ++dt) { dk[u][dt] = (v4f){0.f, 0.f, 0.f, 0.f}; dv[u][dt] = dk[u][dt]; }
+    for (int qt0 = qs; qt0 < qtiles; qt0 += 2 * QS) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = qt * 16 + 4 * g + i;
-        pv[i] = (kv && q < SQ) ? __expf(s[i] * scale - lse[q]) : 0.f;
-        ds[i] = pv[i] * (dp[i] - Dv[q]);
-      }
-      const s4 pf = pack4(pv[0], pv[1], pv[2], pv[3]);
-      const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);
+      for (int u = 0; u < 2; ++u) {
+        const int qt = qt0 + u * QS;
+        if (qt >= qtiles) break;
+        v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int dt = 0; dt < KC; ++dt) {
-        dv[dt] = mma(ld4(Gt + (dt * 16 + l16) * SQP + qt * 16 + 4 * g), pf, dv[dt]);
-        dk[dt] = mma(ld4(Qt + (dt * 16 + l16) * SQP + qt * 16 + 4 * g), df, dk[dt]);
+        for (int kc = 0; kc < KC; ++kc) {
+          s = mma(ld4(Qs + (qt * 16 + l16) * DP + kc * 16 + 4 * g), kf[kc], s);
+          dp = mma(ld4(Gs + (qt * 16 + l16) * DP + kc * 16 + 4 * g), vf[kc], dp);
+        }
+        float pv[4], ds[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = qt * 16 + 4 * g + i;
+          pv[i] = (!MASK || (kv && q < SQ)) ? ex2(s[i] * sl2 - lse[q]) : 0.f;
+          ds[i] = pv[i] * (dp[i] - Dv[q]);
+        }
+        const s4 pf = pack4(pv[0], pv[1], pv[2], pv[3]);
+        const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);
+#pragma unroll
+        for (int dt = 0; dt < KC; ++dt) {
+          dv[u][dt] = mma(ld4(Gt + (dt * 16 + l16) * TQ + qt * 16 + 4 * g), pf, dv[u][dt]);
+          dk[u][dt] = mma(ld4(Qt + (dt * 16 + l16) * TQ + qt * 16 + 4 * g), df, dk[u][dt]);
+        }
       }
     }
-    if (kv) {
+#pragma unroll
+    for (int dt = 0; dt < KC; ++dt) { dk[0][dt] += dk[1][dt]; dv[0][dt] += dv[1][dt]; }
+    if (QS > 1) {  // partials of this query slice -> LDS, summed in slice order below
+      float* r = red + (long)task * 2 * 16 * DP;
+#pragma unroll
+      for (int dt = 0; dt < KC; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          r[(dt * 4 + i) * 64 + lane] = dk[0][dt][i];
+          r[16 * DP + (dt * 4 + i) * 64 + lane] = dv[0][dt][i];
+        }
+    } else if (kv) {
       bf16_t* dkp = (bf16_t*)p.dk + ((long)b * SK + key) * p.lddk + h * DH;
       bf16_t* dvp = (bf16_t*)p.dv + ((long)b * SK + key) * p.lddv + h * DH;
 #pragma unroll
@@ -230,23 +306,58 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
         const int d0 = dt * 16 + 4 * g;
         if (d0 < DH) {
           uint2 w;
-          w.x = pack2(dk[dt][0] * scale, dk[dt][1] * scale);
-          w.y = pack2(dk[dt][2] * scale, dk[dt][3] * scale);
+          w.x = pack2(dk[0][dt][0] * scale, dk[0][dt][1] * scale);
+          w.y = pack2(dk[0][dt][2] * scale, dk[0][dt][3] * scale);
           *(uint2*)(dkp + d0) = w;
-          w.x = pack2(dv[dt][0], dv[dt][1]);
-          w.y = pack2(dv[dt][2], dv[dt][3]);
+          w.x = pack2(dv[0][dt][0], dv[0][dt][1]);
+          w.y = pack2(dv[0][dt][2], dv[0][dt][3]);
           *(uint2*)(dvp + d0) = w;
         }
       }
     }
   }
-  // ---- phase B: dQ (waves own query tiles) ----------------------------------------
+  if (QS > 1) {
+    __syncthreads();
+    // one wave per (head, key tile) adds its QS slices in order and writes dK, dV
+    for (int t = wave; t < hpb * ktiles; t += 4) {
+      const int hl = t / ktiles, kt = t - hl * ktiles;
+      const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
+      const int key = kt * 16 + l16;
+      const float* r0 = red + (long)(t * QS) * 2 * 16 * DP;
+      if (key < SK) {
+        bf16_t* dkp = (bf16_t*)p.dk + ((long)b * SK + key) * p.lddk + h * DH;
+        bf16_t* dvp = (bf16_t*)p.dv + ((long)b * SK + key) * p.lddv + h * DH;
+#pragma unroll
+        for (int dt = 0; dt < KC; ++dt) {
+          const int d0 = dt * 16 + 4 * g;
+          if (d0 >= DH) continue;
+          float a[4], c[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            a[i] = 0.f; c[i] = 0.f;
+            for (int qs = 0; qs < QS; ++qs) {
+              a[i] += r0[(long)qs * 2 * 16 * DP + (dt * 4 + i) * 64 + lane];
+              c[i] += r0[(long)qs * 2 * 16 * DP + 16 * DP + (dt * 4 + i) * 64 + lane];
+            }
+          }
+          uint2 w;
+          w.x = pack2(a[0] * scale, a[1] * scale);
+          w.y = pack2(a[2] * scale, a[3] * scale);
+          *(uint2*)(dkp + d0) = w;
+          w.x = pack2(c[0], c[1]);
+          w.y = pack2(c[2], c[3]);
+          *(uint2*)(dvp + d0) = w;
+        }
+      }
+    }
+  }
+  // ---- phase B: dQ (waves own query tiles; key tiles in pairs) ----------------------
   for (int task = wave; task < hpb * qtiles; task += 4) {
     const int hl = task / qtiles, qt = task - hl * qtiles;
     const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
     const bf16_t* base = sm + hl * per_head;
-    const bf16_t *Qs = base, *Gs = base + 2 * QE;
-    const bf16_t *Ks = base + 4 * QE, *Vs = base + 4 * QE + KE, *Kt = base + 4 * QE + 2 * KE;
+    const bf16_t *Qs = base, *Gs = base + oG;
+    const bf16_t *Ks = base + oK, *Vs = base + oV, *Kt = base + oKt;
     const float* lse = fls + hl * 2 * SQP;
     const float* Dv = lse + SQP;
     const int q = qt * 16 + l16;
@@ -258,26 +369,34 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
       qf[kc] = ld4(Qs + q * DP + kc * 16 + 4 * g);
       gf[kc] = ld4(Gs + q * DP + kc * 16 + 4 * g);
     }
-    v4f dq[KC];
+    v4f dq[2][KC];
 #pragma unroll
-    for (int dt = 0; dt < KC; ++dt) dq[dt] = (v4f){0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < ktiles; ++kt) {
-      v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        st = mma(ld4(Ks + (kt * 16 + l16) * DP + kc * 16 + 4 * g), qf[kc], st);
-        dpt = mma(ld4(Vs + (kt * 16 + l16) * DP + kc * 16 + 4 * g), gf[kc], dpt);
+      for (int dt = 0; dt < KC; ++dt) dq[u][dt] = (v4f){0.f, 0.f, 0.f, 0.f};
+    for (int kt0 = 0; kt0 < ktiles; kt0 += 2) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int kt = kt0 + u;
+        if (kt >= ktiles) break;
+        v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          st = mma(ld4(Ks + (kt * 16 + l16) * DP + kc * 16 + 4 * g), qf[kc], st);
+          dpt = mma(ld4(Vs + (kt * 16 + l16) * DP + kc * 16 + 4 * g), gf[kc], dpt);
+        }
+        float ds[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = kt * 16 + 4 * g + i;
+          const float pr = (!MASK || (qv && key < SK)) ? ex2(st[i] * sl2 - lq) : 0.f;
+          ds[i] = pr * (dpt[i] - Dq);
+        }
+        const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);
+#pragma unroll
+        for (int dt = 0; dt < KC; ++dt)
+          dq[u][dt] = mma(ld4(Kt + (dt * 16 + l16) * TK + kt * 16 + 4 * g), df, dq[u][dt]);
       }
-      float ds[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = kt * 16 + 4 * g + i;
-        const float pr = (qv && key < SK) ? __expf(st[i] * scale - lq) : 0.f;
-        ds[i] = pr * (dpt[i] - Dq);
-      }
-      const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);
-#pragma unroll
-      for (int dt = 0; dt < KC; ++dt) dq[dt] = mma(ld4(Kt + (dt * 16 + l16) * SKP + kt * 16 + 4 * g), df, dq[dt]);
     }
     if (qv) {
       bf16_t* dqp = (bf16_t*)p.dq + ((long)b * SQ + q) * p.lddq + h * DH;
@@ -285,9 +404,10 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
       for (int dt = 0; dt < KC; ++dt) {
         const int d0 = dt * 16 + 4 * g;
         if (d0 < DH) {
+          const v4f t = dq[0][dt] + dq[1][dt];
           uint2 w;
-          w.x = pack2(dq[dt][0] * scale, dq[dt][1] * scale);
-          w.y = pack2(dq[dt][2] * scale, dq[dt][3] * scale);
+          w.x = pack2(t[0] * scale, t[1] * scale);
+          w.y = pack2(t[2] * scale, t[3] * scale);
           *(uint2*)(dqp + d0) = w;
         }
       }
@@ -305,14 +425,19 @@ template <int DH>
 int launch_mfma_fwd(const EncdiffAttnArgs& a, hipStream_t s) {
   constexpr int DP = DH < 16 ? 16 : DH;
   const int hpb = mfma_hpb(a);
-  const int SKP = (a.sk + 15) & ~15;
+  const int SKP = (a.sk + 31) & ~31;
   const int nblk = a.batch * a.heads / hpb;
-  const size_t lds = (size_t)hpb * 2 * SKP * DP * sizeof(bf16_t);
+  const size_t lds = (size_t)hpb * (SKP + SKP + 8) * DP * sizeof(bf16_t);
   if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
-  static const hipError_t attr = hipFuncSetAttribute((const void*)attn_fwd_mfma<DH>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)attr;
-  hipLaunchKernelGGL(attn_fwd_mfma<DH>, dim3(nblk), dim3(256), lds, s, a, hpb);
+  const bool mask = a.sk % 32 != 0;
+  const void* fn = mask ? (const void*)attn_fwd_mfma<DH, true> : (const void*)attn_fwd_mfma<DH, false>;
+  static const hipError_t attr0 = hipFuncSetAttribute((const void*)attn_fwd_mfma<DH, false>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  static const hipError_t attr1 = hipFuncSetAttribute((const void*)attn_fwd_mfma<DH, true>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)attr0; (void)attr1; (void)fn;
+  if (mask) hipLaunchKernelGGL((attn_fwd_mfma<DH, true>), dim3(nblk), dim3(256), lds, s, a, hpb);
+  else hipLaunchKernelGGL((attn_fwd_mfma<DH, false>), dim3(nblk), dim3(256), lds, s, a, hpb);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
@@ -323,12 +448,18 @@ int launch_mfma_bwd(const EncdiffAttnArgs& a, hipStream_t s) {
   const int hpb = mfma_hpb(a);
   const int SQP = (a.sq + 15) & ~15, SKP = (a.sk + 15) & ~15;
   const int nblk = a.batch * a.heads / hpb;
-  const size_t lds = (size_t)hpb * ((4 * SQP + 3 * SKP) * DP * sizeof(bf16_t) + 2 * SQP * sizeof(float));
+  const int QS = attn_qsplit(SKP / 16, hpb);
+  const size_t red = QS > 1 ? (size_t)hpb * (SKP / 16) * QS * 2 * 16 * DP * sizeof(float) : 0;
+  const size_t lds =
+      (size_t)hpb * ((4 * SQP + 3 * SKP + 3 * 8) * DP * sizeof(bf16_t) + 2 * SQP * sizeof(float)) + red;
   if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
-  static const hipError_t attr = hipFuncSetAttribute((const void*)attn_bwd_mfma<DH>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)attr;
-  hipLaunchKernelGGL(attn_bwd_mfma<DH>, dim3(nblk), dim3(256), lds, s, a, hpb);
+  static const hipError_t attr0 = hipFuncSetAttribute((const void*)attn_bwd_mfma<DH, false>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  static const hipError_t attr1 = hipFuncSetAttribute((const void*)attn_bwd_mfma<DH, true>,
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)attr0; (void)attr1;
+  if (a.sq % 16 || a.sk % 16) hipLaunchKernelGGL((attn_bwd_mfma<DH, true>), dim3(nblk), dim3(256), lds, s, a, hpb);
+  else hipLaunchKernelGGL((attn_bwd_mfma<DH, false>), dim3(nblk), dim3(256), lds, s, a, hpb);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
