@@ -19,6 +19,8 @@ OBJ = os.path.join(HERE, "_build")
 ARCH = os.environ.get("ENCDIFF_ARCH", "gfx950")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast",
+         # MFMA results in VGPRs (gfx950 allows it): no v_accvgpr copies around the VALU work on them
+         "-mllvm", "-amdgpu-mfma-vgpr-form=1",
          "-I" + os.path.join(REPO, "include")]
 
 

@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
 }
 
 // q-split of phase A: enough (key tile, query slice) tasks for the 4 waves
-ED_DEV __host__ inline int attn_qsplit(int ktiles, int hpb) {
+__device__ __host__ inline int attn_qsplit(int ktiles, int hpb) {
   const int t = ktiles * hpb;
   return t >= 4 ? 1 : (t >= 2 ? 2 : 4);
 }

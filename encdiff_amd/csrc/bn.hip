@@ -15,7 +15,7 @@ namespace {
 constexpr int BN_T = 256;
 constexpr int BN_MAXBLK = 128;  // workgroups of a reduction (pixel ranges)
 
-ED_DEV __host__ inline int bn_blocks(int rows) {
+__device__ __host__ inline int bn_blocks(int rows) {
   const int b = (rows + 127) / 128;
   return b < BN_MAXBLK ? b : BN_MAXBLK;
 }
