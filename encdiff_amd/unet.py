@@ -316,6 +316,24 @@ class UNetExecutor:
             n = B * r0.hin * r0.hin
             self.xcat.append(t(n, r0.cin))
             self.dxcat.append(t(n, r0.cin))
+        # skip connections and the decoder path are written straight into the concat inputs:
+        # the last layer of input block i writes the upper channel slice of the output block
+        # that consumes it, the layer before each output block its lower slice
+        # (torch.cat([h, hs.pop()], 1), openaimodel_enc.py:740, without the copies)
+        nhs = len(sp.input_blocks)
+        for i in range(nhs):
+            j = nhs - 1 - i
+            c1 = sp.output_blocks[j][0].cin - sp.skip_ch[i]
+            view = self.xcat[j][:, c1:]
+            if i == 0:
+                self.h0 = view
+            else:
+                self.state[sp.input_blocks[i][-1].prefix]["out"] = view
+        prev_last = sp.middle[-1]
+        for j, blk in enumerate(sp.output_blocks):
+            c1 = blk[0].cin - sp.skip_ch[nhs - 1 - j]
+            self.state[prev_last.prefix]["out"] = self.xcat[j][:, :c1]
+            prev_last = blk[-1]
         self.a_out = t(g0.pixels, sp.out_ch)
         self.st_out = t(B, 64, F32)
         self.d_aout = t(g0.pixels, sp.out_ch)
@@ -396,8 +414,8 @@ class UNetExecutor:
             skip = hs[len(hs) - 1 - j]
             xc = self.xcat[j]
             c1 = h.shape[1]
-            ops.ew(L.EW_COPY, h, xc[:, :c1])
-            ops.ew(L.EW_COPY, skip, xc[:, c1:])
+            # both halves were written in place by their producers (see bind)
+            assert h.data_ptr() == xc.data_ptr() and skip.data_ptr() == xc[:, c1:].data_ptr()
             h = xc
             for layer in blk:
                 h = self._layer_fwd(layer, h)
