@@ -198,16 +198,16 @@ def kernel_roofline(tr, reps=10):
     return out
 
 
-def ddim_rate(ldm, B, S):
+def ddim_rate(ldm, B, S, eta=0.0):
     from encdiff_amd.ldm.models.diffusion.ddim import DDIMSampler
     cond = torch.randn(B, 320, device="cuda")
     sampler = DDIMSampler(ldm)
     x_T = torch.randn(B, 3, 16, 16, device="cuda")
     with torch.no_grad():
-        sampler.sample(S, B, (3, 16, 16), cond, eta=0.0, verbose=False, x_T=x_T)  # capture + warm-up
+        sampler.sample(S, B, (3, 16, 16), cond, eta=eta, verbose=False, x_T=x_T)  # capture + warm-up
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        sampler.sample(S, B, (3, 16, 16), cond, eta=0.0, verbose=False, x_T=x_T)
+        sampler.sample(S, B, (3, 16, 16), cond, eta=eta, verbose=False, x_T=x_T)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
     return S / dt
@@ -270,8 +270,11 @@ def main():
                                   "frac": f_step * args.steps / dt / 1e12 / PEAK_BF16_TFLOPS,
                                   "flops_per_img": 3 * F_UNET_FWD_PER_IMG}
         if not args.skip_ddim:
+            # DDIM steps/s at (B=8, S=200, eta=0) and (B=128, S=200, eta=1)
             extra["ddim_steps_per_sec"] = {"value": ddim_rate(ldm, args.ddim_batch, args.ddim_steps),
                                            "batch": args.ddim_batch, "S": args.ddim_steps, "eta": 0.0}
+            extra["ddim_steps_per_sec_b128"] = {"value": ddim_rate(ldm, 128, args.ddim_steps, eta=1.0),
+                                                "batch": 128, "S": args.ddim_steps, "eta": 1.0}
         if not args.skip_cpu:
             extra["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

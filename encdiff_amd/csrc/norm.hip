@@ -419,17 +419,19 @@ int gn_min_slice() {
   return v;
 }
 
-int gn_slice(int C, int HW, int cpg) {
+// small batches (sampling) keep more workgroups: a quarter of the slice size below 64 images
+int gn_slice(int C, int HW, int cpg, int batch) {
   int unit = 8;
   while (unit % cpg) unit += 8;
+  const long min_el = batch >= 64 ? gn_min_slice() : gn_min_slice() / 4;
   for (int w = unit; w < C; w += unit)
-    if (C % w == 0 && (long)w * HW >= gn_min_slice()) return w;
+    if (C % w == 0 && (long)w * HW >= min_el) return w;
   return C;
 }
 
 int gn_check(const EncdiffGroupNormArgs* a) {
   if (a->c % 8 || a->groups <= 0 || a->c % a->groups) return ENCDIFF_ERR_SHAPE;
-  const int cs = gn_slice(a->c, a->hw, a->c / a->groups);
+  const int cs = gn_slice(a->c, a->hw, a->c / a->groups, a->batch);
   if (cs > 512 || cs / (a->c / a->groups) > 64) return ENCDIFF_ERR_UNSUPPORTED;
   return cs;
 }

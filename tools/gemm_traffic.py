@@ -75,8 +75,9 @@ def _window(rows, counter):
     assert len(marks) >= 2, "markers missing"
     win = rows[marks[-2] + 1:marks[-1]]
     cal = [r for r in win if "ew_kernel" in r[1] and r[2] == counter]
-    gem = [r for r in win if ("gemm_kernel" in r[1] or "gemm_finalize" in r[1]) and r[2] == counter]
-    launches = len({r[0] for r in win if "gemm_kernel" in r[1]})
+    fam = ("gemm_kernel", "gemm2_kernel", "gemm_finalize")  # single, paired, split-K finalize kernels
+    gem = [r for r in win if any(k in r[1] for k in fam) and r[2] == counter]
+    launches = len({r[0] for r in win if any(k in r[1] for k in fam)})
     return sum(r[3] for r in cal), sum(r[3] for r in gem), launches
 
 
@@ -87,8 +88,9 @@ def summarize(fdir, wdir, out):
     rd = f_gemm * CAL_BYTES / f_cal        # calibrated: units of the counter -> bytes
     wr = w_gemm * CAL_BYTES / w_cal
     meta = json.load(open(os.path.join(REPO, "gpurun_out", "gemm_traffic_calls.json")))
-    res = {"launches": n1, "read_bytes_per_step": rd, "write_bytes_per_step": wr,
-           "bytes_per_launch": (rd + wr) / n1, "alg_bytes_per_launch": meta["alg_bytes"] / n1,
+    n = meta["launches"]  # API calls (bench.py's launches_per_step); n1 = kernel dispatches
+    res = {"launches": n, "dispatches": n1, "read_bytes_per_step": rd, "write_bytes_per_step": wr,
+           "bytes_per_launch": (rd + wr) / n, "alg_bytes_per_launch": meta["alg_bytes"] / n,
            "traffic_over_alg": (rd + wr) / meta["alg_bytes"],
            "fetch_units_per_cal_byte": f_cal / CAL_BYTES, "write_units_per_cal_byte": w_cal / CAL_BYTES,
            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of tools/gemm_traffic.py run (B=128), "

@@ -1,0 +1,10 @@
+#!/bin/bash
+# GPU-box routine: HBM traffic of the GEMM family from two rocprofv3 PMC passes (FETCH_SIZE,
+# WRITE_SIZE), summarised into profiles/gemm_traffic.json (see tools/gemm_traffic.py).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p $R/gpurun_out
+cd /tmp && export TMPDIR=/tmp
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_f -o run -- python3 $R/tools/gemm_traffic.py run > $R/gpurun_out/pmc_f.log 2>&1 || { echo "fetch pass failed"; exit 1; }
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_w -o run -- python3 $R/tools/gemm_traffic.py run > $R/gpurun_out/pmc_w.log 2>&1 || { echo "write pass failed"; exit 1; }
+cd $R && python tools/gemm_traffic.py summarize gpurun_out/pmc_f gpurun_out/pmc_w --out gpurun_out/gemm_traffic.json
