@@ -457,13 +457,31 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src
   }
 }
 
+// A workgroup owns 32 columns; its 8 row slices (32 lanes each) sum rows slice, slice + 8, ...
+// (4 independent accumulators per lane keep loads in flight), then the slices are added in
+// a fixed order through LDS: deterministic, and 8x more workgroups than one thread per column.
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* part, long ld, int rows, int cols,
                                                               const int* idx, float* grad) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= cols) return;
-  float s = 0.f;
-  for (int r = 0; r < rows; ++r) s += part[(long)r * ld + j];
-  grad[idx[j]] += s;
+  __shared__ float red[8][32];
+  const int cl = threadIdx.x & 31, sl = threadIdx.x >> 5;
+  const int j = blockIdx.x * 32 + cl;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (j < cols) {
+    int r = sl;
+    for (; r + 24 < rows; r += 32) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += part[(long)(r + 8 * u) * ld + j];
+    }
+    for (; r < rows; r += 8) a[0] += part[(long)r * ld + j];
+  }
+  red[sl][cl] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (sl == 0 && j < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][cl];
+    grad[idx[j]] += t;
+  }
 }
 
 int grid_for(long n, int per_thread = 1) {
@@ -613,7 +631,7 @@ extern "C" int encdiff_pack_weights(const float* src, void* dst, const EncdiffPa
 extern "C" int encdiff_reduce_partials(const float* part, long ld, int rows, int cols, const int* idx, float* grad,
                                        void* stream) {
   if (!part || !idx || !grad || cols <= 0) return ENCDIFF_ERR_ARG;
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((cols + 255) / 256), dim3(256), 0, (hipStream_t)stream, part, ld,
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((cols + 31) / 32), dim3(256), 0, (hipStream_t)stream, part, ld,
                      rows, cols, idx, grad);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -79,6 +80,9 @@ def _tile_table():
     return _TILES
 
 
+MAX_SPLIT = int(os.environ.get("ENCDIFF_MAX_SPLIT", "1024"))  # experiment knob: clamp table split-K
+
+
 def plan_key(M, N, K, a_mode, b_mode, c_mode, resample=0):
     key = f"{a_mode},{b_mode},{c_mode},{M},{N},{K}"
     return key + (f",r{resample}" if resample else "")
@@ -89,7 +93,7 @@ def plan(M, N, K, a_mode, b_mode, c_mode, resample=0):
     else a heuristic aiming at >= 256 workgroups with bounded split-K traffic."""
     hit = _tile_table().get(plan_key(M, N, K, a_mode, b_mode, c_mode, resample))
     if hit is not None:
-        tile, split = int(hit[0]), int(hit[1])
+        tile, split = int(hit[0]), min(int(hit[1]), MAX_SPLIT)
         if split == 1 or c_mode in (L.OUT_F32_ATOMIC, L.OUT_F32_ATOMIC_CONVW) or split * M * (N + 1) <= WS_FLOATS:
             return tile, split
     atomic = c_mode in (L.OUT_F32_ATOMIC, L.OUT_F32_ATOMIC_CONVW)
@@ -439,6 +443,22 @@ def small_conv_out_fwd(x, g: Geom, weight, bias, y_nchw):
     a = L.SmallConvArgs(batch=g.batch, h=g.h, w=g.w, cin=cin, cout=cout, x=_p(x), ldx=_ld(x), x_f32=0,
                         weight=_p(weight), bias=_p(bias), y=_p(y_nchw), ldy=0, y_f32=1)
     check(lib.encdiff_small_conv_fwd(C.byref(a), _s()), "encdiff_small_conv_fwd")
+
+
+def nchw_to_rows(x, cpad, y):
+    """fp32 NCHW [B][C][H][W] -> bf16 rows [B*H*W][cpad] (channels C..cpad-1 zero)."""
+    B, Cc, H, W = x.shape
+    assert x.is_contiguous() and x.dtype == F32 and y.shape == (B * H * W, cpad)
+    check(lib.encdiff_nchw_to_rows(_p(x), B, Cc, H * W, cpad, _p(y), _ld(y), _s()), "encdiff_nchw_to_rows")
+
+
+def pack_conv_pad8(w):
+    """[co][ci][3][3] (ci <= 8) -> bf16 [co][9*8] with zero channels ci..7 (the GEMM B layout of
+    a 3x3 conv over channel-padded rows)."""
+    co, ci = w.shape[0], w.shape[1]
+    out = torch.zeros(co, 3, 3, 8, device=w.device, dtype=F32)
+    out[..., :ci] = w.detach().float().permute(0, 2, 3, 1)
+    return out.reshape(co, 72).to(BF16).contiguous()
 
 
 def small_conv_out_bwd(x, g: Geom, weight, dy_nchw, dx, dweight, dbias):

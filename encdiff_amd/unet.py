@@ -213,6 +213,10 @@ class UNetExecutor:
             self.qkv_grad[t.prefix] = a.grad[o:o + n].view(3 * t.c, t.c)
         # plain GEMM weights
         pk.add("time_embed.0.weight", a.offsets["time_embed.0.weight"][0], 4 * self.mc, self.mc)
+        # input conv (3 -> mc): [mc][3][3][3] -> [mc][9 taps][8] (channel-padded GEMM B layout)
+        cin0 = spec.input_blocks[0][0].cin
+        assert cin0 <= 8
+        pk.add("input_conv", a.offsets["input_blocks.0.0.weight"][0], self.mc, 72, kind=2, cin=cin0)
         pk.add("time_embed.2.weight", a.offsets["time_embed.2.weight"][0], 4 * self.mc, 4 * self.mc)
         for r in spec.res:
             for w, cin in (("in_layers.2.weight", r.cin), ("out_layers.3.weight", r.cout)):
@@ -334,6 +338,10 @@ class UNetExecutor:
             c1 = blk[0].cin - sp.skip_ch[nhs - 1 - j]
             self.state[prev_last.prefix]["out"] = self.xcat[j][:, :c1]
             prev_last = blk[-1]
+        self.x8 = t(g0.pixels, 8)           # x_t as channel-padded bf16 rows (input conv operand)
+        self.dw_in = t(self.mc, 72, F32)     # input conv weight gradient, GEMM layout
+        self.deps8 = t(g0.pixels, 8)         # d eps as channel-padded bf16 rows
+        self.dw_out = t(8, 9 * sp.out_ch, F32)
         self.a_out = t(g0.pixels, sp.out_ch)
         self.st_out = t(B, 64, F32)
         self.d_aout = t(g0.pixels, sp.out_ch)
@@ -399,8 +407,9 @@ class UNetExecutor:
         ops.linear_fwd(self.ctx16, self.W("kv_all"), self.KV)
         # input conv
         g0 = Geom(B, self.H, self.H)
-        ops.small_conv_in_fwd(self._x, g0, self.P("input_blocks.0.0.weight"), self.P("input_blocks.0.0.bias"),
-                              self.h0)
+        # input conv on the GEMM engine over channel-padded rows (openaimodel_enc.py:494)
+        ops.nchw_to_rows(self._x, 8, self.x8)
+        ops.conv3x3_fwd(self.x8, g0, 8, self.W("input_conv"), self.h0, bias=self.P("input_blocks.0.0.bias"))
         hs = [self.h0]
         h = self.h0
         for blk in sp.input_blocks[1:]:
@@ -512,8 +521,17 @@ class UNetExecutor:
         sp = self.spec
         g0 = Geom(B, self.H, self.H)
         d_eps = d_eps.contiguous()
-        ops.small_conv_out_bwd(self.a_out, g0, self.P("out.2.weight"), d_eps, self.d_aout, self.G("out.2.weight"),
-                               self.G("out.2.bias"))
+        # out conv (mc -> 3): input gradient on the VALU kernel; weight gradient as a GEMM over
+        # channel-padded d eps rows (rows 3..7 zero), folded into the reference layout; bias = sum
+        ops.small_conv_out_bwd(self.a_out, g0, self.P("out.2.weight"), d_eps, self.d_aout, None, None)
+        ops.nchw_to_rows(d_eps, 8, self.deps8)
+        co = d_eps.shape[1]
+        ops.gemm(8, 9 * sp.out_ch, g0.pixels, self.deps8, 8, self.a_out, self.a_out.stride(0), self.dw_out,
+                 9 * sp.out_ch, a_mode=L.OPA_ROWM, b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32,
+                 conv=L.ConvGeom(batch=B, h=self.H, w=self.H, cin=sp.out_ch, resample=0,
+                                 ld_src=self.a_out.stride(0)))
+        self.G("out.2.weight").view(co, sp.out_ch, 9).add_(self.dw_out.view(8, 9, sp.out_ch)[:co].permute(0, 2, 1))
+        self.G("out.2.bias").add_(d_eps.sum((0, 2, 3)))
         dg, db = self.gn.parts("out.0.weight", sp.out_ch)
         ops.groupnorm_bwd(self._h_last, g0, self.P("out.0.weight"), self.P("out.0.bias"), self.st_out, GN_EPS, True,
                           self.d_aout, self.d_hlast, dg, db, ld_part=self.gn.ld)
@@ -556,8 +574,14 @@ class UNetExecutor:
                 self._layer_bwd(layer, dout, dx_target, acc)
                 dout = dx_target
         # input conv weight grad (no input grad: x_t carries no gradient)
-        ops.small_conv_in_wgrad(self._x, g0, self.P("input_blocks.0.0.weight"), g_hs[0],
-                                self.G("input_blocks.0.0.weight"), self.G("input_blocks.0.0.bias"))
+        dy0 = g_hs[0]
+        ops.gemm(self.mc, 72, g0.pixels, dy0, dy0.stride(0), self.x8, 8, self.dw_in, 72, a_mode=L.OPA_ROWM,
+                 b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32,
+                 conv=L.ConvGeom(batch=B, h=self.H, w=self.H, cin=8, resample=0, ld_src=8),
+                 bias_grad=self.G("input_blocks.0.0.bias"))
+        cin0 = self._x.shape[1]
+        self.G("input_blocks.0.0.weight").view(self.mc, cin0, 9).add_(
+            self.dw_in.view(self.mc, 9, 8)[:, :, :cin0].permute(0, 2, 1))
         # batched emb_layers backward -> time MLP
         ops.ew(L.EW_F32_TO_BF16, self.dE, self.dE16)
         ops.linear_bwd(self.dE16, self.W("emb_all"), self.emb_s, self.d_emb_s, self.emb_w_grad, self.emb_bias_grad)

@@ -66,6 +66,7 @@ class VQEncoderExecutor:
             convs += [(f"mid.{name}.conv1", blk.conv1), (f"mid.{name}.conv2", blk.conv2)]
         for key, conv in convs[1:]:
             P[key] = self._conv_cl(conv.weight)
+        P["conv_in"] = ops.pack_conv_pad8(enc.conv_in.weight)  # GEMM over channel-padded image rows
         a = enc.mid.attn_1
         P["attn.qkv"] = torch.cat([a.q.weight, a.k.weight, a.v.weight], 0).detach()[:, :, 0, 0].to(BF16).contiguous()
         P["attn.qkv_b"] = torch.cat([a.q.bias, a.k.bias, a.v.bias], 0).detach().float().contiguous()
@@ -138,7 +139,9 @@ class VQEncoderExecutor:
         B, _, R, _ = x.shape
         g = Geom(B, R, R)
         h = self._t(B, "conv_in", g.pixels, enc.ch)
-        ops.small_conv_in_fwd(x.contiguous(), g, enc.conv_in.weight, enc.conv_in.bias, h)
+        x8 = self._t(B, "x8", g.pixels, 8)
+        ops.nchw_to_rows(x.contiguous(), 8, x8)
+        ops.conv3x3_fwd(x8, g, 8, self._packed["conv_in"], h, bias=enc.conv_in.bias)
         for i, lvl in enumerate(enc.down):
             for j, blk in enumerate(lvl.block):
                 h = self._resblock(B, h, g, blk, f"d{i}.{j}")
