@@ -48,7 +48,7 @@ class GroupNormArgs(C.Structure):
                 ("dy", vp), ("lddy", C.c_long), ("dx", vp), ("lddx", C.c_long),
                 ("accumulate_dx", C.c_int), ("pad_", C.c_int),
                 ("dgamma_part", vp), ("dbeta_part", vp), ("ld_part", C.c_long), ("dfilm", vp),
-                ("ld_dfilm", C.c_long)]
+                ("ld_dfilm", C.c_long), ("resid", vp), ("ld_resid", C.c_long)]
 
 
 class LayerNormArgs(C.Structure):

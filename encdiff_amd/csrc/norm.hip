@@ -304,12 +304,19 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   }
   bf16_t* DX = (bf16_t*)p.dx + off * p.lddx + L.cb;
   const bool accum = p.accumulate_dx;
+  const bf16_t* RS = p.resid ? (const bf16_t*)p.resid + off * p.ld_resid + L.cb : nullptr;
 #pragma unroll 1
   for (int px = L.tp; px < HW; px += L.np) {
     float v[8], d[8], o[8];
     unpack8(gn_row(L, tx, X, p.ldx, px), v);
     unpack8(gn_row(L, td, DY, p.lddy, px), d);
     if (accum) unpack8(*(const uint4*)(DX + (long)px * p.lddx), o);
+    if (RS) {  // residual-branch gradient added in the same pass (skip connection of the block)
+      float rr[8];
+      unpack8(*(const uint4*)(RS + (long)px * p.ld_resid), rr);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (accum ? o[i] : 0.f) + rr[i];
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float xh = (v[i] - xm[i]) * xr[i];
@@ -318,7 +325,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
       const float dz = silu ? d[i] * silu_grad(z) : d[i];
       const float dn = dz * sc1[i];
       const float r = xr[i] * (dn * ga[i] - m1[i] - xh * m2[i]);
-      o[i] = accum ? o[i] + r : r;
+      o[i] = (accum || RS) ? o[i] + r : r;
     }
     *(uint4*)(DX + (long)px * p.lddx) = pack8(o);
   }

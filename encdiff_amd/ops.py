@@ -345,13 +345,15 @@ def groupnorm_fwd(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_fi
 
 
 def groupnorm_bwd(x, g: Geom, gamma, beta, stats, eps, silu, dy, dx, dgamma_part, dbeta_part, film=None,
-                  ld_film=0, dfilm=None, ld_dfilm=0, accumulate=False, groups=32, ld_part=None):
+                  ld_film=0, dfilm=None, ld_dfilm=0, accumulate=False, groups=32, ld_part=None, resid=None):
+    """dx (+)= GN_bwd(dy) (+ resid: the block's skip-branch gradient, added in the same pass)."""
     c = x.shape[1]
     a = L.GroupNormArgs(batch=g.batch, hw=g.h * g.w, c=c, groups=groups, eps=eps, silu=int(silu),
                         x=_p(x), ldx=_ld(x), gamma=_p(gamma), beta=_p(beta), film=_p(film), ld_film=ld_film,
                         stats=_p(stats), dy=_p(dy), lddy=_ld(dy), dx=_p(dx), lddx=_ld(dx),
                         accumulate_dx=int(accumulate), dgamma_part=_p(dgamma_part), dbeta_part=_p(dbeta_part),
-                        ld_part=c if ld_part is None else ld_part, dfilm=_p(dfilm), ld_dfilm=ld_dfilm)
+                        ld_part=c if ld_part is None else ld_part, dfilm=_p(dfilm), ld_dfilm=ld_dfilm,
+                        resid=_p(resid), ld_resid=_ld(resid) if resid is not None else 0)
     check(lib.encdiff_groupnorm_bwd(C.byref(a), _s()), "encdiff_groupnorm_bwd")
 
 

@@ -641,8 +641,11 @@ class UNetExecutor:
                       self.G(pre + "in_layers.2.bias"), resample=rs)
         if r.updown:
             ops.resample_bwd(S["d_a1r"], d_a1, gi, r.updown)
+        identity = r.cin == r.cout and not r.updown
+        # identity skip: its gradient (dout) rides in the GN1 backward pass
         ops.groupnorm_bwd(x, gi, self.P(pre + "in_layers.0.weight"), self.P(pre + "in_layers.0.bias"), S["st1"],
-                          GN_EPS, True, d_a1, dx, dg, db, accumulate=acc, ld_part=self.gn.ld)
+                          GN_EPS, True, d_a1, dx, dg, db, accumulate=acc, ld_part=self.gn.ld,
+                          resid=dout if identity else None)
         # skip path
         if r.cin != r.cout:
             ops.linear_bwd(dout, self.W(pre + "skip_connection.weight"), x, dx,
@@ -650,8 +653,6 @@ class UNetExecutor:
                            self.G(pre + "skip_connection.bias"), resid=dx)
         elif r.updown:
             ops.resample_bwd(dout, dx, gi, r.updown, accumulate=True)
-        else:
-            ops.ew(L.EW_COPY, dout, dx, accumulate=True)
 
     def _st_bwd(self, s: STSpec, dout, dx, acc):
         B, c = self.B, s.c
@@ -662,8 +663,6 @@ class UNetExecutor:
         ntok = s.h * s.h
         X = self.st_scratch[(s.h, c)]
         d_a, d_n, d_o = X["d_a"], X["d_n"], X["d_o"]
-        # residual x_in
-        ops.ew(L.EW_COPY, dout, dx, accumulate=acc)
         # proj_out
         d_t3 = S["d_t3"]
         ops.linear_bwd(dout, self.W(s.prefix + "proj_out.weight"), S["t3"], d_t3,
@@ -707,5 +706,6 @@ class UNetExecutor:
         ops.linear_bwd(d_t0, self.W(s.prefix + "proj_in.weight"), S["gn"], X["d_g"],
                        self.G(s.prefix + "proj_in.weight").view(c, c), self.G(s.prefix + "proj_in.bias"))
         dg, db = self.gn.parts(s.prefix + "norm.weight", c)
+        # + the residual x_in branch (dout), in the same pass
         ops.groupnorm_bwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["stg"], ST_GN_EPS,
-                          False, X["d_g"], dx, dg, db, accumulate=True, ld_part=self.gn.ld)
+                          False, X["d_g"], dx, dg, db, accumulate=acc, ld_part=self.gn.ld, resid=dout)

@@ -152,6 +152,7 @@ typedef struct EncdiffGroupNormArgs {
   float* dbeta_part;
   long ld_part;
   float* dfilm; long ld_dfilm;       /* fp32 [batch][ld_dfilm]: dscale at [c], dshift at [C + c] */
+  const void* resid; long ld_resid;  /* backward: optional bf16 residual-branch gradient added to dx */
 } EncdiffGroupNormArgs;
 
 int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* args, void* stream);
