@@ -126,8 +126,9 @@ ED_DEV uint4 gn_row(const GnSlice& L, const uint4* tile, const bf16_t* g, long l
   return L.tiled ? tile[px * L.nvc + L.tv] : *(const uint4*)(g + (long)px * ld);
 }
 
-// phase 0: stream the slice from HBM (4 loads in flight per thread), fill the tile, sum.
-ED_DEV void gn_stream_in(const GnSlice& L, uint4* tile, const bf16_t* X, long ld, int HW, float* s) {
+// phase 0: stream the slice from HBM (4 loads in flight per thread), fill the tile, and
+// accumulate the per-channel sum and sum of squares in the same pass.
+ED_DEV void gn_stream_in(const GnSlice& L, uint4* tile, const bf16_t* X, long ld, int HW, float* s, float* ss) {
 #pragma unroll 4
   for (int px = L.tp; px < HW; px += L.np) {
     const uint4 u = *(const uint4*)(X + (long)px * ld);
@@ -135,21 +136,24 @@ ED_DEV void gn_stream_in(const GnSlice& L, uint4* tile, const bf16_t* X, long ld
     float v[8];
     unpack8(u, v);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s[i] += v[i];
+    for (int i = 0; i < 8; ++i) { s[i] += v[i]; ss[i] += v[i] * v[i]; }
   }
 }
 
+// One reduction round: sum and sum of squares together (var = E[x^2] - mean^2 in fp32 over
+// bf16 inputs of O(1) magnitude; the second read of the slice and a second reduction with
+// its barriers were the longest part of this latency-bound kernel).
 __global__ __launch_bounds__(GN_THREADS) void gn_fwd_kernel(const EncdiffGroupNormArgs p, int cs, int tile_cap) {
   extern __shared__ uint4 tile[];  // tile_cap vectors (0: untiled, re-read from L2/HBM)
-  __shared__ float red[2048], chs[512], gsh[2 * 64];
+  __shared__ float red[4096], chs[1024], gsh[2 * 64];
   const GnSlice L(p, cs, tile_cap);
   const int HW = p.hw;
   const float inv_n = 1.f / ((float)HW * L.cpg);
   const bf16_t* X = (const bf16_t*)p.x + (long)L.b * HW * p.ldx + L.cb;
-  float s[1][8];
+  float s[2][8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) s[0][i] = 0.f;
-  if (L.active) gn_stream_in(L, tile, X, p.ldx, HW, s[0]);
+  for (int i = 0; i < 8; ++i) s[0][i] = s[1][i] = 0.f;
+  if (L.active) gn_stream_in(L, tile, X, p.ldx, HW, s[0], s[1]);
   // per-channel affine / FiLM constants (independent of the statistics)
   float ga[8], be[8], sc[8], sf[8];
   load8f(p.gamma + L.cb, ga);
@@ -158,37 +162,24 @@ __global__ __launch_bounds__(GN_THREADS) void gn_fwd_kernel(const EncdiffGroupNo
     load8f(p.film + (long)L.b * p.ld_film + L.cb, sc);
     load8f(p.film + (long)L.b * p.ld_film + p.c + L.cb, sf);
   }
-  slice_reduce<1>(s, L, red, chs);
+  slice_reduce<2>(s, L, red, chs);
   if (threadIdx.x < L.gs) {
-    float a = 0.f;
-    for (int c = threadIdx.x * L.cpg; c < (threadIdx.x + 1) * L.cpg; ++c) a += chs[c];
-    gsh[threadIdx.x] = a * inv_n;
-  }
-  __syncthreads();
-  float mean[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { mean[i] = gsh[(L.tv * 8 + i) / L.cpg]; s[0][i] = 0.f; }
-  if (L.active) {
-#pragma unroll 2
-    for (int px = L.tp; px < HW; px += L.np) {
-      float v[8];
-      unpack8(gn_row(L, tile, X, p.ldx, px), v);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { const float d = v[i] - mean[i]; s[0][i] += d * d; }
-    }
-  }
-  slice_reduce<1>(s, L, red, chs);
-  if (threadIdx.x < L.gs) {
-    float q = 0.f;
-    for (int c = threadIdx.x * L.cpg; c < (threadIdx.x + 1) * L.cpg; ++c) q += chs[c];
-    const float rstd = rsqrtf(q * inv_n + p.eps);
+    float a = 0.f, q = 0.f;
+    for (int c = threadIdx.x * L.cpg; c < (threadIdx.x + 1) * L.cpg; ++c) { a += chs[c]; q += chs[L.cs + c]; }
+    const float mean = a * inv_n;
+    const float var = fmaxf(q * inv_n - mean * mean, 0.f);
+    const float rstd = rsqrtf(var + p.eps);
+    gsh[threadIdx.x] = mean;
     gsh[64 + threadIdx.x] = rstd;
     const long gi = (long)L.b * p.groups + L.g0 + threadIdx.x;
-    p.stats[2 * gi] = gsh[threadIdx.x];
+    p.stats[2 * gi] = mean;
     p.stats[2 * gi + 1] = rstd;
   }
   __syncthreads();
   if (!L.active) return;
+  float mean[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) mean[i] = gsh[(L.tv * 8 + i) / L.cpg];
   float mul[8], add[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
