@@ -103,7 +103,7 @@ ED_DEV uint32_t im2col_row(const Im2colMode& md, uint32_t b, int y, int x, int t
   return ok ? row : 0u;
 }
 
-template <int BM, int BN, int AM, int BMD>
+template <int BM, int BN, int AM, int BMD, int NS = 2>
 struct Gemm {
   static constexpr bool AKI = AKInner<AM>::v;
   static constexpr bool BKI = BKInner<BMD>::v;
@@ -112,10 +112,11 @@ struct Gemm {
   static constexpr int TM = BM / 32;  // 16x16 MFMA tiles per wave along M
   static constexpr int TN = BN / 32;
   static constexpr int STAGE = TA::ELEMS + TB::ELEMS;  // elements per LDS stage
-  // LDS ring depth.  Measured on the step's GEMMs: 3-4 stages (one or two workgroups per CU)
-  // lost 7% overall against 2 stages with up to five resident workgroups per CU hiding the
-  // load latency instead.
-  static constexpr int NSTAGE = 2;
+  // LDS ring depth.  Measured on the step's GEMMs: 3-4 stages for every GEMM (one or two
+  // workgroups per CU) lost 7% overall against 2 stages with up to five resident workgroups
+  // per CU hiding the load latency instead; the deeper rings are tile choices of their own
+  // (tiles 5, 6) that the measured table picks per problem.
+  static constexpr int NSTAGE = NS;
   static constexpr int LPS = TA::PER_THREAD + TB::PER_THREAD;  // LDS-DMA loads per thread per stage
   // the staging ring, reused by the fp32 epilogue tile [BM][BN + 4]
   static constexpr int LDS_BYTES =
@@ -137,10 +138,10 @@ ED_DEV void vm_wait_stages(int ahead) {
 
 // One output tile (bx, by) of split bz.  Shared by the single-GEMM kernel and the paired
 // kernel that runs two independent GEMMs (a layer's input- and weight-gradient) in one grid.
-template <int BM, int BN, int AM, int BMD>
+template <int BM, int BN, int AM, int BMD, int NS = 2>
 __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAux& aux, const int bx, const int by,
                                           const int bz, bf16_t* smem) {
-  using G = Gemm<BM, BN, AM, BMD>;
+  using G = Gemm<BM, BN, AM, BMD, NS>;
   using TA = typename G::TA;
   using TB = typename G::TB;
   constexpr bool AKI = G::AKI, BKI = G::BKI;
@@ -410,8 +411,9 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     }
     return;
   }
-  if (p.split_k > 1 && p.c_mode == ENCDIFF_OUT_F32)  // split-K slab of this z (workspace path)
+  if (p.split_k > 1 && p.c_mode == ENCDIFF_OUT_F32) {  // split-K slab of this z (workspace path)
     p_c_slab = (float*)p.c + (long)bz * p.M * p.N;
+  }
   const bool vec = (p.N % 8 == 0) && (p.ldc % 8 == 0) && (((uintptr_t)p.c & 15) == 0) &&
                    (!add_bias || (((uintptr_t)p.bias & 15) == 0)) &&
                    (!R || ((p.ld_resid % 8 == 0) && (((uintptr_t)R & 15) == 0)));
@@ -462,10 +464,10 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   }
 }
 
-template <int BM, int BN, int AM, int BMD>
+template <int BM, int BN, int AM, int BMD, int NS>
 __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, const GemmAux aux) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  gemm_tile<BM, BN, AM, BMD>(p, aux, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  gemm_tile<BM, BN, AM, BMD, NS>(p, aux, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const int bid, const int nblk);
@@ -477,7 +479,7 @@ __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const in
 // gradient (problem 2) share the machine instead of running back to back, each too small
 // to fill 256 CUs; the previous layer's weight-gradient finalize rides along, so neither
 // needs a launch of its own.
-template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2>
+template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2>
 __global__ __launch_bounds__(256) void gemm2_kernel(const EncdiffGemmArgs p1, const GemmAux aux1,
                                                     const EncdiffGemmArgs p2, const GemmAux aux2, int gx1,
                                                     int gy1, int gx2, int gy2, const EncdiffGemmArgs pf, int nf) {
@@ -491,57 +493,127 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const EncdiffGemmArgs p1, co
   } else if (i < n1 + n2) {
     i -= n1;
     const int bx = i % gx2, t = i / gx2;
-    gemm_tile<BM2, BN2, AM2, BMD2>(p2, aux2, bx, t % gy2, t / gy2, smem);
+    gemm_tile<BM2, BN2, AM2, BMD2, NS2>(p2, aux2, bx, t % gy2, t / gy2, smem);
   } else {
     gemm_finalize(pf, i - n1 - n2, nf);
   }
 }
 
-// split-K finalize: C = alpha * sum_z slab[z] (+bias)(+resid).  A workgroup owns 64
-// consecutive outputs; its 4 wave-rows each sum every 4th slab (8 loads in flight per
-// lane), then the 4 partials are added in a fixed order: bitwise reproducible, no atomics,
-// and a deep split (e.g. 128 slabs of a 64x64 weight gradient) stays bandwidth-bound.
-constexpr int FIN_ZG = 4, FIN_OPB = 64;
+// split-K finalize: C = alpha * sum_z slab[z] (+bias)(+resid).  Each lane owns 4
+// consecutive outputs (float4 slab loads).  Up to 8 slabs one lane sums them all in z order
+// (a workgroup covers 1024 outputs); deeper splits (e.g. 128 slabs of a 64x64 weight
+// gradient) give 4 wave-rows every 4th slab and add the 4 partials in a fixed order.  Either
+// way bitwise reproducible, no atomics.  The first version (one scalar load per lane,
+// 64 outputs per workgroup) spent ~9 us on a 2048x256 split-4 GEMM in workgroup turnover.
+constexpr int FIN_ZG = 4;
+__host__ __device__ inline int fin_zgroups(const EncdiffGemmArgs& p) { return p.split_k > 8 ? FIN_ZG : 1; }
+__host__ __device__ inline bool fin_vec(const EncdiffGemmArgs& p) {
+  return (p.N & 3) == 0 && ((uintptr_t)p.workspace & 15) == 0;
+}
+// outputs one workgroup covers per grid-stride iteration
+__host__ __device__ inline int fin_per_block(const EncdiffGemmArgs& p) {
+  return (fin_vec(p) ? 4 : 1) * 256 / fin_zgroups(p);
+}
+
+__device__ __forceinline__ void fin_store(const EncdiffGemmArgs& p, const bf16_t* R, const long i, float v) {
+  const int row = (int)(i / p.N), col = (int)(i - (long)row * p.N);
+  v *= p.alpha;
+  if (p.bias) v += p.bias[col];
+  if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
+  if (p.c_mode == ENCDIFF_OUT_BF16) ((bf16_t*)p.c)[(long)row * p.ldc + col] = f2bf(v);
+  else if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) ((float*)p.c)[(long)row * p.ldc + col] += v;
+  else ((float*)p.c)[(long)row * p.ldc + col] = v;
+}
+
 __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const int bid, const int nblk) {
-  __shared__ float part[FIN_ZG][FIN_OPB];
+  __shared__ float4 part[FIN_ZG][64];
   const long total = (long)p.M * p.N;
   const bf16_t* R = (const bf16_t*)p.resid;
-  const int o = threadIdx.x % FIN_OPB, zg = threadIdx.x / FIN_OPB;
-  for (long t0 = (long)bid * FIN_OPB; t0 < total; t0 += (long)nblk * FIN_OPB) {
-    const long i = t0 + o;
-    float acc = 0.f;
-    if (i < total) {
-      const float* w = p.workspace + i;
+  const int zgn = fin_zgroups(p);
+  const int tpo = 256 / zgn;  // lanes per z-group
+  const int o = threadIdx.x % tpo, zg = threadIdx.x / tpo;
+  const long per = fin_per_block(p);
+  if (fin_vec(p)) {
+    for (long t0 = (long)bid * per; t0 < total; t0 += (long)nblk * per) {
+      const long i = t0 + 4L * o;  // total % 4 == 0: the 4 outputs are in range together
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < total) {
+        const float* w = p.workspace + i;
 #pragma unroll 8
-      for (int z = zg; z < p.split_k; z += FIN_ZG) acc += w[(long)z * total];
+        for (int z = zg; z < p.split_k; z += zgn) {
+          const float4 v = *(const float4*)(w + (long)z * total);
+          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+      }
+      if (zgn > 1) {  // block-uniform branch
+        part[zg][o] = acc;
+        __syncthreads();
+        if (zg == 0) {
+          const float4 a0 = part[0][o], a1 = part[1][o], a2 = part[2][o], a3 = part[3][o];
+          acc.x = ((a0.x + a1.x) + a2.x) + a3.x;
+          acc.y = ((a0.y + a1.y) + a2.y) + a3.y;
+          acc.z = ((a0.z + a1.z) + a2.z) + a3.z;
+          acc.w = ((a0.w + a1.w) + a2.w) + a3.w;
+        }
+      }
+      if (zg == 0 && i < total) {
+        const int row = (int)(i / p.N), col = (int)(i - (long)row * p.N);  // N % 4 == 0: one row
+        float v[4] = {p.alpha * acc.x, p.alpha * acc.y, p.alpha * acc.z, p.alpha * acc.w};
+        if (p.bias) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] += p.bias[col + k];
+        }
+        if (R) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[k] += bf2f(R[(long)row * p.ld_resid + col + k]);
+        }
+        const long co = (long)row * p.ldc + col;
+        if (p.c_mode == ENCDIFF_OUT_BF16) {
+          bf16_t* c = (bf16_t*)p.c + co;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) c[k] = f2bf(v[k]);
+        } else {
+          float* c = (float*)p.c + co;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) c[k] = p.c_mode == ENCDIFF_OUT_F32_ACCUM ? c[k] + v[k] : v[k];
+        }
+      }
+      if (zgn > 1) __syncthreads();
     }
-    part[zg][o] = acc;
-    __syncthreads();
-    if (zg == 0 && i < total) {
-      const float sum = ((part[0][o] + part[1][o]) + part[2][o]) + part[3][o];
-      const int row = (int)(i / p.N), col = (int)(i - (long)row * p.N);
-      float v = p.alpha * sum;
-      if (p.bias) v += p.bias[col];
-      if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
-      if (p.c_mode == ENCDIFF_OUT_BF16) ((bf16_t*)p.c)[(long)row * p.ldc + col] = f2bf(v);
-      else if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) ((float*)p.c)[(long)row * p.ldc + col] += v;
-      else ((float*)p.c)[(long)row * p.ldc + col] = v;
+  } else {
+    float* pz = (float*)part;
+    for (long t0 = (long)bid * per; t0 < total; t0 += (long)nblk * per) {
+      const long i = t0 + o;
+      float acc = 0.f;
+      if (i < total) {
+        const float* w = p.workspace + i;
+#pragma unroll 8
+        for (int z = zg; z < p.split_k; z += zgn) acc += w[(long)z * total];
+      }
+      if (zgn > 1) {
+        pz[zg * 64 + o] = acc;
+        __syncthreads();
+        if (zg == 0) acc = ((pz[o] + pz[64 + o]) + pz[128 + o]) + pz[192 + o];
+      }
+      if (zg == 0 && i < total) fin_store(p, R, i, acc);
+      if (zgn > 1) __syncthreads();
     }
-    __syncthreads();
   }
-  if (p.bias_grad) {  // bias-gradient slabs [split][M] behind the C slabs, same ordered scheme
+  if (p.bias_grad) {  // bias-gradient slabs [split][M] behind the C slabs: 4 z-groups, fixed order
+    float* pz = (float*)part;
+    const int bo = threadIdx.x & 63, bz = threadIdx.x >> 6;
     const float* bs = p.workspace + (long)p.split_k * total;
-    for (long t0 = (long)bid * FIN_OPB; t0 < p.M; t0 += (long)nblk * FIN_OPB) {
-      const long m = t0 + o;
+    for (long t0 = (long)bid * 64; t0 < p.M; t0 += (long)nblk * 64) {
+      const long m = t0 + bo;
       float acc = 0.f;
       if (m < p.M) {
 #pragma unroll 8
-        for (int z = zg; z < p.split_k; z += FIN_ZG) acc += bs[(long)z * p.M + m];
+        for (int z = bz; z < p.split_k; z += 4) acc += bs[(long)z * p.M + m];
       }
-      part[zg][o] = acc;
+      __syncthreads();  // part may still be read by the C loop above
+      pz[bz * 64 + bo] = acc;
       __syncthreads();
-      if (zg == 0 && m < p.M) p.bias_grad[m] += ((part[0][o] + part[1][o]) + part[2][o]) + part[3][o];
-      __syncthreads();
+      if (bz == 0 && m < p.M) p.bias_grad[m] += ((pz[bo] + pz[64 + bo]) + pz[128 + bo]) + pz[192 + bo];
     }
   }
 }
@@ -557,16 +629,16 @@ __global__ __launch_bounds__(256) void gemm_finalize2_kernel(const EncdiffGemmAr
   else gemm_finalize(p2, blockIdx.x - g1, gridDim.x - g1);
 }
 
-template <int BM, int BN, int AM, int BMD>
+template <int BM, int BN, int AM, int BMD, int NS = 2>
 hipError_t launch_t(const EncdiffGemmArgs& p, const GemmAux& aux, hipStream_t s) {
-  using G = Gemm<BM, BN, AM, BMD>;
+  using G = Gemm<BM, BN, AM, BMD, NS>;
   const size_t lds = G::LDS_BYTES;
   // dynamic LDS above 64 KiB must be opted in once per instantiation (thread-safe static init)
   static const hipError_t attr_ok = hipFuncSetAttribute(
-      (const void*)gemm_kernel<BM, BN, AM, BMD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (const void*)gemm_kernel<BM, BN, AM, BMD, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr_ok != hipSuccess) return attr_ok;
   dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, p.split_k);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, AM, BMD>), grid, dim3(256), lds, s, p, aux);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, AM, BMD, NS>), grid, dim3(256), lds, s, p, aux);
   return hipGetLastError();
 }
 
@@ -576,6 +648,8 @@ hipError_t launch_modes(const EncdiffGemmArgs& p, const GemmAux& aux, int tile, 
     case 1: return launch_t<128, 128, AM, BMD>(p, aux, s);
     case 2: return launch_t<128, 64, AM, BMD>(p, aux, s);
     case 3: return launch_t<64, 128, AM, BMD>(p, aux, s);
+    case 5: return launch_t<64, 64, AM, BMD, 4>(p, aux, s);
+    case 6: return launch_t<64, 128, AM, BMD, 3>(p, aux, s);
     default: return launch_t<64, 64, AM, BMD>(p, aux, s);
   }
 }
@@ -645,9 +719,11 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
 }
 
 int fin_blocks(const EncdiffGemmArgs& u) {
-  long total = (long)u.M * u.N;
-  long g = (total + FIN_OPB - 1) / FIN_OPB;
-  return (int)(g > 8192 ? 8192 : g);
+  const long total = (long)u.M * u.N;
+  const long per = fin_per_block(u);
+  long g = (total + per - 1) / per;
+  if (u.bias_grad && (u.M + 63) / 64 > g) g = (u.M + 63) / 64;
+  return (int)(g > 2048 ? 2048 : g);
 }
 
 int launch_one(const GemmPlan& g, hipStream_t s) {
@@ -670,18 +746,18 @@ int launch_one(const GemmPlan& g, hipStream_t s) {
   return ENCDIFF_OK;
 }
 
-template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2>
+template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2 = 2>
 hipError_t launch_pair_t(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
   using G1 = Gemm<64, 64, AM1, BMD1>;
-  using G2 = Gemm<BM2, BN2, AM2, BMD2>;
+  using G2 = Gemm<BM2, BN2, AM2, BMD2, NS2>;
   constexpr size_t lds = G1::LDS_BYTES > G2::LDS_BYTES ? G1::LDS_BYTES : G2::LDS_BYTES;
   static const hipError_t attr_ok = hipFuncSetAttribute(
-      (const void*)gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (const void*)gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr_ok != hipSuccess) return attr_ok;
   const int gx1 = (g1.p.M + 63) / 64, gy1 = (g1.p.N + 63) / 64;
   const int gx2 = (g2.p.M + BM2 - 1) / BM2, gy2 = (g2.p.N + BN2 - 1) / BN2;
   const long nb = (long)gx1 * gy1 * g1.p.split_k + (long)gx2 * gy2 * g2.p.split_k + nf;
-  hipLaunchKernelGGL((gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2>), dim3((unsigned)nb), dim3(256), lds, s, g1.p,
+  hipLaunchKernelGGL((gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2>), dim3((unsigned)nb), dim3(256), lds, s, g1.p,
                      g1.aux, g2.p, g2.aux, gx1, gy1, gx2, gy2, pf, nf);
   return hipGetLastError();
 }
@@ -693,6 +769,8 @@ hipError_t launch_pair_tiles(const GemmPlan& g1, const GemmPlan& g2, const Encdi
     case 1: return launch_pair_t<AM1, BMD1, 128, 128, AM2, BMD2>(g1, g2, pf, nf, s);
     case 2: return launch_pair_t<AM1, BMD1, 128, 64, AM2, BMD2>(g1, g2, pf, nf, s);
     case 3: return launch_pair_t<AM1, BMD1, 64, 128, AM2, BMD2>(g1, g2, pf, nf, s);
+    case 5: return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 4>(g1, g2, pf, nf, s);
+    case 6: return launch_pair_t<AM1, BMD1, 64, 128, AM2, BMD2, 3>(g1, g2, pf, nf, s);
     default: return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2>(g1, g2, pf, nf, s);
   }
 }

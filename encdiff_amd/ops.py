@@ -141,10 +141,12 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
 
 
 def ws_floats(args) -> int:
-    """Workspace floats a GEMM's split-K slabs (+ bias-gradient slabs) occupy."""
+    """Workspace floats a GEMM's split-K slabs (+ bias-gradient slabs) occupy, rounded up to
+    16 bytes so a slab region placed behind it keeps the finalize's float4 loads aligned."""
     if args.split_k <= 1 or args.c_mode not in (L.OUT_BF16, L.OUT_F32, L.OUT_F32_ACCUM):
         return 0
-    return args.split_k * args.M * args.N + (args.split_k * args.M if args.bias_grad else 0)
+    n = args.split_k * args.M * args.N + (args.split_k * args.M if args.bias_grad else 0)
+    return (n + 3) & ~3
 
 
 _PENDING = {}  # stream -> GemmArgs of a weight gradient whose split-K finalize is deferred

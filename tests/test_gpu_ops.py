@@ -95,6 +95,21 @@ def test_split_k_workspace(O, split):
         assert rel(out, x.float() @ w.float().t() + b + r.float()) < 1e-2
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
+def test_gemm_tiles(O, tile):
+    """Every tile shape / LDS ring depth (tiles 5, 6: 4- and 3-deep rings) on a ragged
+    problem with a k-tile count that is not a multiple of the ring depth, split-K 1 and 3."""
+    torch.manual_seed(3)
+    M, N, K = 328, 200, 1000
+    x, w = bf(M, K), bf(N, K, scale=K ** -0.5)
+    ref = x.float() @ w.float().t()
+    for split in (1, 3):
+        out = torch.empty(M, N, device=dev)
+        O.gemm(M, N, K, x, K, w, K, out, N, c_mode=O.L.OUT_F32, split_k=split, tile=tile)
+        O.flush()
+        assert rel(out, ref) < 1e-4, (tile, split)
+
+
 def test_linear_strided_views(O):
     """q/k/v slices of a fused [M][3C] projection output are strided views."""
     torch.manual_seed(1)
