@@ -31,16 +31,18 @@ template <int BMd> struct BKInner { static constexpr bool v = BMd == B_ROWK; };
 // one wave instruction writes 1 KiB lane-linearly).  Bank conflicts of the fragment reads are
 // removed by an XOR swizzle applied on the SOURCE side: the chunk stored at LDS slot s of
 // row r is the global chunk s ^ (r & 7), and reads apply the same involution.
-template <int ROWS, bool KINNER>
+template <int ROWS, bool KINNER, int KB = BK>
 struct TileShape {
-  // k-inner: [ROWS][BK]; k-outer: [BK][ROWS]
-  static constexpr int LD = KINNER ? BK : ROWS;            // elements per LDS row
+  // k-inner: [ROWS][KB]; k-outer: [KB][ROWS]
+  static constexpr int LD = KINNER ? KB : ROWS;            // elements per LDS row
   static constexpr int SLOTS = LD / 8;                      // 16-byte chunks per row
-  static constexpr int ELEMS = ROWS * BK;
-  static constexpr int CHUNKS = ROWS * BK / 8;  // 16-byte chunks per tile
+  static constexpr int ELEMS = ROWS * KB;
+  static constexpr int CHUNKS = ROWS * KB / 8;  // 16-byte chunks per tile
   static constexpr int PER_THREAD = CHUNKS / 256;
+  // swizzle mask: 16 rows of a 256-byte k-inner row (KB = 128) spread over all 64 banks
+  static constexpr int SWM = (KINNER && KB >= 128) ? 15 : 7;
 };
-ED_DEV int swz(int row, int slot) { return slot ^ (row & 7); }
+ED_DEV int swz(int row, int slot, int mask = 7) { return slot ^ (row & mask); }
 
 // 16 zero bytes in global memory: the source of masked (padding / out-of-range) chunks,
 // so LDS-DMA lanes never need a branch.
@@ -103,12 +105,13 @@ ED_DEV uint32_t im2col_row(const Im2colMode& md, uint32_t b, int y, int x, int t
   return ok ? row : 0u;
 }
 
-template <int BM, int BN, int AM, int BMD, int NS = 2>
+template <int BM, int BN, int AM, int BMD, int NS = 2, int KB = BK>
 struct Gemm {
   static constexpr bool AKI = AKInner<AM>::v;
   static constexpr bool BKI = BKInner<BMD>::v;
-  using TA = TileShape<BM, AKI>;
-  using TB = TileShape<BN, BKI>;
+  static constexpr int KT = KB;  // k per LDS stage
+  using TA = TileShape<BM, AKI, KB>;
+  using TB = TileShape<BN, BKI, KB>;
   static constexpr int TM = BM / 32;  // 16x16 MFMA tiles per wave along M
   static constexpr int TN = BN / 32;
   static constexpr int STAGE = TA::ELEMS + TB::ELEMS;  // elements per LDS stage
@@ -138,10 +141,11 @@ ED_DEV void vm_wait_stages(int ahead) {
 
 // One output tile (bx, by) of split bz.  Shared by the single-GEMM kernel and the paired
 // kernel that runs two independent GEMMs (a layer's input- and weight-gradient) in one grid.
-template <int BM, int BN, int AM, int BMD, int NS = 2>
+template <int BM, int BN, int AM, int BMD, int NS = 2, int KB = BK>
 __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAux& aux, const int bx, const int by,
                                           const int bz, bf16_t* smem) {
-  using G = Gemm<BM, BN, AM, BMD, NS>;
+  using G = Gemm<BM, BN, AM, BMD, NS, KB>;
+  constexpr int BK = G::KT;  // shadows the default stage depth
   using TA = typename G::TA;
   using TB = typename G::TB;
   constexpr bool AKI = G::AKI, BKI = G::BKI;
@@ -180,7 +184,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     for (int i = 0; i < TA::PER_THREAD; ++i) {
       const int c = tid + 256 * i;               // LDS chunk position (lane-linear)
       const int row = c / TA::SLOTS, slot = c % TA::SLOTS;
-      const int gs = swz(row, slot);              // global chunk held at this slot
+      const int gs = swz(row, slot, TA::SWM);     // global chunk held at this slot
       bool ok;
       size_t off;
       if constexpr (AKI) {
@@ -218,7 +222,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     for (int i = 0; i < TB::PER_THREAD; ++i) {
       const int c = tid + 256 * i;
       const int row = c / TB::SLOTS, slot = c % TB::SLOTS;
-      const int gs = swz(row, slot);
+      const int gs = swz(row, slot, TB::SWM);
       bool ok;
       size_t off;
       if constexpr (BKI) {  // B_ROWK: Bt[n][k], row = n
@@ -272,8 +276,8 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   const int g4 = lane >> 4;
   const int tq = l16 >> 2, tp = l16 & 3;  // transpose-read address roles
 
-  auto frag_kinner = [&](const bf16_t* s, int row, int kk) -> v8bf {
-    return *(const v8bf*)(s + row * BK + swz(row, kk * 4 + g4) * 8);
+  auto frag_kinner = [&](const bf16_t* s, int row, int kk, int mask) -> v8bf {
+    return *(const v8bf*)(s + row * BK + swz(row, kk * 4 + g4, mask) * 8);
   };
   auto frag_kouter = [&](const bf16_t* s, int ld, int colbase, int kk) -> v8bf {
     // rows k = kk*32 + g4*8 + tq (+4): 4 bf16 at column colbase + 4*tp, swizzled chunk
@@ -302,12 +306,12 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       v8bf af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        if constexpr (AKI) af[i] = frag_kinner(sa, wr + 16 * i + l16, kk);
+        if constexpr (AKI) af[i] = frag_kinner(sa, wr + 16 * i + l16, kk, TA::SWM);
         else af[i] = frag_kouter(sa, TA::LD, wr + 16 * i, kk);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        if constexpr (BKI) bfr[j] = frag_kinner(sb, wc + 16 * j + l16, kk);
+        if constexpr (BKI) bfr[j] = frag_kinner(sb, wc + 16 * j + l16, kk, TB::SWM);
         else bfr[j] = frag_kouter(sb, TB::LD, wc + 16 * j, kk);
       }
 #pragma unroll
@@ -464,10 +468,10 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   }
 }
 
-template <int BM, int BN, int AM, int BMD, int NS>
+template <int BM, int BN, int AM, int BMD, int NS, int KB>
 __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, const GemmAux aux) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  gemm_tile<BM, BN, AM, BMD, NS>(p, aux, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  gemm_tile<BM, BN, AM, BMD, NS, KB>(p, aux, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const int bid, const int nblk);
@@ -479,7 +483,7 @@ __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const in
 // gradient (problem 2) share the machine instead of running back to back, each too small
 // to fill 256 CUs; the previous layer's weight-gradient finalize rides along, so neither
 // needs a launch of its own.
-template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2>
+template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2, int KB2>
 __global__ __launch_bounds__(256) void gemm2_kernel(const EncdiffGemmArgs p1, const GemmAux aux1,
                                                     const EncdiffGemmArgs p2, const GemmAux aux2, int gx1,
                                                     int gy1, int gx2, int gy2, const EncdiffGemmArgs pf, int nf) {
@@ -493,7 +497,7 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const EncdiffGemmArgs p1, co
   } else if (i < n1 + n2) {
     i -= n1;
     const int bx = i % gx2, t = i / gx2;
-    gemm_tile<BM2, BN2, AM2, BMD2, NS2>(p2, aux2, bx, t % gy2, t / gy2, smem);
+    gemm_tile<BM2, BN2, AM2, BMD2, NS2, KB2>(p2, aux2, bx, t % gy2, t / gy2, smem);
   } else {
     gemm_finalize(pf, i - n1 - n2, nf);
   }
@@ -629,16 +633,16 @@ __global__ __launch_bounds__(256) void gemm_finalize2_kernel(const EncdiffGemmAr
   else gemm_finalize(p2, blockIdx.x - g1, gridDim.x - g1);
 }
 
-template <int BM, int BN, int AM, int BMD, int NS = 2>
+template <int BM, int BN, int AM, int BMD, int NS = 2, int KB = BK>
 hipError_t launch_t(const EncdiffGemmArgs& p, const GemmAux& aux, hipStream_t s) {
-  using G = Gemm<BM, BN, AM, BMD, NS>;
+  using G = Gemm<BM, BN, AM, BMD, NS, KB>;
   const size_t lds = G::LDS_BYTES;
   // dynamic LDS above 64 KiB must be opted in once per instantiation (thread-safe static init)
   static const hipError_t attr_ok = hipFuncSetAttribute(
-      (const void*)gemm_kernel<BM, BN, AM, BMD, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (const void*)gemm_kernel<BM, BN, AM, BMD, NS, KB>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr_ok != hipSuccess) return attr_ok;
   dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, p.split_k);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, AM, BMD, NS>), grid, dim3(256), lds, s, p, aux);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, AM, BMD, NS, KB>), grid, dim3(256), lds, s, p, aux);
   return hipGetLastError();
 }
 
@@ -650,6 +654,8 @@ hipError_t launch_modes(const EncdiffGemmArgs& p, const GemmAux& aux, int tile, 
     case 3: return launch_t<64, 128, AM, BMD>(p, aux, s);
     case 5: return launch_t<64, 64, AM, BMD, 4>(p, aux, s);
     case 6: return launch_t<64, 128, AM, BMD, 3>(p, aux, s);
+    case 7: return launch_t<64, 64, AM, BMD, 2, 128>(p, aux, s);
+    case 8: return launch_t<64, 128, AM, BMD, 2, 128>(p, aux, s);
     default: return launch_t<64, 64, AM, BMD>(p, aux, s);
   }
 }
@@ -746,18 +752,18 @@ int launch_one(const GemmPlan& g, hipStream_t s) {
   return ENCDIFF_OK;
 }
 
-template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2 = 2>
+template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2 = 2, int KB2 = BK>
 hipError_t launch_pair_t(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
   using G1 = Gemm<64, 64, AM1, BMD1>;
-  using G2 = Gemm<BM2, BN2, AM2, BMD2, NS2>;
+  using G2 = Gemm<BM2, BN2, AM2, BMD2, NS2, KB2>;
   constexpr size_t lds = G1::LDS_BYTES > G2::LDS_BYTES ? G1::LDS_BYTES : G2::LDS_BYTES;
   static const hipError_t attr_ok = hipFuncSetAttribute(
-      (const void*)gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (const void*)gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2, KB2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr_ok != hipSuccess) return attr_ok;
   const int gx1 = (g1.p.M + 63) / 64, gy1 = (g1.p.N + 63) / 64;
   const int gx2 = (g2.p.M + BM2 - 1) / BM2, gy2 = (g2.p.N + BN2 - 1) / BN2;
   const long nb = (long)gx1 * gy1 * g1.p.split_k + (long)gx2 * gy2 * g2.p.split_k + nf;
-  hipLaunchKernelGGL((gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2>), dim3((unsigned)nb), dim3(256), lds, s, g1.p,
+  hipLaunchKernelGGL((gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2, KB2>), dim3((unsigned)nb), dim3(256), lds, s, g1.p,
                      g1.aux, g2.p, g2.aux, gx1, gy1, gx2, gy2, pf, nf);
   return hipGetLastError();
 }
@@ -771,6 +777,8 @@ hipError_t launch_pair_tiles(const GemmPlan& g1, const GemmPlan& g2, const Encdi
     case 3: return launch_pair_t<AM1, BMD1, 64, 128, AM2, BMD2>(g1, g2, pf, nf, s);
     case 5: return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 4>(g1, g2, pf, nf, s);
     case 6: return launch_pair_t<AM1, BMD1, 64, 128, AM2, BMD2, 3>(g1, g2, pf, nf, s);
+    case 7: return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 2, 128>(g1, g2, pf, nf, s);
+    case 8: return launch_pair_t<AM1, BMD1, 64, 128, AM2, BMD2, 2, 128>(g1, g2, pf, nf, s);
     default: return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2>(g1, g2, pf, nf, s);
   }
 }

@@ -81,6 +81,7 @@ def _tile_table():
 
 
 MAX_SPLIT = int(os.environ.get("ENCDIFF_MAX_SPLIT", "1024"))  # experiment knob: clamp table split-K
+FORCE_TILE = 0  # tests: override the planned tile of every GEMM that does not pass one
 
 
 def plan_key(M, N, K, a_mode, b_mode, c_mode, resample=0):
@@ -125,7 +126,7 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
     floats into this stream's workspace."""
     if split_k is None or tile == 0:
         t, sp = plan(M, N, K, a_mode, b_mode, c_mode, conv.resample if conv is not None else 0)
-        tile = tile or t
+        tile = tile or FORCE_TILE or t
         split_k = split_k or sp
     ws = None
     if split_k > 1 and c_mode in (L.OUT_BF16, L.OUT_F32, L.OUT_F32_ACCUM):

@@ -99,7 +99,8 @@ typedef struct EncdiffGemmArgs {
   const void* resid; long ld_resid;  /* bf16 [M][N] or NULL                        */
   float* bias_grad;          /* OPA_ROWM only: += sum_k A[m][k] into bias_grad[m]  */
   int tile;                  /* 0 = auto, else 1:128x128 2:128x64 3:64x128 4:64x64, 5:64x64 with a
-                                4-deep LDS ring, 6:64x128 with a 3-deep ring */
+                                4-deep LDS ring, 6:64x128 with a 3-deep ring, 7:64x64 and
+                                8:64x128 with 128-deep k stages (others: 64) */
   int pad2_;
   float* workspace;          /* split_k > 1 with a BF16/F32/F32_ACCUM c_mode: fp32 scratch of split_k*M*N
                                 (+ split_k*M when bias_grad is set: per-split bias-gradient slabs);

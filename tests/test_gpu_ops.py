@@ -95,10 +95,11 @@ def test_split_k_workspace(O, split):
         assert rel(out, x.float() @ w.float().t() + b + r.float()) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_gemm_tiles(O, tile):
-    """Every tile shape / LDS ring depth (tiles 5, 6: 4- and 3-deep rings) on a ragged
-    problem with a k-tile count that is not a multiple of the ring depth, split-K 1 and 3."""
+    """Every tile shape / LDS ring depth (tiles 5, 6: 4- and 3-deep rings; 7, 8: 128-deep k
+    stages) on a ragged problem with a k-tile count that is not a multiple of the ring depth,
+    split-K 1 and 3, and on a 3x3 conv forward + input gradient."""
     torch.manual_seed(3)
     M, N, K = 328, 200, 1000
     x, w = bf(M, K), bf(N, K, scale=K ** -0.5)
@@ -108,6 +109,28 @@ def test_gemm_tiles(O, tile):
         O.gemm(M, N, K, x, K, w, K, out, N, c_mode=O.L.OUT_F32, split_k=split, tile=tile)
         O.flush()
         assert rel(out, ref) < 1e-4, (tile, split)
+    # implicit-im2col forward and input gradient (k-inner A, k-outer flipped-weight B)
+    from encdiff_amd.ops import Geom
+    g = Geom(3, 8, 8)
+    cin, cout = 72, 200
+    xs = bf(g.pixels, cin)
+    wt = torch.randn(cout, cin, 3, 3, device=dev) / math.sqrt(9 * cin)
+    wf = wt.permute(0, 2, 3, 1).reshape(cout, 9 * cin).to(torch.bfloat16).contiguous()
+    wq = wf.float().reshape(cout, 3, 3, cin).permute(0, 3, 1, 2)
+    O.FORCE_TILE = tile
+    try:
+        y = torch.empty(g.pixels, cout, device=dev, dtype=torch.bfloat16)
+        O.conv3x3_fwd(xs, g, cin, wf, y)
+        dy = bf(g.pixels, cout)
+        dx = torch.empty(g.pixels, cin, device=dev, dtype=torch.bfloat16)
+        O.conv3x3_dgrad(dy, g, wf, dx)
+    finally:
+        O.FORCE_TILE = 0
+    xin = nhwc(xs, g).requires_grad_(True)
+    ref = F.conv2d(xin, wq, padding=1)
+    assert rel(nhwc(y, g), ref) < 1e-2, tile
+    ref.backward(nhwc(dy, g))
+    assert rel(nhwc(dx, g), xin.grad) < 1e-2, tile
 
 
 def test_linear_strided_views(O):

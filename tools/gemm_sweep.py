@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--splits", default="1,4")
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--f32", action="store_true", help="fp32 output (no bf16 epilogue)")
+    ap.add_argument("--eager", action="store_true", help="plain launches, no graph (for rocprofv3 --pmc)")
     a = ap.parse_args()
     from encdiff_amd import ops
     L = ops.L
@@ -40,6 +41,12 @@ def main():
                 run = lambda: ops.gemm(M, N, K, x, K, w, K, out, N, c_mode=cm, split_k=split, tile=tile)
                 run()
                 torch.cuda.synchronize()
+                if a.eager:
+                    for _ in range(a.reps):
+                        run()
+                    torch.cuda.synchronize()
+                    print(f"M={M} N={N} K={K} tile={tile} split={split} eager x{a.reps}", flush=True)
+                    continue
                 g = torch.cuda.CUDAGraph()
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
