@@ -20,9 +20,8 @@ ED_DEV v4f mma(const s4& a, const s4& b, const v4f& c) {
 }
 ED_DEV s4 ld4(const bf16_t* p) { return *(const s4*)p; }
 ED_DEV s4 pack4(float a, float b, float c, float d) {
-  s4 r;
-  r[0] = (short)f2bf(a); r[1] = (short)f2bf(b); r[2] = (short)f2bf(c); r[3] = (short)f2bf(d);
-  return r;
+  const uint2 u = {pack2(a, b), pack2(c, d)};
+  return __builtin_bit_cast(s4, u);
 }
 
 // stage rows [n][dh] of a head from a [rows][ld] tensor into LDS row-major [np][DP]
@@ -260,11 +259,9 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int dt = 0; dt < KC; ++dt) { dk[u][dt] = (v4f){0.f, 0.f, 0.f, 0.f}; dv[u][dt] = dk[u][dt]; }
-    for (int qt0 = qs; qt0 < qtiles; qt0 += 2 * QS) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int qt = qt0 + u * QS;
-        if (qt >= qtiles) break;
+    // the two query tiles of a step are independent chains (LDS read -> MFMA -> exp -> MFMA);
+    // without a partial last step they are straight-line code the compiler interleaves
+    auto qstep = [&](const int qt, const int u) {
         v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
@@ -285,6 +282,16 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
           dv[u][dt] = mma(ld4(Gt + (dt * 16 + l16) * TQ + qt * 16 + 4 * g), pf, dv[u][dt]);
           dk[u][dt] = mma(ld4(Qt + (dt * 16 + l16) * TQ + qt * 16 + 4 * g), df, dk[u][dt]);
         }
+    };
+    if (qtiles % (2 * QS) == 0) {
+      for (int qt0 = qs; qt0 < qtiles; qt0 += 2 * QS) {
+        qstep(qt0, 0);
+        qstep(qt0 + QS, 1);
+      }
+    } else {
+      for (int qt0 = qs; qt0 < qtiles; qt0 += 2 * QS) {
+        qstep(qt0, 0);
+        if (qt0 + QS < qtiles) qstep(qt0 + QS, 1);
       }
     }
 #pragma unroll
@@ -374,11 +381,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int dt = 0; dt < KC; ++dt) dq[u][dt] = (v4f){0.f, 0.f, 0.f, 0.f};
-    for (int kt0 = 0; kt0 < ktiles; kt0 += 2) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int kt = kt0 + u;
-        if (kt >= ktiles) break;
+    auto kstep = [&](const int kt, const int u) {
         v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
@@ -396,6 +399,16 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
 #pragma unroll
         for (int dt = 0; dt < KC; ++dt)
           dq[u][dt] = mma(ld4(Kt + (dt * 16 + l16) * TK + kt * 16 + 4 * g), df, dq[u][dt]);
+    };
+    if ((ktiles & 1) == 0) {
+      for (int kt0 = 0; kt0 < ktiles; kt0 += 2) {
+        kstep(kt0, 0);
+        kstep(kt0 + 1, 1);
+      }
+    } else {
+      for (int kt0 = 0; kt0 < ktiles; kt0 += 2) {
+        kstep(kt0, 0);
+        if (kt0 + 1 < ktiles) kstep(kt0 + 1, 1);
       }
     }
     if (qv) {

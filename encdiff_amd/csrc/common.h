@@ -21,7 +21,13 @@ ED_DEV bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN preserving
   return __builtin_bit_cast(bf16_t, b);
 }
-ED_DEV uint32_t pack2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
+// one v_cvt_pk_bf16_f32 (two scalar conversions + a v_perm otherwise)
+ED_DEV uint32_t pack2(float a, float b) {
+  const v2f v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, v2bf));
+}
 
 // 8 bf16 <-> 8 float
 ED_DEV void unpack8(const uint4& u, float* f) {
