@@ -18,7 +18,8 @@ LIB_PATH = os.environ.get("ENCDIFF_LIB", os.path.join(HERE, "libencdiff_hip.so")
 OPA_ROWK, OPA_IM2COL, OPA_ROWM = 0, 1, 2
 OPB_ROWK, OPB_ROWN, OPB_CONV_DGRAD, OPB_IM2COL = 0, 1, 2, 3
 OUT_BF16, OUT_F32, OUT_F32_ATOMIC, OUT_F32_ATOMIC_CONVW, OUT_F32_ACCUM = 0, 1, 2, 3, 4
-RESAMPLE_NONE, RESAMPLE_DOWN2, RESAMPLE_UP2, RESAMPLE_STRIDE2, RESAMPLE_K4S2, RESAMPLE_K4S2_T = 0, 1, 2, 3, 4, 5
+RESAMPLE_NONE, RESAMPLE_DOWN2, RESAMPLE_UP2, RESAMPLE_STRIDE2, RESAMPLE_K4S2, RESAMPLE_K4S2_T, RESAMPLE_K4S2_TP = \
+    0, 1, 2, 3, 4, 5, 6
 (EW_COPY, EW_SILU, EW_SILU_BWD, EW_GEGLU, EW_GEGLU_BWD, EW_ADD, EW_RESAMPLE, EW_RESAMPLE_BWD,
  EW_F32_TO_BF16, EW_BF16_TO_F32) = range(10)
 

@@ -72,34 +72,53 @@ struct GemmAux {
 //   K4S2   (Encoder4 Conv2d(k4, s2, p1), openaimodel_enc.py:1002-1009): 4x4 taps at
 //          (2y + ty - 1, 2x + tx - 1) of the (2h, 2w) source;
 //   K4S2_T (its input gradient): 4x4 taps t' = 15 - t at (y + ty' - 2, x + tx' - 2) of the
-//          full-resolution grid, valid only at even coordinates, source pixel = coordinate / 2.
+//          full-resolution grid, valid only at even coordinates, source pixel = coordinate / 2;
+//   K4S2_TP (the same gradient by output parity): the M rows are ordered [parity q][b][y'][x']
+//          over the half-resolution grid, and an output row (b, 2y'+py, 2x'+px), q = 2py+px,
+//          receives only the 2x2 taps ty' = py + 2jy, tx' = px + 2jx: source (y'+py+jy-1,
+//          x'+px+jx-1) of dY, weight tap 15 - (4ty' + tx').  K = 4*cout instead of 16*cout
+//          (K4S2_T multiplies 3 zero taps of every 4).  A tile never straddles parities
+//          (batch*h*w/4 % 128 == 0), so oy, ox and the weight-tap base are per workgroup.
 struct Im2colMode {
-  int sy, oy, lh, lw, sh, hs, ws, par, k4;
+  int sy, oy, ox, lh, lw, sh, hs, ws, par, k4, tb;
   ED_DEV Im2colMode(const EncdiffConvGeom& g) {
     const bool s2 = g.resample == ENCDIFF_RESAMPLE_STRIDE2;  // VQ Downsample: pad (0,1,0,1), k3 s2 p0
     const bool up = g.resample == ENCDIFF_RESAMPLE_UP2;      // nearest x2 (openaimodel_enc.py:116)
     const bool f4 = g.resample == ENCDIFF_RESAMPLE_K4S2;
     const bool t4 = g.resample == ENCDIFF_RESAMPLE_K4S2_T;
+    const bool tp = g.resample == ENCDIFF_RESAMPLE_K4S2_TP;
     sy = (s2 || f4) ? 2 : 1;
     oy = s2 ? 0 : (t4 ? -2 : -1);
-    lh = (s2 || f4) ? 2 * g.h : g.h;
-    lw = (s2 || f4) ? 2 * g.w : g.w;
+    ox = oy;
+    lh = (s2 || f4) ? 2 * g.h : (tp ? g.h >> 1 : g.h);
+    lw = (s2 || f4) ? 2 * g.w : (tp ? g.w >> 1 : g.w);
     sh = (up || t4) ? 1 : 0;
     hs = lh >> sh;
     ws = lw >> sh;
     par = t4 ? 1 : 0;
-    k4 = (f4 || t4) ? 1 : 0;
+    k4 = tp ? 2 : ((f4 || t4) ? 1 : 0);
+    tb = 15;
+  }
+  // K4S2_TP: the workgroup's parity class q = 2py + px
+  ED_DEV void set_parity(int q) {
+    oy = (q >> 1) - 1;
+    ox = (q & 1) - 1;
+    tb = 15 - 4 * (q >> 1) - (q & 1);
+  }
+  // weight tap of im2col tap `tap` for OPB_CONV_DGRAD (flipped kernel)
+  ED_DEV uint32_t wtap(uint32_t tap) const {
+    return k4 == 2 ? (uint32_t)tb - 8u * (tap >> 1) - 2u * (tap & 1u) : (k4 ? 15u : 8u) - tap;
   }
 };
 
-// tap index -> (ty, tx): 3x3 (tap / 3 via a multiply) or 4x4 taps
+// tap index -> (ty, tx): 3x3 (tap / 3 via a multiply), 4x4 or 2x2 taps
 ED_DEV void tap_yx(const Im2colMode& md, uint32_t tap, int& ty, int& tx) {
-  ty = md.k4 ? (int)(tap >> 2) : (int)((tap * 11u) >> 5);
-  tx = (int)tap - (md.k4 ? 4 : 3) * ty;
+  ty = md.k4 ? (int)(tap >> (3 - md.k4)) : (int)((tap * 11u) >> 5);
+  tx = (int)tap - (md.k4 ? (1 << (3 - md.k4)) : 3) * ty;
 }
 
 ED_DEV uint32_t im2col_row(const Im2colMode& md, uint32_t b, int y, int x, int ty, int tx, bool& ok) {
-  const int ys = md.sy * y + ty + md.oy, xs = md.sy * x + tx + md.oy;
+  const int ys = md.sy * y + ty + md.oy, xs = md.sy * x + tx + md.ox;
   ok = (unsigned)ys < (unsigned)md.lh && (unsigned)xs < (unsigned)md.lw && ((ys | xs) & md.par) == 0;
   const uint32_t row = (b * (uint32_t)md.hs + (uint32_t)(ys >> md.sh)) * (uint32_t)md.ws + (uint32_t)(xs >> md.sh);
   return ok ? row : 0u;
@@ -169,7 +188,11 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   const bf16_t* __restrict__ A = (const bf16_t*)p.a;
   const bf16_t* __restrict__ B = (const bf16_t*)p.b;
 
-  const Im2colMode md(p.conv);
+  Im2colMode md(p.conv);
+  // K4S2_TP: rows [parity][b][y'][x'], one parity per tile (host: batch*h*w/4 % 128 == 0)
+  const int tp_q = md.k4 == 2 ? m0 / (p.M >> 2) : 0;
+  const uint32_t mbase = md.k4 == 2 ? (uint32_t)(tp_q * (p.M >> 2)) : 0u;
+  if (md.k4 == 2) md.set_parity(tp_q);
 
   // LDS-DMA staging: every chunk's global address is computed branch-free (masked chunks
   // read g_zero16) and copied straight into the lane-linear LDS image; tile t+1 is in
@@ -196,10 +219,10 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
         } else {  // IM2COL: this row = output pixel, fixed per (thread, i) only when SLOTS == 8
           const uint32_t mm0 = (uint32_t)(m0 + row);
           const bool min = mm0 < (uint32_t)p.M;
-          const uint32_t mm = min ? mm0 : 0u;
+          const uint32_t mm = min ? mm0 - mbase : 0u;
           const uint32_t bb = fdiv(mm, aux.hw);
-          const uint32_t r = mm - bb * (uint32_t)(p.conv.h * p.conv.w);
-          const int y = (int)fdiv(r, aux.w), x = (int)(r - (uint32_t)y * (uint32_t)p.conv.w);
+          const uint32_t r = mm - bb * aux.hw.d;
+          const int y = (int)fdiv(r, aux.w), x = (int)(r - (uint32_t)y * aux.w.d);
           const uint32_t kk = k < p.K ? (uint32_t)k : 0u;
           const uint32_t tap = fdiv(kk, aux.cin);
           const uint32_t ch = kk - tap * (uint32_t)p.conv.cin;
@@ -240,12 +263,12 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
           const uint32_t tap = fdiv(kk, aux.cout);
           const uint32_t co = kk - tap * (uint32_t)p.conv_cout;
           ok = kn;
-          off = (size_t)co * p.ldb + (size_t)((md.k4 ? 15 : 8) - tap) * p.N + (ok ? n : 0);
+          off = (size_t)co * p.ldb + (size_t)md.wtap(tap) * p.N + (ok ? n : 0);
         } else {  // B_IM2COL: row = output pixel k, column n = (tap, ci)
           const uint32_t kk = kn ? (uint32_t)k : 0u;
           const uint32_t bb = fdiv(kk, aux.hw);
-          const uint32_t r = kk - bb * (uint32_t)(p.conv.h * p.conv.w);
-          const int y = (int)fdiv(r, aux.w), x = (int)(r - (uint32_t)y * (uint32_t)p.conv.w);
+          const uint32_t r = kk - bb * aux.hw.d;
+          const int y = (int)fdiv(r, aux.w), x = (int)(r - (uint32_t)y * aux.w.d);
           const uint32_t nn = kn ? (uint32_t)n : 0u;
           const uint32_t tap = fdiv(nn, aux.cin);
           const uint32_t ci = nn - tap * (uint32_t)p.conv.cin;
@@ -418,6 +441,16 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   if (p.split_k > 1 && p.c_mode == ENCDIFF_OUT_F32) {  // split-K slab of this z (workspace path)
     p_c_slab = (float*)p.c + (long)bz * p.M * p.N;
   }
+  // output row of GEMM row `row`: K4S2_TP rows are parity-major, each written to its pixel
+  // (split-K slabs stay in GEMM row order; the finalize maps them)
+  const bool slab_out = p.split_k > 1 && p.c == (void*)p.workspace;
+  auto orow = [&](int row) -> long {
+    if (md.k4 != 2 || slab_out) return row;
+    const uint32_t mm = (uint32_t)row - mbase;
+    const uint32_t b = fdiv(mm, aux.hw), r = mm - b * aux.hw.d;
+    const uint32_t y = fdiv(r, aux.w), x = r - y * aux.w.d;
+    return ((long)b * p.conv.h + 2 * y + (tp_q >> 1)) * p.conv.w + 2 * x + (tp_q & 1);
+  };
   const bool vec = (p.N % 8 == 0) && (p.ldc % 8 == 0) && (((uintptr_t)p.c & 15) == 0) &&
                    (!add_bias || (((uintptr_t)p.bias & 15) == 0)) &&
                    (!R || ((p.ld_resid % 8 == 0) && (((uintptr_t)R & 15) == 0)));
@@ -427,6 +460,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       const int r = e / CPR, c8 = (e - r * CPR) * 8;
       const int row = m0 + r, col = n0 + c8;
       if (row >= p.M || col >= p.N) continue;
+      const long ro = orow(row);
       float v[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = p.alpha * sc[r * SLD + c8 + k];
@@ -437,14 +471,14 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       }
       if (R) {
         float rr[8];
-        unpack8(*(const uint4*)(R + (long)row * p.ld_resid + col), rr);
+        unpack8(*(const uint4*)(R + ro * p.ld_resid + col), rr);
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] += rr[k];
       }
       if (p.c_mode == ENCDIFF_OUT_BF16) {
-        *(uint4*)((bf16_t*)p.c + (long)row * p.ldc + col) = pack8(v);
+        *(uint4*)((bf16_t*)p.c + ro * p.ldc + col) = pack8(v);
       } else {
-        float* cp = p_c_slab + (long)row * p.ldc + col;
+        float* cp = p_c_slab + ro * p.ldc + col;
         if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) {
           const float4 c0 = *(const float4*)cp, c1 = *(const float4*)(cp + 4);
           v[0] += c0.x; v[1] += c0.y; v[2] += c0.z; v[3] += c0.w;
@@ -459,11 +493,12 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       const int r = e / BN, cc = e - r * BN;
       const int row = m0 + r, col = n0 + cc;
       if (row >= p.M || col >= p.N) continue;
+      const long ro = orow(row);
       float v = p.alpha * sc[r * SLD + cc] + (add_bias ? p.bias[col] : 0.f);
-      if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
-      if (p.c_mode == ENCDIFF_OUT_BF16) ((bf16_t*)p.c)[(long)row * p.ldc + col] = f2bf(v);
-      else if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) p_c_slab[(long)row * p.ldc + col] += v;
-      else p_c_slab[(long)row * p.ldc + col] = v;
+      if (R) v += bf2f(R[ro * p.ld_resid + col]);
+      if (p.c_mode == ENCDIFF_OUT_BF16) ((bf16_t*)p.c)[ro * p.ldc + col] = f2bf(v);
+      else if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) p_c_slab[ro * p.ldc + col] += v;
+      else p_c_slab[ro * p.ldc + col] = v;
     }
   }
 }
@@ -519,8 +554,18 @@ __host__ __device__ inline int fin_per_block(const EncdiffGemmArgs& p) {
   return (fin_vec(p) ? 4 : 1) * 256 / fin_zgroups(p);
 }
 
+// output row of GEMM row m (K4S2_TP: parity-major rows -> their pixel; plain division, the
+// finalize is not on a hot path)
+__device__ __forceinline__ long fin_row(const EncdiffGemmArgs& p, int m) {
+  if (p.a_mode != ENCDIFF_OPA_IM2COL || p.conv.resample != ENCDIFF_RESAMPLE_K4S2_TP) return m;
+  const int mq = p.M >> 2, q = m / mq, hh = p.conv.h >> 1, wh = p.conv.w >> 1;
+  const int mm = m - q * mq, b = mm / (hh * wh), r = mm - b * hh * wh, y = r / wh, x = r - y * wh;
+  return ((long)b * p.conv.h + 2 * y + (q >> 1)) * p.conv.w + 2 * x + (q & 1);
+}
+
 __device__ __forceinline__ void fin_store(const EncdiffGemmArgs& p, const bf16_t* R, const long i, float v) {
-  const int row = (int)(i / p.N), col = (int)(i - (long)row * p.N);
+  const int row0 = (int)(i / p.N), col = (int)(i - (long)row0 * p.N);
+  const long row = fin_row(p, row0);
   v *= p.alpha;
   if (p.bias) v += p.bias[col];
   if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
@@ -561,7 +606,8 @@ __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const in
         }
       }
       if (zg == 0 && i < total) {
-        const int row = (int)(i / p.N), col = (int)(i - (long)row * p.N);  // N % 4 == 0: one row
+        const int row0 = (int)(i / p.N), col = (int)(i - (long)row0 * p.N);  // N % 4 == 0: one row
+        const long row = fin_row(p, row0);
         float v[4] = {p.alpha * acc.x, p.alpha * acc.y, p.alpha * acc.z, p.alpha * acc.w};
         if (p.bias) {
 #pragma unroll
@@ -707,6 +753,13 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
   if (im2col && ((long)p.conv.batch * p.conv.h * p.conv.w >= (1L << 24) || p.conv.h * p.conv.w >= (1 << 16)))
     return ENCDIFF_ERR_SHAPE;
   if (im2col && p.conv.resample == ENCDIFF_RESAMPLE_DOWN2) return ENCDIFF_ERR_UNSUPPORTED;
+  if (im2col && p.conv.resample == ENCDIFF_RESAMPLE_K4S2_TP) {  // parity-major rows, one parity per tile
+    if (p.a_mode != ENCDIFF_OPA_IM2COL || p.b_mode != ENCDIFF_OPB_CONV_DGRAD) return ENCDIFF_ERR_UNSUPPORTED;
+    if ((p.conv.h | p.conv.w) & 1 || (long)p.M != (long)p.conv.batch * p.conv.h * p.conv.w ||
+        (p.M >> 2) % 128 || p.K != 4 * p.conv.cin)
+      return ENCDIFF_ERR_SHAPE;
+    if (p.c_mode == ENCDIFF_OUT_F32_ATOMIC || p.c_mode == ENCDIFF_OUT_F32_ATOMIC_CONVW) return ENCDIFF_ERR_UNSUPPORTED;
+  }
   if (p.K >= (1 << 24)) return ENCDIFF_ERR_SHAPE;
   if (p.bias_grad && p.a_mode != ENCDIFF_OPA_ROWM) return ENCDIFF_ERR_ARG;
   g.tile = p.tile ? p.tile : pick_tile(p);
@@ -719,8 +772,9 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
   g.p = p;
   g.aux.cin = make_fdiv(p.conv.cin);
   g.aux.cout = make_fdiv(p.conv_cout);
-  g.aux.hw = make_fdiv(p.conv.h * p.conv.w);
-  g.aux.w = make_fdiv(p.conv.w);
+  const bool tp = im2col && p.conv.resample == ENCDIFF_RESAMPLE_K4S2_TP;
+  g.aux.hw = make_fdiv(tp ? (p.conv.h >> 1) * (p.conv.w >> 1) : p.conv.h * p.conv.w);  // output grid
+  g.aux.w = make_fdiv(tp ? p.conv.w >> 1 : p.conv.w);
   return ENCDIFF_OK;
 }
 

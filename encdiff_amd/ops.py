@@ -319,6 +319,9 @@ def conv4x4s2_fwd(x, g_out: Geom, cin, wf, out, bias=None):
                          ld_src=_ld(x)), bias=bias)
 
 
+K4S2_PARITY = True  # tests: False forces the 16-tap K4S2_T input gradient
+
+
 def conv4x4s2_bwd_cl(dy, g_out: Geom, wf, x, cin, dw_cl, dx, db=None):
     """Backward of Conv2d(k4, s2, p1): dw_cl[cout][16*cin] += dy^T im2col(x) (+ db) and
     dx (2h, 2w) = transposed conv of dy, one paired launch."""
@@ -330,10 +333,15 @@ def conv4x4s2_bwd_cl(dy, g_out: Geom, wf, x, cin, dw_cl, dx, db=None):
                          conv=L.ConvGeom(batch=g_out.batch, h=g_out.h, w=g_out.w, cin=cin,
                                          resample=L.RESAMPLE_K4S2, ld_src=_ld(x)), bias_grad=db, ws_offset=off)
 
+    # by output parity (2x2 taps each, K = 4*cout) when a GEMM tile never straddles two
+    # parity classes, else all 16 taps with 3 of 4 masked
+    tp = K4S2_PARITY and (gin.pixels // 4) % 128 == 0
+
     def dargs(off):
-        return gemm_args(gin.pixels, cin, 16 * cout, dy, _ld(dy), wf, _ld(wf), dx, _ld(dx), a_mode=L.OPA_IM2COL,
-                         b_mode=L.OPB_CONV_DGRAD, conv=L.ConvGeom(batch=gin.batch, h=gin.h, w=gin.w, cin=cout,
-                                                                  resample=L.RESAMPLE_K4S2_T, ld_src=_ld(dy)),
+        return gemm_args(gin.pixels, cin, (4 if tp else 16) * cout, dy, _ld(dy), wf, _ld(wf), dx, _ld(dx),
+                         a_mode=L.OPA_IM2COL, b_mode=L.OPB_CONV_DGRAD,
+                         conv=L.ConvGeom(batch=gin.batch, h=gin.h, w=gin.w, cin=cout,
+                                         resample=L.RESAMPLE_K4S2_TP if tp else L.RESAMPLE_K4S2_T, ld_src=_ld(dy)),
                          conv_cout=cout, ws_offset=off)
     gemm_pair(wargs, dargs)
 

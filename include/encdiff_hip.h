@@ -71,8 +71,12 @@ enum {
                                   only: F.pad(x,(0,1,0,1)) + Conv2d(k3, s2, p0) (model.py Downsample) */
   ENCDIFF_RESAMPLE_K4S2 = 4,   /* source is (2h,2w); 4x4 taps (K = 16*cin) at (2y+ky-1, 2x+kx-1):
                                   Conv2d(k4, s2, p1) of Encoder4 (openaimodel_enc.py:1002-1009)   */
-  ENCDIFF_RESAMPLE_K4S2_T = 5  /* input gradient of K4S2: source dY is (h/2,w/2); with
+  ENCDIFF_RESAMPLE_K4S2_T = 5, /* input gradient of K4S2: source dY is (h/2,w/2); with
                                   OPB_CONV_DGRAD (16 taps, flipped) computes dX at (h,w)          */
+  ENCDIFF_RESAMPLE_K4S2_TP = 6 /* the same input gradient by output parity: K = 4*cin (the 2x2 taps
+                                  that reach each parity class of (y, x)), M = batch*h*w with
+                                  batch*h*w/4 % 128 == 0; rows are computed parity-major and
+                                  written to their pixel.  OPB_CONV_DGRAD only, no atomic c_mode  */
 };
 
 typedef struct EncdiffConvGeom {

@@ -592,10 +592,12 @@ def Geom_(B, H):
     return Geom(B, H, H)
 
 
+@pytest.mark.parametrize("parity", [True, False])
 @pytest.mark.parametrize("Hout,cin,cout", [(32, 8, 128), (16, 128, 128), (4, 128, 128)])
-def test_conv4x4s2(O, Hout, cin, cout):
-    """Conv2d(k4, s2, p1) forward, input gradient (transposed im2col mode) and weight gradient
-    vs torch fp32 on the same bf16 operands."""
+def test_conv4x4s2(O, Hout, cin, cout, parity):
+    """Conv2d(k4, s2, p1) forward, input gradient (transposed im2col mode: by output parity,
+    K4S2_TP, or all 16 taps, K4S2_T) and weight gradient vs torch fp32 on the same bf16
+    operands; the parity mode also with split-K slabs (rows remapped by the finalize)."""
     torch.manual_seed(6)
     B = 8
     g = Geom_(B, Hout)
@@ -613,12 +615,24 @@ def test_conv4x4s2(O, Hout, cin, cout):
     dw = torch.zeros(cout, 16 * cin, device=dev)
     db = torch.zeros(cout, device=dev)
     dx = torch.empty(gi.pixels, cin, device=dev, dtype=torch.bfloat16)
-    O.conv4x4s2_bwd_cl(dy, g, wf, x, cin, dw, dx, db)
+    O.K4S2_PARITY = parity
+    try:
+        O.conv4x4s2_bwd_cl(dy, g, wf, x, cin, dw, dx, db)
+    finally:
+        O.K4S2_PARITY = True
     O.flush()
     xr = nhwc(x, gi).requires_grad_(True)
     wrr = wr.clone().requires_grad_(True)
     F.conv2d(xr, wrr, None, stride=2, padding=1).backward(nhwc(dy, g))
     assert rel(nhwc(dx, gi), xr.grad) < 1e-2
+    if parity:
+        import encdiff_amd._lib as L
+        dx2 = torch.empty_like(dx)
+        O.gemm(gi.pixels, cin, 4 * cout, dy, cout, wf, 16 * cin, dx2, cin, a_mode=L.OPA_IM2COL,
+               b_mode=L.OPB_CONV_DGRAD, conv=L.ConvGeom(batch=B, h=gi.h, w=gi.w, cin=cout,
+                                                        resample=L.RESAMPLE_K4S2_TP, ld_src=cout),
+               conv_cout=cout, split_k=3, tile=4)
+        assert rel(nhwc(dx2, gi), xr.grad) < 1e-2
     assert rel(dw.view(cout, 4, 4, cin).permute(0, 3, 1, 2), wrr.grad) < 2e-3
     assert rel(db, dy.float().sum(0)) < 2e-3
 
