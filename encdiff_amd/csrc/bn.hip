@@ -13,10 +13,10 @@
 namespace {
 
 constexpr int BN_T = 256;
-constexpr int BN_MAXBLK = 128;  // workgroups of a reduction (pixel ranges)
+constexpr int BN_MAXBLK = 256;  // workgroups of a reduction (pixel ranges of >= 256 rows)
 
 __device__ __host__ inline int bn_blocks(int rows) {
-  const int b = (rows + 127) / 128;
+  const int b = (rows + 255) / 256;
   return b < BN_MAXBLK ? b : BN_MAXBLK;
 }
 
@@ -54,41 +54,50 @@ ED_DEV void bn_block_partial(const float (&q)[NQ][8], const BnLayout& L, int c, 
   }
 }
 
-// fold the per-workgroup partials [nblk][2][c] in a fixed order (fp64): thread t sums
-// channel t % c over blocks t / c, t / c + S, ... (S = 256 / c), then the S partial sums
-// of a channel are added in order through LDS.  Result out[2][c].
+// fold the per-workgroup partials [nblk][2][c] in a fixed order (fp64): the 2c values of a
+// block are c/2 float4 groups; thread t owns group t % (c/2) and sums blocks t / (c/2),
+// + J, ... (J = 256 / (c/2) block lanes, 8 loads in flight), then the J lane sums of each
+// value are added in lane order through LDS.  Result out[2][c].
 ED_DEV void bn_fold(const float* part, int nblk, int c, double* out) {
-  __shared__ double fold[2][BN_T];
-  const int S = BN_T / c, ch = threadIdx.x % c, j = threadIdx.x / c;
-  double s0 = 0.0, s1 = 0.0;
-  if (j < S) {
-#pragma unroll 4
-    for (int b = j; b < nblk; b += S) {
-      s0 += part[(long)b * 2 * c + ch];
-      s1 += part[(long)b * 2 * c + c + ch];
-    }
+  __shared__ double fold[4 * BN_T];  // [J][2c]: J * 2c == 4 * 256
+  const int V4 = c >> 1, J = BN_T / V4;
+  const int g = threadIdx.x % V4, j = threadIdx.x / V4;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll 8
+  for (int b = j; b < nblk; b += J) {
+    const float4 v = *(const float4*)(part + (long)b * 2 * c + 4 * g);
+    a0 += v.x; a1 += v.y; a2 += v.z; a3 += v.w;
   }
-  fold[0][threadIdx.x] = s0;
-  fold[1][threadIdx.x] = s1;
+  double* f = fold + j * 2 * c + 4 * g;
+  f[0] = a0; f[1] = a1; f[2] = a2; f[3] = a3;
   __syncthreads();
-  if (threadIdx.x < c) {
-    double a0 = 0.0, a1 = 0.0;
-    for (int k = 0; k < S; ++k) { a0 += fold[0][k * c + threadIdx.x]; a1 += fold[1][k * c + threadIdx.x]; }
-    out[threadIdx.x] = a0;
-    out[c + threadIdx.x] = a1;
+  for (int e = threadIdx.x; e < 2 * c; e += BN_T) {
+    double t = 0.0;
+    for (int k = 0; k < J; ++k) t += fold[k * 2 * c + e];
+    out[e] = t;
   }
   __syncthreads();
 }
 
-// true in exactly one workgroup: the last to arrive (after its partials are visible)
+// true in exactly one workgroup: the last to arrive, after every workgroup's partials are
+// visible to it (cdna_hip_programming.md in-launch reduction recipe: stores drained, one
+// agent-scope release by lane 0 before the ticket, one acquire in the last arriver)
 ED_DEV bool bn_last_block(unsigned int* counter) {
-  __shared__ bool last;
-  __threadfence();
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(counter, 1u) == gridDim.x - 1;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
   __syncthreads();
-  if (last) __threadfence();
-  return last;
+  return last != 0;
 }
 
 __global__ __launch_bounds__(BN_T) void bn_stats_kernel(const EncdiffBatchNormArgs p) {
@@ -100,6 +109,7 @@ __global__ __launch_bounds__(BN_T) void bn_stats_kernel(const EncdiffBatchNormAr
 #pragma unroll
   for (int i = 0; i < 8; ++i) q[0][i] = q[1][i] = 0.f;
   if (L.pl < L.lanes) {
+#pragma unroll 4
     for (int r = r0 + L.pl; r < r1; r += L.lanes) {
       float x[8];
       unpack8(*(const uint4*)(X + (long)r * p.ldx + L.v * 8), x);
@@ -167,6 +177,7 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const EncdiffBatchN
     ld8f(p.rstd + cb, rs);
     ld8f(p.gamma + cb, ga);
     ld8f(p.beta + cb, be);
+#pragma unroll 4
     for (int r = r0 + L.pl; r < r1; r += L.lanes) {
       float x[8], d[8];
       unpack8(*(const uint4*)(X + (long)r * p.ldx + cb), x);
