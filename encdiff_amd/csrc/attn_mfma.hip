@@ -24,27 +24,54 @@ ED_DEV s4 pack4(float a, float b, float c, float d) {
   return __builtin_bit_cast(s4, u);
 }
 
-// stage rows [n][dh] of a head from a [rows][ld] tensor into LDS row-major [np][DP]
-// (and optionally transposed [DP][np]); zero padding for rows >= n and dims >= dh.
-// Transposed copies use a row stride of np + 8 elements (16 B of padding): the MFMA operand
-// reads take 16 consecutive rows per instruction, which an unpadded power-of-two stride
-// would put in the same LDS banks (16-way conflicts).
-template <int DH, int DP>
-ED_DEV void stage_rows(const bf16_t* __restrict__ src, long ld, int n, int np, bf16_t* rm, bf16_t* tr, int tid,
-                       int nthr) {
-  const int tld = np + 8;
-  constexpr int CH = DP / 8;  // 16-byte chunks per padded row
-  for (int e = tid; e < np * CH; e += nthr) {
-    const int r = e / CH, c8 = (e - r * CH) * 8;
-    uint4 v = {0u, 0u, 0u, 0u};
-    if (r < n && c8 < DH) v = *(const uint4*)(src + (long)r * ld + c8);
-    *(uint4*)(rm + r * DP + c8) = v;
-    if (tr) {
-      const bf16_t* h = (const bf16_t*)&v;
+// Transposed LDS copies use a row stride of rows + 8 elements (16 B of padding): the MFMA
+// operand reads take 16 consecutive rows per instruction, which an unpadded power-of-two
+// stride would put in the same LDS banks (16-way conflicts).
+// Stage one tensor (rows [S][DH] of head h of image b, row stride ld) for the hpb heads
+// bh0 .. bh0+hpb-1 of the workgroup into LDS row-major [SP][DP] per head (rm + hl * rm_hs)
+// and optionally transposed [DP][SP + 8] (tr + hl * tr_hs); zero padding.  Loads are issued U
+// at a time before their LDS writes: the staging of a small head used to be one dependent
+// global round trip per 16-byte chunk per thread (the latency of the short launches).
+template <int DH, int DP, int U>
+ED_DEV void stage_heads_u(const bf16_t* __restrict__ base, long ld, int S, int SP, int H, int bh0, int hpb,
+                          bf16_t* rm, int rm_hs, bf16_t* tr, int tr_hs) {
+  constexpr int CH = DP / 8;
+  const int ph = SP * CH, total = hpb * ph, tld = SP + 8;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * U) {
+    uint4 v[U];
+    int hl[U], r[U], c8[U];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) tr[(c8 + k) * tld + r] = h[k];
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * 256;
+      hl[u] = hpb == 1 ? 0 : e / ph;
+      const int t = e - hl[u] * ph;
+      r[u] = t / CH;
+      c8[u] = (t - r[u] * CH) * 8;
+      v[u] = (uint4){0u, 0u, 0u, 0u};
+      if (e < total && r[u] < S && c8[u] < DH) {
+        const int bh = bh0 + hl[u], b = bh / H, h = bh - b * H;
+        v[u] = *(const uint4*)(base + ((long)b * S + r[u]) * ld + h * DH + c8[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (e0 + u * 256 >= total) break;
+      if (rm) *(uint4*)(rm + hl[u] * rm_hs + r[u] * DP + c8[u]) = v[u];
+      if (tr) {
+        const bf16_t* hv = (const bf16_t*)&v[u];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) tr[hl[u] * tr_hs + (c8[u] + k) * tld + r[u]] = hv[k];
+      }
     }
   }
+}
+template <int DH, int DP>
+ED_DEV void stage_heads(const bf16_t* __restrict__ base, long ld, int S, int SP, int H, int bh0, int hpb,
+                        bf16_t* rm, int rm_hs, bf16_t* tr, int tr_hs) {
+  // several heads (short sequences): 4 chunks per thread in flight; one long head: the
+  // plain loop measured faster (fewer live registers in the 2-workgroup-per-CU kernels)
+  if (hpb > 1) stage_heads_u<DH, DP, 4>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs, tr, tr_hs);
+  else stage_heads_u<DH, DP, 1>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs, tr, tr_hs);
 }
 
 constexpr float LOG2E = 1.4426950408889634f;
@@ -70,20 +97,8 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
   const int bh0 = blockIdx.x * hpb;
   bf16_t* Ks = sm;                        // [hpb][SKP][DP]
   bf16_t* Vt = sm + hpb * SKP * DP;       // [hpb][DP][TK] (padded rows)
-  for (int hl = 0; hl < hpb; ++hl) {
-    const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
-    stage_rows<DH, DP>((const bf16_t*)p.k + (long)b * SK * p.ldk + h * DH, p.ldk, SK, SKP, Ks + hl * SKP * DP,
-                       nullptr, tid, 256);
-    constexpr int CH = DP / 8;
-    for (int e = tid; e < SKP * CH; e += 256) {
-      const int r = e / CH, c8 = (e - r * CH) * 8;
-      uint4 v = {0u, 0u, 0u, 0u};
-      if (r < SK && c8 < DH) v = *(const uint4*)((const bf16_t*)p.v + ((long)b * SK + r) * p.ldv + h * DH + c8);
-      const bf16_t* hv = (const bf16_t*)&v;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) Vt[hl * DP * TK + (c8 + k) * TK + r] = hv[k];
-    }
-  }
+  stage_heads<DH, DP>((const bf16_t*)p.k, p.ldk, SK, SKP, H, bh0, hpb, Ks, SKP * DP, nullptr, 0);
+  stage_heads<DH, DP>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, nullptr, 0, Vt, DP * TK);
   __syncthreads();
   const int qtiles = (SQ + 15) >> 4, npairs = (qtiles + 1) >> 1;
   const float sl2 = p.scale * LOG2E;
@@ -204,33 +219,40 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
   const int qtiles = SQP >> 4, ktiles = SKP >> 4;
   const int QS = attn_qsplit(ktiles, hpb);
   float* red = fls + hpb * 2 * SQP;  // phase-A partials [task][2][16*DP lanes-major] when QS > 1
-  for (int hl = 0; hl < hpb; ++hl) {
-    const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
-    bf16_t* base = sm + hl * per_head;
-    stage_rows<DH, DP>((const bf16_t*)p.q + (long)b * SQ * p.ldq + h * DH, p.ldq, SQ, SQP, base, base + oQt, tid,
-                       256);
-    stage_rows<DH, DP>((const bf16_t*)p.d_o + (long)b * SQ * p.lddo + h * DH, p.lddo, SQ, SQP, base + oG,
-                       base + oGt, tid, 256);
-    stage_rows<DH, DP>((const bf16_t*)p.k + (long)b * SK * p.ldk + h * DH, p.ldk, SK, SKP, base + oK, base + oKt,
-                       tid, 256);
-    stage_rows<DH, DP>((const bf16_t*)p.v + (long)b * SK * p.ldv + h * DH, p.ldv, SK, SKP, base + oV, nullptr,
-                       tid, 256);
-    for (int q = tid; q < SQP; q += 256) {
-      float lse = 0.f, D = 0.f;
-      if (q < SQ) {
-        lse = p.lse[(long)bh * SQ + q] * LOG2E;
+  stage_heads<DH, DP>((const bf16_t*)p.q, p.ldq, SQ, SQP, H, bh0, hpb, sm, per_head, sm + oQt, per_head);
+  stage_heads<DH, DP>((const bf16_t*)p.d_o, p.lddo, SQ, SQP, H, bh0, hpb, sm + oG, per_head, sm + oGt, per_head);
+  stage_heads<DH, DP>((const bf16_t*)p.k, p.ldk, SK, SKP, H, bh0, hpb, sm + oK, per_head, sm + oKt, per_head);
+  stage_heads<DH, DP>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, sm + oV, per_head, nullptr, 0);
+  // lse (log2 domain) and D = rowsum(dO * O) per query: 4 rows per thread in flight
+  for (int e0 = tid; e0 < hpb * SQP; e0 += 256 * 4) {
+    float lse[4], D[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * 256, hl = e / SQP, q = e - hl * SQP;
+      lse[u] = 0.f;
+      D[u] = 0.f;
+      if (e < hpb * SQP && q < SQ) {
+        const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
+        lse[u] = p.lse[(long)bh * SQ + q] * LOG2E;
         const bf16_t* op = (const bf16_t*)p.o + ((long)b * SQ + q) * p.ldo + h * DH;
         const bf16_t* gp = (const bf16_t*)p.d_o + ((long)b * SQ + q) * p.lddo + h * DH;
+#pragma unroll
         for (int d = 0; d < DH; d += 8) {
           float a[8], c[8];
           unpack8(*(const uint4*)(op + d), a);
           unpack8(*(const uint4*)(gp + d), c);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) D += a[k] * c[k];
+          for (int k = 0; k < 8; ++k) D[u] += a[k] * c[k];
         }
       }
-      fls[hl * 2 * SQP + q] = lse;
-      fls[hl * 2 * SQP + SQP + q] = D;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * 256, hl = e / SQP, q = e - hl * SQP;
+      if (e < hpb * SQP) {
+        fls[hl * 2 * SQP + q] = lse[u];
+        fls[hl * 2 * SQP + SQP + q] = D[u];
+      }
     }
   }
   __syncthreads();
