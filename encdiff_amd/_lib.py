@@ -17,7 +17,8 @@ LIB_PATH = os.environ.get("ENCDIFF_LIB", os.path.join(HERE, "libencdiff_hip.so")
 # enums (mirror include/encdiff_hip.h)
 OPA_ROWK, OPA_IM2COL, OPA_ROWM = 0, 1, 2
 OPB_ROWK, OPB_ROWN, OPB_CONV_DGRAD, OPB_IM2COL = 0, 1, 2, 3
-OUT_BF16, OUT_F32, OUT_F32_ATOMIC, OUT_F32_ATOMIC_CONVW, OUT_F32_ACCUM = 0, 1, 2, 3, 4
+OUT_BF16, OUT_F32, OUT_F32_ATOMIC, OUT_F32_ATOMIC_CONVW, OUT_F32_ACCUM, OUT_BF16_GEGLU, OUT_BF16_GEGLU_BWD = \
+    0, 1, 2, 3, 4, 5, 6
 RESAMPLE_NONE, RESAMPLE_DOWN2, RESAMPLE_UP2, RESAMPLE_STRIDE2, RESAMPLE_K4S2, RESAMPLE_K4S2_T, RESAMPLE_K4S2_TP = \
     0, 1, 2, 3, 4, 5, 6
 (EW_COPY, EW_SILU, EW_SILU_BWD, EW_GEGLU, EW_GEGLU_BWD, EW_ADD, EW_RESAMPLE, EW_RESAMPLE_BWD,
@@ -38,7 +39,8 @@ class GemmArgs(C.Structure):
                 ("conv", ConvGeom), ("conv_cout", C.c_int), ("convw_cin", C.c_int),
                 ("alpha", C.c_float), ("split_k", C.c_int),
                 ("bias", vp), ("resid", vp), ("ld_resid", C.c_long), ("bias_grad", vp),
-                ("tile", C.c_int), ("pad2_", C.c_int), ("workspace", vp)]
+                ("tile", C.c_int), ("pad2_", C.c_int), ("workspace", vp),
+                ("aux", vp), ("ld_aux", C.c_long)]
 
 
 class GroupNormArgs(C.Structure):

@@ -45,6 +45,15 @@ ED_DEV uint4 pack8(const float* f) {
   return u;
 }
 
+// exact (erf) GELU, F.gelu's default (attention.py GEGLU)
+ED_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+ED_DEV float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+ED_DEV float bf16_round(float x) { return bf2f(f2bf(x)); }
+
 // sigmoid via the hardware reciprocal (v_rcp_f32, 1 ulp): results are rounded to bf16
 ED_DEV float sigmoid_f(float z) { return __builtin_amdgcn_rcpf(1.0f + __expf(-z)); }
 ED_DEV float silu_f(float z) { return z * sigmoid_f(z); }

@@ -6,12 +6,6 @@
 
 namespace {
 
-ED_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-ED_DEV float gelu_erf_grad(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
 
 // One thread per 8 contiguous output elements of a row ([rows][cols], cols % 8 == 0).
 __global__ __launch_bounds__(256) void ew_kernel(const EncdiffEwArgs p) {

@@ -199,6 +199,12 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   // flight while tile t is multiplied (depth-1 prefetch, no staging VGPRs).
   typedef __attribute__((address_space(3))) void lds_void;
   typedef __attribute__((address_space(1))) const void gbl_void;
+  // GEGLU proj (OUT_BF16_GEGLU): tile column c < BN/2 is value column by*BN/2 + c of f, the
+  // rest gate column N/2 + by*BN/2 + c - BN/2, so one tile holds both halves of its outputs
+  const bool gfwd = p.c_mode == ENCDIFF_OUT_BF16_GEGLU;
+  auto gcol = [&](int c) -> int {
+    return c < BN / 2 ? by * (BN / 2) + c : (p.N >> 1) + by * (BN / 2) + c - BN / 2;
+  };
   auto stage = [&](bf16_t* s, int kt) {
     const int k0 = kt * BK;
     bf16_t* sa = s;
@@ -249,7 +255,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       bool ok;
       size_t off;
       if constexpr (BKI) {  // B_ROWK: Bt[n][k], row = n
-        const int n = n0 + row, k = k0 + gs * 8;
+        const int n = gfwd ? gcol(row) : n0 + row, k = k0 + gs * 8;
         ok = n < p.N && k < p.K;
         off = (size_t)(ok ? n : 0) * p.ldb + (ok ? k : 0);
       } else {  // k-outer: row = k, chunk = 8 columns of n
@@ -440,6 +446,49 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   }
   if (p.split_k > 1 && p.c_mode == ENCDIFF_OUT_F32) {  // split-K slab of this z (workspace path)
     p_c_slab = (float*)p.c + (long)bz * p.M * p.N;
+  }
+  if (p.c_mode == ENCDIFF_OUT_BF16_GEGLU) {  // f (both halves) and y = value * gelu(gate)
+    constexpr int H2 = BN / 2, CPH = H2 / 8;
+    for (int e = tid; e < BM * CPH; e += 256) {
+      const int r = e / CPH, c8 = (e - r * CPH) * 8, row = m0 + r;
+      if (row >= p.M) continue;
+      const int jv = gcol(c8), jg = gcol(c8 + H2);
+      float a[8], g[8], y[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        a[k] = p.alpha * sc[r * SLD + c8 + k] + (p.bias ? p.bias[jv + k] : 0.f);
+        g[k] = p.alpha * sc[r * SLD + H2 + c8 + k] + (p.bias ? p.bias[jg + k] : 0.f);
+      }
+      bf16_t* F = (bf16_t*)p.c + (long)row * p.ldc;
+      *(uint4*)(F + jv) = pack8(a);
+      *(uint4*)(F + jg) = pack8(g);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) y[k] = bf16_round(a[k]) * gelu_erf(bf16_round(g[k]));  // from the stored f
+      *(uint4*)((bf16_t*)p.aux + (long)row * p.ld_aux + jv) = pack8(y);
+    }
+    return;
+  }
+  if (p.c_mode == ENCDIFF_OUT_BF16_GEGLU_BWD) {  // dy tile -> d(value), d(gate) from f
+    constexpr int CPR = BN / 8;
+    for (int e = tid; e < BM * CPR; e += 256) {
+      const int r = e / CPR, c8 = (e - r * CPR) * 8;
+      const int row = m0 + r, col = n0 + c8;
+      if (row >= p.M || col >= p.N) continue;
+      const bf16_t* F = (const bf16_t*)p.aux + (long)row * p.ld_aux;
+      float a[8], g[8], da[8], dg[8];
+      unpack8(*(const uint4*)(F + col), a);
+      unpack8(*(const uint4*)(F + p.N + col), g);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = bf16_round(p.alpha * sc[r * SLD + c8 + k]);  // dy as the unfused path stores it
+        da[k] = d * gelu_erf(g[k]);
+        dg[k] = d * a[k] * gelu_erf_grad(g[k]);
+      }
+      bf16_t* D = (bf16_t*)p.c + (long)row * p.ldc;
+      *(uint4*)(D + col) = pack8(da);
+      *(uint4*)(D + p.N + col) = pack8(dg);
+    }
+    return;
   }
   // output row of GEMM row `row`: K4S2_TP rows are parity-major, each written to its pixel
   // (split-K slabs stay in GEMM row order; the finalize maps them)
@@ -762,6 +811,11 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
   }
   if (p.K >= (1 << 24)) return ENCDIFF_ERR_SHAPE;
   if (p.bias_grad && p.a_mode != ENCDIFF_OPA_ROWM) return ENCDIFF_ERR_ARG;
+  if (p.c_mode == ENCDIFF_OUT_BF16_GEGLU || p.c_mode == ENCDIFF_OUT_BF16_GEGLU_BWD) {
+    const bool fwd = p.c_mode == ENCDIFF_OUT_BF16_GEGLU;
+    if (!p.aux || p.resid || p.split_k != 1 || p.N % 8 || p.ldc % 8 || p.ld_aux % 8) return ENCDIFF_ERR_ARG;
+    if (fwd && (p.a_mode != ENCDIFF_OPA_ROWK || p.b_mode != ENCDIFF_OPB_ROWK || p.N % 128)) return ENCDIFF_ERR_ARG;
+  }
   g.tile = p.tile ? p.tile : pick_tile(p);
   g.user = p;
   g.ws_path = ws_path;

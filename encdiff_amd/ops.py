@@ -121,7 +121,7 @@ def plan(M, N, K, a_mode, b_mode, c_mode, resample=0):
 
 def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK, c_mode=L.OUT_BF16,
               conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=None, bias=None,
-              resid=None, ld_resid=0, bias_grad=None, tile=0, ws_offset=0):
+              resid=None, ld_resid=0, bias_grad=None, tile=0, ws_offset=0, aux=None, ld_aux=0):
     """EncdiffGemmArgs with the measured (tile, split) plan; split-K slabs start `ws_offset`
     floats into this stream's workspace."""
     if split_k is None or tile == 0:
@@ -138,7 +138,7 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
                       conv=conv if conv is not None else L.ConvGeom(),
                       conv_cout=conv_cout, convw_cin=convw_cin, alpha=alpha, split_k=split_k,
                       bias=_p(bias), resid=_p(resid), ld_resid=ld_resid, bias_grad=_p(bias_grad), tile=tile,
-                      workspace=None if ws is None else ws.data_ptr() + 4 * ws_offset)
+                      workspace=None if ws is None else ws.data_ptr() + 4 * ws_offset, aux=_p(aux), ld_aux=ld_aux)
 
 
 def ws_floats(args) -> int:
@@ -250,6 +250,40 @@ def linear_wgrad(dy, x, dw, db=None):
 def linear_bwd(dy, w, x, dx, dw, db=None, resid=None):
     """Backward of one linear layer: dw += dy^T x (+ db), dx = dy w (+ resid), one launch."""
     gemm_pair(lambda off: linear_wgrad_args(dy, x, dw, db, off), lambda off: linear_dgrad_args(dy, w, dx, resid, off))
+
+
+# GEGLU feed-forward (attention.py GEGLU / FeedForward): the activation runs in the GEMM
+# epilogues -- the proj GEMM writes f and y = f_value * gelu(f_gate); the next layer's input
+# gradient GEMM turns its dy tile into df.  ENCDIFF_GEGLU_FUSED=0: separate ew launches.
+GEGLU_FUSED = os.environ.get("ENCDIFF_GEGLU_FUSED", "1") != "0"
+
+
+def linear_fwd_geglu(x, w, f, y, bias=None):
+    """f[M][2I] = x w^T (+bias); y[M][I] = f[:, :I] * gelu(f[:, I:])."""
+    M, K = x.shape
+    N = w.shape[0]
+    if not GEGLU_FUSED or N % 128:
+        linear_fwd(x, w, f, bias=bias)
+        geglu_fwd(f, y)
+        return
+    gemm(M, N, K, x, _ld(x), w, _ld(w), f, _ld(f), c_mode=L.OUT_BF16_GEGLU, bias=bias, split_k=1, aux=y,
+         ld_aux=_ld(y))
+
+
+def linear_bwd_geglu(dy, w, a, f, df, dw, db=None, d_a=None):
+    """Backward of y2 = Linear(GEGLU(f)): dw += dy^T a (+ db) and df = GEGLU'(f) * (dy w), the
+    GEGLU backward in the input-gradient GEMM's epilogue (d_a: scratch of the unfused path)."""
+    if not GEGLU_FUSED or 2 * w.shape[1] % 128:
+        linear_bwd(dy, w, a, d_a, dw, db)
+        geglu_bwd(f, d_a, df)
+        return
+    M = dy.shape[0]
+    inner = w.shape[1]
+
+    def dargs(off):
+        return gemm_args(M, inner, w.shape[0], dy, _ld(dy), w, _ld(w), df, _ld(df), b_mode=L.OPB_ROWN,
+                         c_mode=L.OUT_BF16_GEGLU_BWD, split_k=1, aux=f, ld_aux=_ld(f), ws_offset=off)
+    gemm_pair(lambda off: linear_wgrad_args(dy, a, dw, db, off), dargs)
 
 
 # ------------------------------------------------------------------ 3x3 convolutions

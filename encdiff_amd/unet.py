@@ -505,8 +505,8 @@ class UNetExecutor:
                        resid=S["t1"])
         # GEGLU feed-forward
         ops.layernorm_fwd(S["t2"], self.P(tb + "norm3.weight"), self.P(tb + "norm3.bias"), S["n3"], S["s3"], LN_EPS)
-        ops.linear_fwd(S["n3"], self.W(tb + "ff.net.0.proj.weight"), S["f"], bias=self.P(tb + "ff.net.0.proj.bias"))
-        ops.geglu_fwd(S["f"], S["a"])
+        ops.linear_fwd_geglu(S["n3"], self.W(tb + "ff.net.0.proj.weight"), S["f"], S["a"],
+                             bias=self.P(tb + "ff.net.0.proj.bias"))
         ops.linear_fwd(S["a"], self.W(tb + "ff.net.2.weight"), S["t3"], bias=self.P(tb + "ff.net.2.bias"),
                        resid=S["t2"])
         ops.linear_fwd(S["t3"], self.W(s.prefix + "proj_out.weight"), S["out"], bias=self.P(s.prefix + "proj_out.bias"),
@@ -668,9 +668,8 @@ class UNetExecutor:
         ops.linear_bwd(dout, self.W(s.prefix + "proj_out.weight"), S["t3"], d_t3,
                        self.G(s.prefix + "proj_out.weight").view(c, c), self.G(s.prefix + "proj_out.bias"))
         # FF
-        ops.linear_bwd(d_t3, self.W(tb + "ff.net.2.weight"), S["a"], d_a, self.G(tb + "ff.net.2.weight"),
-                       self.G(tb + "ff.net.2.bias"))
-        ops.geglu_bwd(S["f"], d_a, S["d_f"])
+        ops.linear_bwd_geglu(d_t3, self.W(tb + "ff.net.2.weight"), S["a"], S["f"], S["d_f"],
+                             self.G(tb + "ff.net.2.weight"), self.G(tb + "ff.net.2.bias"), d_a=d_a)
         ops.linear_bwd(S["d_f"], self.W(tb + "ff.net.0.proj.weight"), S["n3"], d_n,
                        self.G(tb + "ff.net.0.proj.weight"), self.G(tb + "ff.net.0.proj.bias"))
         dg, db = self.ln.parts(tb + "norm3.weight", c)

@@ -59,9 +59,15 @@ enum {
   ENCDIFF_OUT_F32_ATOMIC = 2,       /* atomicAdd into fp32 C (split-K / grad accumulate)   */
   ENCDIFF_OUT_F32_ATOMIC_CONVW = 3, /* atomicAdd, column n=(tap,ci) scattered to the reference
                                        Conv2d weight layout [co][ci][3][3]                   */
-  ENCDIFF_OUT_F32_ACCUM = 4         /* fp32 C += result, single writer per element (weight
+  ENCDIFF_OUT_F32_ACCUM = 4,        /* fp32 C += result, single writer per element (weight
                                        gradients): with split_k > 1 the slabs are summed in a
                                        fixed order -> bitwise reproducible                   */
+  ENCDIFF_OUT_BF16_GEGLU = 5,       /* GEGLU proj (attention.py GEGLU): C = f [M][N] bf16 (N = 2*inner,
+                                       +bias) and aux = y [M][N/2] = f[:, :N/2] * gelu(f[:, N/2:])
+                                       from the bf16-rounded f; OPA_ROWK x OPB_ROWK, split_k 1   */
+  ENCDIFF_OUT_BF16_GEGLU_BWD = 6    /* GEGLU backward fused into the dgrad producing dy [M][N]
+                                       (N = inner): aux = f [M][2N] input, C = df [M][2N] bf16
+                                       (d of the value half, d of the gate half); split_k 1   */
 };
 enum {
   ENCDIFF_RESAMPLE_NONE = 0,
@@ -110,6 +116,7 @@ typedef struct EncdiffGemmArgs {
                                 (+ split_k*M when bias_grad is set: per-split bias-gradient slabs);
                                 each split writes its own [M][N] slab, a finalize pass sums the
                                 slabs in order (reproducible) and applies alpha/bias/resid    */
+  void* aux; long ld_aux;    /* GEGLU c_modes: y output (BF16_GEGLU) / f input (BF16_GEGLU_BWD)  */
 } EncdiffGemmArgs;
 
 int encdiff_gemm(const EncdiffGemmArgs* args, void* stream);

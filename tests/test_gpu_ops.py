@@ -663,3 +663,41 @@ def test_gemm_pair_chain_deferred_finalize(O):
         assert torch.equal(a, b)
     for (dy, x, w), k in zip(ins, range(0, 15, 3)):
         assert rel(res[1][k], dy.float().t() @ x.float()) < 2e-3
+
+
+@pytest.mark.parametrize("M,C,inner", [(4096, 64, 256), (1000, 128, 512), (256, 256, 1024)])
+def test_geglu_fused(O, M, C, inner):
+    """GEGLU in the GEMM epilogues (proj: f and y = f_v * gelu(f_g); next layer's input
+    gradient: df) equals the separate ew kernels bitwise, and torch fp32 within bf16 tolerance."""
+    torch.manual_seed(9)
+    x = bf(M, C)
+    w1 = bf(2 * inner, C, scale=C ** -0.5)
+    b1 = torch.randn(2 * inner, device=dev) * 0.1
+    w2 = bf(C, inner, scale=inner ** -0.5)
+    dy = bf(M, C)
+    outs = {}
+    for fused in (True, False):
+        O.GEGLU_FUSED = fused
+        try:
+            f = torch.empty(M, 2 * inner, device=dev, dtype=torch.bfloat16)
+            y = torch.empty(M, inner, device=dev, dtype=torch.bfloat16)
+            O.linear_fwd_geglu(x, w1, f, y, bias=b1)
+            df = torch.empty_like(f)
+            d_a = torch.empty_like(y)
+            dw = torch.zeros(C, inner, device=dev)
+            db = torch.zeros(C, device=dev)
+            O.linear_bwd_geglu(dy, w2, y, f, df, dw, db, d_a=d_a)
+            O.flush()
+        finally:
+            O.GEGLU_FUSED = True
+        outs[fused] = (f, y, df, dw, db)
+    for a, b in zip(outs[True], outs[False]):
+        assert torch.equal(a, b)
+    f, y, df, dw, db = outs[True]
+    fr = x.float() @ w1.float().t() + b1
+    assert rel(f, fr) < 1e-2
+    fv, fg = f.float()[:, :inner], f.float()[:, inner:]
+    assert rel(y, fv * F.gelu(fg)) < 1e-2
+    fvr, fgr = fv.clone().requires_grad_(True), fg.clone().requires_grad_(True)
+    (fvr * F.gelu(fgr)).backward((dy.float() @ w2.float()).to(torch.bfloat16).float())
+    assert rel(df[:, :inner], fvr.grad) < 1e-2 and rel(df[:, inner:], fgr.grad) < 1e-2
