@@ -40,7 +40,7 @@ class GemmArgs(C.Structure):
                 ("alpha", C.c_float), ("split_k", C.c_int),
                 ("bias", vp), ("resid", vp), ("ld_resid", C.c_long), ("bias_grad", vp),
                 ("tile", C.c_int), ("pad2_", C.c_int), ("workspace", vp),
-                ("aux", vp), ("ld_aux", C.c_long)]
+                ("aux", vp), ("ld_aux", C.c_long), ("gn_stats", vp), ("ld_gn_stats", C.c_long)]
 
 
 class GroupNormArgs(C.Structure):
@@ -51,7 +51,8 @@ class GroupNormArgs(C.Structure):
                 ("dy", vp), ("lddy", C.c_long), ("dx", vp), ("lddx", C.c_long),
                 ("accumulate_dx", C.c_int), ("pad_", C.c_int),
                 ("dgamma_part", vp), ("dbeta_part", vp), ("ld_part", C.c_long), ("dfilm", vp),
-                ("ld_dfilm", C.c_long), ("resid", vp), ("ld_resid", C.c_long)]
+                ("ld_dfilm", C.c_long), ("resid", vp), ("ld_resid", C.c_long), ("in_stats", vp),
+                ("ld_in_stats", C.c_long)]
 
 
 class LayerNormArgs(C.Structure):

@@ -525,7 +525,14 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
         for (int k = 0; k < 8; ++k) v[k] += rr[k];
       }
       if (p.c_mode == ENCDIFF_OUT_BF16) {
-        *(uint4*)((bf16_t*)p.c + ro * p.ldc + col) = pack8(v);
+        const uint4 pk = pack8(v);
+        *(uint4*)((bf16_t*)p.c + ro * p.ldc + col) = pk;
+        if (p.gn_stats) {  // the stored (bf16) values feed the GroupNorm statistics below
+          float rv[8];
+          unpack8(pk, rv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) sc[r * SLD + c8 + k] = rv[k];
+        }
       } else {
         float* cp = p_c_slab + ro * p.ldc + col;
         if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) {
@@ -548,6 +555,50 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       if (p.c_mode == ENCDIFF_OUT_BF16) ((bf16_t*)p.c)[ro * p.ldc + col] = f2bf(v);
       else if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) p_c_slab[ro * p.ldc + col] += v;
       else p_c_slab[ro * p.ldc + col] = v;
+      if (p.gn_stats) sc[r * SLD + cc] = bf16_round(v);
+    }
+  }
+  if (p.gn_stats) {
+    // GroupNorm statistics of the produced tensor (host: OUT_BF16, split_k 1, M % 64 == 0):
+    // per 64-row segment and column, sum and sum of squares of the stored bf16 values.  Q row
+    // phases per column, their partials added in phase order through LDS: deterministic.
+    constexpr int Q = 256 / BN, NSEG = BM / 64;
+    const int c = tid % BN, q = tid / BN;
+    float ps[NSEG], pq[NSEG];
+    __syncthreads();
+#pragma unroll
+    for (int sg = 0; sg < NSEG; ++sg) {
+      float a = 0.f, b = 0.f;
+#pragma unroll 4
+      for (int r = sg * 64 + q; r < sg * 64 + 64; r += Q) {
+        const float v = sc[r * SLD + c];
+        a += v;
+        b += v * v;
+      }
+      ps[sg] = a;
+      pq[sg] = b;
+    }
+    __syncthreads();
+    float* red = sc;  // [NSEG][2][Q][BN]
+#pragma unroll
+    for (int sg = 0; sg < NSEG; ++sg) {
+      red[((sg * 2) * Q + q) * BN + c] = ps[sg];
+      red[((sg * 2 + 1) * Q + q) * BN + c] = pq[sg];
+    }
+    __syncthreads();
+    if (q == 0 && n0 + c < p.N) {
+#pragma unroll
+      for (int sg = 0; sg < NSEG; ++sg) {
+        if (m0 + sg * 64 >= p.M) break;
+        float a = 0.f, b = 0.f;
+        for (int qq = 0; qq < Q; ++qq) {
+          a += red[((sg * 2) * Q + qq) * BN + c];
+          b += red[((sg * 2 + 1) * Q + qq) * BN + c];
+        }
+        const long slot = (m0 >> 6) + sg;
+        p.gn_stats[(2 * slot) * p.ld_gn_stats + n0 + c] = a;
+        p.gn_stats[(2 * slot + 1) * p.ld_gn_stats + n0 + c] = b;
+      }
     }
   }
 }
@@ -567,7 +618,7 @@ __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const in
 // gradient (problem 2) share the machine instead of running back to back, each too small
 // to fill 256 CUs; the previous layer's weight-gradient finalize rides along, so neither
 // needs a launch of its own.
-template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2, int KB2>
+template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2, int KB2, int KB1>
 __global__ __launch_bounds__(256) void gemm2_kernel(const EncdiffGemmArgs p1, const GemmAux aux1,
                                                     const EncdiffGemmArgs p2, const GemmAux aux2, int gx1,
                                                     int gy1, int gx2, int gy2, const EncdiffGemmArgs pf, int nf) {
@@ -577,7 +628,7 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const EncdiffGemmArgs p1, co
   int i = blockIdx.x;
   if (i < n1) {
     const int bx = i % gx1, t = i / gx1;
-    gemm_tile<64, 64, AM1, BMD1>(p1, aux1, bx, t % gy1, t / gy1, smem);
+    gemm_tile<64, 64, AM1, BMD1, 2, KB1>(p1, aux1, bx, t % gy1, t / gy1, smem);
   } else if (i < n1 + n2) {
     i -= n1;
     const int bx = i % gx2, t = i / gx2;
@@ -811,6 +862,8 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
   }
   if (p.K >= (1 << 24)) return ENCDIFF_ERR_SHAPE;
   if (p.bias_grad && p.a_mode != ENCDIFF_OPA_ROWM) return ENCDIFF_ERR_ARG;
+  if (p.gn_stats && (p.c_mode != ENCDIFF_OUT_BF16 || p.split_k != 1 || p.M % 64 || p.ld_gn_stats < p.N))
+    return ENCDIFF_ERR_ARG;
   if (p.c_mode == ENCDIFF_OUT_BF16_GEGLU || p.c_mode == ENCDIFF_OUT_BF16_GEGLU_BWD) {
     const bool fwd = p.c_mode == ENCDIFF_OUT_BF16_GEGLU;
     if (!p.aux || p.resid || p.split_k != 1 || p.N % 8 || p.ldc % 8 || p.ld_aux % 8) return ENCDIFF_ERR_ARG;
@@ -860,18 +913,18 @@ int launch_one(const GemmPlan& g, hipStream_t s) {
   return ENCDIFF_OK;
 }
 
-template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2 = 2, int KB2 = BK>
+template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2 = 2, int KB2 = BK, int KB1 = BK>
 hipError_t launch_pair_t(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
-  using G1 = Gemm<64, 64, AM1, BMD1>;
+  using G1 = Gemm<64, 64, AM1, BMD1, 2, KB1>;
   using G2 = Gemm<BM2, BN2, AM2, BMD2, NS2, KB2>;
   constexpr size_t lds = G1::LDS_BYTES > G2::LDS_BYTES ? G1::LDS_BYTES : G2::LDS_BYTES;
   static const hipError_t attr_ok = hipFuncSetAttribute(
-      (const void*)gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2, KB2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (const void*)gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2, KB2, KB1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr_ok != hipSuccess) return attr_ok;
   const int gx1 = (g1.p.M + 63) / 64, gy1 = (g1.p.N + 63) / 64;
   const int gx2 = (g2.p.M + BM2 - 1) / BM2, gy2 = (g2.p.N + BN2 - 1) / BN2;
   const long nb = (long)gx1 * gy1 * g1.p.split_k + (long)gx2 * gy2 * g2.p.split_k + nf;
-  hipLaunchKernelGGL((gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2, KB2>), dim3((unsigned)nb), dim3(256), lds, s, g1.p,
+  hipLaunchKernelGGL((gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2, KB2, KB1>), dim3((unsigned)nb), dim3(256), lds, s, g1.p,
                      g1.aux, g2.p, g2.aux, gx1, gy1, gx2, gy2, pf, nf);
   return hipGetLastError();
 }
@@ -879,6 +932,10 @@ hipError_t launch_pair_t(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGe
 template <int AM1, int BMD1, int AM2, int BMD2>
 hipError_t launch_pair_tiles(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf,
                              hipStream_t s) {
+  if (g1.tile == 7) {  // weight gradient with 128-deep k stages (64 KB of LDS): dgrad tile 7 or 64x64
+    if (g2.tile == 7) return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 2, 128, 128>(g1, g2, pf, nf, s);
+    return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 2, 64, 128>(g1, g2, pf, nf, s);
+  }
   switch (g2.tile) {
     case 1: return launch_pair_t<AM1, BMD1, 128, 128, AM2, BMD2>(g1, g2, pf, nf, s);
     case 2: return launch_pair_t<AM1, BMD1, 128, 64, AM2, BMD2>(g1, g2, pf, nf, s);
@@ -927,7 +984,7 @@ extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffG
   // both split-K problems need disjoint slabs
   if (g1.ws_path && g2.ws_path && g1.p.workspace == g2.p.workspace) return ENCDIFF_ERR_ARG;
   const bool defer1 = defer && g1.ws_path;
-  if ((!lin && !conv) || g1.tile != 4) {  // pairs the fused kernel does not cover: back to back
+  if ((!lin && !conv) || (g1.tile != 4 && g1.tile != 7)) {  // pairs the fused kernel does not cover: back to back
     if (have_prev && (e = launch_finalize(gp.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
     GemmPlan w = g1;
     w.ws_path = g1.ws_path && !defer1;

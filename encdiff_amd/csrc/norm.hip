@@ -207,6 +207,171 @@ __global__ __launch_bounds__(GN_THREADS) void gn_fwd_kernel(const EncdiffGroupNo
   }
 }
 
+// Forward from the producer GEMM's per-64-row-segment channel sums (p.in_stats): no
+// reduction pass and no LDS tile -- x is streamed once.  The first PF rows of each thread are
+// loaded before the group statistics are formed, so their latency overlaps it.
+__global__ __launch_bounds__(GN_THREADS) void gn_fwd_stats_kernel(const EncdiffGroupNormArgs p, int cs) {
+  __shared__ float gsh[2 * 64];
+  const GnSlice L(p, cs, 0);
+  const int HW = p.hw, nseg = HW >> 6;
+  const bf16_t* X = (const bf16_t*)p.x + (long)L.b * HW * p.ldx + L.cb;
+  constexpr int PF = 4;
+  uint4 pre[PF];
+#pragma unroll
+  for (int i = 0; i < PF; ++i) {
+    const int px = L.tp + i * L.np;
+    pre[i] = (L.active && px < HW) ? *(const uint4*)(X + (long)px * p.ldx) : (uint4){0u, 0u, 0u, 0u};
+  }
+  // the slice's segment sums in one round trip: [2][nseg][cs] into LDS (host: nseg*cs <= 2048)
+  __shared__ float pst[2 * 2048];
+  const int ns = nseg * L.cs;
+  for (int e = threadIdx.x; e < 2 * ns; e += GN_THREADS) {
+    const int k = e / ns, r = e - k * ns, sg = r / L.cs, c = r - sg * L.cs;
+    pst[e] = p.in_stats[(2 * ((long)L.b * nseg + sg) + k) * p.ld_in_stats + L.c0 + c];
+  }
+  __syncthreads();
+  if (threadIdx.x < L.gs) {
+    const float inv_n = 1.f / ((float)HW * L.cpg);
+    const int c0 = threadIdx.x * L.cpg;
+    float a = 0.f, q = 0.f;
+    for (int sg = 0; sg < nseg; ++sg)
+      for (int c = 0; c < L.cpg; ++c) { a += pst[sg * L.cs + c0 + c]; q += pst[ns + sg * L.cs + c0 + c]; }
+    const float mean = a * inv_n;
+    const float var = fmaxf(q * inv_n - mean * mean, 0.f);
+    const float rstd = rsqrtf(var + p.eps);
+    gsh[threadIdx.x] = mean;
+    gsh[64 + threadIdx.x] = rstd;
+    const long gi = (long)L.b * p.groups + L.g0 + threadIdx.x;
+    p.stats[2 * gi] = mean;
+    p.stats[2 * gi + 1] = rstd;
+  }
+  float ga[8], be[8], sc[8], sf[8];
+  load8f(p.gamma + L.cb, ga);
+  load8f(p.beta + L.cb, be);
+  if (p.film) {
+    load8f(p.film + (long)L.b * p.ld_film + L.cb, sc);
+    load8f(p.film + (long)L.b * p.ld_film + p.c + L.cb, sf);
+  }
+  __syncthreads();
+  if (!L.active) return;
+  float mul[8], add[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int g = (L.tv * 8 + i) / L.cpg;
+    const float r = gsh[64 + g];
+    float a = r * ga[i], bb = be[i] - gsh[g] * a;
+    if (p.film) {
+      a *= (1.f + sc[i]);
+      bb = bb * (1.f + sc[i]) + sf[i];
+    }
+    mul[i] = a; add[i] = bb;
+  }
+  bf16_t* Y = (bf16_t*)p.y + (long)L.b * HW * p.ldy + L.cb;
+  const bool silu = p.silu;
+  auto emit = [&](const uint4& u, int px) {
+    float v[8];
+    unpack8(u, v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float z = v[i] * mul[i] + add[i];
+      v[i] = silu ? silu_f(z) : z;
+    }
+    *(uint4*)(Y + (long)px * p.ldy) = pack8(v);
+  };
+#pragma unroll
+  for (int i = 0; i < PF; ++i) {
+    const int px = L.tp + i * L.np;
+    if (px < HW) emit(pre[i], px);
+  }
+#pragma unroll 2
+  for (int px = L.tp + PF * L.np; px < HW; px += L.np) emit(*(const uint4*)(X + (long)px * p.ldx), px);
+}
+
+// Large images (hw >= 1024, the VQ encoder's levels): per-image group statistics from the
+// producer's segment sums in a small kernel (thread (channel, segment lane) sums every J-th
+// segment, lanes added in order), then a streaming apply over (pixel chunk, image) blocks that
+// span all channels -- coalesced rows instead of the narrow channel slices a per-(image,
+// slice) reduction needs.
+__global__ __launch_bounds__(GN_THREADS) void gn_group_stats_kernel(const EncdiffGroupNormArgs p) {
+  __shared__ float part[2][GN_THREADS];
+  __shared__ float chs[2][512];
+  const int b = blockIdx.x, C = p.c, nseg = p.hw >> 6, cpg = C / p.groups;
+  for (int c0 = 0; c0 < C; c0 += GN_THREADS) {  // channel chunks of <= 256
+    const int cw = min(GN_THREADS, C - c0), J = GN_THREADS / cw;
+    const int c = threadIdx.x % cw, j = threadIdx.x / cw;
+    float a = 0.f, q = 0.f;
+    if (j < J) {
+#pragma unroll 8
+      for (int sg = j; sg < nseg; sg += J) {
+        const float* st = p.in_stats + 2 * ((long)b * nseg + sg) * p.ld_in_stats + c0 + c;
+        a += st[0];
+        q += st[p.ld_in_stats];
+      }
+    }
+    part[0][threadIdx.x] = a;
+    part[1][threadIdx.x] = q;
+    __syncthreads();
+    if (threadIdx.x < cw) {
+      float s0 = 0.f, s1 = 0.f;
+      for (int k = 0; k < J; ++k) { s0 += part[0][k * cw + threadIdx.x]; s1 += part[1][k * cw + threadIdx.x]; }
+      chs[0][c0 + threadIdx.x] = s0;
+      chs[1][c0 + threadIdx.x] = s1;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < p.groups) {
+    float a = 0.f, q = 0.f;
+    for (int c = threadIdx.x * cpg; c < (threadIdx.x + 1) * cpg; ++c) { a += chs[0][c]; q += chs[1][c]; }
+    const float inv_n = 1.f / ((float)p.hw * cpg);
+    const float mean = a * inv_n;
+    const float var = fmaxf(q * inv_n - mean * mean, 0.f);
+    const long gi = (long)b * p.groups + threadIdx.x;
+    p.stats[2 * gi] = mean;
+    p.stats[2 * gi + 1] = rsqrtf(var + p.eps);
+  }
+}
+
+// streaming apply: block (chunk of rows, image b), all C channels; thread = (row lane, vector)
+__global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const EncdiffGroupNormArgs p, int rows_per_block) {
+  const int b = blockIdx.y, nvc = p.c >> 3, np = GN_THREADS / nvc;
+  const int tv = threadIdx.x % nvc, tp = threadIdx.x / nvc;
+  if (tp >= np) return;
+  const int cb = tv * 8, cpg = p.c / p.groups;
+  float ga[8], be[8], sc[8], sf[8], mul[8], add[8];
+  load8f(p.gamma + cb, ga);
+  load8f(p.beta + cb, be);
+  if (p.film) {
+    load8f(p.film + (long)b * p.ld_film + cb, sc);
+    load8f(p.film + (long)b * p.ld_film + p.c + cb, sf);
+  }
+  const float* st = p.stats + (long)b * p.groups * 2;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int g = (cb + i) / cpg;
+    float a = st[2 * g + 1] * ga[i], bb = be[i] - st[2 * g] * a;
+    if (p.film) {
+      a *= (1.f + sc[i]);
+      bb = bb * (1.f + sc[i]) + sf[i];
+    }
+    mul[i] = a; add[i] = bb;
+  }
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(p.hw, r0 + rows_per_block);
+  const bf16_t* X = (const bf16_t*)p.x + (long)b * p.hw * p.ldx + cb;
+  bf16_t* Y = (bf16_t*)p.y + (long)b * p.hw * p.ldy + cb;
+  const bool silu = p.silu;
+#pragma unroll 4
+  for (int px = r0 + tp; px < r1; px += np) {
+    float v[8];
+    unpack8(*(const uint4*)(X + (long)px * p.ldx), v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float z = v[i] * mul[i] + add[i];
+      v[i] = silu ? silu_f(z) : z;
+    }
+    *(uint4*)(Y + (long)px * p.ldy) = pack8(v);
+  }
+}
+
 __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNormArgs p, int cs) {
   __shared__ uint4 tx[GN_TILE], td[GN_TILE];
   __shared__ float red[4 * 2048], chs[4 * 512], gsh[2 * 64];
@@ -440,6 +605,23 @@ extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream
   if (!a || !a->x || !a->y || !a->stats || !a->gamma || !a->beta) return ENCDIFF_ERR_ARG;
   const int cs = gn_check(a);
   if (cs < 0) return cs;
+  if (a->in_stats && a->hw >= 1024) {  // large images: group-statistics kernel + streaming apply
+    if (a->hw % 64 || a->ld_in_stats < a->c || a->c > 512 || a->groups > 64 || GN_THREADS % (a->c >> 3))
+      return ENCDIFF_ERR_ARG;
+    hipLaunchKernelGGL(gn_group_stats_kernel, dim3(a->batch), dim3(GN_THREADS), 0, (hipStream_t)stream, *a);
+    const int rpb = 256;
+    hipLaunchKernelGGL(gn_apply_kernel, dim3((a->hw + rpb - 1) / rpb, a->batch), dim3(GN_THREADS), 0,
+                       (hipStream_t)stream, *a, rpb);
+    ED_CHECK_LAUNCH();
+    return ENCDIFF_OK;
+  }
+  if (a->in_stats) {  // statistics from the producer GEMM's segment sums
+    if (a->hw % 64 || a->ld_in_stats < a->c || (a->hw / 64) * cs > 2048) return ENCDIFF_ERR_ARG;
+    hipLaunchKernelGGL(gn_fwd_stats_kernel, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream,
+                       *a, cs);
+    ED_CHECK_LAUNCH();
+    return ENCDIFF_OK;
+  }
   const long need = (long)(cs / 8) * a->hw;  // 16-byte vectors of one slice
   const int cap = need <= GN_TILE_FWD ? (int)need : 0;
   static const hipError_t attr = hipFuncSetAttribute((const void*)gn_fwd_kernel,

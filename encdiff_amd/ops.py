@@ -121,7 +121,8 @@ def plan(M, N, K, a_mode, b_mode, c_mode, resample=0):
 
 def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK, c_mode=L.OUT_BF16,
               conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=None, bias=None,
-              resid=None, ld_resid=0, bias_grad=None, tile=0, ws_offset=0, aux=None, ld_aux=0):
+              resid=None, ld_resid=0, bias_grad=None, tile=0, ws_offset=0, aux=None, ld_aux=0,
+              gn_stats=None):
     """EncdiffGemmArgs with the measured (tile, split) plan; split-K slabs start `ws_offset`
     floats into this stream's workspace."""
     if split_k is None or tile == 0:
@@ -138,7 +139,8 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
                       conv=conv if conv is not None else L.ConvGeom(),
                       conv_cout=conv_cout, convw_cin=convw_cin, alpha=alpha, split_k=split_k,
                       bias=_p(bias), resid=_p(resid), ld_resid=ld_resid, bias_grad=_p(bias_grad), tile=tile,
-                      workspace=None if ws is None else ws.data_ptr() + 4 * ws_offset, aux=_p(aux), ld_aux=ld_aux)
+                      workspace=None if ws is None else ws.data_ptr() + 4 * ws_offset, aux=_p(aux), ld_aux=ld_aux,
+                      gn_stats=_p(gn_stats), ld_gn_stats=_ld(gn_stats) if gn_stats is not None else 0)
 
 
 def ws_floats(args) -> int:
@@ -208,12 +210,14 @@ def gemm_pair(wgrad_fn, dgrad_fn):
 
 
 # ------------------------------------------------------------------ linear layers
-def linear_fwd(x, w, out, bias=None, resid=None, alpha=1.0, out_f32=False):
-    """out[M][N] = x[M][K] w[N][K]^T (+bias)(+resid)."""
+def linear_fwd(x, w, out, bias=None, resid=None, alpha=1.0, out_f32=False, gn_stats=None):
+    """out[M][N] = x[M][K] w[N][K]^T (+bias)(+resid); gn_stats: [2*M/64][ld] fp32 view that
+    receives the per-64-row-segment channel sums of out (the next GroupNorm's statistics)."""
     M, K = x.shape
     N = w.shape[0]
     gemm(M, N, K, x, _ld(x), w, _ld(w), out, _ld(out), c_mode=L.OUT_F32 if out_f32 else L.OUT_BF16,
-         bias=bias, resid=resid, ld_resid=_ld(resid) if resid is not None else 0, alpha=alpha)
+         bias=bias, resid=resid, ld_resid=_ld(resid) if resid is not None else 0, alpha=alpha,
+         gn_stats=gn_stats, split_k=1 if gn_stats is not None else None)
 
 
 def linear_dgrad(dy, w, dx, resid=None):
@@ -287,12 +291,14 @@ def linear_bwd_geglu(dy, w, a, f, df, dw, db=None, d_a=None):
 
 
 # ------------------------------------------------------------------ 3x3 convolutions
-def conv3x3_fwd(x, g: Geom, cin, wf, out, bias=None, resid=None, resample=L.RESAMPLE_NONE):
-    """out[pixels][cout] = conv3x3(resample(x)) with packed weights wf [cout][9*cin]."""
+def conv3x3_fwd(x, g: Geom, cin, wf, out, bias=None, resid=None, resample=L.RESAMPLE_NONE, gn_stats=None):
+    """out[pixels][cout] = conv3x3(resample(x)) with packed weights wf [cout][9*cin]
+    (gn_stats: as linear_fwd)."""
     cout = wf.shape[0]
     gemm(g.pixels, cout, 9 * cin, x, _ld(x), wf, _ld(wf), out, _ld(out), a_mode=L.OPA_IM2COL,
          conv=_conv_geom(g, cin, resample, x), bias=bias, resid=resid,
-         ld_resid=_ld(resid) if resid is not None else 0)
+         ld_resid=_ld(resid) if resid is not None else 0, gn_stats=gn_stats,
+         split_k=1 if gn_stats is not None else None)
 
 
 def conv3x3_dgrad(dy, g: Geom, wf, dx, resid=None):
@@ -381,11 +387,13 @@ def conv4x4s2_bwd_cl(dy, g_out: Geom, wf, x, cin, dw_cl, dx, db=None):
 
 
 # ------------------------------------------------------------------ normalisation
-def groupnorm_fwd(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_film=0, groups=32):
+def groupnorm_fwd(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_film=0, groups=32, in_stats=None):
+    """in_stats: the segment sums x's producer GEMM wrote (gn_stats), else a reduction pass."""
     c = x.shape[1]
     a = L.GroupNormArgs(batch=g.batch, hw=g.h * g.w, c=c, groups=groups, eps=eps, silu=int(silu),
                         x=_p(x), ldx=_ld(x), gamma=_p(gamma), beta=_p(beta), film=_p(film), ld_film=ld_film,
-                        y=_p(y), ldy=_ld(y), stats=_p(stats))
+                        y=_p(y), ldy=_ld(y), stats=_p(stats), in_stats=_p(in_stats),
+                        ld_in_stats=_ld(in_stats) if in_stats is not None else 0)
     check(lib.encdiff_groupnorm_fwd(C.byref(a), _s()), "encdiff_groupnorm_fwd")
 
 

@@ -20,6 +20,7 @@ Fusions relative to the reference op graph:
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -34,6 +35,9 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 GN_EPS = 1e-5      # GroupNorm32 (util.py:227-233)
 ST_GN_EPS = 1e-6   # Normalize (attention.py:76-77)
+# GroupNorm forward statistics from the producing GEMM's epilogue at >= 8x8 (0: reduce in the
+# GroupNorm kernel, for A/B runs)
+GN_FROM_PRODUCER = os.environ.get("ENCDIFF_GN_FROM_PRODUCER", "1") != "0"
 LN_EPS = 1e-5      # nn.LayerNorm default (attention.py:206-208)
 
 
@@ -358,6 +362,45 @@ class UNetExecutor:
             c = t_.c
             self.st_scratch[key] = dict(d_a=t(M, 4 * c), d_n=t(M, c), d_o=t(M, c), d_g=t(M, c))
         self.res_scratch = {}
+        self._bind_gn_stats(B)
+
+    def _bind_gn_stats(self, B):
+        """GroupNorm statistics from the producers: every tensor a GroupNorm forward reads at
+        >= 8x8 (layer outputs, the concat inputs, each ResBlock's conv1 output) gets a
+        [2 * pixels/64][C] fp32 buffer that its producing GEMM fills with per-64-row-segment
+        channel sums (EncdiffGemmArgs.gn_stats); a concat input's two producers fill their
+        channel ranges of one buffer.  Keyed by the tensor's data pointer."""
+        self.gst = {}
+        if not GN_FROM_PRODUCER:
+            return
+        sp = self.spec
+
+        def add(x, hw, key_views=()):
+            if hw < 64:
+                return
+            st = self._t(2 * x.shape[0] // 64, x.shape[1], F32)
+            self.gst[x.data_ptr()] = st
+            for v in key_views:
+                off = v.data_ptr() - x.data_ptr()
+                self.gst[v.data_ptr()] = st[:, off // x.element_size():]
+        nhs = len(sp.input_blocks)
+        for j, blk in enumerate(sp.output_blocks):
+            c1 = blk[0].cin - sp.skip_ch[nhs - 1 - j]
+            add(self.xcat[j], blk[0].hin ** 2, (self.xcat[j][:, c1:],))
+        for blk in sp.input_blocks + [sp.middle] + sp.output_blocks:
+            for layer in blk:
+                if not isinstance(layer, (ResSpec, STSpec)):
+                    continue  # the input conv (its output h0 is a concat view)
+                S = self.state[layer.prefix]
+                hw = (layer.hout if isinstance(layer, ResSpec) else layer.h) ** 2
+                if S["out"].data_ptr() not in self.gst:
+                    add(S["out"], hw)
+                if isinstance(layer, ResSpec):
+                    add(S["h1"], layer.hout ** 2)
+
+    def _gst(self, x):
+        """The producer-statistics buffer of tensor x (None: the GroupNorm reduces itself)."""
+        return self.gst.get(x.data_ptr())
 
     def _res_bufs(self, r: ResSpec, B):
         t = self._t
@@ -409,7 +452,8 @@ class UNetExecutor:
         g0 = Geom(B, self.H, self.H)
         # input conv on the GEMM engine over channel-padded rows (openaimodel_enc.py:494)
         ops.nchw_to_rows(self._x, 8, self.x8)
-        ops.conv3x3_fwd(self.x8, g0, 8, self.W("input_conv"), self.h0, bias=self.P("input_blocks.0.0.bias"))
+        ops.conv3x3_fwd(self.x8, g0, 8, self.W("input_conv"), self.h0, bias=self.P("input_blocks.0.0.bias"),
+                        gn_stats=self._gst(self.h0))
         hs = [self.h0]
         h = self.h0
         for blk in sp.input_blocks[1:]:
@@ -429,7 +473,8 @@ class UNetExecutor:
             for layer in blk:
                 h = self._layer_fwd(layer, h)
         self._h_last = h
-        ops.groupnorm_fwd(h, g0, self.P("out.0.weight"), self.P("out.0.bias"), self.a_out, self.st_out, GN_EPS, True)
+        ops.groupnorm_fwd(h, g0, self.P("out.0.weight"), self.P("out.0.bias"), self.a_out, self.st_out, GN_EPS, True,
+                          in_stats=self._gst(h))
         ops.small_conv_out_fwd(self.a_out, g0, self.P("out.2.weight"), self.P("out.2.bias"), self.eps)
         return self.eps
 
@@ -445,13 +490,14 @@ class UNetExecutor:
         S["x"] = x
         gi, go = Geom(B, r.hin, r.hin), Geom(B, r.hout, r.hout)
         ops.groupnorm_fwd(x, gi, self.P(r.prefix + "in_layers.0.weight"), self.P(r.prefix + "in_layers.0.bias"),
-                          S["a1"], S["st1"], GN_EPS, True)
+                          S["a1"], S["st1"], GN_EPS, True, in_stats=self._gst(x))
         a1, rs = self._conv1_input(r, S, go)
         ops.conv3x3_fwd(a1, go, r.cin, self.W(r.prefix + "in_layers.2.weight"), S["h1"],
-                        bias=self.P(r.prefix + "in_layers.2.bias"), resample=rs)
+                        bias=self.P(r.prefix + "in_layers.2.bias"), resample=rs, gn_stats=self._gst(S["h1"]))
         film = self.E[:, r.film_off:]
         ops.groupnorm_fwd(S["h1"], go, self.P(r.prefix + "out_layers.0.weight"), self.P(r.prefix + "out_layers.0.bias"),
-                          S["a2"], S["st2"], GN_EPS, True, film=film, ld_film=self.E.shape[1])
+                          S["a2"], S["st2"], GN_EPS, True, film=film, ld_film=self.E.shape[1],
+                          in_stats=self._gst(S["h1"]))
         # skip path into the output buffer, then conv2 adds onto it
         out = S["out"]
         if r.cin != r.cout:
@@ -464,7 +510,7 @@ class UNetExecutor:
         else:
             resid = x
         ops.conv3x3_fwd(S["a2"], go, r.cout, self.W(r.prefix + "out_layers.3.weight"), out,
-                        bias=self.P(r.prefix + "out_layers.3.bias"), resid=resid)
+                        bias=self.P(r.prefix + "out_layers.3.bias"), resid=resid, gn_stats=self._gst(out))
         return out
 
     @staticmethod
@@ -486,7 +532,7 @@ class UNetExecutor:
         tb = s.prefix + "transformer_blocks.0."
         ntok = s.h * s.h
         ops.groupnorm_fwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["gn"], S["stg"],
-                          ST_GN_EPS, False)
+                          ST_GN_EPS, False, in_stats=self._gst(x))
         ops.linear_fwd(S["gn"], self.W(s.prefix + "proj_in.weight"), S["t0"], bias=self.P(s.prefix + "proj_in.bias"))
         # self-attention
         ops.layernorm_fwd(S["t0"], self.P(tb + "norm1.weight"), self.P(tb + "norm1.bias"), S["n1"], S["s1"], LN_EPS)
@@ -510,7 +556,7 @@ class UNetExecutor:
         ops.linear_fwd(S["a"], self.W(tb + "ff.net.2.weight"), S["t3"], bias=self.P(tb + "ff.net.2.bias"),
                        resid=S["t2"])
         ops.linear_fwd(S["t3"], self.W(s.prefix + "proj_out.weight"), S["out"], bias=self.P(s.prefix + "proj_out.bias"),
-                       resid=x)
+                       resid=x, gn_stats=self._gst(S["out"]))
         return S["out"]
 
     # ---------------------------------------------------------------- backward

@@ -23,6 +23,7 @@ import torch
 from . import _lib as L
 from . import ops
 from .ops import Geom
+from .unet import GN_FROM_PRODUCER
 
 BF16 = torch.bfloat16
 VQ_GN_EPS = 1e-6  # Normalize (model.py:30-31)
@@ -30,6 +31,7 @@ VQ_GN_EPS = 1e-6  # Normalize (model.py:30-31)
 
 class VQEncoderExecutor:
     def __init__(self, vq):
+        self._gsts = {}
         self.vq = vq
         enc = vq.encoder
         self.enc = enc
@@ -89,10 +91,20 @@ class VQEncoderExecutor:
         return t
 
     # ------------------------------------------------------------ forward
+    def _gst(self, B, name, out, g: Geom):
+        """Producer-side GroupNorm statistics buffer for `out` (a GroupNorm input of >= 64
+        pixels per image): the producing GEMM fills it, the GroupNorm skips its reduction."""
+        if not GN_FROM_PRODUCER or g.h * g.w < 64 or (g.h * g.w) % 64:
+            return None
+        st = self._t(B, name + ".gst", 2 * g.pixels // 64, out.shape[1], torch.float32)
+        self._gsts[out.data_ptr()] = st
+        return st
+
     def _gn_swish(self, B, x, g: Geom, norm, name):
         out = self._t(B, name, g.pixels, x.shape[1])
         stats = self._t(B, "gn_stats", B, 2 * 32, torch.float32)
-        ops.groupnorm_fwd(x, g, norm.weight, norm.bias, out, stats, VQ_GN_EPS, True, groups=norm.num_groups)
+        ops.groupnorm_fwd(x, g, norm.weight, norm.bias, out, stats, VQ_GN_EPS, True, groups=norm.num_groups,
+                          in_stats=self._gsts.get(x.data_ptr()))
         return out
 
     def _resblock(self, B, x, g: Geom, blk, key):
@@ -100,14 +112,16 @@ class VQEncoderExecutor:
         cin, cout = blk.in_channels, blk.out_channels
         a = self._gn_swish(B, x, g, blk.norm1, key + ".a1")
         h = self._t(B, key + ".h", g.pixels, cout)
-        ops.conv3x3_fwd(a, g, cin, self._packed[key + ".conv1"], h, bias=blk.conv1.bias)
+        ops.conv3x3_fwd(a, g, cin, self._packed[key + ".conv1"], h, bias=blk.conv1.bias,
+                        gn_stats=self._gst(B, key + ".h", h, g))
         a2 = self._gn_swish(B, h, g, blk.norm2, key + ".a2")
         sc = x
         if cin != cout:
             sc = self._t(B, key + ".sc", g.pixels, cout)
             ops.linear_fwd(x, self._packed[key + ".nin"], sc, bias=blk.nin_shortcut.bias)
         out = self._t(B, key + ".out", g.pixels, cout)
-        ops.conv3x3_fwd(a2, g, cout, self._packed[key + ".conv2"], out, bias=blk.conv2.bias, resid=sc)
+        ops.conv3x3_fwd(a2, g, cout, self._packed[key + ".conv2"], out, bias=blk.conv2.bias, resid=sc,
+                        gn_stats=self._gst(B, key + ".out", out, g))
         return out
 
     def _attn(self, B, x, g: Geom, attn):
@@ -120,13 +134,15 @@ class VQEncoderExecutor:
         lse = self._t(B, "attn.lse", B, g.h * g.w, torch.float32)
         ops.attention_fwd(qkv[:, :c], qkv[:, c:2 * c], qkv[:, 2 * c:], o, lse, B, 1, g.h * g.w, g.h * g.w, c)
         out = self._t(B, "attn.out", g.pixels, c)
-        ops.linear_fwd(o, self._packed["attn.proj"], out, bias=attn.proj_out.bias, resid=x)
+        ops.linear_fwd(o, self._packed["attn.proj"], out, bias=attn.proj_out.bias, resid=x,
+                       gn_stats=self._gst(B, "attn.out", out, g))
         return out
 
     def _gn_swish_free(self, B, x, g, norm):
         out = self._t(B, "attn.norm", g.pixels, x.shape[1])
         stats = self._t(B, "gn_stats", B, 2 * 32, torch.float32)
-        ops.groupnorm_fwd(x, g, norm.weight, norm.bias, out, stats, VQ_GN_EPS, False, groups=norm.num_groups)
+        ops.groupnorm_fwd(x, g, norm.weight, norm.bias, out, stats, VQ_GN_EPS, False, groups=norm.num_groups,
+                          in_stats=self._gsts.get(x.data_ptr()))
         return out
 
     @torch.no_grad()
@@ -138,10 +154,12 @@ class VQEncoderExecutor:
         enc = self.enc
         B, _, R, _ = x.shape
         g = Geom(B, R, R)
+        self._gsts = {}  # tensor -> statistics its producer wrote in THIS pass
         h = self._t(B, "conv_in", g.pixels, enc.ch)
         x8 = self._t(B, "x8", g.pixels, 8)
         ops.nchw_to_rows(x.contiguous(), 8, x8)
-        ops.conv3x3_fwd(x8, g, 8, self._packed["conv_in"], h, bias=enc.conv_in.bias)
+        ops.conv3x3_fwd(x8, g, 8, self._packed["conv_in"], h, bias=enc.conv_in.bias,
+                        gn_stats=self._gst(B, "conv_in", h, g))
         for i, lvl in enumerate(enc.down):
             for j, blk in enumerate(lvl.block):
                 h = self._resblock(B, h, g, blk, f"d{i}.{j}")
@@ -150,7 +168,7 @@ class VQEncoderExecutor:
                 go = Geom(B, g.h // 2, g.w // 2)
                 d = self._t(B, f"d{i}.down", go.pixels, c)
                 ops.conv3x3_fwd(h, go, c, self._packed[f"d{i}.down"], d, bias=lvl.downsample.conv.bias,
-                                resample=L.RESAMPLE_STRIDE2)
+                                resample=L.RESAMPLE_STRIDE2, gn_stats=self._gst(B, f"d{i}.down", d, go))
                 h, g = d, go
         h = self._resblock(B, h, g, enc.mid.block_1, "mid.block_1")
         h = self._attn(B, h, g, enc.mid.attn_1)

@@ -117,6 +117,11 @@ typedef struct EncdiffGemmArgs {
                                 each split writes its own [M][N] slab, a finalize pass sums the
                                 slabs in order (reproducible) and applies alpha/bias/resid    */
   void* aux; long ld_aux;    /* GEGLU c_modes: y output (BF16_GEGLU) / f input (BF16_GEGLU_BWD)  */
+  float* gn_stats; long ld_gn_stats;  /* optional, OUT_BF16 with split_k 1 and M % 64 == 0: per
+                                64-row segment s and column n, the sum and sum of squares of the
+                                bf16 outputs at gn_stats[(2s)*ld + n] and [(2s+1)*ld + n] -- the
+                                GroupNorm statistics of the tensor this GEMM produces, so that
+                                encdiff_groupnorm_fwd needs no reduction pass (in_stats)       */
 } EncdiffGemmArgs;
 
 int encdiff_gemm(const EncdiffGemmArgs* args, void* stream);
@@ -166,6 +171,9 @@ typedef struct EncdiffGroupNormArgs {
   long ld_part;
   float* dfilm; long ld_dfilm;       /* fp32 [batch][ld_dfilm]: dscale at [c], dshift at [C + c] */
   const void* resid; long ld_resid;  /* backward: optional bf16 residual-branch gradient added to dx */
+  const float* in_stats; long ld_in_stats;  /* forward, optional: per-64-row-segment channel sums
+                                of x written by its producer GEMM (EncdiffGemmArgs.gn_stats; hw
+                                a multiple of 64): the statistics come from them, x is read once */
 } EncdiffGroupNormArgs;
 
 int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* args, void* stream);

@@ -499,11 +499,21 @@ def test_encoder_warp(O, B):
         assert rel(p.grad, pr.grad) < 1e-4, n
 
 
+@pytest.mark.parametrize("force", [0, 7])
 @pytest.mark.parametrize("kind,M,C,K", [("lin", 32768, 64, 64), ("lin", 2048, 256, 256), ("lin", 8192, 128, 512),
                                          ("conv", 16, 64, 64), ("conv", 8, 256, 256), ("conv", 4, 256, 512)])
-def test_gemm_pair_matches_two_launches(O, kind, M, C, K):
+def test_gemm_pair_matches_two_launches(O, kind, M, C, K, force):
     """encdiff_gemm_pair (weight + input gradient of one layer in ONE launch) is bitwise
-    identical to the two separate GEMMs, whatever tiles / split-K the plan picks."""
+    identical to the two separate GEMMs, whatever tiles / split-K the plan picks (force=7:
+    both with 128-deep k stages, the paired kernel's KB1 = KB2 = 128 instantiation)."""
+    O.FORCE_TILE = force
+    try:
+        _pair_case(O, kind, M, C, K)
+    finally:
+        O.FORCE_TILE = 0
+
+
+def _pair_case(O, kind, M, C, K):
     import encdiff_amd._lib as L
     from encdiff_amd.ops import Geom
     torch.manual_seed(3)
@@ -701,3 +711,42 @@ def test_geglu_fused(O, M, C, inner):
     fvr, fgr = fv.clone().requires_grad_(True), fg.clone().requires_grad_(True)
     (fvr * F.gelu(fgr)).backward((dy.float() @ w2.float()).to(torch.bfloat16).float())
     assert rel(df[:, :inner], fvr.grad) < 1e-2 and rel(df[:, inner:], fgr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("H,C,silu,film", [(16, 64, True, True), (16, 192, False, False), (8, 384, True, True),
+                                         (64, 32, True, False), (32, 64, False, False)])
+def test_groupnorm_from_producer_stats(O, H, C, silu, film):
+    """A GEMM's epilogue segment sums (gn_stats) feed GroupNorm forward: same output and saved
+    statistics as the reducing kernel up to fp32 summation order; also for a channel slice of
+    a wider (concat) buffer."""
+    from encdiff_amd.ops import Geom
+    torch.manual_seed(12)
+    B = 16
+    g = Geom(B, H, H)
+    K = 96
+    xin = bf(g.pixels, K)
+    w = bf(C, K, scale=K ** -0.5)
+    bias = torch.randn(C, device=dev)
+    wide = torch.zeros(g.pixels, C + 64, device=dev, dtype=torch.bfloat16)
+    stw = torch.full((2 * g.pixels // 64, C + 64), float("nan"), device=dev)
+    x = wide[:, 64:]
+    O.linear_fwd(xin, w, x, bias=bias, gn_stats=stw[:, 64:])
+    gam = torch.randn(C, device=dev)
+    bet = torch.randn(C, device=dev)
+    fl = torch.randn(B, 2 * C, device=dev) * 0.2 if film else None
+    outs = []
+    for st_in in (None, stw[:, 64:]):
+        y = torch.empty(g.pixels, C, device=dev, dtype=torch.bfloat16)
+        st = torch.empty(B * 32 * 2, device=dev)
+        O.groupnorm_fwd(x, g, gam, bet, y, st, 1e-5, silu, film=fl, ld_film=2 * C if film else 0, in_stats=st_in)
+        outs.append((y, st))
+    assert rel(outs[1][1], outs[0][1]) < 1e-5
+    assert rel(outs[1][0], outs[0][0]) < 1e-2
+    assert (outs[1][0].float() - outs[0][0].float()).abs().max().item() < 0.05
+    xf = nhwc(x, g)
+    ref = F.group_norm(xf, 32, gam, bet, 1e-5)
+    if film:
+        ref = ref * (1 + fl[:, :C, None, None]) + fl[:, C:, None, None]
+    if silu:
+        ref = F.silu(ref)
+    assert rel(nhwc(outs[1][0], g), ref) < 1e-2

@@ -132,10 +132,10 @@ def main():
             continue
         cur = timeit(a, a.tile)
         best_t, best_tile, best_split = cur, a.tile, a.split_k
-        # weight gradients run inside the paired kernel (64 x 64 tiles) with their slabs in
+        # weight gradients run inside the paired kernel (64 x 64 tiles, k stages 64 or 128) with their slabs in
         # one workspace half (deferred finalize): only splits that fit are candidates
         wgrad = a.a_mode == L.OPA_ROWM
-        for tile in ((4,) if wgrad else (1, 2, 3, 4, 5, 6, 7, 8)):
+        for tile in ((4, 7) if wgrad else (1, 2, 3, 4, 5, 6, 7, 8)):
             for split in (1, 2, 4, 8, 16, 32, 64, 128, 256):
                 if split > 1 and a.K // split < 64:
                     continue
