@@ -40,7 +40,9 @@ class GemmArgs(C.Structure):
                 ("alpha", C.c_float), ("split_k", C.c_int),
                 ("bias", vp), ("resid", vp), ("ld_resid", C.c_long), ("bias_grad", vp),
                 ("tile", C.c_int), ("pad2_", C.c_int), ("workspace", vp),
-                ("aux", vp), ("ld_aux", C.c_long), ("gn_stats", vp), ("ld_gn_stats", C.c_long)]
+                ("aux", vp), ("ld_aux", C.c_long), ("gn_stats", vp), ("ld_gn_stats", C.c_long),
+                ("ln_gamma", vp), ("ln_beta", vp), ("ln_y", vp), ("ld_ln_y", C.c_long), ("ln_stats", vp),
+                ("ln_eps", C.c_float), ("pad3_", C.c_int)]
 
 
 class GroupNormArgs(C.Structure):

@@ -527,7 +527,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       if (p.c_mode == ENCDIFF_OUT_BF16) {
         const uint4 pk = pack8(v);
         *(uint4*)((bf16_t*)p.c + ro * p.ldc + col) = pk;
-        if (p.gn_stats) {  // the stored (bf16) values feed the GroupNorm statistics below
+        if (p.gn_stats || p.ln_y) {  // the stored (bf16) values feed the statistics below
           float rv[8];
           unpack8(pk, rv);
 #pragma unroll
@@ -555,7 +555,39 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       if (p.c_mode == ENCDIFF_OUT_BF16) ((bf16_t*)p.c)[ro * p.ldc + col] = f2bf(v);
       else if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) p_c_slab[ro * p.ldc + col] += v;
       else p_c_slab[ro * p.ldc + col] = v;
-      if (p.gn_stats) sc[r * SLD + cc] = bf16_round(v);
+      if (p.gn_stats || p.ln_y) sc[r * SLD + cc] = bf16_round(v);
+    }
+  }
+  if (p.ln_y) {
+    // LayerNorm of each produced row (host: n0 == 0 and N <= BN, OUT_BF16, split_k 1): TPR
+    // adjacent lanes per row, mean then centred variance (two-pass, as the LayerNorm kernel),
+    // from the stored bf16 values; normalised row written to ln_y.
+    constexpr int TPR = 256 / BM;
+    __syncthreads();
+    const int r = tid / TPR, part = tid % TPR, row = m0 + r;
+    const float* sr = sc + r * SLD;
+    float sm = 0.f;
+    for (int c8 = part * 8; c8 < p.N; c8 += TPR * 8)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sm += sr[c8 + k];
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) sm += __shfl_xor(sm, o, 64);
+    const float mean = sm / (float)p.N;
+    float sq = 0.f;
+    for (int c8 = part * 8; c8 < p.N; c8 += TPR * 8)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { const float d = sr[c8 + k] - mean; sq += d * d; }
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) sq += __shfl_xor(sq, o, 64);
+    const float rstd = rsqrtf(sq / (float)p.N + p.ln_eps);
+    if (row < p.M) {
+      if (part == 0) { p.ln_stats[2L * row] = mean; p.ln_stats[2L * row + 1] = rstd; }
+      for (int c8 = part * 8; c8 < p.N; c8 += TPR * 8) {
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = (sr[c8 + k] - mean) * rstd * p.ln_gamma[c8 + k] + p.ln_beta[c8 + k];
+        *(uint4*)((bf16_t*)p.ln_y + (long)row * p.ld_ln_y + c8) = pack8(o);
+      }
     }
   }
   if (p.gn_stats) {
@@ -864,6 +896,12 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
   if (p.bias_grad && p.a_mode != ENCDIFF_OPA_ROWM) return ENCDIFF_ERR_ARG;
   if (p.gn_stats && (p.c_mode != ENCDIFF_OUT_BF16 || p.split_k != 1 || p.M % 64 || p.ld_gn_stats < p.N))
     return ENCDIFF_ERR_ARG;
+  if (p.ln_y) {  // the tile must span every column: N <= BN, 8-column vectors
+    const int bn = (p.tile == 1 || p.tile == 3 || p.tile == 6 || p.tile == 8) ? 128 : 64;
+    if (p.c_mode != ENCDIFF_OUT_BF16 || p.split_k != 1 || !p.tile || p.N > bn || p.N % 8 || p.ld_ln_y % 8 ||
+        !p.ln_gamma || !p.ln_beta || !p.ln_stats)
+      return ENCDIFF_ERR_ARG;
+  }
   if (p.c_mode == ENCDIFF_OUT_BF16_GEGLU || p.c_mode == ENCDIFF_OUT_BF16_GEGLU_BWD) {
     const bool fwd = p.c_mode == ENCDIFF_OUT_BF16_GEGLU;
     if (!p.aux || p.resid || p.split_k != 1 || p.N % 8 || p.ldc % 8 || p.ld_aux % 8) return ENCDIFF_ERR_ARG;

@@ -122,7 +122,7 @@ def plan(M, N, K, a_mode, b_mode, c_mode, resample=0):
 def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK, c_mode=L.OUT_BF16,
               conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=None, bias=None,
               resid=None, ld_resid=0, bias_grad=None, tile=0, ws_offset=0, aux=None, ld_aux=0,
-              gn_stats=None):
+              gn_stats=None, ln=None):
     """EncdiffGemmArgs with the measured (tile, split) plan; split-K slabs start `ws_offset`
     floats into this stream's workspace."""
     if split_k is None or tile == 0:
@@ -140,7 +140,9 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
                       conv_cout=conv_cout, convw_cin=convw_cin, alpha=alpha, split_k=split_k,
                       bias=_p(bias), resid=_p(resid), ld_resid=ld_resid, bias_grad=_p(bias_grad), tile=tile,
                       workspace=None if ws is None else ws.data_ptr() + 4 * ws_offset, aux=_p(aux), ld_aux=ld_aux,
-                      gn_stats=_p(gn_stats), ld_gn_stats=_ld(gn_stats) if gn_stats is not None else 0)
+                      gn_stats=_p(gn_stats), ld_gn_stats=_ld(gn_stats) if gn_stats is not None else 0,
+                      **({} if ln is None else dict(ln_gamma=_p(ln[0]), ln_beta=_p(ln[1]), ln_y=_p(ln[2]),
+                                                    ld_ln_y=_ld(ln[2]), ln_stats=_p(ln[3]), ln_eps=ln[4])))
 
 
 def ws_floats(args) -> int:
@@ -218,6 +220,31 @@ def linear_fwd(x, w, out, bias=None, resid=None, alpha=1.0, out_f32=False, gn_st
     gemm(M, N, K, x, _ld(x), w, _ld(w), out, _ld(out), c_mode=L.OUT_F32 if out_f32 else L.OUT_BF16,
          bias=bias, resid=resid, ld_resid=_ld(resid) if resid is not None else 0, alpha=alpha,
          gn_stats=gn_stats, split_k=1 if gn_stats is not None else None)
+
+
+# LayerNorm in the producing GEMM's epilogue when one tile spans the row (N <= 128):
+# attention.py norm1/2/3 after proj_in / to_out.  ENCDIFF_LN_FUSED=0: separate kernel.
+LN_FUSED = os.environ.get("ENCDIFF_LN_FUSED", "1") != "0"
+_TILE_BN = {1: 128, 2: 64, 3: 128, 4: 64, 5: 64, 6: 128, 7: 64, 8: 128}
+
+
+def linear_fwd_ln(x, w, out, gamma, beta, y, stats, eps, bias=None, resid=None):
+    """out = x w^T (+bias)(+resid), then y = LayerNorm(out) with per-row (mean, rstd) stats; in
+    the GEMM epilogue when the planned tile spans the row, else the LayerNorm kernel."""
+    M, K = x.shape
+    N = w.shape[0]
+    if not LN_FUSED or N > 128 or N % 8:
+        linear_fwd(x, w, out, bias=bias, resid=resid)
+        layernorm_fwd(out, gamma, beta, y, stats, eps)
+        return
+    tile, _ = plan(M, N, K, L.OPA_ROWK, L.OPB_ROWK, L.OUT_BF16)
+    if _TILE_BN.get(tile, 64) < N:  # forcing a wider tile (fewer workgroups) measured slower
+        linear_fwd(x, w, out, bias=bias, resid=resid)
+        layernorm_fwd(out, gamma, beta, y, stats, eps)
+        return
+    gemm(M, N, K, x, _ld(x), w, _ld(w), out, _ld(out), bias=bias, resid=resid,
+         ld_resid=_ld(resid) if resid is not None else 0, split_k=1, tile=tile,
+         ln=(gamma, beta, y, stats.view(-1, 2) if stats.dim() != 2 else stats, eps))
 
 
 def linear_dgrad(dy, w, dx, resid=None):

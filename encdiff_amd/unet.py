@@ -533,24 +533,24 @@ class UNetExecutor:
         ntok = s.h * s.h
         ops.groupnorm_fwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["gn"], S["stg"],
                           ST_GN_EPS, False, in_stats=self._gst(x))
-        ops.linear_fwd(S["gn"], self.W(s.prefix + "proj_in.weight"), S["t0"], bias=self.P(s.prefix + "proj_in.bias"))
-        # self-attention
-        ops.layernorm_fwd(S["t0"], self.P(tb + "norm1.weight"), self.P(tb + "norm1.bias"), S["n1"], S["s1"], LN_EPS)
+        # proj_in, then norm1 in its epilogue (self-attention input)
+        ops.linear_fwd_ln(S["gn"], self.W(s.prefix + "proj_in.weight"), S["t0"], self.P(tb + "norm1.weight"),
+                          self.P(tb + "norm1.bias"), S["n1"], S["s1"], LN_EPS, bias=self.P(s.prefix + "proj_in.bias"))
         ops.linear_fwd(S["n1"], self.W(s.prefix + "qkv"), S["qkv"])
         q, k, v = S["qkv"][:, :c], S["qkv"][:, c:2 * c], S["qkv"][:, 2 * c:]
         ops.attention_fwd(q, k, v, S["o1"], S["lse1"], B, s.heads, ntok, ntok, s.dh)
-        ops.linear_fwd(S["o1"], self.W(tb + "attn1.to_out.0.weight"), S["t1"], bias=self.P(tb + "attn1.to_out.0.bias"),
-                       resid=S["t0"])
-        # cross-attention to the concept tokens
-        ops.layernorm_fwd(S["t1"], self.P(tb + "norm2.weight"), self.P(tb + "norm2.bias"), S["n2"], S["s2"], LN_EPS)
+        # cross-attention to the concept tokens (norm2 in the to_out epilogue)
+        ops.linear_fwd_ln(S["o1"], self.W(tb + "attn1.to_out.0.weight"), S["t1"], self.P(tb + "norm2.weight"),
+                          self.P(tb + "norm2.bias"), S["n2"], S["s2"], LN_EPS,
+                          bias=self.P(tb + "attn1.to_out.0.bias"), resid=S["t0"])
         ops.linear_fwd(S["n2"], self.W(tb + "attn2.to_q.weight"), S["q2"])
         k2 = self.KV[:, s.kv_off:s.kv_off + c]
         v2 = self.KV[:, s.kv_off + c:s.kv_off + 2 * c]
         ops.attention_fwd(S["q2"], k2, v2, S["o2"], S["lse2"], B, s.heads, ntok, self.lu, s.dh)
-        ops.linear_fwd(S["o2"], self.W(tb + "attn2.to_out.0.weight"), S["t2"], bias=self.P(tb + "attn2.to_out.0.bias"),
-                       resid=S["t1"])
-        # GEGLU feed-forward
-        ops.layernorm_fwd(S["t2"], self.P(tb + "norm3.weight"), self.P(tb + "norm3.bias"), S["n3"], S["s3"], LN_EPS)
+        # GEGLU feed-forward (norm3 in the to_out epilogue)
+        ops.linear_fwd_ln(S["o2"], self.W(tb + "attn2.to_out.0.weight"), S["t2"], self.P(tb + "norm3.weight"),
+                          self.P(tb + "norm3.bias"), S["n3"], S["s3"], LN_EPS,
+                          bias=self.P(tb + "attn2.to_out.0.bias"), resid=S["t1"])
         ops.linear_fwd_geglu(S["n3"], self.W(tb + "ff.net.0.proj.weight"), S["f"], S["a"],
                              bias=self.P(tb + "ff.net.0.proj.bias"))
         ops.linear_fwd(S["a"], self.W(tb + "ff.net.2.weight"), S["t3"], bias=self.P(tb + "ff.net.2.bias"),

@@ -122,6 +122,12 @@ typedef struct EncdiffGemmArgs {
                                 bf16 outputs at gn_stats[(2s)*ld + n] and [(2s+1)*ld + n] -- the
                                 GroupNorm statistics of the tensor this GEMM produces, so that
                                 encdiff_groupnorm_fwd needs no reduction pass (in_stats)       */
+  const float* ln_gamma;     /* optional LayerNorm of the produced rows (attention.py norm1/2/3): */
+  const float* ln_beta;      /*   OUT_BF16, split_k 1, the tile spans all N columns (N <= 128);   */
+  void* ln_y; long ld_ln_y;  /*   ln_y = LN(C) bf16 from the stored bf16 C, two-pass fp32 stats,   */
+  float* ln_stats;           /*   ln_stats [M][2] (mean, rstd) for the backward                  */
+  float ln_eps;
+  int pad3_;
 } EncdiffGemmArgs;
 
 int encdiff_gemm(const EncdiffGemmArgs* args, void* stream);

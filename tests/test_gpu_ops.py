@@ -750,3 +750,33 @@ def test_groupnorm_from_producer_stats(O, H, C, silu, film):
     if silu:
         ref = F.silu(ref)
     assert rel(nhwc(outs[1][0], g), ref) < 1e-2
+
+
+@pytest.mark.parametrize("M,C,resid", [(4096, 64, True), (1024, 128, False), (8192, 128, True)])
+def test_linear_layernorm_fused(O, M, C, resid):
+    """LayerNorm in the producing GEMM's epilogue (attention.py norm1/2/3 after proj_in /
+    to_out) vs the separate LayerNorm kernel: same GEMM output bitwise, normalised rows and
+    (mean, rstd) within fp32 summation-order noise, and torch fp32 within bf16 tolerance."""
+    torch.manual_seed(13)
+    x = bf(M, C)
+    w = bf(C, C, scale=C ** -0.5)
+    b = torch.randn(C, device=dev) * 0.1
+    r = bf(M, C) if resid else None
+    gam = torch.randn(C, device=dev)
+    bet = torch.randn(C, device=dev)
+    res = []
+    for fused in (True, False):
+        O.LN_FUSED = fused
+        try:
+            out = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+            y = torch.empty_like(out)
+            st = torch.empty(M, 2, device=dev)
+            O.linear_fwd_ln(x, w, out, gam, bet, y, st, 1e-5, bias=b, resid=r)
+        finally:
+            O.LN_FUSED = True
+        res.append((out, y, st))
+    assert torch.equal(res[0][0], res[1][0])
+    assert rel(res[0][2], res[1][2]) < 1e-5
+    assert (res[0][1].float() - res[1][1].float()).abs().max().item() < 0.05
+    ref = F.layer_norm(res[0][0].float(), (C,), gam, bet, 1e-5)
+    assert rel(res[0][1], ref) < 1e-2
