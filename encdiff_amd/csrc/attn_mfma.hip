@@ -4,11 +4,13 @@
 // Forward: per wave a 16-query tile; S^T = K Q^T is computed "swapped" so each lane holds
 // 4 consecutive keys of ONE query: the row max / sum of the online softmax are in-register
 // plus two cross-lane xor-shuffles, and the bf16 P is already the B operand of
-// O^T = V^T P^T (no LDS round trip for P).  K and V^T of the block's heads live in LDS.
+// O^T = V^T P^T (no LDS round trip for P).  K and V of the block's heads live in LDS
+// row-major; the V^T operand is read transposed (ds_read_b64_tr_b16).
 // Backward (recompute from LSE, no score matrix in HBM): phase A -- waves own key tiles and
 // accumulate dK^T, dV^T over all query tiles; phase B -- waves own query tiles and
-// accumulate dQ^T over all key tiles.  Q, K, V, dO and the transposed copies Q^T, K^T, dO^T
-// are staged in LDS once per (image, head group); rowsum(dO * O) is computed while staging.
+// accumulate dQ^T over all key tiles.  Q, K, V, dO are staged row-major in LDS once per
+// (image, head group) -- the Q^T, K^T, dO^T operands are transposed reads of them -- and
+// rowsum(dO * O) is computed while staging.
 #include "common.h"
 
 namespace {
@@ -19,24 +21,27 @@ ED_DEV v4f mma(const s4& a, const s4& b, const v4f& c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
 }
 ED_DEV s4 ld4(const bf16_t* p) { return *(const s4*)p; }
+// Transposed MFMA operand from a row-major LDS tile [rows][ld]: lane (l16, g) receives
+// t[r0 + 4g + i][c0 + l16], i = 0..3 -- the A (or B) fragment whose k runs along the tile's
+// rows -- via ds_read_b64_tr_b16: lane (tq, tp) = (l16 >> 2, l16 & 3) addresses row
+// r0 + 4g + tq, columns c0 + 4tp .. +3.  Needs every lane of the wave active.
+typedef __attribute__((address_space(3))) s4 lds_s4;
+ED_DEV s4 ldtr(const bf16_t* t, int ld, int r0, int c0, int l16, int g) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(t + (r0 + 4 * g + (l16 >> 2)) * ld + c0 + 4 * (l16 & 3)));
+}
 ED_DEV s4 pack4(float a, float b, float c, float d) {
   const uint2 u = {pack2(a, b), pack2(c, d)};
   return __builtin_bit_cast(s4, u);
 }
 
-// Transposed LDS copies use a row stride of rows + 8 elements (16 B of padding): the MFMA
-// operand reads take 16 consecutive rows per instruction, which an unpadded power-of-two
-// stride would put in the same LDS banks (16-way conflicts).
 // Stage one tensor (rows [S][DH] of head h of image b, row stride ld) for the hpb heads
-// bh0 .. bh0+hpb-1 of the workgroup into LDS row-major [SP][DP] per head (rm + hl * rm_hs)
-// and optionally transposed [DP][SP + 8] (tr + hl * tr_hs); zero padding.  Loads are issued U
-// at a time before their LDS writes: the staging of a small head used to be one dependent
-// global round trip per 16-byte chunk per thread (the latency of the short launches).
+// bh0 .. bh0+hpb-1 of the workgroup into LDS row-major [SP][DP] per head (rm + hl * rm_hs),
+// zero padding.  Loads are issued U at a time before their LDS writes.
 template <int DH, int DP, int U>
 ED_DEV void stage_heads_u(const bf16_t* __restrict__ base, long ld, int S, int SP, int H, int bh0, int hpb,
-                          bf16_t* rm, int rm_hs, bf16_t* tr, int tr_hs) {
+                          bf16_t* rm, int rm_hs) {
   constexpr int CH = DP / 8;
-  const int ph = SP * CH, total = hpb * ph, tld = SP + 8;
+  const int ph = SP * CH, total = hpb * ph;
   for (int e0 = threadIdx.x; e0 < total; e0 += 256 * U) {
     uint4 v[U];
     int hl[U], r[U], c8[U];
@@ -56,22 +61,17 @@ ED_DEV void stage_heads_u(const bf16_t* __restrict__ base, long ld, int S, int S
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (e0 + u * 256 >= total) break;
-      if (rm) *(uint4*)(rm + hl[u] * rm_hs + r[u] * DP + c8[u]) = v[u];
-      if (tr) {
-        const bf16_t* hv = (const bf16_t*)&v[u];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) tr[hl[u] * tr_hs + (c8[u] + k) * tld + r[u]] = hv[k];
-      }
+      *(uint4*)(rm + hl[u] * rm_hs + r[u] * DP + c8[u]) = v[u];
     }
   }
 }
 template <int DH, int DP>
 ED_DEV void stage_heads(const bf16_t* __restrict__ base, long ld, int S, int SP, int H, int bh0, int hpb,
-                        bf16_t* rm, int rm_hs, bf16_t* tr, int tr_hs) {
+                        bf16_t* rm, int rm_hs) {
   // several heads (short sequences): 4 chunks per thread in flight; one long head: the
   // plain loop measured faster (fewer live registers in the 2-workgroup-per-CU kernels)
-  if (hpb > 1) stage_heads_u<DH, DP, 4>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs, tr, tr_hs);
-  else stage_heads_u<DH, DP, 1>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs, tr, tr_hs);
+  if (hpb > 1) stage_heads_u<DH, DP, 4>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs);
+  else stage_heads_u<DH, DP, 1>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs);
 }
 
 constexpr float LOG2E = 1.4426950408889634f;
@@ -91,14 +91,14 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
   constexpr int KC = DP / 16;
   extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
   const int H = p.heads, SQ = p.sq, SK = p.sk;
-  const int SKP = (SK + 31) & ~31, TK = SKP + 8;
+  const int SKP = (SK + 31) & ~31;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const int bh0 = blockIdx.x * hpb;
   bf16_t* Ks = sm;                        // [hpb][SKP][DP]
-  bf16_t* Vt = sm + hpb * SKP * DP;       // [hpb][DP][TK] (padded rows)
-  stage_heads<DH, DP>((const bf16_t*)p.k, p.ldk, SK, SKP, H, bh0, hpb, Ks, SKP * DP, nullptr, 0);
-  stage_heads<DH, DP>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, nullptr, 0, Vt, DP * TK);
+  bf16_t* Vs = sm + hpb * SKP * DP;       // [hpb][SKP][DP], read transposed (ds_read_b64_tr_b16)
+  stage_heads<DH, DP>((const bf16_t*)p.k, p.ldk, SK, SKP, H, bh0, hpb, Ks, SKP * DP);
+  stage_heads<DH, DP>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, Vs, SKP * DP);
   __syncthreads();
   const int qtiles = (SQ + 15) >> 4, npairs = (qtiles + 1) >> 1;
   const float sl2 = p.scale * LOG2E;
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
     const int hl = task / npairs, qp = task - hl * npairs;
     const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
     const bf16_t* kb = Ks + hl * SKP * DP;
-    const bf16_t* vb = Vt + hl * DP * TK;
+    const bf16_t* vb = Vs + hl * SKP * DP;
     s4 qf[2][KC];
     int q[2];
 #pragma unroll
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
       for (int dt = 0; dt < KC; ++dt)
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const s4 vf = ld4(vb + (dt * 16 + l16) * TK + k0 + t * 16 + 4 * g);
+          const s4 vf = ldtr(vb, DP, k0 + t * 16, dt * 16, l16, g);  // V^T fragment
           o[0][dt] = mma(vf, pf[0][t], o[0][dt]);
           o[1][dt] = mma(vf, pf[1][t], o[1][dt]);
         }
@@ -210,19 +210,19 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const int bh0 = blockIdx.x * hpb;
-  // per head: Q, dO [SQP][DP]; Qt, dOt [DP][SQP + 8]; K, V [SKP][DP]; Kt [DP][SKP + 8]; lse2, D [SQP]
-  const int TQ = SQP + 8, TK = SKP + 8;
-  const int QE = SQP * DP, KE = SKP * DP, QT = DP * TQ;
-  const int oQt = QE, oG = QE + QT, oGt = 2 * QE + QT, oK = 2 * QE + 2 * QT, oV = oK + KE, oKt = oK + 2 * KE;
-  const int per_head = oKt + DP * TK;
+  // per head, row-major: Q, dO [SQP][DP]; K, V [SKP][DP]; lse2, D [SQP].  The transposed
+  // operands (Q^T, dO^T, K^T) are read with ds_read_b64_tr_b16 instead of being stored.
+  const int QE = SQP * DP, KE = SKP * DP;
+  const int oG = QE, oK = 2 * QE, oV = oK + KE;
+  const int per_head = oV + KE;
   float* fls = (float*)(sm + hpb * per_head);
   const int qtiles = SQP >> 4, ktiles = SKP >> 4;
   const int QS = attn_qsplit(ktiles, hpb);
   float* red = fls + hpb * 2 * SQP;  // phase-A partials [task][2][16*DP lanes-major] when QS > 1
-  stage_heads<DH, DP>((const bf16_t*)p.q, p.ldq, SQ, SQP, H, bh0, hpb, sm, per_head, sm + oQt, per_head);
-  stage_heads<DH, DP>((const bf16_t*)p.d_o, p.lddo, SQ, SQP, H, bh0, hpb, sm + oG, per_head, sm + oGt, per_head);
-  stage_heads<DH, DP>((const bf16_t*)p.k, p.ldk, SK, SKP, H, bh0, hpb, sm + oK, per_head, sm + oKt, per_head);
-  stage_heads<DH, DP>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, sm + oV, per_head, nullptr, 0);
+  stage_heads<DH, DP>((const bf16_t*)p.q, p.ldq, SQ, SQP, H, bh0, hpb, sm, per_head);
+  stage_heads<DH, DP>((const bf16_t*)p.d_o, p.lddo, SQ, SQP, H, bh0, hpb, sm + oG, per_head);
+  stage_heads<DH, DP>((const bf16_t*)p.k, p.ldk, SK, SKP, H, bh0, hpb, sm + oK, per_head);
+  stage_heads<DH, DP>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, sm + oV, per_head);
   // lse (log2 domain) and D = rowsum(dO * O) per query: 4 rows per thread in flight
   for (int e0 = tid; e0 < hpb * SQP; e0 += 256 * 4) {
     float lse[4], D[4];
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
     const int kt = rem / QS, qs = rem - kt * QS;
     const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
     const bf16_t* base = sm + hl * per_head;
-    const bf16_t *Qs = base, *Qt = base + oQt, *Gs = base + oG, *Gt = base + oGt;
+    const bf16_t *Qs = base, *Gs = base + oG;
     const bf16_t *Ks = base + oK, *Vs = base + oV;
     const float* lse = fls + hl * 2 * SQP;
     const float* Dv = lse + SQP;
@@ -301,8 +301,8 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
         const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);
 #pragma unroll
         for (int dt = 0; dt < KC; ++dt) {
-          dv[u][dt] = mma(ld4(Gt + (dt * 16 + l16) * TQ + qt * 16 + 4 * g), pf, dv[u][dt]);
-          dk[u][dt] = mma(ld4(Qt + (dt * 16 + l16) * TQ + qt * 16 + 4 * g), df, dk[u][dt]);
+          dv[u][dt] = mma(ldtr(Gs, DP, qt * 16, dt * 16, l16, g), pf, dv[u][dt]);  // dO^T fragment
+          dk[u][dt] = mma(ldtr(Qs, DP, qt * 16, dt * 16, l16, g), df, dk[u][dt]);  // Q^T fragment
         }
     };
     if (qtiles % (2 * QS) == 0) {
@@ -386,7 +386,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
     const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
     const bf16_t* base = sm + hl * per_head;
     const bf16_t *Qs = base, *Gs = base + oG;
-    const bf16_t *Ks = base + oK, *Vs = base + oV, *Kt = base + oKt;
+    const bf16_t *Ks = base + oK, *Vs = base + oV;
     const float* lse = fls + hl * 2 * SQP;
     const float* Dv = lse + SQP;
     const int q = qt * 16 + l16;
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
         const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);
 #pragma unroll
         for (int dt = 0; dt < KC; ++dt)
-          dq[u][dt] = mma(ld4(Kt + (dt * 16 + l16) * TK + kt * 16 + 4 * g), df, dq[u][dt]);
+          dq[u][dt] = mma(ldtr(Ks, DP, kt * 16, dt * 16, l16, g), df, dq[u][dt]);  // K^T fragment
     };
     if ((ktiles & 1) == 0) {
       for (int kt0 = 0; kt0 < ktiles; kt0 += 2) {
@@ -462,7 +462,7 @@ int launch_mfma_fwd(const EncdiffAttnArgs& a, hipStream_t s) {
   const int hpb = mfma_hpb(a);
   const int SKP = (a.sk + 31) & ~31;
   const int nblk = a.batch * a.heads / hpb;
-  const size_t lds = (size_t)hpb * (SKP + SKP + 8) * DP * sizeof(bf16_t);
+  const size_t lds = (size_t)hpb * 2 * SKP * DP * sizeof(bf16_t);
   if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
   const bool mask = a.sk % 32 != 0;
   const void* fn = mask ? (const void*)attn_fwd_mfma<DH, true> : (const void*)attn_fwd_mfma<DH, false>;
@@ -486,7 +486,7 @@ int launch_mfma_bwd(const EncdiffAttnArgs& a, hipStream_t s) {
   const int QS = attn_qsplit(SKP / 16, hpb);
   const size_t red = QS > 1 ? (size_t)hpb * (SKP / 16) * QS * 2 * 16 * DP * sizeof(float) : 0;
   const size_t lds =
-      (size_t)hpb * ((4 * SQP + 3 * SKP + 3 * 8) * DP * sizeof(bf16_t) + 2 * SQP * sizeof(float)) + red;
+      (size_t)hpb * ((2 * SQP + 2 * SKP) * DP * sizeof(bf16_t) + 2 * SQP * sizeof(float)) + red;
   if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
   static const hipError_t attr0 = hipFuncSetAttribute((const void*)attn_bwd_mfma<DH, false>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
