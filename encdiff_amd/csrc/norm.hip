@@ -586,7 +586,10 @@ int gn_min_slice() {
 int gn_slice(int C, int HW, int cpg, int batch) {
   int unit = 8;
   while (unit % cpg) unit += 8;
-  const long min_el = batch >= 64 ? gn_min_slice() : gn_min_slice() / 4;
+  // smaller images: smaller slices (more workgroups); measured per UNet level with
+  // tools/gn_bench.py: 8K elements at 16x16, 4K at 8x8, 2K at 4x4, 1K at 2x2
+  const int shrink = HW >= 256 ? 1 : (HW >= 64 ? 2 : (HW >= 16 ? 4 : 8));
+  const long min_el = (batch >= 64 ? gn_min_slice() : gn_min_slice() / 4) / shrink;
   for (int w = unit; w < C; w += unit)
     if (C % w == 0 && (long)w * HW >= min_el) return w;
   return C;
