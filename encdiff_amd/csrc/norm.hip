@@ -530,36 +530,51 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const EncdiffLayerNormArgs 
   float ga[8], dga[8], dbe[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { ga[i] = p.gamma[lr * 8 + i]; dga[i] = 0.f; dbe[i] = 0.f; }
-  for (int row = blockIdx.x * RPB + rr; row < p.rows; row += gridDim.x * RPB) {
-    float v[8], d[8];
-    unpack8(*(const uint4*)((const bf16_t*)p.x + (long)row * p.ldx + lr * 8), v);
-    unpack8(*(const uint4*)((const bf16_t*)p.dy + (long)row * p.lddy + lr * 8), d);
-    const float mean = p.stats[2 * row], rstd = p.stats[2 * row + 1];
-    float s1 = 0.f, s2 = 0.f, xh[8];
+  // two rows per thread in flight: every load of both is issued before either's store (the
+  // stores to dx may alias the loaded tensors, so the compiler would not hoist them itself)
+  constexpr int U = 2;
+  const int stride = gridDim.x * RPB;
+  for (int row0 = blockIdx.x * RPB + rr; row0 < p.rows; row0 += U * stride) {
+    float v[U][8], d[U][8], o8[U][8], mean[U], rstd[U];
+    bool rp_on[U];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      xh[i] = (v[i] - mean) * rstd;
-      const float g = d[i] * ga[i];
-      s1 += g; s2 += g * xh[i];
-      dga[i] += d[i] * xh[i];
-      dbe[i] += d[i];
+    for (int u = 0; u < U; ++u) {
+      const int row = row0 + u * stride;
+      rp_on[u] = false;
+      if (row >= p.rows) continue;
+      unpack8(*(const uint4*)((const bf16_t*)p.x + (long)row * p.ldx + lr * 8), v[u]);
+      unpack8(*(const uint4*)((const bf16_t*)p.dy + (long)row * p.lddy + lr * 8), d[u]);
+      mean[u] = p.stats[2 * row];
+      rstd[u] = p.stats[2 * row + 1];
+      // residual-branch gradient: dx itself (in place) or a separate tensor (out of place, so a
+      // weight gradient still reading that tensor on another stream is not overwritten)
+      const bf16_t* rp = p.resid ? (const bf16_t*)p.resid + (long)row * p.ld_resid + lr * 8
+                                 : (p.accumulate_dx ? (const bf16_t*)p.dx + (long)row * p.lddx + lr * 8 : nullptr);
+      if (rp) { unpack8(*(const uint4*)rp, o8[u]); rp_on[u] = true; }
     }
 #pragma unroll
-    for (int o = LPR / 2; o > 0; o >>= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
-    s1 *= (1.f / C); s2 *= (1.f / C);
-    bf16_t* dxp = (bf16_t*)p.dx + (long)row * p.lddx + lr * 8;
-    float o8[8];
-    // residual-branch gradient: dx itself (in place) or a separate tensor (out of place, so a
-    // weight gradient still reading that tensor on another stream is not overwritten)
-    const bf16_t* rp = p.resid ? (const bf16_t*)p.resid + (long)row * p.ld_resid + lr * 8
-                               : (p.accumulate_dx ? dxp : nullptr);
-    if (rp) unpack8(*(const uint4*)rp, o8);
+    for (int u = 0; u < U; ++u) {
+      const int row = row0 + u * stride;
+      if (row >= p.rows) continue;  // (uniform across the row's LPR lanes)
+      float s1 = 0.f, s2 = 0.f, xh[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float r = rstd * (d[i] * ga[i] - s1 - xh[i] * s2);
-      o8[i] = rp ? o8[i] + r : r;
+      for (int i = 0; i < 8; ++i) {
+        xh[i] = (v[u][i] - mean[u]) * rstd[u];
+        const float g = d[u][i] * ga[i];
+        s1 += g; s2 += g * xh[i];
+        dga[i] += d[u][i] * xh[i];
+        dbe[i] += d[u][i];
+      }
+#pragma unroll
+      for (int o = LPR / 2; o > 0; o >>= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      s1 *= (1.f / C); s2 *= (1.f / C);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float r = rstd[u] * (d[u][i] * ga[i] - s1 - xh[i] * s2);
+        o8[u][i] = rp_on[u] ? o8[u][i] + r : r;
+      }
+      *(uint4*)((bf16_t*)p.dx + (long)row * p.lddx + lr * 8) = pack8(o8[u]);
     }
-    *(uint4*)dxp = pack8(o8);
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) { red[0][rr][lr * 8 + i] = dga[i]; red[1][rr][lr * 8 + i] = dbe[i]; }
