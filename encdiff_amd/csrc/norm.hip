@@ -461,29 +461,48 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   bf16_t* DX = (bf16_t*)p.dx + off * p.lddx + L.cb;
   const bool accum = p.accumulate_dx;
   const bf16_t* RS = p.resid ? (const bf16_t*)p.resid + off * p.ld_resid + L.cb : nullptr;
-#pragma unroll 1
-  for (int px = L.tp; px < HW; px += L.np) {
-    float v[8], d[8], o[8];
-    unpack8(gn_row(L, tx, X, p.ldx, px), v);
-    unpack8(gn_row(L, td, DY, p.lddy, px), d);
-    if (accum) unpack8(*(const uint4*)(DX + (long)px * p.lddx), o);
-    if (RS) {  // residual-branch gradient added in the same pass (skip connection of the block)
-      float rr[8];
-      unpack8(*(const uint4*)(RS + (long)px * p.ld_resid), rr);
+  // U rows per thread: the global (resid / accumulate) reads of all U are issued before the
+  // first dx store -- one latency per U rows instead of one per row
+  constexpr int U = 4;
+  for (int px0 = L.tp; px0 < HW; px0 += U * L.np) {
+    uint4 gr[U];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = (accum ? o[i] : 0.f) + rr[i];
+    for (int u = 0; u < U; ++u) {
+      const int px = px0 + u * L.np;
+      gr[u] = (uint4){0u, 0u, 0u, 0u};
+      if (px < HW) {
+        if (RS) gr[u] = *(const uint4*)(RS + (long)px * p.ld_resid);
+        else if (accum) gr[u] = *(const uint4*)(DX + (long)px * p.lddx);
+      }
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float xh = (v[i] - xm[i]) * xr[i];
-      const float n = xh * ga[i] + be[i];
-      const float z = n * sc1[i] + sf[i];
-      const float dz = silu ? d[i] * silu_grad(z) : d[i];
-      const float dn = dz * sc1[i];
-      const float r = xr[i] * (dn * ga[i] - m1[i] - xh * m2[i]);
-      o[i] = (accum || RS) ? o[i] + r : r;
+    for (int u = 0; u < U; ++u) {
+      const int px = px0 + u * L.np;
+      if (px >= HW) break;
+      float v[8], d[8], o[8];
+      unpack8(gn_row(L, tx, X, p.ldx, px), v);
+      unpack8(gn_row(L, td, DY, p.lddy, px), d);
+      if (RS && accum) {  // both: dx (in place) + resid
+        float rr[8];
+        unpack8(*(const uint4*)(DX + (long)px * p.lddx), o);
+        unpack8(gr[u], rr);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] += rr[i];
+      } else if (RS || accum) {
+        unpack8(gr[u], o);  // residual-branch gradient (skip connection) or the dx being accumulated
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xh = (v[i] - xm[i]) * xr[i];
+        const float n = xh * ga[i] + be[i];
+        const float z = n * sc1[i] + sf[i];
+        const float dz = silu ? d[i] * silu_grad(z) : d[i];
+        const float dn = dz * sc1[i];
+        const float r = xr[i] * (dn * ga[i] - m1[i] - xh * m2[i]);
+        o[i] = (accum || RS) ? o[i] + r : r;
+      }
+      *(uint4*)(DX + (long)px * p.lddx) = pack8(o);
     }
-    *(uint4*)(DX + (long)px * p.lddx) = pack8(o);
   }
 }
 
