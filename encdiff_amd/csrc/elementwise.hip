@@ -430,9 +430,22 @@ __global__ __launch_bounds__(256) void adamw_ema_kernel(float* __restrict__ p, c
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst,
                                                    const EncdiffPackJob* __restrict__ jobs) {
   const EncdiffPackJob j = jobs[blockIdx.y];
-  const long total = (long)j.rows * j.cols;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int r = (int)(i / j.cols), c = (int)(i - (long)r * j.cols);
+  const int total = j.rows * j.cols;  // < 2^31 (host)
+  const int stride = gridDim.x * 256;
+  if (j.kind == 0 && (total & 7) == 0 && (j.src_off & 3) == 0 && (j.dst_off & 7) == 0) {
+    // plain copy-cast: 8 elements per lane (two float4 loads, one 16-byte store)
+    const float* s0 = src + j.src_off;
+    bf16_t* d0 = dst + j.dst_off;
+    for (int i = (blockIdx.x * 256 + threadIdx.x) * 8; i < total; i += stride * 8) {
+      float v[8];
+      const float4 a = *(const float4*)(s0 + i), b = *(const float4*)(s0 + i + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      *(uint4*)(d0 + i) = pack8(v);
+    }
+    return;
+  }
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += stride) {
+    const int r = i / j.cols, c = i - r * j.cols;  // 32-bit: the 64-bit divide was most of the time
     long s;
     if (j.kind == 1) {  // conv [co][ci][3][3] -> [co][tap][ci]; c = tap*cin + ci
       const int tap = c / j.cin, ci = c - tap * j.cin;
@@ -617,7 +630,7 @@ extern "C" int encdiff_adamw_ema(float* p, const float* g, float* m, float* v, f
 
 extern "C" int encdiff_pack_weights(const float* src, void* dst, const EncdiffPackJob* jobs, int njobs, void* stream) {
   if (!src || !dst || !jobs || njobs <= 0 || njobs > 65535) return ENCDIFF_ERR_ARG;
-  hipLaunchKernelGGL(pack_kernel, dim3(64, njobs), dim3(256), 0, (hipStream_t)stream, src, (bf16_t*)dst, jobs);
+  hipLaunchKernelGGL(pack_kernel, dim3(128, njobs), dim3(256), 0, (hipStream_t)stream, src, (bf16_t*)dst, jobs);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
