@@ -233,7 +233,7 @@ def linear_fwd_ln(x, w, out, gamma, beta, y, stats, eps, bias=None, resid=None):
     the GEMM epilogue when the planned tile spans the row, else the LayerNorm kernel."""
     M, K = x.shape
     N = w.shape[0]
-    if not LN_FUSED or N > 128 or N % 8:
+    if not LN_FUSED or N > 128 or N % 8 or M < 8192:  # small (sampling) batches keep split-K
         linear_fwd(x, w, out, bias=bias, resid=resid)
         layernorm_fwd(out, gamma, beta, y, stats, eps)
         return

@@ -371,7 +371,7 @@ class UNetExecutor:
         channel sums (EncdiffGemmArgs.gn_stats); a concat input's two producers fill their
         channel ranges of one buffer.  Keyed by the tensor's data pointer."""
         self.gst = {}
-        if not GN_FROM_PRODUCER:
+        if not GN_FROM_PRODUCER or B < 64:  # small (sampling) batches: the producers keep split-K
             return
         sp = self.spec
 
