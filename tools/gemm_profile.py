@@ -135,7 +135,11 @@ def main():
         # weight gradients run inside the paired kernel (64 x 64 tiles, k stages 64 or 128) with their slabs in
         # one workspace half (deferred finalize): only splits that fit are candidates
         wgrad = a.a_mode == L.OPA_ROWM
-        for tile in ((4, 7) if wgrad else (1, 2, 3, 4, 5, 6, 7, 8)):
+        # input gradients run paired with their weight gradient: one grid sizes every workgroup's
+        # LDS for the larger tile, so the deep-ring / deep-k tiles (5-8) cost the weight-gradient
+        # blocks occupancy in the step (this standalone timing cannot see it): not candidates
+        dgrad = a.b_mode in (L.OPB_ROWN, L.OPB_CONV_DGRAD) and not wgrad
+        for tile in ((4, 7) if wgrad else ((1, 2, 3, 4) if dgrad else (1, 2, 3, 4, 5, 6, 7, 8))):
             for split in (1, 2, 4, 8, 16, 32, 64, 128, 256):
                 if split > 1 and a.K // split < 64:
                     continue
