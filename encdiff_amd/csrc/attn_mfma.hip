@@ -509,6 +509,8 @@ int encdiff_attention_mfma(const EncdiffAttnArgs* a, bool bwd, void* stream) {
     case 8: return bwd ? launch_mfma_bwd<8>(*a, s) : launch_mfma_fwd<8>(*a, s);
     case 16: return bwd ? launch_mfma_bwd<16>(*a, s) : launch_mfma_fwd<16>(*a, s);
     case 32: return bwd ? launch_mfma_bwd<32>(*a, s) : launch_mfma_fwd<32>(*a, s);
+    // wider UNets (configs[4], model_channels=128: C=512 over 8 heads at the 8x8 / 4x4 levels)
+    case 64: return bwd ? launch_mfma_bwd<64>(*a, s) : launch_mfma_fwd<64>(*a, s);
     case 128:  // single-head AttnBlock of the VQ encoder (model.py AttnBlock): forward only (frozen)
       return bwd ? ENCDIFF_ERR_UNSUPPORTED : launch_mfma_fwd<128>(*a, s);
     default: return ENCDIFF_ERR_UNSUPPORTED;

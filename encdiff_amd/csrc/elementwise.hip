@@ -529,9 +529,9 @@ extern "C" int encdiff_small_conv_bwd(const EncdiffSmallConvArgs* a, void* strea
   if (!a || !a->x || !a->dy || !a->weight) return ENCDIFF_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int HW = a->h * a->w;
-  if (a->cout * a->cin * 9 > 256 * 8) return ENCDIFF_ERR_SHAPE;
   if (a->dx) {
     if (!a->dy_f32 || a->cout > 3 || a->cin % 8) return ENCDIFF_ERR_UNSUPPORTED;
+    if (a->cin > 512) return ENCDIFF_ERR_SHAPE;  // LDS weight copy holds 3 x 9 x 512
     hipLaunchKernelGGL(small_conv_out_dgrad, dim3(grid_for((long)a->batch * HW * (a->cin / 8))), dim3(256), 0, s,
                        *a);
     ED_CHECK_LAUNCH();
