@@ -642,9 +642,11 @@ extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream
   if (!a || !a->x || !a->y || !a->stats || !a->gamma || !a->beta) return ENCDIFF_ERR_ARG;
   const int cs = gn_check(a);
   if (cs < 0) return cs;
-  if (a->in_stats && a->hw >= 1024) {  // large images: group-statistics kernel + streaming apply
-    if (a->hw % 64 || a->ld_in_stats < a->c || a->c > 512 || a->groups > 64 || GN_THREADS % (a->c >> 3))
-      return ENCDIFF_ERR_ARG;
+  // producer statistics feed the two statistics kernels where their layout fits; other
+  // shapes (e.g. a 384-channel concat at 32x32) take the self-reducing kernel below
+  const bool st_ok = a->in_stats && a->hw % 64 == 0 && a->ld_in_stats >= a->c;
+  if (st_ok && a->hw >= 1024 && a->c <= 512 && a->groups <= 64 && GN_THREADS % (a->c >> 3) == 0) {
+    // large images: group-statistics kernel + streaming apply
     hipLaunchKernelGGL(gn_group_stats_kernel, dim3(a->batch), dim3(GN_THREADS), 0, (hipStream_t)stream, *a);
     const int rpb = 256;
     hipLaunchKernelGGL(gn_apply_kernel, dim3((a->hw + rpb - 1) / rpb, a->batch), dim3(GN_THREADS), 0,
@@ -652,8 +654,7 @@ extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream
     ED_CHECK_LAUNCH();
     return ENCDIFF_OK;
   }
-  if (a->in_stats) {  // statistics from the producer GEMM's segment sums
-    if (a->hw % 64 || a->ld_in_stats < a->c || (a->hw / 64) * cs > 2048) return ENCDIFF_ERR_ARG;
+  if (st_ok && (a->hw / 64) * cs <= 2048) {  // statistics from the producer GEMM's segment sums
     hipLaunchKernelGGL(gn_fwd_stats_kernel, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream,
                        *a, cs);
     ED_CHECK_LAUNCH();

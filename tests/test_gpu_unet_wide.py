@@ -87,15 +87,24 @@ def test_wide_unet_fwd_bwd_matches_oracle(wide):
 
 
 def test_wide_unet_batch_consistency(wide):
-    """Image i's output does not depend on the batch it runs in (B=4 vs its own B=1 run) beyond
-    bf16 rounding: the GEMM tile / split-K plan differs per batch size, so the summation
-    order (and each bf16 rounding after it) differs; bound = the eps tolerance."""
+    """Training batch sizes switch on the producer-statistics GroupNorm and the training GEMM
+    plans; image i's eps and d(context) at B=64 must match its own B=1 run (oracle-pinned
+    path above) up to bf16 rounding: the GEMM tile / split-K plan differs per batch size, so
+    the summation order (and each bf16 rounding after it) differs; bound = the tolerances."""
     m, _, _ = wide
     torch.manual_seed(8)
-    x = torch.randn(4, 3, 32, 32, device="cuda")
-    t = torch.randint(0, 1000, (4,), device="cuda")
-    c = torch.randn(4, 640, device="cuda")
-    with torch.no_grad():
-        full = m(x, t, [c]).clone()
-        one = m(x[2:3], t[2:3], [c[2:3]]).clone()
-    assert rel(one, full[2:3]) < EPS_TOL
+    B, i = 64, 37
+    x = torch.randn(B, 3, 32, 32, device="cuda")
+    t = torch.randint(0, 1000, (B,), device="cuda")
+    c = torch.randn(B, 640, device="cuda")
+    g = torch.randn(B, 3, 32, 32, device="cuda")
+    cf = c.clone().requires_grad_(True)
+    full = m(x, t, [cf])
+    full.backward(g)
+    c1 = c[i:i + 1].clone().requires_grad_(True)
+    one = m(x[i:i + 1], t[i:i + 1], [c1])
+    one.backward(g[i:i + 1])
+    e = rel(one.detach(), full.detach()[i:i + 1])
+    d = rel(c1.grad, cf.grad[i:i + 1])
+    print("B=64 vs B=1 eps", e, "dctx", d)
+    assert e < EPS_TOL and d < GRAD_TOL
