@@ -201,7 +201,22 @@ class NormPartials:
         base = self.slots[gamma_name]
         return self.buf[:, base:base + c], self.buf[:, base + c:base + 2 * c]
 
-    def reduce(self):
+    def reduce(self, lo: int = 0, hi: Optional[int] = None):
+        """Fold columns [lo, hi) (default: all) into the gradient arena."""
         from . import ops
-        if self.cols:
-            ops.reduce_partials(self.buf, self.ld, self.rows, self.cols, self.index_dev, self.arena.grad)
+        hi = self.cols if hi is None else hi
+        if hi > lo:
+            ops.reduce_partials(self.buf[:, lo:], self.ld, self.rows, hi - lo, self.index_dev[lo:],
+                                self.arena.grad)
+
+    def split_col(self, sel) -> Optional[int]:
+        """Column c such that the layers `sel(gamma_name)` selects own exactly [c, cols)
+        (None when they do not form that suffix)."""
+        names = sorted(self.slots, key=self.slots.get)
+        flags = [bool(sel(n)) for n in names]
+        if not any(flags):
+            return self.cols
+        k = flags.index(True)
+        if not all(flags[k:]):
+            return None
+        return self.slots[names[k]]

@@ -70,7 +70,12 @@ class FusedArenaAdamW(torch.optim.Optimizer):
         self.ema = ema
         self.repack = repack
         self.step_count = 0
-        self._host = torch.zeros(8, dtype=torch.float32).pin_memory() if torch.cuda.is_available() else None
+        # ring of pinned staging rows: a row is rewritten only after the H2D copy that read it
+        # has run (its event), so a host running steps ahead of the GPU never changes the
+        # scalars of a step still queued
+        self._host = torch.zeros(4, 8, dtype=torch.float32).pin_memory() if torch.cuda.is_available() else None
+        self._host_ev = [None] * 4
+        self._host_i = 0
 
     def hyper_values(self):
         g = self.param_groups[0]
@@ -84,8 +89,15 @@ class FusedArenaAdamW(torch.optim.Optimizer):
         self._opt_called = True  # tells torch LR schedulers the optimizer stepped (launch() bypasses step())
         vals = self.hyper_values()
         if self._host is not None:
-            self._host.copy_(torch.tensor(vals, dtype=torch.float32))
-            self.arena.hyper.copy_(self._host, non_blocking=True)
+            i = self._host_i
+            self._host_i = (i + 1) % len(self._host_ev)
+            if self._host_ev[i] is not None:
+                self._host_ev[i].synchronize()
+            row = self._host[i]
+            row.copy_(torch.tensor(vals, dtype=torch.float32))
+            self.arena.hyper.copy_(row, non_blocking=True)
+            ev = self._host_ev[i] = self._host_ev[i] or torch.cuda.Event()
+            ev.record()
         else:
             self.arena.hyper.copy_(torch.tensor(vals, dtype=torch.float32))
 

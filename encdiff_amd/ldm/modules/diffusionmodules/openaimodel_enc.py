@@ -72,7 +72,9 @@ class _UNetFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        dc = ctx.ex.backward(g.float())
+        # ex.split_requested (data-parallel trainer): only the output blocks run here; the
+        # d(context) buffer is filled by ex.backward_rest(), which the trainer calls itself
+        dc = ctx.ex.backward(g.float(), split=ctx.ex.split_requested)
         return None, None, dc.clone(), None
 
 

@@ -7,19 +7,23 @@ Step = (per rank)
   eps_hat = UNet(x_t, t, c)          (HIP executor, forward)
   L1 loss + gradient seed            (HIP)
   backward: UNet (HIP) -> d c -> Encoder4 (torch autograd)
-  [world > 1: RCCL all-reduce (mean) of the gradient arena in two buckets (dp.py):
-   the UNet bucket on a side stream while Encoder4's backward runs, then Encoder4's]
+  [world > 1: RCCL all-reduce (mean) of the gradient arena in buckets (dp.py), each on a
+   side stream as soon as its gradients are final: the output-block / out parameters while
+   the rest of the UNet backward runs, the remaining UNet parameters while Encoder4's
+   backward runs, then Encoder4's]
   AdamW + EMA over the flat arena, bf16 repack of GEMM weights   (HIP)
 
 The device work of a step is replayed from captured graphs: one graph for the
-single-GPU step; with DP three graphs sharing one memory pool -- (forward + UNet
-backward), (Encoder4 backward), (optimizer) -- around the bucket all-reduces.  Only the per-step scalars (lr, bias corrections,
+single-GPU step; with DP four graphs sharing one memory pool -- (forward + UNet output-block
+backward), (rest of the UNet backward), (Encoder4 backward), (optimizer) -- around the bucket
+all-reduces.  Only the per-step scalars (lr, bias corrections,
 EMA decay) cross the host->device boundary, through a pinned 8-float buffer.
 Reference: ddpm_enc.py:360-375, 399-401, 1040-1053, 1183-1253, 1598-1639;
 main_val.py:818-842 (lr = ngpu * batch * base_lr).
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Optional
 
@@ -51,6 +55,13 @@ class HipTrainer:
             self.opt, self.sched = opt, None
         self.buckets = GradBuckets.from_arena(arena)
         self._comm = torch.cuda.Stream() if self.world > 1 else None
+        self.unet = ldm.model.diffusion_model
+        # DP: split the UNet backward after the output blocks so their gradient bucket is
+        # all-reduced while the middle / input blocks run (ENCDIFF_DP_SPLIT=0 disables)
+        self._split_want = self.world > 1 and os.environ.get("ENCDIFF_DP_SPLIT", "1") != "0"
+        self._split_lo: Optional[int] = None
+        self._split_checked = False
+        self._g_rest = None
         if data is None:  # synthetic uint8 images of the Shapes3D shape/size, resident in HBM
             data = ImagePool.synthetic(pool_size, batch_size, self.dev, seed=seed, rank=self.rank, world=self.world)
         self.data = data
@@ -86,10 +97,34 @@ class HipTrainer:
         else:
             c_det = c.detach().requires_grad_(True)
             loss, ld = ldm.p_losses(z, c_det, t, noise)
+            ex = self.unet._ex
+            if not self._split_checked:
+                self._plan_split(ex)
+            ex.split_requested = self._split_lo is not None
             loss.backward()
-            self._c, self._dc = c, c_det.grad
+            ex.split_requested = False
+            # split: d(context) is the executor's buffer, complete after backward_rest()
+            self._c, self._dc = c, (ex.d_ctx if self._split_lo is not None else c_det.grad)
         self.loss_buf[0].copy_(ld["train/loss_simple"])
         self.loss_buf[1].copy_(ld["train/loss_vlb"])
+
+    def _plan_split(self, ex):
+        """Bucket bounds [0, lo) remaining UNet, [lo, ema_numel) output blocks + out,
+        [ema_numel, numel) cond stage -- when the arena layout allows the split."""
+        self._split_checked = True
+        if not self._split_want:
+            return
+        a = self.arena
+        lo = ex.split_plan(list(dict(self.unet.named_parameters())))
+        if lo is None or not 0 < lo < a.ema_numel < a.numel:
+            return
+        if any(lo <= o < a.ema_numel and not ex._early_final(n) for n, (o, _) in a.offsets.items()):
+            return
+        self._split_lo = lo
+        self.buckets = GradBuckets(a.grad, [0, lo, a.ema_numel, a.numel], self.buckets.group)
+
+    def _unet_rest(self):
+        self.unet._ex.backward_rest()
 
     def _cond_bwd(self):
         self._c.backward(self._dc)
@@ -97,10 +132,27 @@ class HipTrainer:
         # nodes created on another stream, which breaks the next capture
         self._c = self._dc = None
 
-    def _exchange(self, cond_bwd):
-        """DP gradient mean: bucket 0 (UNet) on the side stream overlapped with the cond
-        stage backward, then bucket 1 (cond stage); the current stream waits for both."""
+    def _exchange(self, cond_bwd, unet_rest=None):
+        """DP gradient mean.  Unsplit: bucket 0 (UNet) on the side stream overlapped with
+        the cond stage backward, then bucket 1 (cond stage).  Split (`unet_rest` given):
+        bucket 1 (output blocks + out) overlapped with the rest of the UNet backward, bucket 0
+        (remaining UNet) with the cond stage backward, then bucket 2.  The current stream
+        waits for all of them."""
         cur = torch.cuda.current_stream()
+        if unet_rest is not None:
+            self._comm.wait_stream(cur)
+            with torch.cuda.stream(self._comm):
+                w_out = self.buckets.start(1)
+            unet_rest()
+            self._comm.wait_stream(cur)
+            with torch.cuda.stream(self._comm):
+                w_unet = self.buckets.start(0)
+            cond_bwd()
+            w_cond = self.buckets.start(2)
+            self.buckets.finish(1, w_out)
+            self.buckets.finish(0, w_unet)
+            self.buckets.finish(2, w_cond)
+            return
         self._comm.wait_stream(cur)
         with torch.cuda.stream(self._comm):
             w0 = self.buckets.start(0)
@@ -137,6 +189,10 @@ class HipTrainer:
                     self.opt.launch()
             if self.world > 1:
                 pool = self._g_fb.pool()
+                if self._split_lo is not None:
+                    self._g_rest = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self._g_rest, stream=s, pool=pool):
+                        self._unet_rest()
                 self._g_cond = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self._g_cond, stream=s, pool=pool):
                     self._cond_bwd()
@@ -151,7 +207,7 @@ class HipTrainer:
         self.opt.stage_hyper()
         self._fwd_bwd()
         if self.world > 1:
-            self._exchange(self._cond_bwd)
+            self._exchange(self._cond_bwd, self._unet_rest if self._split_lo is not None else None)
         self.opt.launch()
         self._post()
 
@@ -161,7 +217,7 @@ class HipTrainer:
         self.opt.stage_hyper()
         self._g_fb.replay()
         if self.world > 1:
-            self._exchange(self._g_cond.replay)
+            self._exchange(self._g_cond.replay, self._g_rest.replay if self._g_rest is not None else None)
             self._g_opt.replay()
         self._post()
 

@@ -22,7 +22,7 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence
 
 import torch
 
@@ -249,6 +249,8 @@ class UNetExecutor:
         for t in spec.sts:
             self._gn_names.append((t.prefix + "norm.weight", t.prefix + "norm.bias"))
         self._gn_names.append(("out.0.weight", "out.0.bias"))
+        # output-block / out columns last: the split backward folds that suffix early
+        self._gn_names.sort(key=lambda p: self._early_final(p[0]))
         self.ln = NormPartials(arena, ops.LN_PARTS)
         for t in spec.sts:
             tb = t.prefix + "transformer_blocks.0."
@@ -258,6 +260,7 @@ class UNetExecutor:
         self.gn: Optional[NormPartials] = None
         self.B = None
         self._sets: Dict[int, dict] = {}
+        self.split_requested = False  # data-parallel trainer: backward(split=True) via autograd
         self._base_names = set(self.__dict__) | {"_base_names"}
         self.pack.repack()
 
@@ -292,6 +295,8 @@ class UNetExecutor:
             self.__dict__.update(self._sets[B])
             return
         sp = self.spec
+        self._split = False  # split_plan() not computed for this batch size yet
+        self._cont = None
         self.gn = NormPartials(self.arena, B)
         for gname, bname in self._gn_names:
             self.gn.add(gname, bname)
@@ -560,9 +565,69 @@ class UNetExecutor:
         return S["out"]
 
     # ---------------------------------------------------------------- backward
-    def backward(self, d_eps: torch.Tensor) -> torch.Tensor:
+    # ---------------------------------------------------------------- split backward (DP)
+    @staticmethod
+    def _early_final(name: str) -> bool:
+        """Parameters whose gradient is complete once the output blocks' backward has run
+        (the batched emb / cross-K/V / q,k,v weights are written later or live in the arena
+        prefix, so they never count)."""
+        n = name.split("diffusion_model.", 1)[-1]
+        if not (n.startswith("output_blocks.") or n.startswith("out.")):
+            return False
+        return not any(k in n for k in (".emb_layers.1.", ".attn2.to_k.", ".attn2.to_v.", ".attn1.to_q.",
+                                        ".attn1.to_k.", ".attn1.to_v."))
+
+    def split_plan(self, names: Sequence[str]) -> Optional[int]:
+        """For data-parallel overlap: the arena offset `lo` such that [lo, end of the UNet
+        parameters) holds exactly the output-block / out parameters (their gradients are final
+        after `backward(split=True)`, and can be all-reduced while `backward_rest` runs), and
+        the GroupNorm / LayerNorm partial columns of those layers form suffixes.  None when the
+        layout does not allow it (the caller then runs the backward unsplit)."""
+        if getattr(self, "_split", False) is not False:
+            return self._split[0] if self._split else None
+        self._split = None
+        offs = {n: self.arena.offsets[n] for n in names}
+        span = {n: (o, o + int(torch.Size(sh).numel())) for n, (o, sh) in offs.items()}
+        early = [n for n in names if self._early_final(n)]
+        if not early:
+            return None
+        lo = min(span[n][0] for n in early)
+        if any(span[n][1] > lo for n in names if not self._early_final(n)):
+            return None
+        gcol = self.gn.split_col(self._early_final)
+        lcol = self.ln.split_col(self._early_final)
+        if gcol is None or lcol is None:
+            return None
+        self._split = (lo, gcol, lcol)
+        return lo
+
+    def backward(self, d_eps: torch.Tensor, split: bool = False) -> torch.Tensor:
         """d_eps (B,C,H,W) fp32 -> d_context (B, latent_unit*context_dim) fp32.  Accumulates
-        every UNet weight gradient into the arena (which the caller zeroed)."""
+        every UNet weight gradient into the arena (which the caller zeroed).
+
+        split=True (data-parallel overlap, needs a successful `split_plan`): stop after the
+        output blocks with their gradients final in the arena; `backward_rest()` then runs the
+        middle / input blocks and the batched emb / K,V GEMMs and fills the returned d_context
+        buffer.  Launch for launch the same work as the unsplit backward (the last deferred
+        finalize and the norm partial fold are issued in two parts)."""
+        out = self._bwd_outputs(d_eps)
+        if split and self._split:
+            _, gcol, lcol = self._split
+            ops.flush()
+            self.gn.reduce(gcol)
+            self.ln.reduce(lcol)
+            self._cont = out
+            return self.d_ctx
+        self._cont = None
+        return self._bwd_rest(out, self.gn.cols, self.ln.cols)
+
+    def backward_rest(self) -> torch.Tensor:
+        assert self._cont is not None, "backward_rest() follows backward(split=True)"
+        out, self._cont = self._cont, None
+        _, gcol, lcol = self._split
+        return self._bwd_rest(out, gcol, lcol)
+
+    def _bwd_outputs(self, d_eps: torch.Tensor):
         B = self.B
         sp = self.spec
         g0 = Geom(B, self.H, self.H)
@@ -598,6 +663,14 @@ class UNetExecutor:
             c1 = blk[0].cin - sp.skip_ch[nhs - 1 - j]
             g_hs[nhs - 1 - j] = self.dxcat[j][:, c1:]
             dout = self.dxcat[j][:, :c1]
+        return dout, g_hs
+
+    def _bwd_rest(self, state, gcol: int, lcol: int) -> torch.Tensor:
+        B = self.B
+        sp = self.spec
+        g0 = Geom(B, self.H, self.H)
+        dout, g_hs = state
+        nhs = len(self._hs)
         # middle block: its input is hs[-1]
         for li in range(len(sp.middle) - 1, -1, -1):
             layer = sp.middle[li]
@@ -641,9 +714,10 @@ class UNetExecutor:
                  self.d_ctx, self.cd, b_mode=L.OPB_ROWN, c_mode=L.OUT_F32)
         ops.linear_wgrad(self.dKV, self.ctx16, self.kv_w_grad)
         ops.flush()  # the last deferred weight-gradient finalize
-        # fold all norm affine partial sums into the arena
-        self.gn.reduce()
-        self.ln.reduce()
+        # fold the norm affine partial sums into the arena (all of them, or what the split
+        # backward left: the columns before the output blocks' suffix)
+        self.gn.reduce(0, gcol)
+        self.ln.reduce(0, lcol)
         return self.d_ctx
 
     def conv_bwd(self, dy, g, cin, name, x, dx, db, resample=0):

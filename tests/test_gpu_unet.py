@@ -84,3 +84,46 @@ def test_unet_deterministic(unet):
         a = unet(x, t, [c]).clone()
         b = unet(x, t, [c]).clone()
     assert torch.equal(a, b)
+
+
+def test_unet_split_backward_bitwise(unet):
+    """The data-parallel trainer's split backward (output blocks, then `backward_rest`) is
+    launch for launch the unsplit backward: gradients and d(context) bitwise equal, and the
+    output-block bucket [lo, end) is final after the first part."""
+    torch.manual_seed(17)
+    B = 64  # a training batch size: producer-statistics GroupNorm and the training GEMM plans
+    x = torch.randn(B, 3, 16, 16, device="cuda")
+    t = torch.randint(0, 1000, (B,), device="cuda")
+    c = torch.randn(B, 320, device="cuda")
+    g = torch.randn(B, 3, 16, 16, device="cuda")
+    names = [n for n, _ in unet.named_parameters()]
+
+    def run(split):
+        ex = unet.executor()
+        unet._arena.zero_grad()
+        cc = c.clone().requires_grad_(True)
+        eps = unet(x, t, context=[cc])
+        ex.split_requested = split
+        if split:
+            lo = ex.split_plan(names)
+            assert lo is not None
+        eps.backward(g)
+        ex.split_requested = False
+        part = None
+        if split:
+            torch.cuda.synchronize()
+            part = unet._arena.grad[lo:].clone()
+            ex.backward_rest()
+            dctx = ex.d_ctx.clone()
+        else:
+            dctx = cc.grad.clone()
+        torch.cuda.synchronize()
+        return unet._arena.grad.clone(), dctx, part
+
+    g0, d0, _ = run(False)
+    g1, d1, part = run(True)
+    lo = unet.executor().split_plan(names)
+    assert 0 < lo < g0.numel()
+    assert torch.equal(g0, g1)
+    assert torch.equal(d0, d1)
+    assert torch.equal(part, g0[lo:])
