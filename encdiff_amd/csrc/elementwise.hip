@@ -210,11 +210,64 @@ __global__ __launch_bounds__(256) void small_conv_out_fwd(const EncdiffSmallConv
   }
 }
 
+// output conv (cout = 3), many-lane form: thread per (pixel, 8-channel chunk); the 2^vshift
+// chunk lanes of a pixel are adjacent in the wave and fold their 3 partial sums with xor
+// shuffles.  8-16x the threads of the thread-per-pixel kernel (which filled half the CUs at
+// 32K pixels and ran its 9 x CI/8 vector loads serially).
+__global__ __launch_bounds__(256) void small_conv_out_fwd_lanes(const EncdiffSmallConvArgs p, int vshift) {
+  extern __shared__ float w[];  // [3][9][CI] weights + 3 biases (sized at launch: occupancy)
+  const int CO = p.cout, CI = p.cin, HW = p.h * p.w;
+  for (int i = threadIdx.x; i < CO * CI * 9; i += 256) {
+    const int co = i / (CI * 9), rem = i - co * CI * 9, ci = rem / 9, t = rem - ci * 9;
+    w[(co * 9 + t) * CI + ci] = p.weight[i];
+  }
+  for (int i = threadIdx.x; i < CO; i += 256) w[CO * CI * 9 + i] = p.bias[i];
+  __syncthreads();
+  const int V = 1 << vshift;
+  const long total = (long)p.batch * HW * V;  // a multiple of V: lane groups are all-or-none valid
+  for (long base = blockIdx.x * 256L; base < total; base += (long)gridDim.x * 256) {
+    const long idx = base + threadIdx.x;
+    const bool valid = idx < total;
+    const long pix = idx >> vshift;
+    const int ci0 = (int)(idx & (V - 1)) * 8;
+    const int b = (int)(pix / HW), rem = (int)(pix - (long)b * HW);
+    const int y = rem / p.w, x = rem - y * p.w;
+    float acc[3] = {0.f, 0.f, 0.f};
+    if (valid) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+        if (yy < 0 || yy >= p.h || xx < 0 || xx >= p.w) continue;
+        float v[8];
+        unpack8(*(const uint4*)((const bf16_t*)p.x + ((long)b * HW + yy * p.w + xx) * p.ldx + ci0), v);
+#pragma unroll
+        for (int co = 0; co < 3; ++co) {
+          const float* wr = w + (co * 9 + t) * CI + ci0;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) acc[co] += v[i] * wr[i];
+        }
+      }
+    }
+    for (int o = V >> 1; o > 0; o >>= 1)
+#pragma unroll
+      for (int co = 0; co < 3; ++co) acc[co] += __shfl_xor(acc[co], o, 64);
+    if (valid && ci0 == 0) {
+      float* Y = (float*)p.y + (long)b * CO * HW + rem;
+      for (int co = 0; co < CO; ++co) Y[(long)co * HW] = acc[co] + w[CO * CI * 9 + co];
+    }
+  }
+}
+
 // dx of the output conv: dy fp32 NCHW [b][3][hw] -> dx bf16 NHWC [pix][cin].  thread per (pix, 8 ci)
 __global__ __launch_bounds__(256) void small_conv_out_dgrad(const EncdiffSmallConvArgs p) {
   __shared__ float w[3 * 9 * 512];
   const int CO = p.cout, CI = p.cin, HW = p.h * p.w;
-  for (int i = threadIdx.x; i < CO * CI * 9; i += 256) w[i] = p.weight[i];  // [co][ci][tap]
+  // [co][tap][ci]: the chunk lanes of a pixel read consecutive 32-byte runs (the source
+  // [co][ci][tap] order put them 72 floats apart: bank conflicts)
+  for (int i = threadIdx.x; i < CO * CI * 9; i += 256) {
+    const int co = i / (CI * 9), rem = i - co * CI * 9, ci = rem / 9, t = rem - ci * 9;
+    w[(co * 9 + t) * CI + ci] = p.weight[i];
+  }
   __syncthreads();
   const int vpp = CI / 8;
   const long total = (long)p.batch * HW * vpp;
@@ -232,7 +285,7 @@ __global__ __launch_bounds__(256) void small_conv_out_dgrad(const EncdiffSmallCo
       for (int co = 0; co < CO; ++co) {
         const float d = DY[(long)co * HW + yo * p.w + xo];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] += d * w[(co * CI + ci0 + i) * 9 + t];
+        for (int i = 0; i < 8; ++i) acc[i] += d * w[(co * 9 + t) * CI + ci0 + i];
       }
     }
     *(uint4*)((bf16_t*)p.dx + pix * p.lddx + ci0) = pack8(acc);
@@ -491,6 +544,16 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* part,
   }
 }
 
+// workgroup cap of the output-conv kernels: each workgroup stages all 3 x 9 x CI weights in
+// LDS first, so a few grid-stride rounds per workgroup amortise that (tools/kbench.py sconv)
+int sconv_wgs() {
+  static const int v = [] {
+    const char* e = getenv("ENCDIFF_SCONV_WGS");
+    return e ? atoi(e) : 512;
+  }();
+  return v;
+}
+
 int grid_for(long n, int per_thread = 1) {
   long g = (n / per_thread + 255) / 256;
   if (g > 4096) g = 4096;
@@ -517,7 +580,16 @@ extern "C" int encdiff_small_conv_fwd(const EncdiffSmallConvArgs* a, void* strea
     hipLaunchKernelGGL(small_conv_in_fwd, dim3(grid_for(pix)), dim3(256), 0, s, *a);
   } else if (!a->x_f32 && a->y_f32) {  // output conv
     if (a->cout > 3 || a->cin > 512 || a->cin % 8) return ENCDIFF_ERR_SHAPE;
-    hipLaunchKernelGGL(small_conv_out_fwd, dim3(grid_for(pix)), dim3(256), 0, s, *a);
+    const int v = a->cin / 8;
+    if ((v & (v - 1)) == 0) {  // power-of-two chunk count (<= 64): lane groups within a wave
+      int vshift = 0;
+      while ((1 << vshift) < v) ++vshift;
+      const size_t lds = (size_t)(3 * 9 * a->cin + 3) * sizeof(float);
+      hipLaunchKernelGGL(small_conv_out_fwd_lanes, dim3(std::min(grid_for(pix * v), sconv_wgs())), dim3(256), lds, s,
+                         *a, vshift);
+    } else {
+      hipLaunchKernelGGL(small_conv_out_fwd, dim3(grid_for(pix)), dim3(256), 0, s, *a);
+    }
   } else {
     return ENCDIFF_ERR_UNSUPPORTED;
   }
@@ -532,8 +604,8 @@ extern "C" int encdiff_small_conv_bwd(const EncdiffSmallConvArgs* a, void* strea
   if (a->dx) {
     if (!a->dy_f32 || a->cout > 3 || a->cin % 8) return ENCDIFF_ERR_UNSUPPORTED;
     if (a->cin > 512) return ENCDIFF_ERR_SHAPE;  // LDS weight copy holds 3 x 9 x 512
-    hipLaunchKernelGGL(small_conv_out_dgrad, dim3(grid_for((long)a->batch * HW * (a->cin / 8))), dim3(256), 0, s,
-                       *a);
+    hipLaunchKernelGGL(small_conv_out_dgrad, dim3(std::min(grid_for((long)a->batch * HW * (a->cin / 8)), sconv_wgs())),
+                       dim3(256), 0, s, *a);
     ED_CHECK_LAUNCH();
   }
   if (a->dweight) {

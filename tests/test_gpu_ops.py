@@ -276,7 +276,10 @@ def test_layernorm(O, rows, C):
 
 @pytest.mark.parametrize("B,heads,sq,sk,dh,cross", [(4, 8, 256, 256, 8, False), (4, 8, 64, 64, 16, False),
                                                     (4, 8, 16, 16, 32, False), (4, 8, 4, 4, 32, False),
-                                                    (4, 8, 256, 20, 8, True), (4, 8, 16, 20, 32, True)])
+                                                    (4, 8, 256, 20, 8, True), (4, 8, 16, 20, 32, True),
+                                                    # configs[4] wide UNet: S=1024 at dh 16, dh 64 levels
+                                                    (2, 8, 1024, 1024, 16, False), (4, 8, 64, 64, 64, False),
+                                                    (4, 8, 16, 40, 64, True)])
 def test_attention(O, B, heads, sq, sk, dh, cross):
     torch.manual_seed(5)
     C = heads * dh
@@ -388,6 +391,29 @@ def test_small_convs(O):
     O.small_conv_out_bwd(h, g, w2, d2, dh, dw2, db2)
     assert rel(nhwc(dh, g), hr.grad) < 1e-2
     assert rel(dw2, w2r.grad) < 2e-3 and rel(db2, b2r.grad) < 2e-3
+
+
+@pytest.mark.parametrize("cin,H", [(64, 16), (128, 16), (128, 32), (96, 8), (512, 4)])
+def test_small_conv_out_channels(O, cin, H):
+    """Output conv cin -> 3 forward (lane-group kernel for power-of-two cin/8, the per-pixel
+    kernel otherwise) and input gradient, against torch fp32."""
+    from encdiff_amd.ops import Geom
+    torch.manual_seed(cin + H)
+    B = 3
+    g = Geom(B, H, H)
+    h = bf(g.pixels, cin)
+    w2 = torch.randn(3, cin, 3, 3, device=dev) * 0.05
+    b2 = torch.randn(3, device=dev)
+    out = torch.empty(B, 3, H, H, device=dev)
+    O.small_conv_out_fwd(h, g, w2, b2, out)
+    hr = nhwc(h, g).requires_grad_(True)
+    ref = F.conv2d(hr, w2, b2, padding=1)
+    assert rel(out, ref) < 1e-4
+    d2 = torch.randn(B, 3, H, H, device=dev)
+    ref.backward(d2)
+    dh = torch.empty_like(h)
+    O.small_conv_out_bwd(h, g, w2, d2, dh, None, None)
+    assert rel(nhwc(dh, g), hr.grad) < 1e-2
 
 
 def test_diffusion_math(O):

@@ -1,6 +1,6 @@
 """Micro-benchmarks of the HBM-bound kernels at the EncDiff B=128 shapes (HIP events).
 
-    python tools/kbench.py [--only gn,ln,attn]
+    python tools/kbench.py [--only gn,ln,attn,gemm,ew,sconv]
 
 Prints per-shape microseconds and effective GB/s (algorithmic bytes: each operand read
 once, each output written once).
@@ -126,6 +126,21 @@ def main():
         z = torch.empty(1, device=dev)
         t0 = timed(lambda: z.zero_())
         print(f"tiny kernels: 64K-elem copy {t1:.2f} us, torch 1-elem zero_ {t0:.2f} us")
+
+    if "sconv" in only:  # output conv cin -> 3 (UNet out at 16x16 / 64, VQ conv_out at 16x16 / 128)
+        for cin in (64, 128):
+            g = Geom(B, 16, 16)
+            h = torch.randn(g.pixels, cin, device=dev).to(bf)
+            w = torch.randn(3, cin, 3, 3, device=dev) * 0.05
+            b = torch.randn(3, device=dev)
+            out = torch.empty(B, 3, 16, 16, device=dev)
+            dy = torch.randn(B, 3, 16, 16, device=dev)
+            dh = torch.empty_like(h)
+            tf = timed(lambda: ops.small_conv_out_fwd(h, g, w, b, out))
+            td = timed(lambda: ops.small_conv_out_bwd(h, g, w, dy, dh, None, None))
+            nb = 2.0 * g.pixels * cin + 4.0 * g.pixels * 3
+            print(f"out conv cin={cin:4d} 16x16  fwd {tf:6.1f} us {nb / tf / 1e3:6.0f} GB/s   "
+                  f"dgrad {td:6.1f} us {nb / td / 1e3:6.0f} GB/s")
 
 
 if __name__ == "__main__":
