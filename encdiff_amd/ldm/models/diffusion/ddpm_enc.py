@@ -17,6 +17,7 @@ concept encoder Encoder4 are called as-is.
 """
 from __future__ import annotations
 
+import os
 from contextlib import contextmanager
 from functools import partial
 
@@ -73,8 +74,9 @@ class FusedArenaAdamW(torch.optim.Optimizer):
         # ring of pinned staging rows: a row is rewritten only after the H2D copy that read it
         # has run (its event), so a host running steps ahead of the GPU never changes the
         # scalars of a step still queued
-        self._host = torch.zeros(4, 8, dtype=torch.float32).pin_memory() if torch.cuda.is_available() else None
-        self._host_ev = [None] * 4
+        ring = int(os.environ.get("ENCDIFF_HYPER_RING", "32"))
+        self._host = torch.zeros(ring, 8, dtype=torch.float32).pin_memory() if torch.cuda.is_available() else None
+        self._host_ev = [None] * ring
         self._host_i = 0
 
     def hyper_values(self):
