@@ -577,6 +577,22 @@ class UNetExecutor:
         return not any(k in n for k in (".emb_layers.1.", ".attn2.to_k.", ".attn2.to_v.", ".attn1.to_q.",
                                         ".attn1.to_k.", ".attn1.to_v."))
 
+    @classmethod
+    def arena_split_offset(cls, arena: ParamArena, names: Sequence[str]) -> Optional[int]:
+        """Arena offset where the output-block / out parameters begin, when every other UNet
+        parameter of `names` ends before it (None otherwise)."""
+        span = {}
+        for n in names:
+            o, sh = arena.offsets[n]
+            span[n] = (o, o + int(torch.Size(sh).numel()))
+        early = [n for n in names if cls._early_final(n)]
+        if not early:
+            return None
+        lo = min(span[n][0] for n in early)
+        if any(span[n][1] > lo for n in names if not cls._early_final(n)):
+            return None
+        return lo
+
     def split_plan(self, names: Sequence[str]) -> Optional[int]:
         """For data-parallel overlap: the arena offset `lo` such that [lo, end of the UNet
         parameters) holds exactly the output-block / out parameters (their gradients are final
@@ -586,13 +602,8 @@ class UNetExecutor:
         if getattr(self, "_split", False) is not False:
             return self._split[0] if self._split else None
         self._split = None
-        offs = {n: self.arena.offsets[n] for n in names}
-        span = {n: (o, o + int(torch.Size(sh).numel())) for n, (o, sh) in offs.items()}
-        early = [n for n in names if self._early_final(n)]
-        if not early:
-            return None
-        lo = min(span[n][0] for n in early)
-        if any(span[n][1] > lo for n in names if not self._early_final(n)):
+        lo = self.arena_split_offset(self.arena, names)
+        if lo is None:
             return None
         gcol = self.gn.split_col(self._early_final)
         lcol = self.ln.split_col(self._early_final)

@@ -65,3 +65,45 @@ def test_unet_refuses_cpu():
     m = UNetModel(**UNET_PARAMS)
     with pytest.raises(RuntimeError):
         m(torch.zeros(1, 3, 16, 16), torch.zeros(1, dtype=torch.long), [torch.zeros(1, 320)])
+
+
+@pytest.mark.parametrize("params", [UNET_PARAMS, dict(UNET_PARAMS, image_size=32, model_channels=128,
+                                                        latent_unit=40)])
+def test_dp_split_layout(params):
+    """The data-parallel split (trainer.py / UNetExecutor.split_plan): in the arena the
+    output-block + out parameters form one contiguous tail [lo, end) that excludes every
+    parameter the UNet backward writes after the output blocks (batched emb / cross-K,V /
+    q,k,v weights), and the norm-partial columns of those layers form a suffix."""
+    from encdiff_amd.arena import NormPartials
+    from encdiff_amd.ldm.modules.diffusionmodules.openaimodel_enc import UNetModel
+    from encdiff_amd.unet import UNetExecutor
+    m = UNetModel(**params)
+    arena = m.bind_arena()
+    names = [n for n, _ in m.named_parameters()]
+    lo = UNetExecutor.arena_split_offset(arena, names)
+    assert lo is not None and 0 < lo < arena.numel
+    early = {n for n in names if UNetExecutor._early_final(n)}
+    late_written = [n for n in names if ".emb_layers.1." in n or ".attn2.to_k." in n or ".attn1.to_q." in n]
+    assert late_written and not early & set(late_written)
+    assert all(arena.offsets[n][0] >= lo for n in early)
+    assert all(arena.offsets[n][0] < lo for n in names if n not in early)
+    assert {n.split(".")[0] for n in early} == {"output_blocks", "out"}
+    # norm partial columns in the executor's registration order (output-block layers last)
+    np_ = NormPartials(arena, 4)
+    spec = m._spec
+    gn = [(r.prefix + "in_layers.0.weight", r.prefix + "in_layers.0.bias") for r in spec.res]
+    gn += [(r.prefix + "out_layers.0.weight", r.prefix + "out_layers.0.bias") for r in spec.res]
+    gn += [(t.prefix + "norm.weight", t.prefix + "norm.bias") for t in spec.sts] + [("out.0.weight", "out.0.bias")]
+    gn.sort(key=lambda p: UNetExecutor._early_final(p[0]))
+    for gname, bname in gn:
+        np_.add(gname, bname)
+    c = np_.split_col(UNetExecutor._early_final)
+    assert c is not None and 0 < c < np_.cols
+    tail = [np_.index[j] for j in range(c, np_.cols)]
+    head = [np_.index[j] for j in range(c)]
+    assert min(tail) >= lo and max(head) < lo
+    # unsorted (forward) order would not be a suffix: the plan must refuse it
+    bad = NormPartials(arena, 4)
+    for gname, bname in sorted(gn, key=lambda p: not UNetExecutor._early_final(p[0])):
+        bad.add(gname, bname)
+    assert bad.split_col(UNetExecutor._early_final) is None
