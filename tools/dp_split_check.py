@@ -4,7 +4,8 @@ prints a checksum of the parameters and the AdamW state.  Run it with ENCDIFF_DP
 =0: the split backward only reorders launches and all-reduce buckets, so the two checksums
 must be bitwise equal (and equal across repeated runs).
 
-DP_CHECK_SAVE=<file> also saves rank 0's parameters for an element-wise comparison.
+DP_CHECK_SAVE=<file> also saves rank 0's parameters for an element-wise comparison;
+DP_CHECK_TIME=1 times each captured graph of the DP step alone (rank 0).
 
 usage: ENCDIFF_DIST_BACKEND=gloo python -m torch.distributed.run --nproc-per-node 2 \
            --master-addr 127.0.0.1 --master-port 29531 tools/dp_split_check.py [--batch 64]
@@ -54,6 +55,20 @@ def main():
         print(f"split={os.environ.get('ENCDIFF_DP_SPLIT', '1')} split_lo={tr._split_lo} "
               f"buckets={tr.buckets.bounds} loss={tr.loss():.6f} ranks_equal={len(set(other)) == 1} "
               f"digest={other[0]}", flush=True)
+    if dist.get_rank() == 0 and os.environ.get("DP_CHECK_TIME"):
+        # GPU time of each captured piece of the DP step (replayed alone, rank 0)
+        for name in ("_g_fb", "_g_rest", "_g_cond", "_g_opt"):
+            g = getattr(tr, name)
+            if g is None:
+                continue
+            g.replay()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            print(f"graph {name}: {e0.elapsed_time(e1) / 5:.3f} ms", flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
