@@ -215,22 +215,24 @@ __global__ __launch_bounds__(256) void small_conv_out_fwd(const EncdiffSmallConv
 // shuffles.  8-16x the threads of the thread-per-pixel kernel (which filled half the CUs at
 // 32K pixels and ran its 9 x CI/8 vector loads serially).
 __global__ __launch_bounds__(256) void small_conv_out_fwd_lanes(const EncdiffSmallConvArgs p, int vshift) {
-  extern __shared__ float w[];  // [3][9][CI] weights + 3 biases (sized at launch: occupancy)
+  extern __shared__ __attribute__((aligned(16))) float w[];  // [3][9][CI] + 3 biases (sized at launch)
   const int CO = p.cout, CI = p.cin, HW = p.h * p.w;
-  for (int i = threadIdx.x; i < CO * CI * 9; i += 256) {
-    const int co = i / (CI * 9), rem = i - co * CI * 9, ci = rem / 9, t = rem - ci * 9;
-    w[(co * 9 + t) * CI + ci] = p.weight[i];
+  // staged in destination order (consecutive lanes -> consecutive LDS words, no conflicts)
+  for (int j = threadIdx.x; j < CO * CI * 9; j += 256) {
+    const int ct = j / CI, ci = j - ct * CI, co = ct / 9, t = ct - co * 9;
+    w[j] = p.weight[(co * CI + ci) * 9 + t];
   }
   for (int i = threadIdx.x; i < CO; i += 256) w[CO * CI * 9 + i] = p.bias[i];
   __syncthreads();
   const int V = 1 << vshift;
-  const long total = (long)p.batch * HW * V;  // a multiple of V: lane groups are all-or-none valid
-  for (long base = blockIdx.x * 256L; base < total; base += (long)gridDim.x * 256) {
-    const long idx = base + threadIdx.x;
+  // 32-bit indices (the launcher checks batch * HW * V < 2^31): no 64-bit divisions
+  const int total = p.batch * HW * V;  // a multiple of V: lane groups are all-or-none valid
+  for (int base = blockIdx.x * 256; base < total; base += gridDim.x * 256) {
+    const int idx = base + threadIdx.x;
     const bool valid = idx < total;
-    const long pix = idx >> vshift;
-    const int ci0 = (int)(idx & (V - 1)) * 8;
-    const int b = (int)(pix / HW), rem = (int)(pix - (long)b * HW);
+    const int pix = idx >> vshift;
+    const int ci0 = (idx & (V - 1)) * 8;
+    const int b = pix / HW, rem = pix - b * HW;
     const int y = rem / p.w, x = rem - y * p.w;
     float acc[3] = {0.f, 0.f, 0.f};
     if (valid) {
@@ -242,9 +244,11 @@ __global__ __launch_bounds__(256) void small_conv_out_fwd_lanes(const EncdiffSma
         unpack8(*(const uint4*)((const bf16_t*)p.x + ((long)b * HW + yy * p.w + xx) * p.ldx + ci0), v);
 #pragma unroll
         for (int co = 0; co < 3; ++co) {
-          const float* wr = w + (co * 9 + t) * CI + ci0;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) acc[co] += v[i] * wr[i];
+          // (co * 9 + t) * CI + ci0 is a multiple of 8 floats: two 16-byte LDS reads
+          const float4* wr = (const float4*)(w + (co * 9 + t) * CI + ci0);
+          const float4 w0 = wr[0], w1 = wr[1];
+          acc[co] += v[0] * w0.x + v[1] * w0.y + v[2] * w0.z + v[3] * w0.w + v[4] * w1.x + v[5] * w1.y +
+                     v[6] * w1.z + v[7] * w1.w;
         }
       }
     }
@@ -260,32 +264,37 @@ __global__ __launch_bounds__(256) void small_conv_out_fwd_lanes(const EncdiffSma
 
 // dx of the output conv: dy fp32 NCHW [b][3][hw] -> dx bf16 NHWC [pix][cin].  thread per (pix, 8 ci)
 __global__ __launch_bounds__(256) void small_conv_out_dgrad(const EncdiffSmallConvArgs p) {
-  __shared__ float w[3 * 9 * 512];
+  extern __shared__ __attribute__((aligned(16))) float w[];  // [3][9][CI], sized at launch
   const int CO = p.cout, CI = p.cin, HW = p.h * p.w;
   // [co][tap][ci]: the chunk lanes of a pixel read consecutive 32-byte runs (the source
   // [co][ci][tap] order put them 72 floats apart: bank conflicts)
-  for (int i = threadIdx.x; i < CO * CI * 9; i += 256) {
-    const int co = i / (CI * 9), rem = i - co * CI * 9, ci = rem / 9, t = rem - ci * 9;
-    w[(co * 9 + t) * CI + ci] = p.weight[i];
+  for (int j = threadIdx.x; j < CO * CI * 9; j += 256) {  // destination order: conflict-free
+    const int ct = j / CI, ci = j - ct * CI, co = ct / 9, t = ct - co * 9;
+    w[j] = p.weight[(co * CI + ci) * 9 + t];
   }
   __syncthreads();
   const int vpp = CI / 8;
-  const long total = (long)p.batch * HW * vpp;
-  for (long idx = blockIdx.x * 256L + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
-    const long pix = idx / vpp;
-    const int ci0 = (int)(idx - pix * vpp) * 8;
-    const int b = (int)(pix / HW), rem = (int)(pix - (long)b * HW);
+  const int total = p.batch * HW * vpp;  // < 2^31 (launcher check): 32-bit index math
+  for (int idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
+    const int pix = idx / vpp;
+    const int ci0 = (idx - pix * vpp) * 8;
+    const int b = pix / HW, rem = pix - b * HW;
     const int y = rem / p.w, x = rem - y * p.w;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const float* DY = (const float*)p.dy + (long)b * CO * HW;
+#pragma unroll
     for (int t = 0; t < 9; ++t) {
       // output pixel o = in - (t offset): y_out = y - (t/3 - 1)
       const int yo = y - (t / 3 - 1), xo = x - (t % 3 - 1);
       if (yo < 0 || yo >= p.h || xo < 0 || xo >= p.w) continue;
-      for (int co = 0; co < CO; ++co) {
-        const float d = DY[(long)co * HW + yo * p.w + xo];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] += d * w[(co * 9 + t) * CI + ci0 + i];
+      for (int co = 0; co < 3; ++co) {
+        if (co >= CO) break;
+        const float d = DY[co * HW + yo * p.w + xo];
+        const float4* wr = (const float4*)(w + (co * 9 + t) * CI + ci0);  // 32-byte aligned
+        const float4 w0 = wr[0], w1 = wr[1];
+        acc[0] += d * w0.x; acc[1] += d * w0.y; acc[2] += d * w0.z; acc[3] += d * w0.w;
+        acc[4] += d * w1.x; acc[5] += d * w1.y; acc[6] += d * w1.z; acc[7] += d * w1.w;
       }
     }
     *(uint4*)((bf16_t*)p.dx + pix * p.lddx + ci0) = pack8(acc);
@@ -549,7 +558,7 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* part,
 int sconv_wgs() {
   static const int v = [] {
     const char* e = getenv("ENCDIFF_SCONV_WGS");
-    return e ? atoi(e) : 512;
+    return e ? atoi(e) : 1024;
   }();
   return v;
 }
@@ -581,7 +590,7 @@ extern "C" int encdiff_small_conv_fwd(const EncdiffSmallConvArgs* a, void* strea
   } else if (!a->x_f32 && a->y_f32) {  // output conv
     if (a->cout > 3 || a->cin > 512 || a->cin % 8) return ENCDIFF_ERR_SHAPE;
     const int v = a->cin / 8;
-    if ((v & (v - 1)) == 0) {  // power-of-two chunk count (<= 64): lane groups within a wave
+    if ((v & (v - 1)) == 0 && pix * v < (1L << 31)) {  // 32-bit indices in the lane kernel  // power-of-two chunk count (<= 64): lane groups within a wave
       int vshift = 0;
       while ((1 << vshift) < v) ++vshift;
       const size_t lds = (size_t)(3 * 9 * a->cin + 3) * sizeof(float);
@@ -604,8 +613,9 @@ extern "C" int encdiff_small_conv_bwd(const EncdiffSmallConvArgs* a, void* strea
   if (a->dx) {
     if (!a->dy_f32 || a->cout > 3 || a->cin % 8) return ENCDIFF_ERR_UNSUPPORTED;
     if (a->cin > 512) return ENCDIFF_ERR_SHAPE;  // LDS weight copy holds 3 x 9 x 512
+    if ((long)a->batch * HW * (a->cin / 8) >= (1L << 31)) return ENCDIFF_ERR_SHAPE;  // 32-bit indices
     hipLaunchKernelGGL(small_conv_out_dgrad, dim3(std::min(grid_for((long)a->batch * HW * (a->cin / 8)), sconv_wgs())),
-                       dim3(256), 0, s, *a);
+                       dim3(256), (size_t)3 * 9 * a->cin * sizeof(float), s, *a);
     ED_CHECK_LAUNCH();
   }
   if (a->dweight) {

@@ -75,7 +75,7 @@ class FusedArenaAdamW(torch.optim.Optimizer):
         # has run (its event), so a host running steps ahead of the GPU never changes the
         # scalars of a step still queued
         ring = int(os.environ.get("ENCDIFF_HYPER_RING", "32"))
-        self._host = torch.zeros(ring, 8, dtype=torch.float32).pin_memory() if torch.cuda.is_available() else None
+        self._host = torch.zeros(max(ring, 1), 8, dtype=torch.float32).pin_memory() if torch.cuda.is_available() else None
         self._host_ev = [None] * ring
         self._host_i = 0
 
@@ -91,6 +91,10 @@ class FusedArenaAdamW(torch.optim.Optimizer):
         self._opt_called = True  # tells torch LR schedulers the optimizer stepped (launch() bypasses step())
         vals = self.hyper_values()
         if self._host is not None:
+            if not self._host_ev:  # ENCDIFF_HYPER_RING=0: one unguarded row (A/B only)
+                self._host[0].copy_(torch.tensor(vals, dtype=torch.float32))
+                self.arena.hyper.copy_(self._host[0], non_blocking=True)
+                return
             i = self._host_i
             self._host_i = (i + 1) % len(self._host_ev)
             if self._host_ev[i] is not None:
