@@ -275,7 +275,7 @@ def main():
                                            "batch": args.ddim_batch, "S": args.ddim_steps, "eta": 0.0}
             extra["ddim_steps_per_sec_b128"] = {"value": ddim_rate(ldm, 128, args.ddim_steps, eta=1.0),
                                                 "batch": 128, "S": args.ddim_steps, "eta": 1.0}
-        if not args.skip_cpu:
+        if not args.skip_cpu and world == 1:  # the CPU baseline is reported at N=1 only
             extra["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
         out = {"metric": "training imgs/sec (node) Shapes3D 64x64 LDM", "value": value, "unit": "imgs/s",
