@@ -30,9 +30,13 @@ struct BnLayout {  // thread -> (8-channel vector, pixel lane)
   }
 };
 
+// 8 per-channel fp32 constants as two 16-byte loads (p is 32-byte aligned: channel offsets
+// are multiples of 8 and the per-channel arrays are allocator-aligned); scalar loads made the
+// apply kernels issue 33-49 load instructions per 16-byte activation vector
 ED_DEV void ld8f(const float* p, float* v) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = p[i];
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
 // per-workgroup partial [blk][NQ][c] from q[NQ][8] of every thread: LDS rows summed in order
@@ -109,7 +113,9 @@ __global__ __launch_bounds__(BN_T) void bn_stats_kernel(const EncdiffBatchNormAr
 #pragma unroll
   for (int i = 0; i < 8; ++i) q[0][i] = q[1][i] = 0.f;
   if (L.pl < L.lanes) {
-#pragma unroll 4
+    // 8 rows (16-byte loads) in flight per thread: one workgroup per CU needs them to cover
+    // HBM latency (4 in flight measured ~3 TB/s at 131K rows, tools/bn_bench.py)
+#pragma unroll 8
     for (int r = r0 + L.pl; r < r1; r += L.lanes) {
       float x[8];
       unpack8(*(const uint4*)(X + (long)r * p.ldx + L.v * 8), x);
@@ -141,10 +147,10 @@ __global__ __launch_bounds__(BN_T) void bn_stats_kernel(const EncdiffBatchNormAr
 
 __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const EncdiffBatchNormArgs p) {
   const int nv = p.c >> 3;
-  const long total = (long)p.rows * nv;
-  for (long e = (long)blockIdx.x * BN_T + threadIdx.x; e < total; e += (long)gridDim.x * BN_T) {
-    const long r = e / nv;
-    const int cb = (int)(e - r * nv) * 8;
+  const int total = p.rows * nv;  // < 2^31 (bn_check): 32-bit index math
+  for (int e = blockIdx.x * BN_T + threadIdx.x; e < total; e += gridDim.x * BN_T) {
+    const int r = e / nv;
+    const int cb = (e - r * nv) * 8;
     float x[8], m[8], rs[8], g[8], b[8];
     unpack8(*(const uint4*)((const bf16_t*)p.x + r * p.ldx + cb), x);
     ld8f(p.mean + cb, m);
@@ -177,7 +183,7 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const EncdiffBatchN
     ld8f(p.rstd + cb, rs);
     ld8f(p.gamma + cb, ga);
     ld8f(p.beta + cb, be);
-#pragma unroll 4
+#pragma unroll 8
     for (int r = r0 + L.pl; r < r1; r += L.lanes) {
       float x[8], d[8];
       unpack8(*(const uint4*)(X + (long)r * p.ldx + cb), x);
@@ -210,11 +216,11 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const EncdiffBatchN
 // dx = gamma * rstd * (g - mean(g) - xhat * mean(g * xhat))
 __global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const EncdiffBatchNormArgs p, int nblk_reduce) {
   const int nv = p.c >> 3;
-  const long total = (long)p.rows * nv;
+  const int total = p.rows * nv;  // < 2^31 (bn_check): 32-bit index math
   const float* coef = p.partials + (long)nblk_reduce * 2 * p.c;
-  for (long e = (long)blockIdx.x * BN_T + threadIdx.x; e < total; e += (long)gridDim.x * BN_T) {
-    const long r = e / nv;
-    const int cb = (int)(e - r * nv) * 8;
+  for (int e = blockIdx.x * BN_T + threadIdx.x; e < total; e += gridDim.x * BN_T) {
+    const int r = e / nv;
+    const int cb = (e - r * nv) * 8;
     float x[8], d[8], m[8], rs[8], ga[8], be[8], c0[8], c1[8];
     unpack8(*(const uint4*)((const bf16_t*)p.x + r * p.ldx + cb), x);
     unpack8(*(const uint4*)((const bf16_t*)p.dy + r * p.lddy + cb), d);
@@ -256,6 +262,10 @@ int bn_check(const EncdiffBatchNormArgs* a) {
   if (a->rows <= 0 || a->c <= 0 || a->c % 8 || a->c > 256 || BN_T % (a->c / 8) || BN_T % a->c)
     return ENCDIFF_ERR_SHAPE;
   if (a->ldx % 8) return ENCDIFF_ERR_SHAPE;
+  if ((long)a->rows * (a->c / 8) >= (1L << 31)) return ENCDIFF_ERR_SHAPE;  // 32-bit apply indices
+  for (const void* q : {(const void*)a->mean, (const void*)a->rstd, (const void*)a->gamma, (const void*)a->beta,
+                        (const void*)a->partials})
+    if ((uintptr_t)q % 16) return ENCDIFF_ERR_ARG;  // ld8f's 16-byte loads
   return ENCDIFF_OK;
 }
 
