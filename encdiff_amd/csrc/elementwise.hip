@@ -10,10 +10,10 @@ namespace {
 // One thread per 8 contiguous output elements of a row ([rows][cols], cols % 8 == 0).
 __global__ __launch_bounds__(256) void ew_kernel(const EncdiffEwArgs p) {
   const int vpr = p.cols >> 3;
-  const long total = (long)p.rows * vpr;
-  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-    const int r = (int)(idx / vpr);
-    const int c = (int)(idx - (long)r * vpr) * 8;
+  const int total = p.rows * vpr;  // < 2^31 (launcher check): 32-bit division
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int r = idx / vpr;
+    const int c = (idx - r * vpr) * 8;
     const bf16_t* X = (const bf16_t*)p.x;
     bf16_t* Y = (bf16_t*)p.y;
     float out[8];
@@ -574,7 +574,7 @@ int grid_for(long n, int per_thread = 1) {
 
 extern "C" int encdiff_elementwise(const EncdiffEwArgs* a, void* stream) {
   if (!a || !a->x || !a->y) return ENCDIFF_ERR_ARG;
-  if (a->cols % 8) return ENCDIFF_ERR_SHAPE;
+  if (a->cols % 8 || (long)a->rows * (a->cols / 8) >= (1L << 31)) return ENCDIFF_ERR_SHAPE;
   hipLaunchKernelGGL(ew_kernel, dim3(grid_for((long)a->rows * a->cols, 8)), dim3(256), 0, (hipStream_t)stream, *a);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
