@@ -738,7 +738,9 @@ __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const in
         }
       }
       if (zg == 0 && i < total) {
-        const int row0 = (int)(i / p.N), col = (int)(i - (long)row0 * p.N);  // N % 4 == 0: one row
+        // N % 4 == 0: one row.  32-bit division whenever the problem fits (uniform branch)
+        const int row0 = total < (1L << 31) ? (int)i / p.N : (int)(i / p.N);
+        const int col = (int)(i - (long)row0 * p.N);
         const long row = fin_row(p, row0);
         float v[4] = {p.alpha * acc.x, p.alpha * acc.y, p.alpha * acc.z, p.alpha * acc.w};
         if (p.bias) {
@@ -752,8 +754,12 @@ __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const in
         const long co = (long)row * p.ldc + col;
         if (p.c_mode == ENCDIFF_OUT_BF16) {
           bf16_t* c = (bf16_t*)p.c + co;
+          if (((uintptr_t)c & 7) == 0) {  // one 8-byte store
+            *(uint2*)c = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          } else {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) c[k] = f2bf(v[k]);
+            for (int k = 0; k < 4; ++k) c[k] = f2bf(v[k]);
+          }
         } else {
           float* c = (float*)p.c + co;
 #pragma unroll
