@@ -6,7 +6,7 @@
 // 100 forward / ~300 backward tiny launches; here one workgroup per unit runs the whole
 // MLP in fp32 (VALU FMA, weights and WR-row activation chunks in LDS).  The grid is
 // (unit, batch chunk): every workgroup runs one unit's MLP on WR rows, so B = 128 fills
-// 160 workgroups instead of 20 serial loops.  The backward writes d u and each chunk's
+// 320 workgroups instead of 20 serial loops.  The backward writes d u and each chunk's
 // weight-gradient partials to a caller-provided scratch; a second launch adds the chunks
 // in a fixed order into the fp32 gradient arena (deterministic, no atomics).
 #include "common.h"
@@ -14,7 +14,7 @@
 namespace {
 
 constexpr int WT = 256;   // threads
-constexpr int WR = 16;    // batch rows per chunk (one workgroup each)
+constexpr int WR = 8;     // batch rows per chunk (one workgroup each): 320 workgroups at B = 128
 constexpr int H1 = 64, H2 = 128;
 
 ED_DEV float elu_f(float z) { return z > 0.f ? z : expm1f(z); }
@@ -202,9 +202,9 @@ __global__ __launch_bounds__(WT) void warp_bwd_kernel(const float* __restrict__ 
 // grads[unit * stride + i] += sum over chunks (in order) of part[(unit * chunks + c) * stride + i]
 __global__ __launch_bounds__(WT) void warp_grad_reduce_kernel(const float* __restrict__ part, int units, int chunks,
                                                              long stride, long n_per_unit, float* __restrict__ grads) {
-  const long total = (long)units * n_per_unit;
-  for (long e = (long)blockIdx.x * WT + threadIdx.x; e < total; e += (long)gridDim.x * WT) {
-    const long unit = e / n_per_unit, i = e - unit * n_per_unit;
+  const int total = units * (int)n_per_unit;  // < 2^31 (launcher check): 32-bit division
+  for (int e = blockIdx.x * WT + threadIdx.x; e < total; e += gridDim.x * WT) {
+    const long unit = e / (int)n_per_unit, i = e - unit * n_per_unit;
     float a = 0.f;
     for (int c = 0; c < chunks; ++c) a += part[(unit * chunks + c) * stride + i];
     grads[unit * stride + i] += a;
@@ -245,6 +245,7 @@ extern "C" int encdiff_encoder_warp_bwd(const float* u, long ldu, int batch, int
                      ldu, batch, params, unit_stride, context_dim, dout, lddo, du, lddu, partials);
   ED_CHECK_LAUNCH();
   const long n_per_unit = 2 * H1 + H2 * H1 + H2 + (long)context_dim * H2 + context_dim;
+  if ((long)units * n_per_unit >= (1L << 31)) return ENCDIFF_ERR_SHAPE;
   long g = ((long)units * n_per_unit + WT - 1) / WT;
   hipLaunchKernelGGL(warp_grad_reduce_kernel, dim3((unsigned)(g > 1024 ? 1024 : g)), dim3(WT), 0, (hipStream_t)stream,
                      partials, units, chunks, unit_stride, n_per_unit, grads);

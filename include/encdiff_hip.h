@@ -365,7 +365,7 @@ int encdiff_gather_images_u8(const void* pool, long long n_images, int h, int w,
  * params: unit i's tensors contiguous at params + i*unit_stride in nn.Sequential order
  * [W1 64][b1 64][W2 128x64][b2 128][W3 context_dim x 128][b3 context_dim] (the layout
  * of the parameter arena).  The backward ADDS the weight gradients into `grads` (same
- * layout) and writes du: one workgroup per (unit, 16-row batch chunk), chunk partials in
+ * layout) and writes du: one workgroup per (unit, 8-row batch chunk), chunk partials in
  * `partials`, folded in a fixed order by a second launch (deterministic). context_dim <= 16. */
 int encdiff_encoder_warp_fwd(const float* u, long ldu, int batch, int units, const float* params,
                              long unit_stride, int context_dim, float* out, long ldo, void* stream);
