@@ -13,11 +13,20 @@
 namespace {
 
 constexpr int BN_T = 256;
-constexpr int BN_MAXBLK = 256;  // workgroups of a reduction (pixel ranges of >= 256 rows)
+// workgroups of a reduction (pixel ranges of >= 256 rows, at most 128); ENCDIFF_BN_MAXBLK tunes the cap
+// (more workgroups: more loads in flight, longer serial fold in the last one)
+int bn_maxblk() {
+  static const int v = [] {
+    const char* e = getenv("ENCDIFF_BN_MAXBLK");
+    const int n = e ? atoi(e) : 128;  // tools/bn_bench.py sweep 64..1024: 128 best at 131K rows
+    return n < 1 ? 1 : n;
+  }();
+  return v;
+}
 
-__device__ __host__ inline int bn_blocks(int rows) {
+int bn_blocks(int rows) {
   const int b = (rows + 255) / 256;
-  return b < BN_MAXBLK ? b : BN_MAXBLK;
+  return b < bn_maxblk() ? b : bn_maxblk();
 }
 
 struct BnLayout {  // thread -> (8-channel vector, pixel lane)
