@@ -91,10 +91,10 @@ class SmallConvArgs(C.Structure):
 
 class BatchNormArgs(C.Structure):
     _fields_ = [("rows", C.c_int), ("c", C.c_int), ("eps", C.c_float), ("momentum", C.c_float),
-                ("relu", C.c_int), ("pad_", C.c_int), ("x", vp), ("ldx", C.c_long), ("gamma", vp), ("beta", vp),
+                ("relu", C.c_int), ("x_f32", C.c_int), ("x", vp), ("ldx", C.c_long), ("gamma", vp), ("beta", vp),
                 ("y", vp), ("ldy", C.c_long), ("mean", vp), ("rstd", vp), ("running_mean", vp), ("running_var", vp),
                 ("partials", vp), ("counter", vp), ("dy", vp), ("lddy", C.c_long), ("dx", vp), ("lddx", C.c_long),
-                ("dgamma", vp), ("dbeta", vp)]
+                ("dgamma", vp), ("dbeta", vp), ("y_split", C.c_int), ("pad2_", C.c_int)]
 
 
 class PackJob(C.Structure):
@@ -118,7 +118,7 @@ _PROTOS = {
     "encdiff_small_conv_bwd": [C.POINTER(SmallConvArgs), vp],
     "encdiff_timestep_embedding": [vp, C.c_int, C.c_int, C.c_float, vp, vp],
     "encdiff_q_sample": [vp, vp, vp, vp, vp, C.c_int, C.c_int, vp, vp],
-    "encdiff_l1_loss": [vp, vp, vp, vp, C.c_int, C.c_int, C.c_float, vp, vp, vp],
+    "encdiff_l1_loss": [vp, vp, vp, vp, C.c_int, C.c_int, C.c_float, vp, vp, vp, vp, vp],
     "encdiff_ddim_step": [vp, vp, vp, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, vp, vp, vp],
     "encdiff_ddim_step_indexed": [vp, vp, vp, C.c_int, vp, vp, C.c_int, vp, vp, vp],
     "encdiff_adamw_ema": [vp, vp, vp, vp, vp, C.c_longlong, vp, C.c_longlong, vp],
@@ -133,7 +133,9 @@ _PROTOS = {
     "encdiff_batchnorm_partials_floats": [C.c_int, C.c_int],
     "encdiff_batchnorm_fwd": [C.POINTER(BatchNormArgs), vp],
     "encdiff_batchnorm_bwd": [C.POINTER(BatchNormArgs), vp],
+    "encdiff_batchnorm_apply": [C.POINTER(BatchNormArgs), vp],
     "encdiff_nchw_to_rows": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_long, vp],
+    "encdiff_nchw_to_rows_split3": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_long, vp],
     "encdiff_version": [],
 }
 

@@ -67,6 +67,14 @@ class ParamArena:
                 p.grad = self.view_in(self.grad, name)
         self.step = 0
         self.hyper = torch.zeros(8, device=self.device, dtype=torch.float32)
+        # bumped by every host-side write of parameter values (EMA swap, load_state_dict):
+        # consumers of bf16 weight copies (UNet / Encoder4 packs) repack when it moves.
+        # Writes through a parameter's .data do not bump master._version (p.data is a view
+        # with a version counter of its own), so this counter is the signal.
+        self.gen = 0
+
+    def mark_dirty(self):
+        self.gen += 1
 
     # -------------------------------------------------------------- views
     def alias(self, local: str, name: str):

@@ -1,6 +1,6 @@
 """HIP executor of the concept encoder's convolution trunk.
 
-Encoder4.encoder (openaimodel_enc.py:1002-1012) is
+Encoder4.encoder (openaimodel_enc.py:996-1012) is
 
     Conv2d(3, d, 4, 2, 1)  BN ReLU      64x64 -> 32x32
     Conv2d(d, d, 4, 2, 1)  BN ReLU            -> 16x16
@@ -14,10 +14,25 @@ trained with batch statistics.  The reference runs it in fp32 through cuDNN/MIOp
 the UNet's implicit-im2col MFMA GEMMs (Conv2d(k4,s2,p1) is an im2col mode; its input
 gradient the transposed mode; each layer's input and weight gradients one paired launch),
 BatchNorm+ReLU are two launches each way (deterministic last-workgroup folds), and
-activations are NHWC bf16.  Both EncResBlock inputs are ReLU outputs, so their leading
+activations are NHWC: bf16 GEMM operands, fp32 pre-BatchNorm tensors (conv outputs and the
+residual sums), so the batch statistics and the ReLU masks are taken on fp32 values as in
+the reference.  Both EncResBlock inputs are ReLU outputs, so their leading
 ReLU is the identity and its gradient mask equals the preceding BN-ReLU's (mask^2 = mask).
 The trunk hands its output to the reference modules as the fp32 NCHW-flattened
 (B, d*16) tensor, so `Linear(d*16, latent_unit)` and the warp MLPs follow unchanged.
+
+Forward precision (bf16x3).  Four BatchNorm+ReLU stages sit between the image and the
+trunk's output, so the backward's ReLU masks are as good as the forward's pre-BN values.  Plain
+bf16 operands (fp32 accumulation) move ~0.2 % of those values across zero, which shows as
+~13 % rel-L2 in the first convolutions' weight gradients against the fp32 reference (measured
+on the GPU and reproduced by a CPU emulation; split-bf16 operands: 0.5 %).  So every forward
+GEMM of the trunk runs on split-bf16 operands, v = hi + lo with hi = bf16(v), lo = bf16(v - hi):
+activations are stored as [hi | lo | hi] channel blocks (written by the BatchNorm apply / image
+repack), weights packed [hi | hi | lo] (PackJob kinds 3-5), and ONE GEMM over K' = 3K forms
+a_hi w_hi + a_lo w_hi + a_hi w_lo -- ~16 significant bits per product.  The EncResBlock 1x1 conv
+also takes its residual input as [h_hi | h_lo] blocks against identity weights, so the residual
+sum is formed in fp32 inside the same GEMM.  The backward stays bf16 (hi blocks, hi weights):
+gradient rounding does not move masks.
 
 Weight gradients are written into the fp32 parameter arena (the modules' .grad views);
 only d(input image) is not computed (the image carries no gradient).
@@ -73,14 +88,25 @@ class Encoder4TrunkExecutor:
         pk = PackTable(arena)
         a = arena
         c0 = self.convs[0]
+        d = self.d
+        # bf16 weights of the backward (input gradients) ...
         # first conv: [d][3][4][4] -> [d][16 taps][8] (channels padded with zeros)
-        pk.add("c0", a.offsets[self.pn(c0.name + ".weight")][0], self.d, 16 * 8, kind=2, cin=self.cin_img)
+        pk.add("c0", a.offsets[self.pn(c0.name + ".weight")][0], d, 16 * 8, kind=2, cin=self.cin_img)
         for c in self.convs[1:]:
             pk.add(c.name, a.offsets[self.pn(c.name + ".weight")][0], c.cout, 16 * c.cin)
         for r in self.res:
             p = r["prefix"]
-            pk.add(p + "1", a.offsets[self.pn(p + "1.weight")][0], self.d, 9 * self.d)
-            pk.add(p + "4", a.offsets[self.pn(p + "4.weight")][0], self.d, self.d)
+            pk.add(p + "1", a.offsets[self.pn(p + "1.weight")][0], d, 9 * d)
+            pk.add(p + "4", a.offsets[self.pn(p + "4.weight")][0], d, d)
+        # ... and the split-bf16 [hi|hi|lo] weights of the forward (bf16x3, see the module doc)
+        pk.add("c0x3", a.offsets[self.pn(c0.name + ".weight")][0], d, 16 * 24, kind=4, cin=self.cin_img)
+        for c in self.convs[1:]:
+            pk.add(c.name + "x3", a.offsets[self.pn(c.name + ".weight")][0], c.cout, 16 * 3 * c.cin, kind=3,
+                   cin=c.cin)
+        for r in self.res:
+            p = r["prefix"]
+            pk.add(p + "1x3", a.offsets[self.pn(p + "1.weight")][0], d, 9 * 3 * d, kind=3, cin=d)
+            pk.add(p + "4x5", a.offsets[self.pn(p + "4.weight")][0], d, 5 * d, kind=5, cin=d)
         pk.finalize()
         pk.repack()
         self.pack = pk
@@ -121,14 +147,21 @@ class Encoder4TrunkExecutor:
             return self._bufs[B]
         t = lambda rows, c, dt=BF16: torch.empty(rows, c, device=self.dev, dtype=dt)  # noqa: E731
         d = self.d
-        b = dict(x0=t(B * 64 * 64, 8))
+        # forward GEMM operands are split-bf16 rows [hi | lo | hi]; pre-BatchNorm tensors (conv
+        # outputs, residual sums) are fp32 (see the module doc)
+        b = dict(x0=t(B * 64 * 64, 24))
         for i, c in enumerate(self.convs):
             n = B * c.hout * c.hout
-            b[f"c{i}"], b[f"a{i}"], b[f"dc{i}"], b[f"da{i}"] = t(n, d), t(n, d), t(n, d), t(n, d)
+            b[f"c{i}"], b[f"dc{i}"], b[f"da{i}"] = t(n, d, F32), t(n, d), t(n, d)
+            if i < 3:
+                b[f"a{i}"] = t(n, 3 * d)
         n4 = B * 16
         for j in range(2):
-            for k in ("t", "u", "r", "h", "dt", "du", "dr", "dh"):
-                b[f"{k}{j}"] = t(n4, d)
+            # res block j operand rows: [u_hi u_lo u_hi | h_hi h_lo h_hi] -- the 3x3 conv reads the
+            # h blocks, the 1x1 conv + identity residual the first five
+            b[f"R{j}"] = t(n4, 6 * d)
+            for k in ("t", "r", "dt", "du", "dr", "dh"):
+                b[f"{k}{j}"] = t(n4, d, F32 if k in ("t", "r") else BF16)
         b["dw0"] = t(d, 16 * 8, F32)
         b["flat"] = torch.empty(B, 16 * d, device=self.dev, dtype=F32)
         self._bufs[B] = b
@@ -136,19 +169,26 @@ class Encoder4TrunkExecutor:
 
     def _bn_fwd(self, B, key, mod, x, y, relu):
         st = self._bn_state(B, key, x.shape[0], x.shape[1])
+        if mod.momentum is None:
+            raise NotImplementedError("BatchNorm2d(momentum=None) (cumulative average) is not on the Encoder4 path")
         a = L.BatchNormArgs(rows=x.shape[0], c=x.shape[1], eps=mod.eps, momentum=mod.momentum, relu=int(relu),
-                            x=x.data_ptr(), ldx=x.stride(0), gamma=self.P(key + ".weight").data_ptr(),
+                            x_f32=int(x.dtype == F32), x=x.data_ptr(), ldx=x.stride(0),
+                            gamma=self.P(key + ".weight").data_ptr(),
                             beta=self.P(key + ".bias").data_ptr(), y=y.data_ptr(), ldy=y.stride(0),
+                            y_split=int(y.shape[1] == 3 * x.shape[1]),
                             mean=st["mean"].data_ptr(), rstd=st["rstd"].data_ptr(),
                             running_mean=mod.running_mean.data_ptr() if mod.training else None,
                             running_var=mod.running_var.data_ptr() if mod.training else None,
                             partials=st["part"].data_ptr(), counter=st["counter"].data_ptr())
         L.check(L.lib.encdiff_batchnorm_fwd(C.byref(a), ops._s()), "encdiff_batchnorm_fwd")
+        if mod.training and mod.num_batches_tracked is not None:
+            mod.num_batches_tracked.add_(1)  # as BatchNorm2d.train() does (state_dict parity)
 
     def _bn_bwd(self, B, key, mod, x, dy, dx, relu):
         st = self._bn_state(B, key, x.shape[0], x.shape[1])
         a = L.BatchNormArgs(rows=x.shape[0], c=x.shape[1], eps=mod.eps, momentum=mod.momentum, relu=int(relu),
-                            x=x.data_ptr(), ldx=x.stride(0), gamma=self.P(key + ".weight").data_ptr(),
+                            x_f32=int(x.dtype == F32), x=x.data_ptr(), ldx=x.stride(0),
+                            gamma=self.P(key + ".weight").data_ptr(),
                             beta=self.P(key + ".bias").data_ptr(), mean=st["mean"].data_ptr(),
                             rstd=st["rstd"].data_ptr(), partials=st["part"].data_ptr(),
                             counter=st["counter"].data_ptr(), dy=dy.data_ptr(), lddy=dy.stride(0),
@@ -156,39 +196,59 @@ class Encoder4TrunkExecutor:
                             dbeta=self.G(key + ".bias").data_ptr())
         L.check(L.lib.encdiff_batchnorm_bwd(C.byref(a), ops._s()), "encdiff_batchnorm_bwd")
 
+    def _bn_eval(self, B, key, mod, x, y, relu):
+        """BatchNorm2d.eval() (+ReLU): the running statistics, no reduction."""
+        st = self._bufs[B].get("bn_eval:" + key)
+        if st is None:
+            c = x.shape[1]
+            st = self._bufs[B]["bn_eval:" + key] = dict(mean=torch.empty(c, device=self.dev),
+                                                        rstd=torch.empty(c, device=self.dev))
+        st["mean"].copy_(mod.running_mean)
+        torch.rsqrt(mod.running_var + mod.eps, out=st["rstd"])
+        a = L.BatchNormArgs(rows=x.shape[0], c=x.shape[1], eps=mod.eps, momentum=0.0, relu=int(relu),
+                            x_f32=int(x.dtype == F32), x=x.data_ptr(), ldx=x.stride(0),
+                            gamma=self.P(key + ".weight").data_ptr(), beta=self.P(key + ".bias").data_ptr(),
+                            y=y.data_ptr(), ldy=y.stride(0), y_split=int(y.shape[1] == 3 * x.shape[1]),
+                            mean=st["mean"].data_ptr(), rstd=st["rstd"].data_ptr())
+        L.check(L.lib.encdiff_batchnorm_apply(C.byref(a), ops._s()), "encdiff_batchnorm_apply")
+
     # ------------------------------------------------------------ forward
-    def forward(self, img: torch.Tensor) -> torch.Tensor:
-        """img fp32 NCHW (B, 3, 64, 64) -> trunk output fp32 (B, d*16) in NCHW-flatten order."""
+    def forward(self, img: torch.Tensor, train: bool = True) -> torch.Tensor:
+        """img fp32 NCHW (B, 3, 64, 64) -> trunk output fp32 (B, d*16) in NCHW-flatten order.
+        train=False: BatchNorm with the running statistics (eval mode; no backward)."""
         assert img.is_cuda and img.dtype == F32 and img.shape[1:] == (self.cin_img, 64, 64), \
             "HIP Encoder4 trunk: fp32 (B, 3, 64, 64) device input"
         B = img.shape[0]
         b = self._bind(B)
         img = img.contiguous()
-        L.check(L.lib.encdiff_nchw_to_rows(img.data_ptr(), B, self.cin_img, 64 * 64, 8, b["x0"].data_ptr(), 8,
-                                           ops._s()), "encdiff_nchw_to_rows")
-        x, cin = b["x0"], 8
+        d = self.d
+        L.check(L.lib.encdiff_nchw_to_rows_split3(img.data_ptr(), B, self.cin_img, 64 * 64, 8, b["x0"].data_ptr(), 24,
+                                                  ops._s()), "encdiff_nchw_to_rows_split3")
+        bn = self._bn_fwd if train else self._bn_eval
+        x = b["x0"]
         for i, c in enumerate(self.convs):
             g = Geom(B, c.hout, c.hout)
-            w = self.pack.view("c0" if i == 0 else c.name)
-            ops.conv4x4s2_fwd(x, g, cin, w, b[f"c{i}"], bias=self.P(c.name + ".bias"))
+            w = self.pack.view("c0x3" if i == 0 else c.name + "x3")
+            ops.conv4x4s2_fwd(x, g, x.shape[1], w, b[f"c{i}"], bias=self.P(c.name + ".bias"), out_f32=True)
             key, mod, relu = self.bns[i]
-            self._bn_fwd(B, key, mod, b[f"c{i}"], b[f"a{i}"], relu)
-            x, cin = b[f"a{i}"], c.cout
+            y = b[f"a{i}"] if i < 3 else b["R0"][:, 3 * d:]  # the last one feeds res block 0
+            bn(B, key, mod, b[f"c{i}"], y, relu)
+            x = y
         g4 = Geom(B, 4, 4)
-        h = x
         for j, r in enumerate(self.res):
             p = r["prefix"]
-            b[f"in{j}"] = h
-            ops.conv3x3_fwd(h, g4, self.d, self.pack.view(p + "1"), b[f"t{j}"], bias=self.P(p + "1.bias"))
-            self._bn_fwd(B, p + "2", r["bn"], b[f"t{j}"], b[f"u{j}"], True)
-            ops.linear_fwd(b[f"u{j}"], self.pack.view(p + "4"), b[f"r{j}"], bias=self.P(p + "4.bias"), resid=h)
-            h = b[f"r{j}"]
+            R = b[f"R{j}"]
+            ops.conv3x3_fwd(R[:, 3 * d:], g4, 3 * d, self.pack.view(p + "1x3"), b[f"t{j}"], bias=self.P(p + "1.bias"),
+                            out_f32=True)
+            bn(B, p + "2", r["bn"], b[f"t{j}"], R[:, :3 * d], True)
+            # r = h + conv1x1(u): [u_hi u_lo u_hi h_hi h_lo] x [W_hi W_hi W_lo I I]^T in one GEMM
+            ops.linear_fwd(R[:, :5 * d], self.pack.view(p + "4x5"), b[f"r{j}"], bias=self.P(p + "4.bias"),
+                           out_f32=True)
             if r["post_bn"] is not None:
                 key, mod = r["post_bn"]
-                self._bn_fwd(B, key, mod, h, b[f"h{j}"], True)
-                h = b[f"h{j}"]
+                bn(B, key, mod, b[f"r{j}"], b[f"R{j + 1}"][:, 3 * d:], True)
         flat = b["flat"]
-        flat.view(B, self.d, 4, 4).copy_(h.view(B, 4, 4, self.d).permute(0, 3, 1, 2))
+        flat.view(B, d, 4, 4).copy_(b["r1"].view(B, 4, 4, d).permute(0, 3, 1, 2))
         return flat
 
     # ------------------------------------------------------------ backward
@@ -203,16 +263,17 @@ class Encoder4TrunkExecutor:
         for j in (1, 0):
             r = self.res[j]
             p = r["prefix"]
-            if r["post_bn"] is not None:  # h_j = ReLU(BN(r_j))
+            R = b[f"R{j}"]
+            if r["post_bn"] is not None:  # h_{j+1} = ReLU(BN(r_j))
                 key, mod = r["post_bn"]
                 self._bn_bwd(B, key, mod, b[f"r{j}"], dh, b[f"dr{j}"], True)
                 dh = b[f"dr{j}"]
-            # r = in + conv1x1(u): dgrad + wgrad of the 1x1 in one launch
-            ops.linear_bwd(dh, self.pack.view(p + "4"), b[f"u{j}"], b[f"du{j}"],
+            # r = in + conv1x1(u): dgrad + wgrad of the 1x1 in one launch (u_hi = R[:, :d])
+            ops.linear_bwd(dh, self.pack.view(p + "4"), R[:, :d], b[f"du{j}"],
                            self.G(p + "4.weight").view(d, d), self.G(p + "4.bias"))
             self._bn_bwd(B, p + "2", r["bn"], b[f"t{j}"], b[f"du{j}"], b[f"dt{j}"], True)
             # in-gradient = dh (residual) + conv3x3^T(dt): the residual rides the dgrad epilogue
-            ops.conv3x3_bwd_cl(b[f"dt{j}"], g4, self.pack.view(p + "1"), b[f"in{j}"], d,
+            ops.conv3x3_bwd_cl(b[f"dt{j}"], g4, self.pack.view(p + "1"), R[:, 3 * d:4 * d], d,
                                self.Graw(p + "1.weight"), b[f"dh{j}"], self.G(p + "1.bias"), resid=dh)
             dh = b[f"dh{j}"]
         for i in (3, 2, 1, 0):
@@ -225,13 +286,14 @@ class Encoder4TrunkExecutor:
                 x = b["x0"]
                 ops.gemm(c.cout, 16 * 8, g.pixels, dy, dy.stride(0), x, x.stride(0), b["dw0"], 16 * 8,
                          a_mode=L.OPA_ROWM, b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32,
-                         conv=L.ConvGeom(batch=B, h=c.hout, w=c.hout, cin=8, resample=L.RESAMPLE_K4S2, ld_src=8),
+                         conv=L.ConvGeom(batch=B, h=c.hout, w=c.hout, cin=8, resample=L.RESAMPLE_K4S2,
+                                         ld_src=x.stride(0)),
                          bias_grad=self.G(c.name + ".bias"))
                 gw = self.G(c.name + ".weight").view(c.cout, self.cin_img, 16)
                 gw.add_(b["dw0"].view(c.cout, 16, 8)[:, :, :self.cin_img].permute(0, 2, 1))
                 ops.flush()
                 break
-            x = b[f"a{i - 1}"]
+            x = b[f"a{i - 1}"][:, :d]  # the hi block of the split operand
             ops.conv4x4s2_bwd_cl(dy, g, self.pack.view(c.name), x, c.cin, self.Graw(c.name + ".weight"),
                                  b[f"da{i - 1}"], self.G(c.name + ".bias"))
             dh = b[f"da{i - 1}"]

@@ -1,4 +1,4 @@
-// bn.hip -- training-mode BatchNorm2d (+ReLU) over NHWC bf16 activations for the concept
+// bn.hip -- training-mode BatchNorm2d (+ReLU) over NHWC activations for the concept
 // encoder Encoder4 (openaimodel_enc.py:1002-1012: Conv2d(k4,s2,p1) + BatchNorm2d (+ReLU)
 // trunk, EncResBlock(bn=True) at :969-989), and the image repack feeding its first conv.
 //
@@ -8,6 +8,8 @@
 // LAST workgroup to finish (device-scope counter) folds the partials in a fixed order, in
 // fp64 -- deterministic, no atomics on data -- and resets the counter for the next launch
 // (graph-replay safe).  The elementwise apply is a second launch.
+// The pre-BN input x is fp32 (x_f32: the producing conv's fp32 output, so the ReLU masks are
+// taken on values as the fp32 reference computes them) or bf16; outputs are bf16.
 #include "common.h"
 
 namespace {
@@ -27,6 +29,18 @@ int bn_maxblk() {
 int bn_blocks(int rows) {
   const int b = (rows + 255) / 256;
   return b < bn_maxblk() ? b : bn_maxblk();
+}
+
+// 8 consecutive channels of row r of x as fp32: bf16 (one 16-byte load) or fp32 (two)
+template <bool F32>
+ED_DEV void ld_x8(const void* x, long off, float* v) {
+  if constexpr (F32) {
+    const float4 a = *(const float4*)((const float*)x + off), b = *(const float4*)((const float*)x + off + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+    unpack8(*(const uint4*)((const bf16_t*)x + off), v);
+  }
 }
 
 struct BnLayout {  // thread -> (8-channel vector, pixel lane)
@@ -113,9 +127,9 @@ ED_DEV bool bn_last_block(unsigned int* counter) {
   return last != 0;
 }
 
+template <bool F32>
 __global__ __launch_bounds__(BN_T) void bn_stats_kernel(const EncdiffBatchNormArgs p) {
   const BnLayout L(p.c);
-  const bf16_t* X = (const bf16_t*)p.x;
   const int per = (p.rows + gridDim.x - 1) / gridDim.x;
   const int r0 = blockIdx.x * per, r1 = min(p.rows, r0 + per);
   float q[2][8];
@@ -127,7 +141,7 @@ __global__ __launch_bounds__(BN_T) void bn_stats_kernel(const EncdiffBatchNormAr
 #pragma unroll 8
     for (int r = r0 + L.pl; r < r1; r += L.lanes) {
       float x[8];
-      unpack8(*(const uint4*)(X + (long)r * p.ldx + L.v * 8), x);
+      ld_x8<F32>(p.x, (long)r * p.ldx + L.v * 8, x);
 #pragma unroll
       for (int i = 0; i < 8; ++i) { q[0][i] += x[i]; q[1][i] += x[i] * x[i]; }
     }
@@ -154,6 +168,7 @@ __global__ __launch_bounds__(BN_T) void bn_stats_kernel(const EncdiffBatchNormAr
   if (threadIdx.x == 0) *p.counter = 0u;
 }
 
+template <bool F32>
 __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const EncdiffBatchNormArgs p) {
   const int nv = p.c >> 3;
   const int total = p.rows * nv;  // < 2^31 (bn_check): 32-bit index math
@@ -161,7 +176,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const EncdiffBatchNormAr
     const int r = e / nv;
     const int cb = (e - r * nv) * 8;
     float x[8], m[8], rs[8], g[8], b[8];
-    unpack8(*(const uint4*)((const bf16_t*)p.x + r * p.ldx + cb), x);
+    ld_x8<F32>(p.x, (long)r * p.ldx + cb, x);
     ld8f(p.mean + cb, m);
     ld8f(p.rstd + cb, rs);
     ld8f(p.gamma + cb, g);
@@ -171,15 +186,25 @@ __global__ __launch_bounds__(BN_T) void bn_apply_kernel(const EncdiffBatchNormAr
       const float z = (x[i] - m[i]) * rs[i] * g[i] + b[i];
       x[i] = p.relu ? fmaxf(z, 0.f) : z;
     }
-    *(uint4*)((bf16_t*)p.y + r * p.ldy + cb) = pack8(x);
+    bf16_t* y = (bf16_t*)p.y + (long)r * p.ldy + cb;
+    const uint4 hi = pack8(x);
+    *(uint4*)y = hi;
+    if (p.y_split) {  // [hi | lo | hi]: lo = bf16(z - hi), exact in fp32
+      float h[8], lo[8];
+      unpack8(hi, h);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) lo[i] = x[i] - h[i];
+      *(uint4*)(y + p.c) = pack8(lo);
+      *(uint4*)(y + 2 * p.c) = hi;
+    }
   }
 }
 
 // backward reduction: g = dy * relu'(z) (z recomputed from x and the saved statistics);
 // sums of g and g * xhat per channel -> dbeta, dgamma (+=) and the apply constants
+template <bool F32>
 __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const EncdiffBatchNormArgs p) {
   const BnLayout L(p.c);
-  const bf16_t* X = (const bf16_t*)p.x;
   const bf16_t* DY = (const bf16_t*)p.dy;
   const int per = (p.rows + gridDim.x - 1) / gridDim.x;
   const int r0 = blockIdx.x * per, r1 = min(p.rows, r0 + per);
@@ -195,7 +220,7 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const EncdiffBatchN
 #pragma unroll 8
     for (int r = r0 + L.pl; r < r1; r += L.lanes) {
       float x[8], d[8];
-      unpack8(*(const uint4*)(X + (long)r * p.ldx + cb), x);
+      ld_x8<F32>(p.x, (long)r * p.ldx + cb, x);
       unpack8(*(const uint4*)(DY + (long)r * p.lddy + cb), d);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -223,6 +248,7 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_reduce_kernel(const EncdiffBatchN
 }
 
 // dx = gamma * rstd * (g - mean(g) - xhat * mean(g * xhat))
+template <bool F32>
 __global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const EncdiffBatchNormArgs p, int nblk_reduce) {
   const int nv = p.c >> 3;
   const int total = p.rows * nv;  // < 2^31 (bn_check): 32-bit index math
@@ -231,7 +257,7 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const EncdiffBatchNo
     const int r = e / nv;
     const int cb = (e - r * nv) * 8;
     float x[8], d[8], m[8], rs[8], ga[8], be[8], c0[8], c1[8];
-    unpack8(*(const uint4*)((const bf16_t*)p.x + r * p.ldx + cb), x);
+    ld_x8<F32>(p.x, (long)r * p.ldx + cb, x);
     unpack8(*(const uint4*)((const bf16_t*)p.dy + r * p.lddy + cb), d);
     ld8f(p.mean + cb, m);
     ld8f(p.rstd + cb, rs);
@@ -249,9 +275,10 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_apply_kernel(const EncdiffBatchNo
   }
 }
 
-// fp32 NCHW [B][C][H][W] -> bf16 [B*H*W][ld] with channels [C, cpad) zero
+// fp32 NCHW [B][C][H][W] -> bf16 [B*H*W][ld] with channels [C, cpad) zero; split: the row is
+// the split-bf16 blocks [hi | lo | hi] of cpad channels each
 __global__ __launch_bounds__(256) void nchw_to_rows_kernel(const float* __restrict__ x, int B, int C, int HW,
-                                                           int cpad, bf16_t* __restrict__ y, long ld) {
+                                                           int cpad, bf16_t* __restrict__ y, long ld, int split) {
   const long total = (long)B * HW;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
     const long b = i / HW, px = i - b * HW;
@@ -259,7 +286,16 @@ __global__ __launch_bounds__(256) void nchw_to_rows_kernel(const float* __restri
       float v[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = (c0 + k < C) ? x[(b * C + c0 + k) * HW + px] : 0.f;
-      *(uint4*)(y + i * ld + c0) = pack8(v);
+      const uint4 hi = pack8(v);
+      *(uint4*)(y + i * ld + c0) = hi;
+      if (split) {
+        float h[8];
+        unpack8(hi, h);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] -= h[k];
+        *(uint4*)(y + i * ld + cpad + c0) = pack8(v);
+        *(uint4*)(y + i * ld + 2 * cpad + c0) = hi;
+      }
     }
   }
 }
@@ -271,6 +307,7 @@ int bn_check(const EncdiffBatchNormArgs* a) {
   if (a->rows <= 0 || a->c <= 0 || a->c % 8 || a->c > 256 || BN_T % (a->c / 8) || BN_T % a->c)
     return ENCDIFF_ERR_SHAPE;
   if (a->ldx % 8) return ENCDIFF_ERR_SHAPE;
+  if (a->x_f32 && ((uintptr_t)a->x % 16)) return ENCDIFF_ERR_ARG;  // float4 loads
   if ((long)a->rows * (a->c / 8) >= (1L << 31)) return ENCDIFF_ERR_SHAPE;  // 32-bit apply indices
   for (const void* q : {(const void*)a->mean, (const void*)a->rstd, (const void*)a->gamma, (const void*)a->beta,
                         (const void*)a->partials})
@@ -292,13 +329,32 @@ extern "C" int encdiff_batchnorm_partials_floats(int rows, int c) {
 extern "C" int encdiff_batchnorm_fwd(const EncdiffBatchNormArgs* a, void* stream) {
   const int rc = bn_check(a);
   if (rc) return rc;
-  if (!a->y || a->ldy % 8) return ENCDIFF_ERR_ARG;
+  if (!a->y || a->ldy % 8 || (a->y_split && a->ldy < 3L * a->c)) return ENCDIFF_ERR_ARG;
   if (a->running_mean && !a->running_var) return ENCDIFF_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int nblk = bn_blocks(a->rows);
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(nblk), dim3(BN_T), 0, s, *a);
+  if (a->x_f32) hipLaunchKernelGGL(bn_stats_kernel<true>, dim3(nblk), dim3(BN_T), 0, s, *a);
+  else hipLaunchKernelGGL(bn_stats_kernel<false>, dim3(nblk), dim3(BN_T), 0, s, *a);
   ED_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(a)), dim3(BN_T), 0, s, *a);
+  if (a->x_f32) hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(apply_grid(a)), dim3(BN_T), 0, s, *a);
+  else hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(apply_grid(a)), dim3(BN_T), 0, s, *a);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_batchnorm_apply(const EncdiffBatchNormArgs* a, void* stream) {
+  // eval-mode BatchNorm (+ReLU): y = (x - mean) * rstd * gamma + beta with the caller's mean /
+  // rstd (running statistics); partials / counter unused
+  if (!a || !a->x || !a->y || !a->mean || !a->rstd || !a->gamma || !a->beta) return ENCDIFF_ERR_ARG;
+  if (a->rows <= 0 || a->c <= 0 || a->c % 8 || a->ldx % 8 || a->ldy % 8) return ENCDIFF_ERR_SHAPE;
+  if (a->y_split && a->ldy < 3L * a->c) return ENCDIFF_ERR_ARG;
+  if ((long)a->rows * (a->c / 8) >= (1L << 31)) return ENCDIFF_ERR_SHAPE;
+  for (const void* q : {(const void*)a->mean, (const void*)a->rstd, (const void*)a->gamma, (const void*)a->beta})
+    if ((uintptr_t)q % 16) return ENCDIFF_ERR_ARG;
+  if (a->x_f32 && ((uintptr_t)a->x % 16)) return ENCDIFF_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (a->x_f32) hipLaunchKernelGGL(bn_apply_kernel<true>, dim3(apply_grid(a)), dim3(BN_T), 0, s, *a);
+  else hipLaunchKernelGGL(bn_apply_kernel<false>, dim3(apply_grid(a)), dim3(BN_T), 0, s, *a);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
@@ -309,20 +365,32 @@ extern "C" int encdiff_batchnorm_bwd(const EncdiffBatchNormArgs* a, void* stream
   if (!a->dy || !a->dx || !a->dgamma || !a->dbeta || a->lddy % 8 || a->lddx % 8) return ENCDIFF_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int nblk = bn_blocks(a->rows);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nblk), dim3(BN_T), 0, s, *a);
+  if (a->x_f32) hipLaunchKernelGGL(bn_bwd_reduce_kernel<true>, dim3(nblk), dim3(BN_T), 0, s, *a);
+  else hipLaunchKernelGGL(bn_bwd_reduce_kernel<false>, dim3(nblk), dim3(BN_T), 0, s, *a);
   ED_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(apply_grid(a)), dim3(BN_T), 0, s, *a, nblk);
+  if (a->x_f32) hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(apply_grid(a)), dim3(BN_T), 0, s, *a, nblk);
+  else hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(apply_grid(a)), dim3(BN_T), 0, s, *a, nblk);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+static int nchw_to_rows(const float* x, int batch, int c, int hw, int cpad, void* y, long ldy, int split,
+                        void* stream) {
+  if (!x || !y || batch <= 0 || c <= 0 || hw <= 0 || cpad < c || cpad % 8 || ldy < (split ? 3 : 1) * cpad || ldy % 8)
+    return ENCDIFF_ERR_ARG;
+  long g = ((long)batch * hw + 255) / 256;
+  hipLaunchKernelGGL(nchw_to_rows_kernel, dim3((unsigned)(g > 4096 ? 4096 : g)), dim3(256), 0, (hipStream_t)stream,
+                     x, batch, c, hw, cpad, (bf16_t*)y, ldy, split);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
 
 extern "C" int encdiff_nchw_to_rows(const float* x, int batch, int c, int hw, int cpad, void* y, long ldy,
                                     void* stream) {
-  if (!x || !y || batch <= 0 || c <= 0 || hw <= 0 || cpad < c || cpad % 8 || ldy < cpad || ldy % 8)
-    return ENCDIFF_ERR_ARG;
-  long g = ((long)batch * hw + 255) / 256;
-  hipLaunchKernelGGL(nchw_to_rows_kernel, dim3((unsigned)(g > 4096 ? 4096 : g)), dim3(256), 0, (hipStream_t)stream,
-                     x, batch, c, hw, cpad, (bf16_t*)y, ldy);
-  ED_CHECK_LAUNCH();
-  return ENCDIFF_OK;
+  return nchw_to_rows(x, batch, c, hw, cpad, y, ldy, 0, stream);
+}
+
+extern "C" int encdiff_nchw_to_rows_split3(const float* x, int batch, int c, int hw, int cpad, void* y, long ldy,
+                                           void* stream) {
+  return nchw_to_rows(x, batch, c, hw, cpad, y, ldy, 1, stream);
 }

@@ -370,10 +370,14 @@ __global__ void qsample_kernel(const float* x0, const float* eps, const long lon
   }
 }
 
+// L1 loss: block b writes loss_simple[b] to partials; the LAST block to arrive (device-scope
+// ticket, agent release / acquire as in bn.hip) folds the batch in a fixed order and resets the
+// ticket.  No memset and no float atomics: graph-replay safe and bitwise reproducible.
 __global__ __launch_bounds__(256) void l1_kernel(const float* pred, const float* eps, const long long* t,
                                                  const float* lvlb, int batch, int per, float lsw, float* out2,
-                                                 float* grad) {
-  __shared__ float red[4];
+                                                 float* grad, float* partials, unsigned int* counter) {
+  __shared__ float red[8];
+  __shared__ int last;
   const int b = blockIdx.x;
   float s = 0.f;
   const float gscale = lsw / ((float)batch * per);
@@ -387,9 +391,33 @@ __global__ __launch_bounds__(256) void l1_kernel(const float* pred, const float*
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float ls = (red[0] + red[1] + red[2] + red[3]) / (float)per;  // loss_simple[b]
-    atomicAdd(out2, lsw * ls / (float)batch);
-    atomicAdd(out2 + 1, lvlb[t[b]] * ls / (float)batch);
+    partials[b] = (red[0] + red[1] + red[2] + red[3]) / (float)per;  // loss_simple[b]
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned tk = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = tk == (unsigned)batch - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  float a = 0.f, v = 0.f;  // thread i: samples i, i + 256, ... in order
+  for (int k = threadIdx.x; k < batch; k += 256) {
+    const float ls = partials[k];
+    a += ls;
+    v += lvlb[t[k]] * ls;
+  }
+  a = wave_sum(a);
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) { red[threadIdx.x >> 6] = a; red[4 + (threadIdx.x >> 6)] = v; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out2[0] = lsw * (((red[0] + red[1]) + red[2]) + red[3]) / (float)batch;
+    out2[1] = (((red[4] + red[5]) + red[6]) + red[7]) / (float)batch;
+    *counter = 0u;
   }
 }
 
@@ -519,6 +547,31 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src
         continue;
       }
       s = (long)r * j.cin * taps + ci * taps + tap;
+    } else if (j.kind >= 3) {
+      // split-bf16 operands (bf16x3): w = hi + lo, hi = bf16(w), lo = bf16(w - hi).  Per tap the
+      // K block is [hi | hi | lo] (kind 3: src [co][tap][cin] row-major, cin channels per block;
+      // kind 4: src [co][cin][taps], cin <= 8, blocks of 8 channels zero-padded) or, kind 5
+      // (1x1 conv + identity residual), [hi | hi | lo | I | I] over src [co][cin].  Paired with
+      // activations stored [hi | lo | hi] (and the residual input as [hi | lo]) one GEMM computes
+      // a_hi w_hi + a_lo w_hi + a_hi w_lo (+ x_hi + x_lo): ~16 significant bits per product.
+      const int cb = j.kind == 4 ? 8 : j.cin;  // channels per block
+      const int tap = c / (j.kind == 5 ? 5 * cb : 3 * cb);
+      const int rem = c - tap * (j.kind == 5 ? 5 * cb : 3 * cb);
+      const int blk = rem / cb, ci = rem - blk * cb;
+      if (blk >= 3) {  // kind 5 identity blocks
+        dst[j.dst_off + i] = f2bf(ci == r ? 1.f : 0.f);
+        continue;
+      }
+      if (ci >= j.cin) {  // kind 4 channel padding
+        dst[j.dst_off + i] = 0;
+        continue;
+      }
+      const int taps = j.kind == 4 ? j.cols / 24 : (j.kind == 5 ? 1 : j.cols / (3 * j.cin));
+      const long si = j.kind == 4 ? (long)r * j.cin * taps + ci * taps + tap : (long)r * taps * j.cin + tap * j.cin + ci;
+      const float w = src[j.src_off + si];
+      const float hi = bf16_round(w);
+      dst[j.dst_off + i] = f2bf(blk < 2 ? hi : w - hi);
+      continue;
     } else {
       s = i;
     }
@@ -652,12 +705,11 @@ extern "C" int encdiff_q_sample(const float* x0, const float* eps, const long lo
 }
 
 extern "C" int encdiff_l1_loss(const float* pred, const float* eps, const long long* t, const float* lvlb, int batch,
-                               int per, float lsw, float* out2, float* grad, void* stream) {
-  if (!pred || !eps || !t || !lvlb || !out2) return ENCDIFF_ERR_ARG;
-  hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemsetAsync(out2, 0, 2 * sizeof(float), s);
-  if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
-  hipLaunchKernelGGL(l1_kernel, dim3(batch), dim3(256), 0, s, pred, eps, t, lvlb, batch, per, lsw, out2, grad);
+                               int per, float lsw, float* out2, float* grad, float* partials, unsigned int* counter,
+                               void* stream) {
+  if (!pred || !eps || !t || !lvlb || !out2 || !partials || !counter || batch <= 0 || per <= 0) return ENCDIFF_ERR_ARG;
+  hipLaunchKernelGGL(l1_kernel, dim3(batch), dim3(256), 0, (hipStream_t)stream, pred, eps, t, lvlb, batch, per, lsw,
+                     out2, grad, partials, counter);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }

@@ -63,9 +63,10 @@ class ImagePool:
         self.step.zero_()
         self.epoch += 1
 
-    def draw(self, out: torch.Tensor):
-        """Gather the next batch into out (fp32 [B, C, H, W]); stream-ordered, graph-safe."""
-        ops.gather_images_u8(self.images, self.perm, self.step, self.batch, out, advance=True)
+    def draw(self, out: torch.Tensor, advance: bool = True):
+        """Gather the next batch into out (fp32 [B, C, H, W]); stream-ordered, graph-safe.
+        advance=False: peek (the device step counter stays, e.g. the scale_by_std batch)."""
+        ops.gather_images_u8(self.images, self.perm, self.step, self.batch, out, advance=advance)
 
     def after_step(self):
         """Host bookkeeping once per step (outside graphs): new permutation per epoch."""

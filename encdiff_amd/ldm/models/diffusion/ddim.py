@@ -1,12 +1,24 @@
 """DDIMSampler -- mirror of ldm/models/diffusion/ddim.py:11-207 on the HIP path.
 
 Same schedule construction (make_schedule, :24-54), same sampling loop order and
-RNG consumption (one torch.randn of x's shape per step, :201), same update
-(p_sample_ddim, :188-207) -- the update itself is one HIP kernel.  With
-``use_graph=True`` (default on a HIP device, when no per-step callbacks, masks or
-guidance are requested) one step -- UNet forward + DDIM update -- is captured into
-a HIP graph whose coefficients and timestep are looked up from device tables at a
-device step index, and the graph is replayed S times.
+noise consumption (one N(0, I) draw of x's shape per step, :201), same update
+(p_sample_ddim, :188-207) -- the update itself is one HIP kernel.
+
+With ``use_graph=True`` (default on a HIP device, when no per-step callbacks, masks or
+guidance are requested) the WHOLE S-step loop -- S x (UNet forward + DDIM update), plus
+the copies of the logged intermediates -- is captured into one HIP graph per (batch shape,
+S, eta, log_every_t) and replayed once per ``sample()`` call.  Everything the graph reads
+lives in buffers owned by its cache entry (x_T, the conditioning, the per-step noise table,
+the timestep rows), so a later call with other inputs copies them in and replays; the
+schedule coefficients are kernel arguments of the unrolled steps.  Loops longer than
+``GRAPH_MAX_STEPS`` capture one step (coefficients and timestep looked up at a device step
+index) and replay it S times.
+
+Noise: the S draws of a loop are generated up front as one (S, *x.shape) table
+(one launch); ``normals_sequence`` (the reference's kwarg, unused there) injects a given
+table instead -- step i (in loop order, i = 0 .. S-1) adds sigma_i * normals_sequence[i] --
+which is how the eta > 0 trajectory is pinned against the reference's CPU noise stream.
+At eta == 0 sigma is 0 for every step and no noise is drawn.
 """
 from __future__ import annotations
 
@@ -15,6 +27,8 @@ import torch
 
 from encdiff_amd import ops
 from ...modules.diffusionmodules.util import make_ddim_sampling_parameters, make_ddim_timesteps, noise_like
+
+GRAPH_MAX_STEPS = 256  # longer loops replay a one-step graph (device step index)
 
 
 class DDIMSampler(object):
@@ -25,6 +39,9 @@ class DDIMSampler(object):
         self.schedule = schedule
         self.use_graph = use_graph
         self._graphs = {}
+        # (S, eta) -> device coefficient / timestep tables.  Allocated once and kept: a
+        # captured graph holds their addresses, so they are never rebound or freed.
+        self._tables = {}
 
     def register_buffer(self, name, attr):
         if isinstance(attr, torch.Tensor):
@@ -36,7 +53,7 @@ class DDIMSampler(object):
                                                   verbose=verbose)
         alphas_cumprod = self.model.alphas_cumprod
         assert alphas_cumprod.shape[0] == self.ddpm_num_timesteps
-        to_t = lambda x: x.clone().detach().to(torch.float32).to(self.model.device)
+        to_t = lambda x: x.clone().detach().to(torch.float32).to(self.model.device)  # noqa: E731
         self.register_buffer("betas", to_t(self.model.betas))
         self.register_buffer("alphas_cumprod", to_t(alphas_cumprod))
         self.register_buffer("alphas_cumprod_prev", to_t(self.model.alphas_cumprod_prev))
@@ -47,10 +64,16 @@ class DDIMSampler(object):
         self.ddim_sigmas, self.ddim_alphas, self.ddim_alphas_prev, self.ddim_alphas_next = sig, a, ap, an
         self.ddim_sqrt_one_minus_alphas = np.sqrt(1. - a)
         self.ddim_eta = ddim_eta
-        # device tables for the captured step: coef[index] = (a_t, a_prev, sigma, sqrt(1-a_t)); ts[index]
-        coef = np.stack([a, ap, sig, self.ddim_sqrt_one_minus_alphas], axis=1).astype(np.float32)
-        self._coef = torch.tensor(coef, device=self.model.device)
-        self._ts = torch.tensor(np.asarray(self.ddim_timesteps, dtype=np.int64), device=self.model.device)
+        key = (ddim_discretize, int(ddim_num_steps), float(ddim_eta))
+        tab = self._tables.get(key)
+        if tab is None:
+            # coef[index] = (a_t, a_prev, sigma, sqrt(1 - a_t)); ts[index]
+            coef = np.stack([a, ap, sig, self.ddim_sqrt_one_minus_alphas], axis=1).astype(np.float32)
+            tab = self._tables[key] = (torch.tensor(coef, device=self.model.device),
+                                       torch.tensor(np.asarray(self.ddim_timesteps, dtype=np.int64),
+                                                    device=self.model.device))
+        self._coef, self._ts = tab
+        self._sched_key = key
 
     @torch.no_grad()
     def sample(self, S, batch_size, shape, conditioning=None, callback=None, normals_sequence=None,
@@ -65,13 +88,14 @@ class DDIMSampler(object):
                                   noise_dropout=noise_dropout, score_corrector=score_corrector,
                                   corrector_kwargs=corrector_kwargs, x_T=x_T, log_every_t=log_every_t,
                                   unconditional_guidance_scale=unconditional_guidance_scale,
-                                  unconditional_conditioning=unconditional_conditioning)
+                                  unconditional_conditioning=unconditional_conditioning,
+                                  normals_sequence=normals_sequence)
 
     @torch.no_grad()
     def ddim_sampling(self, cond, shape, x_T=None, ddim_use_original_steps=False, callback=None, timesteps=None,
                       quantize_denoised=False, mask=None, x0=None, img_callback=None, log_every_t=100,
                       temperature=1., noise_dropout=0., score_corrector=None, corrector_kwargs=None,
-                      unconditional_guidance_scale=1., unconditional_conditioning=None):
+                      unconditional_guidance_scale=1., unconditional_conditioning=None, normals_sequence=None):
         device = self.model.betas.device
         b = shape[0]
         img = torch.randn(shape, device=device) if x_T is None else x_T.to(device).float().contiguous()
@@ -83,12 +107,16 @@ class DDIMSampler(object):
         else:
             steps = self.ddim_timesteps
         total = steps.shape[0]
+        if normals_sequence is not None:
+            normals_sequence = self._noise_table(normals_sequence, total, img.shape, device)
         intermediates = {"x_inter": [img], "pred_x0": [img]}
         simple = (callback is None and img_callback is None and mask is None and not quantize_denoised and
                   noise_dropout == 0. and score_corrector is None and temperature == 1. and
                   (unconditional_conditioning is None or unconditional_guidance_scale == 1.))
-        if self.use_graph and simple and img.is_cuda and timesteps is None:
-            return self._graph_sampling(cond, img, total, log_every_t, intermediates)
+        if self.use_graph and simple and img.is_cuda and timesteps is None and isinstance(cond, torch.Tensor):
+            if total <= GRAPH_MAX_STEPS:
+                return self._loop_graph(cond, img, total, log_every_t, intermediates, normals_sequence)
+            return self._step_graph(cond, img, total, log_every_t, intermediates, normals_sequence)
         for i, step in enumerate(np.flip(steps)):
             index = total - i - 1
             ts = torch.full((b,), int(step), device=device, dtype=torch.long)
@@ -98,7 +126,8 @@ class DDIMSampler(object):
                                               temperature=temperature, noise_dropout=noise_dropout,
                                               score_corrector=score_corrector, corrector_kwargs=corrector_kwargs,
                                               unconditional_guidance_scale=unconditional_guidance_scale,
-                                              unconditional_conditioning=unconditional_conditioning)
+                                              unconditional_conditioning=unconditional_conditioning,
+                                              noise=None if normals_sequence is None else normals_sequence[i])
             if callback:
                 callback(i)
             if img_callback:
@@ -108,10 +137,18 @@ class DDIMSampler(object):
                 intermediates["pred_x0"].append(pred_x0)
         return img, intermediates
 
+    @staticmethod
+    def _noise_table(seq, total, shape, device):
+        t = torch.stack(list(seq)) if not isinstance(seq, torch.Tensor) else seq
+        t = t.to(device=device, dtype=torch.float32).contiguous()
+        if t.shape[0] < total or tuple(t.shape[1:]) != tuple(shape):
+            raise ValueError(f"normals_sequence must hold {total} draws of shape {tuple(shape)}, got {tuple(t.shape)}")
+        return t
+
     @torch.no_grad()
     def p_sample_ddim(self, x, c, t, index, repeat_noise=False, use_original_steps=False, quantize_denoised=False,
                       temperature=1., noise_dropout=0., score_corrector=None, corrector_kwargs=None,
-                      unconditional_guidance_scale=1., unconditional_conditioning=None):
+                      unconditional_guidance_scale=1., unconditional_conditioning=None, noise=None):
         b = x.shape[0]
         if unconditional_conditioning is None or unconditional_guidance_scale == 1.:
             e_t = self.model.apply_model(x, t, c)
@@ -124,7 +161,9 @@ class DDIMSampler(object):
             e_t = score_corrector.modify_score(self.model, e_t, x, t, c, **corrector_kwargs)
         a_t, a_prev = float(self.ddim_alphas[index]), float(self.ddim_alphas_prev[index])
         sigma, s1 = float(self.ddim_sigmas[index]), float(self.ddim_sqrt_one_minus_alphas[index])
-        noise = noise_like(x.shape, x.device, repeat_noise) * temperature
+        if noise is None:
+            noise = noise_like(x.shape, x.device, repeat_noise)
+        noise = noise * temperature
         if noise_dropout > 0.:
             noise = torch.nn.functional.dropout(noise, p=noise_dropout)
         x = x.float().contiguous()
@@ -136,43 +175,123 @@ class DDIMSampler(object):
             pred_x0, _, _ = self.model.first_stage_model.quantize(pred_x0)
             x_prev = np.sqrt(a_prev) * pred_x0 + np.sqrt(1. - a_prev - sigma ** 2) * e_t + sigma * noise
             return x_prev, pred_x0
-        ops.ddim_step(x, e_t, noise.contiguous(), a_t, a_prev, sigma, s1, x_prev, pred_x0)
+        ops.ddim_step(x, e_t, noise.float().contiguous(), a_t, a_prev, sigma, s1, x_prev, pred_x0)
         return x_prev, pred_x0
 
-    # ------------------------------------------------------------ captured loop
-    def _graph_sampling(self, cond, img, total, log_every_t, intermediates):
-        dev = img.device
-        b = img.shape[0]
-        key = (tuple(img.shape), total, cond.data_ptr() if isinstance(cond, torch.Tensor) else id(cond))
+    # ------------------------------------------------------------ captured loops
+    def _entry(self, kind, cond, img, total, log_every_t):
+        """Cache entry (static input / output buffers) of a captured loop."""
+        key = (kind, tuple(img.shape), total, self._sched_key, tuple(cond.shape), cond.dtype, log_every_t)
         st = self._graphs.get(key)
         if st is None:
-            st = dict(x=torch.empty_like(img), x_next=torch.empty_like(img), px0=torch.empty_like(img),
-                      t=torch.empty(b, device=dev, dtype=torch.long), idx=torch.zeros(1, device=dev, dtype=torch.int32))
-            st["idx"].fill_(total - 1)
-            self._step_eager(st, cond)  # warm-up (allocations, kernel attributes)
+            dev = img.device
+            logs = [i for i in range(total) if (total - i - 1) % log_every_t == 0 or i == 0]
+            st = dict(key=key, x=torch.empty_like(img), x2=torch.empty_like(img), px0=torch.empty_like(img),
+                      cond=torch.empty_like(cond), logs=logs,
+                      log_x=torch.empty(len(logs), *img.shape, device=dev),
+                      log_px0=torch.empty(len(logs), *img.shape, device=dev),
+                      noise=torch.zeros((total if self.ddim_eta else 1), *img.shape, device=dev),
+                      graph=None)
+            self._graphs[key] = st
+        st["cond"].copy_(cond)
+        st["x"].copy_(img)
+        return st
+
+    def _fill_noise(self, st, normals_sequence, total):
+        if not self.ddim_eta:
+            return  # sigma == 0 at every step: the noise term vanishes
+        if normals_sequence is not None:
+            st["noise"].copy_(normals_sequence[:total])
+        else:
+            st["noise"].normal_()
+
+    def _loop_graph(self, cond, img, total, log_every_t, intermediates, normals_sequence):
+        """The whole loop as one HIP graph (unrolled: step i's coefficients and timestep are
+        kernel arguments / a static timestep row)."""
+        st = self._entry("loop", cond, img, total, log_every_t)
+        self._fill_noise(st, normals_sequence, total)
+        if st["graph"] is None:
+            b = img.shape[0]
+            steps = np.flip(self.ddim_timesteps)
+            st["ts"] = torch.tensor(np.repeat(np.asarray(steps, dtype=np.int64)[:, None], b, axis=1), device=img.device)
+            x0 = st["x"].clone()
+            self._loop_body(st, total)  # warm-up: allocations, kernel attributes, GEMM plans
+            st["x"].copy_(x0)
             g = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
                 with torch.cuda.graph(g, stream=s):
-                    self._step_eager(st, cond)
+                    self._loop_body(st, total)
             torch.cuda.current_stream().wait_stream(s)
             st["graph"] = g
-            self._graphs[key] = st
-        st["x"].copy_(img)
-        st["idx"].fill_(total - 1)
+            st["x"].copy_(x0)
+        st["graph"].replay()
+        for j in range(len(st["logs"])):
+            intermediates["x_inter"].append(st["log_x"][j].clone())
+            intermediates["pred_x0"].append(st["log_px0"][j].clone())
+        return st["out"].clone(), intermediates
+
+    def _loop_body(self, st, total):
+        x, xn = st["x"], st["x2"]
+        logs = st["logs"]
+        noise_n = st["noise"].shape[0]
         for i in range(total):
             index = total - i - 1
+            e_t = self.model.apply_model(x, st["ts"][i], st["cond"])
+            a_t, a_prev = float(self.ddim_alphas[index]), float(self.ddim_alphas_prev[index])
+            sigma, s1 = float(self.ddim_sigmas[index]), float(self.ddim_sqrt_one_minus_alphas[index])
+            ops.ddim_step(x, e_t.float().contiguous(), st["noise"][i if noise_n > 1 else 0], a_t, a_prev, sigma, s1,
+                          xn, st["px0"])
+            x, xn = xn, x
+            if i in logs:
+                j = logs.index(i)
+                st["log_x"][j].copy_(x)
+                st["log_px0"][j].copy_(st["px0"])
+        st["out"] = x
+
+    def _step_graph(self, cond, img, total, log_every_t, intermediates, normals_sequence):
+        """Loops longer than GRAPH_MAX_STEPS: one captured step (coefficients, timestep and
+        noise row looked up at a device step index), replayed S times."""
+        st = self._entry("step", cond, img, total, log_every_t)
+        self._fill_noise(st, normals_sequence, total)
+        b = img.shape[0]
+        if st["graph"] is None:
+            dev = img.device
+            st.update(t=torch.empty(b, device=dev, dtype=torch.long), idx=torch.zeros(1, device=dev, dtype=torch.int32),
+                      i=torch.zeros(1, device=dev, dtype=torch.long), zrow=torch.empty_like(img))
+            x0 = st["x"].clone()
+            st["idx"].fill_(total - 1)
+            self._step_body(st)
+            st["x"].copy_(x0)
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    self._step_body(st)
+            torch.cuda.current_stream().wait_stream(s)
+            st["graph"] = g
+            st["x"].copy_(x0)
+        st["idx"].fill_(total - 1)
+        st["i"].zero_()
+        for i in range(total):
             st["graph"].replay()
-            if index % log_every_t == 0 or index == total - 1:
+            if i in st["logs"]:
                 intermediates["x_inter"].append(st["x"].clone())
                 intermediates["pred_x0"].append(st["px0"].clone())
         return st["x"].clone(), intermediates
 
-    def _step_eager(self, st, cond):
+    def _step_body(self, st):
         idx = st["idx"]
         st["t"].copy_(self._ts.index_select(0, idx.long()).expand(st["t"].shape[0]))
-        e_t = self.model.apply_model(st["x"], st["t"], cond)
-        noise = torch.randn(st["x"].shape, device=st["x"].device)
-        ops.ddim_step_indexed(st["x"], e_t, noise, self._coef, idx, st["x_next"], st["px0"], advance=True)
-        st["x"].copy_(st["x_next"])
+        e_t = self.model.apply_model(st["x"], st["t"], st["cond"])
+        if st["noise"].shape[0] > 1:  # noise row of loop step i (device counter)
+            st["zrow"].copy_(st["noise"].index_select(0, st["i"]).view_as(st["zrow"]))
+            st["i"].add_(1)
+            z = st["zrow"]
+        else:
+            z = st["noise"][0]
+        ops.ddim_step_indexed(st["x"], e_t.float().contiguous(), z, self._coef, idx, st["x2"], st["px0"],
+                              advance=True)
+        st["x"].copy_(st["x2"])

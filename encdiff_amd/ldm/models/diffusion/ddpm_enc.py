@@ -213,11 +213,20 @@ class DDPM(nn.Module):
         if self.use_ema:
             self.model_ema.store(self.model.parameters())
             self.model_ema.copy_to(self.model)
+            self._weights_changed()
         try:
             yield None
         finally:
             if self.use_ema:
                 self.model_ema.restore(self.model.parameters())
+                self._weights_changed()
+
+    def _weights_changed(self):
+        """Parameters were rewritten through their .data views (EMA swap): the UNet's bf16
+        weight packs must be refreshed before the next forward."""
+        a = getattr(self.model.diffusion_model, "_arena", None)
+        if a is not None:
+            a.mark_dirty()
 
     def init_from_ckpt(self, path, ignore_keys=list(), only_model=False):
         """ddpm_enc.py:204-220 (weights-only load; strict=False)."""
@@ -509,6 +518,93 @@ class LatentDiffusion(DDPM):
         return sampler.sample(ddim_steps, batch_size, shape, cond, verbose=False, **kwargs)
 
     @torch.no_grad()
+    def sample_swap(self, orc, N, ddim_steps=200, eta=1., x_T=None, normals_sequence=None):
+        """The log_images sample_swap workload (ddpm_enc.py:1522-1535) as ONE sampler run: for
+        every concept unit cdx the batch's scalar codes `orc` (B, latent_unit) get unit cdx
+        replaced by the first image's, are warped to concept tokens, and sampled with DDIM.
+        The reference runs latent_unit separate DDIM loops of batch N; the UNet treats every
+        sample independently (per-sample GroupNorm, attention within a sample), so the
+        latent_unit x N conditionings are stacked into one (latent_unit * N) batch and sampled by
+        one captured loop.  Returns latents (latent_unit * N, C, H, W), row-block cdx = the
+        reference's cdx-th call."""
+        lu = self.model.diffusion_model.latent_unit
+        orc = orc[:N]
+        n = orc.shape[0]
+        sc = orc[None].repeat(lu, 1, 1)                       # [cdx][b][unit]
+        idx = torch.arange(lu, device=orc.device)
+        sc[idx, :, idx] = orc[0][:, None].expand(lu, n)       # unit cdx <- image 0's unit cdx
+        cond = self.cond_stage_model.warp(sc.reshape(lu * n, lu))
+        shape = (self.channels, self.image_size, self.image_size)
+        sampler = DDIMSampler(self)
+        samples, _ = sampler.sample(ddim_steps, lu * n, shape, cond.reshape(lu * n, -1), eta=eta, verbose=False,
+                                    x_T=x_T, normals_sequence=normals_sequence)
+        return samples
+
+    # ------------------------------------------------------------ validation (§8(f) row 4)
+    @torch.no_grad()
+    def validation_step(self, batch, batch_idx=0):
+        """ddpm_enc.py:377-390: concept tokens c (B, latent_unit, context_dim) and scalar codes
+        orc (B, latent_unit) of the batch, collected for the epoch-end metrics (eval_func is
+        out of scope; on_validation_epoch_end returns the stacked arrays)."""
+        x, oc = self.get_input(batch, self.first_stage_key)
+        c, orc = self.encode_concepts(oc)
+        if not hasattr(self, "validation_step_outputs"):
+            self.validation_step_outputs, self.validation_step_scalars = [], []
+        self.validation_step_outputs.append(c.detach().cpu().numpy())
+        self.validation_step_scalars.append(orc.detach().cpu().numpy())
+
+    def on_validation_epoch_end(self, *args, **kwargs):
+        """Returns (codes (N, latent_unit), tokens (N, latent_unit, context_dim)) -- what the
+        reference hands to eval_func (ddpm_enc.py:403-425) -- and clears the lists."""
+        outs = getattr(self, "validation_step_outputs", [])
+        scal = getattr(self, "validation_step_scalars", [])
+        res = (np.concatenate(scal, 0) if scal else None, np.concatenate(outs, 0) if outs else None)
+        if outs:
+            outs.clear()
+            scal.clear()
+        return res
+
+    @torch.no_grad()
+    def encode_concepts(self, img):
+        """Encoder4 in eval mode (running BatchNorm statistics): tokens c (B, latent_unit,
+        context_dim) = warp(orc) and codes orc (B, latent_unit)."""
+        cs = self.cond_stage_model
+        was = cs.training
+        cs.eval()
+        try:
+            orc = cs.encoding(img)
+            c = cs.warp(orc)
+        finally:
+            cs.train(was)
+        return c.reshape(c.shape[0], self.model.diffusion_model.latent_unit, -1), orc
+
+    @torch.no_grad()
+    def encode_dataset(self, pool, chunk=4096):
+        """Validation encoding pass over a GPU-resident uint8 image pool
+        (encdiff_amd.data.ImagePool, or a uint8 [N, H, W, C] device tensor): fused
+        gather + ToTensor/Normalize, the HIP Encoder4 trunk in eval mode, Linear and the warp
+        MLPs, `chunk` images per pass, results kept on the device.  Returns (codes (N,
+        latent_unit), tokens (N, latent_unit, context_dim)) in dataset order -- the arrays the
+        reference collects batch by batch through validation_step (ddpm_enc.py:377-390)."""
+        images = pool.images if hasattr(pool, "images") else pool
+        n = images.shape[0]
+        dev = images.device
+        lu = self.model.diffusion_model.latent_unit
+        cd = self.cond_stage_model.context_dim
+        codes = torch.empty(n, lu, device=dev)
+        toks = torch.empty(n, lu, cd, device=dev)
+        order = torch.arange(n, device=dev, dtype=torch.int64)
+        for s in range(0, n, chunk):
+            b = min(chunk, n - s)
+            img = torch.empty(b, images.shape[3], images.shape[1], images.shape[2], device=dev)
+            step = torch.zeros(1, device=dev, dtype=torch.int64)
+            ops.gather_images_u8(images, order[s:s + b], step, b, img, advance=False)
+            c, orc = self.encode_concepts(img)
+            codes[s:s + b].copy_(orc)
+            toks[s:s + b].copy_(c)
+        return codes, toks
+
+    @torch.no_grad()
     def log_images(self, batch, N=8, n_row=4, sample=True, ddim_steps=200, ddim_eta=1., return_keys=None,
                    quantize_denoised=True, inpaint=True, plot_denoise_rows=False, plot_progressive_rows=True,
                    sample_swap=False, plot_diffusion_rows=True, **kwargs):
@@ -530,17 +626,9 @@ class LatentDiffusion(DDPM):
                     rows.append(self.decode_first_stage(self.q_sample(z_start, tt, torch.randn_like(z_start))))
             log["diffusion_row"] = torch.stack(rows)
         if sample_swap:
-            outs = []
-            lu = self.model.diffusion_model.latent_unit
             with self.ema_scope("Plotting Swapping"):
-                for cdx in range(lu):
-                    sc = orc.clone()
-                    sc[:, cdx] = sc[0, cdx][None].repeat(orc.shape[0])
-                    sc = self.cond_stage_model.warp(sc)
-                    samples, _ = self.sample_log(cond=sc.reshape(orc.shape[0], -1), batch_size=N, ddim=True,
-                                                 ddim_steps=ddim_steps, eta=ddim_eta)
-                    outs.append(self.decode_first_stage(samples))
-            log["samples_swapping"] = torch.cat(outs, dim=0)
+                log["samples_swapping"] = self.decode_first_stage(
+                    self.sample_swap(orc, N, ddim_steps=ddim_steps, eta=ddim_eta))
         if sample:
             with self.ema_scope("Plotting"):
                 samples, _ = self.sample_log(cond=c, batch_size=N, ddim=True, ddim_steps=ddim_steps, eta=ddim_eta)

@@ -142,6 +142,10 @@ class UNetModel(nn.Module):
         self._arena: Optional[ParamArena] = None
         self._ex: Optional[UNetExecutor] = None
         self._packed_version = -1
+        self._packed_gen = -1
+        # load_state_dict writes the arena through the parameters' .data views, which no
+        # version counter sees: mark the bf16 packs stale explicitly
+        self.register_load_state_dict_post_hook(_mark_arena_dirty)
 
     # ------------------------------------------------------------- HIP binding
     def bind_arena(self, arena: Optional[ParamArena] = None):
@@ -161,18 +165,21 @@ class UNetModel(nn.Module):
     def executor(self) -> UNetExecutor:
         if self._arena is None:
             self.bind_arena()
-        if self._ex is None or self._ex.arena is not self._arena:
-            self._ex = UNetExecutor(self._spec, self._arena)
-            self._packed_version = self._arena.master._version
-        elif self._arena.master._version != self._packed_version:
-            # parameters were modified in place (load_state_dict, EMA swap...): refresh bf16 copies
+        a = self._arena
+        if self._ex is None or self._ex.arena is not a:
+            self._ex = UNetExecutor(self._spec, a)
+            self.mark_repacked()
+        elif a.master._version != self._packed_version or a.gen != self._packed_gen:
+            # parameters were modified in place (arena writes, load_state_dict, EMA swap
+            # -- ParamArena.mark_dirty): refresh the bf16 copies
             self._ex.pack.repack()
-            self._packed_version = self._arena.master._version
+            self.mark_repacked()
         return self._ex
 
     def mark_repacked(self):
         if self._arena is not None:
             self._packed_version = self._arena.master._version
+            self._packed_gen = self._arena.gen
 
     def forward(self, x, timesteps=None, context=None, y=None, **kwargs):
         if not x.is_cuda:
@@ -183,6 +190,12 @@ class UNetModel(nn.Module):
         if torch.is_grad_enabled():
             self._arena.attach_grads()
         return _UNetFn.apply(x.float(), timesteps.long(), c, ex)
+
+
+def _mark_arena_dirty(module, incompatible_keys):
+    a = getattr(module, "_arena", None) or getattr(getattr(module, "_trunk", None), "arena", None)
+    if a is not None:
+        a.mark_dirty()
 
 
 # --------------------------------------------------------------------------- Encoder4 (as-is)
@@ -256,6 +269,7 @@ class Encoder4(nn.Module):
                                                 nn.Linear(128, context_dim)) for _ in range(latent_unit)])
         self._warp_bind = None
         self._trunk = None
+        self.register_load_state_dict_post_hook(_mark_arena_dirty)
 
     def bind_arena(self, arena, prefix: str):
         """Run warp() on the HIP kernels (encdiff_encoder_warp_*): the per-unit MLP
@@ -280,23 +294,27 @@ class Encoder4(nn.Module):
         self._trunk = None
         if all(n in arena.cl for n in Encoder4TrunkExecutor.channels_last_names(self, prefix)):
             self._trunk = Encoder4TrunkExecutor(self, arena, prefix)
-            self._trunk_version = arena.master._version
+            self._trunk_version = (arena.master._version, arena.gen)
 
     def repack_hip(self):
         """Refresh the trunk's bf16 weights from the arena (after an optimizer step)."""
         if getattr(self, "_trunk", None) is not None:
             self._trunk.pack.repack()
-            self._trunk_version = self._trunk.arena.master._version
+            self._trunk_version = (self._trunk.arena.master._version, self._trunk.arena.gen)
 
     def _encode(self, x):
-        """Trunk + Linear: on HIP in training mode (batch-statistics BatchNorm), else the
-        reference modules (eval mode uses the running statistics)."""
+        """Trunk + Linear on HIP once the trunk is bound to the arena: training mode with
+        batch-statistics BatchNorm (TrunkFn, gradients into the arena), eval mode with the
+        running statistics (no gradient; the validation encoding pass).  Unbound, or on CPU
+        tensors, the reference modules run."""
         ex = getattr(self, "_trunk", None)
-        if ex is None or not self.training or not x.is_cuda:
+        if ex is None or not x.is_cuda or (not self.training and torch.is_grad_enabled()):
             return self.encoder(x)
         from encdiff_amd.cond import TrunkFn
-        if ex.arena.master._version != self._trunk_version:  # parameters modified in place
+        if (ex.arena.master._version, ex.arena.gen) != self._trunk_version:  # parameters modified in place
             self.repack_hip()
+        if not self.training:
+            return self.encoder[-1](ex.forward(x.float(), train=False))
         flat = TrunkFn.apply(x, self.encoder[0].weight, ex)
         return self.encoder[-1](flat)
 

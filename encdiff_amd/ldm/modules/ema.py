@@ -41,13 +41,26 @@ class LitEma(nn.Module):
                 self._buffers[s_name] = view
         self._arena, self._prefix = arena, prefix
 
+    def _host_counters(self):
+        """Host mirror of (decay, num_updates): read from the buffers once (or after a
+        state_dict load), then advanced on the host, so a training step never waits on the
+        device for the EMA scalars.  The buffers are written back (one small H2D copy, no
+        sync) at every update so state_dict() stays exact."""
+        key = (self.decay.data_ptr(), self.num_updates.data_ptr(), self.num_updates._version)
+        if getattr(self, "_host", None) is None or self._host[2] != key:
+            self._host = [float(self.decay), int(self.num_updates), key]
+        return self._host
+
     def next_decay(self) -> float:
         """ema.py:29-33: decay = min(decay, (1 + n) / (10 + n)) after n += 1 (returns 1 - decay)."""
-        decay = float(self.decay)
-        if int(self.num_updates) >= 0:
-            self.num_updates += 1
-            n = int(self.num_updates)
+        h = self._host_counters()
+        decay = h[0]
+        if h[1] >= 0:
+            h[1] += 1
+            n = h[1]
             decay = min(decay, (1 + n) / (10 + n))
+            self.num_updates.fill_(n)  # device-side fill: no host sync
+            h[2] = (self.decay.data_ptr(), self.num_updates.data_ptr(), self.num_updates._version)
         return float(1.0 - torch.tensor(decay, dtype=torch.float32))
 
     def forward(self, model):
@@ -70,6 +83,7 @@ class LitEma(nn.Module):
         for key, p in m_param.items():
             if p.requires_grad:
                 p.data.copy_(shadow[self.m_name2s_name[key]].data)
+        self._dirty()
 
     def store(self, parameters):
         self.collected_params = [p.clone() for p in parameters]
@@ -77,3 +91,9 @@ class LitEma(nn.Module):
     def restore(self, parameters):
         for c, p in zip(self.collected_params, parameters):
             p.data.copy_(c.data)
+        self._dirty()
+
+    def _dirty(self):
+        """Parameter values changed behind the arena's back: bf16 weight packs are stale."""
+        if self._arena is not None:
+            self._arena.mark_dirty()

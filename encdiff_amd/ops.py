@@ -93,6 +93,8 @@ def plan(M, N, K, a_mode, b_mode, c_mode, resample=0):
     """(tile, split_k) for a GEMM: measured table (tools/gemm_profile.py --write-table) first,
     else a heuristic aiming at >= 256 workgroups with bounded split-K traffic."""
     hit = _tile_table().get(plan_key(M, N, K, a_mode, b_mode, c_mode, resample))
+    if hit is None and c_mode == L.OUT_F32:  # same problem with a bf16 output: same tile plan
+        hit = _tile_table().get(plan_key(M, N, K, a_mode, b_mode, L.OUT_BF16, resample))
     if hit is not None:
         tile, split = int(hit[0]), min(int(hit[1]), MAX_SPLIT)
         if split == 1 or c_mode in (L.OUT_F32_ATOMIC, L.OUT_F32_ATOMIC_CONVW) or split * M * (N + 1) <= WS_FLOATS:
@@ -318,12 +320,13 @@ def linear_bwd_geglu(dy, w, a, f, df, dw, db=None, d_a=None):
 
 
 # ------------------------------------------------------------------ 3x3 convolutions
-def conv3x3_fwd(x, g: Geom, cin, wf, out, bias=None, resid=None, resample=L.RESAMPLE_NONE, gn_stats=None):
+def conv3x3_fwd(x, g: Geom, cin, wf, out, bias=None, resid=None, resample=L.RESAMPLE_NONE, gn_stats=None,
+                out_f32=False):
     """out[pixels][cout] = conv3x3(resample(x)) with packed weights wf [cout][9*cin]
-    (gn_stats: as linear_fwd)."""
+    (gn_stats: as linear_fwd; out_f32: fp32 output)."""
     cout = wf.shape[0]
     gemm(g.pixels, cout, 9 * cin, x, _ld(x), wf, _ld(wf), out, _ld(out), a_mode=L.OPA_IM2COL,
-         conv=_conv_geom(g, cin, resample, x), bias=bias, resid=resid,
+         c_mode=L.OUT_F32 if out_f32 else L.OUT_BF16, conv=_conv_geom(g, cin, resample, x), bias=bias, resid=resid,
          ld_resid=_ld(resid) if resid is not None else 0, gn_stats=gn_stats,
          split_k=1 if gn_stats is not None else None)
 
@@ -377,11 +380,12 @@ def conv3x3_bwd_cl(dy, g: Geom, wf, x, cin, dw_cl, dx, db=None, resample=L.RESAM
 
 
 # ------------------------------------------------------------------ 4x4 stride-2 convolutions
-def conv4x4s2_fwd(x, g_out: Geom, cin, wf, out, bias=None):
+def conv4x4s2_fwd(x, g_out: Geom, cin, wf, out, bias=None, out_f32=False):
     """Conv2d(k4, s2, p1) (Encoder4, openaimodel_enc.py:1002-1009): x at (2h, 2w), out at
-    g_out = (h, w); wf packed [cout][16*cin] ([co][kh][kw][ci])."""
+    g_out = (h, w); wf packed [cout][16*cin] ([co][kh][kw][ci]); out_f32: fp32 output."""
     cout = wf.shape[0]
     gemm(g_out.pixels, cout, 16 * cin, x, _ld(x), wf, _ld(wf), out, _ld(out), a_mode=L.OPA_IM2COL,
+         c_mode=L.OUT_F32 if out_f32 else L.OUT_BF16,
          conv=L.ConvGeom(batch=g_out.batch, h=g_out.h, w=g_out.w, cin=cin, resample=L.RESAMPLE_K4S2,
                          ld_src=_ld(x)), bias=bias)
 
@@ -563,10 +567,20 @@ def q_sample(x0, eps, t, sqrt_ac, sqrt_1mac, xt):
                                _s()), "encdiff_q_sample")
 
 
+_L1_SCRATCH = {}
+
+
 def l1_loss(pred, eps, t, lvlb, out2, grad=None, l_simple_weight=1.0):
+    """out2 = (loss, loss_vlb); grad = the L1 seed.  Per-sample partials and the last-block
+    ticket live in a per-(device, stream, batch) scratch (stream-ordered reuse is safe)."""
     b = pred.shape[0]
+    key = (pred.device.index, torch.cuda.current_stream().cuda_stream, b)
+    sc = _L1_SCRATCH.get(key)
+    if sc is None:
+        sc = _L1_SCRATCH[key] = (torch.empty(b, device=pred.device, dtype=torch.float32),
+                                 torch.zeros(1, device=pred.device, dtype=torch.int32))
     check(lib.encdiff_l1_loss(_p(pred), _p(eps), _p(t), _p(lvlb), b, pred.numel() // b, l_simple_weight,
-                              _p(out2), _p(grad), _s()), "encdiff_l1_loss")
+                              _p(out2), _p(grad), _p(sc[0]), _p(sc[1]), _s()), "encdiff_l1_loss")
 
 
 def ddim_step(x, e, noise, a_t, a_prev, sigma, s1, x_prev, pred_x0=None):

@@ -68,15 +68,32 @@ class HipTrainer:
         self.img = torch.empty(batch_size, 3, 64, 64, device=self.dev)
         self.loss_buf = torch.zeros(4, device=self.dev)
         self.graph = graph
+        self._feed = None  # test hook: batch, t and noise from static buffers (enable_feed)
         self._g_fb = None
         self._g_cond = None
         self._g_opt = None
         self._c = self._dc = None
         torch.manual_seed(rank_seed(seed, self.rank))
 
+    # ---------------------------------------------------------------- test hook
+    def enable_feed(self):
+        """Parity-test hook (call before capture): the step reads its image batch, timesteps
+        and noise from static buffers -- ``feed_img`` (B, 3, 64, 64) fp32, ``feed_t`` (B,)
+        int64, ``feed_noise`` like z -- instead of the image pool and the RNG.  The captured
+        graph reads them on every replay, so a checker writes a step's inputs and replays the
+        same graph the benchmark times."""
+        z_shape = (self.B, self.ldm.channels, self.ldm.image_size, self.ldm.image_size)
+        self._feed = dict(img=torch.zeros(self.B, 3, 64, 64, device=self.dev),
+                          t=torch.zeros(self.B, dtype=torch.long, device=self.dev),
+                          noise=torch.zeros(z_shape, device=self.dev))
+        return self._feed
+
     # ---------------------------------------------------------------- device work
-    def _draw_batch(self):
-        self.data.draw(self.img)
+    def _draw_batch(self, advance=True):
+        if self._feed is not None:
+            self.img.copy_(self._feed["img"])
+        else:
+            self.data.draw(self.img, advance=advance)
 
     def _fwd_bwd(self):
         """Everything up to the UNet backward.  At world size 1 Encoder4's backward runs
@@ -89,8 +106,11 @@ class HipTrainer:
         with torch.no_grad():
             z = ldm.get_first_stage_encoding(ldm.encode_first_stage(self.img)).detach()
         c = ldm.get_learned_conditioning(self.img)
-        t = torch.randint(0, ldm.num_timesteps, (self.B,), device=self.dev)
-        noise = torch.randn_like(z)
+        if self._feed is not None:
+            t, noise = self._feed["t"], self._feed["noise"]
+        else:
+            t = torch.randint(0, ldm.num_timesteps, (self.B,), device=self.dev)
+            noise = torch.randn_like(z)
         if self.world == 1:
             loss, ld = ldm.p_losses(z, c, t, noise)
             loss.backward()
@@ -165,8 +185,10 @@ class HipTrainer:
     # ---------------------------------------------------------------- setup
     def init_scale_factor(self):
         """scale_by_std on the first batch (ddpm_enc.py:586-608), computed on rank 0 and
-        broadcast (the reference's @rank_zero_only re-registration never reaches other ranks)."""
-        self._draw_batch()
+        broadcast (the reference's @rank_zero_only re-registration never reaches other ranks).
+        The batch is peeked (the pool's step counter does not advance), so the epoch still
+        visits every batch once."""
+        self._draw_batch(advance=False)
         self.ldm.init_scale_factor({"image": self.img.permute(0, 2, 3, 1)})
         if self.world > 1:
             dist.broadcast(self.ldm.scale_factor, 0)

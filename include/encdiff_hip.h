@@ -298,10 +298,13 @@ int encdiff_q_sample(const float* x0, const float* eps, const long long* t, cons
 
 /* p_losses L1 (ddpm_enc.py:1194-1213): loss_simple[b] = mean|eps - pred|,
  * out[0] = mean_b loss_simple (= loss with logvar 0), out[1] = mean_b lvlb[t_b] loss_simple[b];
- * grad_pred = sign(pred - eps) / (batch * per_sample) * l_simple_weight. */
+ * grad_pred = sign(pred - eps) / (batch * per_sample) * l_simple_weight.
+ * partials: caller scratch of `batch` floats (receives loss_simple[b]); counter: a
+ * zero-initialised device uint32 the kernel leaves at zero (the last block folds the batch in a
+ * fixed order: one launch, no memset, bitwise reproducible). */
 int encdiff_l1_loss(const float* pred, const float* eps, const long long* t, const float* lvlb,
                     int batch, int per_sample, float l_simple_weight, float* out2, float* grad_pred,
-                    void* stream);
+                    float* partials, unsigned int* counter, void* stream);
 
 /* DDIM update (ddim.py:197-206) for one step with scalar coefficients:
  * pred_x0 = (x - s1 e) / sqrt(a_t); x' = sqrt(a_prev) pred_x0 + sqrt(1-a_prev-sigma^2) e + sigma z. */
@@ -332,7 +335,12 @@ int encdiff_adamw_ema(float* p, const float* g, float* m, float* v, float* ema, 
  * elements: dst[r*dst_ld + c] = src[src_index(r, c)], kind 0: src[r*cols + c]
  * (identity), kind 1: conv [co][ci][3][3] -> [co][tap][ci] (r=co, c=tap*cin+ci), kind 2:
  * conv [co][cin][taps] -> [co][tap][8] with channels cin..7 zero (cols = 8*taps; the
- * first Encoder4 conv, image channels padded to 8). */
+ * first Encoder4 conv, image channels padded to 8).  Split-bf16 (bf16x3) forms, hi = bf16(w),
+ * lo = bf16(w - hi): kind 3: [co][tap][cin] -> [co][tap][hi|hi|lo] (cols = 3*cin*taps); kind 4:
+ * [co][cin][taps] (cin <= 8) -> [co][tap][hi8|hi8|lo8] (cols = 24*taps); kind 5: [co][cin] ->
+ * [co][hi|hi|lo|I|I] (cols = 5*cin, co == cin: a 1x1 conv plus an identity residual).  With
+ * activations stored [hi|lo|hi] (+ [hi|lo] for the residual) one GEMM forms a_hi w_hi + a_lo w_hi +
+ * a_hi w_lo: fp32-class products for the Encoder4 forward (see cond.py). */
 typedef struct EncdiffPackJob {
   long long src_off, dst_off;
   int rows, cols, kind, cin;
@@ -390,8 +398,8 @@ int encdiff_encoder_warp_partials_floats(int batch, int units, long unit_stride)
 typedef struct EncdiffBatchNormArgs {
   int rows, c;
   float eps, momentum;
-  int relu, pad_;
-  const void* x; long ldx;          /* bf16 [rows][c] (pre-BN activations)           */
+  int relu, x_f32;                  /* x_f32: x is fp32 (else bf16)                  */
+  const void* x; long ldx;          /* [rows][c] pre-BN activations, bf16 or fp32    */
   const float* gamma; const float* beta;
   void* y; long ldy;                /* fwd: bf16 out                                 */
   float* mean; float* rstd;         /* [c]: written by fwd, read by bwd              */
@@ -401,15 +409,24 @@ typedef struct EncdiffBatchNormArgs {
   const void* dy; long lddy;        /* bwd: gradient of the (activated) output       */
   void* dx; long lddx;              /* bwd: bf16 out                                 */
   float* dgamma; float* dbeta;      /* bwd: fp32 +=                                  */
+  int y_split, pad2_;               /* fwd / apply: y as split-bf16 blocks [hi|lo|hi] of c
+                                       channels each (bf16x3 GEMM operand), else plain bf16 */
 } EncdiffBatchNormArgs;
 
 int encdiff_batchnorm_partials_floats(int rows, int c);
 int encdiff_batchnorm_fwd(const EncdiffBatchNormArgs* args, void* stream);
 int encdiff_batchnorm_bwd(const EncdiffBatchNormArgs* args, void* stream);
+/* Eval-mode BatchNorm2d (+ReLU) (BatchNorm2d.eval(): running statistics): y = (x - mean) *
+ * rstd * gamma + beta with the caller's mean / rstd; no reduction (validation encoding pass,
+ * ddpm_enc.py:377-390).  partials / counter are not used. */
+int encdiff_batchnorm_apply(const EncdiffBatchNormArgs* args, void* stream);
 
 /* fp32 NCHW [batch][c][hw] -> bf16 rows [batch*hw][ldy], channels c..cpad-1 zero
  * (the image as the first Encoder4 conv's im2col source, channels padded to 8). */
 int encdiff_nchw_to_rows(const float* x, int batch, int c, int hw, int cpad, void* y, long ldy, void* stream);
+/* The same as split-bf16 blocks [hi | lo | hi] of cpad channels each (ldy >= 3 * cpad). */
+int encdiff_nchw_to_rows_split3(const float* x, int batch, int c, int hw, int cpad, void* y, long ldy,
+                                void* stream);
 
 /* Library/device information (for tests): returns the number of exported kernels. */
 int encdiff_version(void);

@@ -478,8 +478,9 @@ def encoder4_params(seed=0, **kw):
     return P
 
 
-def encoder4_forward(P, x, latent_unit=20, train=True):
-    """openaimodel_enc.py:996-1031 (BatchNorm in train mode uses batch stats)."""
+def encoder4_forward(P, x, latent_unit=20, train=True, return_u=False):
+    """openaimodel_enc.py:996-1031 (BatchNorm in train mode uses batch stats, eval mode the
+    running statistics).  return_u: also the scalar codes u = encoding(x) (:1034-1035)."""
     e = 'encoder.'
 
     def bn(h, i):
@@ -514,7 +515,117 @@ def encoder4_forward(P, x, latent_unit=20, train=True):
         y = F.elu(F.linear(y, P[f'net.{i}.0.weight'], P[f'net.{i}.0.bias']))
         y = F.elu(F.linear(y, P[f'net.{i}.2.weight'], P[f'net.{i}.2.bias']))
         outs.append(F.linear(y, P[f'net.{i}.4.weight'], P[f'net.{i}.4.bias']))
-    return torch.cat(outs, dim=1)
+    c = torch.cat(outs, dim=1)
+    return (c, u) if return_u else c
+
+
+# ----------------------------------------------------------------------------
+# Frozen VQ first-stage encoder (VQModelInterface.encode, autoencoder.py:313-316 =
+# quant_conv(Encoder(x)); Encoder model.py:368-459, ResnetBlock :82-141, AttnBlock
+# :150-200, Downsample :60-80, Normalize :38-39 (GroupNorm 32, eps 1e-6),
+# nonlinearity :33-35 (x * sigmoid(x))), functional.  Parameter names are the
+# first_stage_model state_dict names.
+# ----------------------------------------------------------------------------
+
+VQ_F4 = dict(ch=32, ch_mult=(1, 2, 4), num_res_blocks=2, attn_resolutions=(), in_channels=3, z_channels=3,
+             embed_dim=3, resolution=64)  # shapes3d-vq-4-16-encdiff.yaml first_stage_config
+
+
+def vq_encoder_shapes(cfg=VQ_F4) -> Dict[str, Tuple[int, ...]]:
+    S: Dict[str, Tuple[int, ...]] = {}
+
+    def conv(pre, co, ci, k):
+        S[pre + 'weight'] = (co, ci, k, k)
+        S[pre + 'bias'] = (co,)
+
+    def norm(pre, c):
+        S[pre + 'weight'] = (c,)
+        S[pre + 'bias'] = (c,)
+
+    def resnet(pre, ci, co):  # model.py:82-119 (temb_channels = 0: no temb_proj)
+        norm(pre + 'norm1.', ci)
+        conv(pre + 'conv1.', co, ci, 3)
+        norm(pre + 'norm2.', co)
+        conv(pre + 'conv2.', co, co, 3)
+        if ci != co:
+            conv(pre + 'nin_shortcut.', co, ci, 1)
+
+    def attn(pre, c):  # model.py:150-176
+        norm(pre + 'norm.', c)
+        for n in ('q', 'k', 'v', 'proj_out'):
+            conv(pre + n + '.', c, c, 1)
+
+    ch, mult = cfg['ch'], tuple(cfg['ch_mult'])
+    conv('encoder.conv_in.', ch, cfg['in_channels'], 3)
+    in_mult = (1,) + mult
+    curr = cfg['resolution']
+    bi = ch
+    for i, m in enumerate(mult):  # model.py:386-408
+        bi, bo = ch * in_mult[i], ch * m
+        for j in range(cfg['num_res_blocks']):
+            resnet(f'encoder.down.{i}.block.{j}.', bi, bo)
+            bi = bo
+            if curr in cfg['attn_resolutions']:
+                attn(f'encoder.down.{i}.attn.{j}.', bi)
+        if i != len(mult) - 1:
+            conv(f'encoder.down.{i}.downsample.conv.', bi, bi, 3)
+            curr //= 2
+    resnet('encoder.mid.block_1.', bi, bi)
+    attn('encoder.mid.attn_1.', bi)
+    resnet('encoder.mid.block_2.', bi, bi)
+    norm('encoder.norm_out.', bi)
+    conv('encoder.conv_out.', cfg['z_channels'], bi, 3)
+    conv('quant_conv.', cfg['embed_dim'], cfg['z_channels'], 1)
+    return S
+
+
+def vq_encoder_params(seed=0, cfg=VQ_F4) -> Dict[str, torch.Tensor]:
+    """Recipe weights under the fixtures' naming ('vq.' + state_dict name)."""
+    return {k: recipe_tensor('vq.' + k, sh, seed) for k, sh in vq_encoder_shapes(cfg).items()}
+
+
+def vq_encode(P: Dict[str, torch.Tensor], x: torch.Tensor, cfg=VQ_F4) -> torch.Tensor:
+    """autoencoder.py:313-316: quant_conv(Encoder(x)) (no quantisation on encode)."""
+    def gn(h, pre):
+        return F.group_norm(h, 32, P[pre + 'weight'], P[pre + 'bias'], eps=1e-6)
+
+    def swish(h):
+        return h * torch.sigmoid(h)
+
+    def conv(h, pre, stride=1, padding=1):
+        return F.conv2d(h, P[pre + 'weight'], P[pre + 'bias'], stride=stride, padding=padding)
+
+    def resnet(h, pre):  # model.py:121-141
+        y = conv(swish(gn(h, pre + 'norm1.')), pre + 'conv1.')
+        y = conv(swish(gn(y, pre + 'norm2.')), pre + 'conv2.')
+        if pre + 'nin_shortcut.weight' in P:
+            h = conv(h, pre + 'nin_shortcut.', padding=0)
+        return h + y
+
+    def attn(h, pre):  # model.py:178-200
+        hn = gn(h, pre + 'norm.')
+        q, k, v = (conv(hn, pre + n + '.', padding=0) for n in ('q', 'k', 'v'))
+        b, c, hh, ww = q.shape
+        w_ = torch.bmm(q.reshape(b, c, hh * ww).permute(0, 2, 1), k.reshape(b, c, hh * ww)) * (int(c) ** (-0.5))
+        w_ = torch.softmax(w_, dim=2)
+        o = torch.bmm(v.reshape(b, c, hh * ww), w_.permute(0, 2, 1)).reshape(b, c, hh, ww)
+        return h + conv(o, pre + 'proj_out.', padding=0)
+
+    mult = tuple(cfg['ch_mult'])
+    h = conv(x, 'encoder.conv_in.')
+    for i in range(len(mult)):  # model.py:434-450
+        for j in range(cfg['num_res_blocks']):
+            h = resnet(h, f'encoder.down.{i}.block.{j}.')
+            if f'encoder.down.{i}.attn.{j}.norm.weight' in P:
+                h = attn(h, f'encoder.down.{i}.attn.{j}.')
+        if i != len(mult) - 1:  # Downsample(with_conv): pad (0,1,0,1), conv k3 s2 p0 (model.py:72-76)
+            h = conv(F.pad(h, (0, 1, 0, 1), mode='constant', value=0), f'encoder.down.{i}.downsample.conv.',
+                     stride=2, padding=0)
+    h = resnet(h, 'encoder.mid.block_1.')
+    h = attn(h, 'encoder.mid.attn_1.')
+    h = resnet(h, 'encoder.mid.block_2.')
+    h = conv(swish(gn(h, 'encoder.norm_out.')), 'encoder.conv_out.')
+    return conv(h, 'quant_conv.', padding=0)
 
 
 # ----------------------------------------------------------------------------
@@ -536,33 +647,70 @@ def images_to_input(images_u8: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
 
 
 class OracleTrainer:
-    """CPU restatement of one LatentDiffusion training step on latents
-    (ddpm_enc.py:1040-1053, 1183-1253, 399-401, 1598-1639).  The frozen VQ
-    encode is skipped (latents given); Encoder4 is included."""
+    """CPU restatement of one LatentDiffusion training step (ddpm_enc.py:360-375 ->
+    get_input :773-844 (VQ encode * scale_factor), forward :1040-1053, p_losses
+    :1183-1253, AdamW :1598-1639, EMA :399-401 -> ema.py:25-44).  ``step`` takes latents
+    x0 (the frozen VQ encode skipped); ``step_images`` runs the VQ encode of the images
+    first, as the reference's get_input does.  Encoder4 is included (training-mode BN)."""
 
-    def __init__(self, plan: Plan, seed=0, lr=4 * 2e-6, dtype=torch.float32):
+    def __init__(self, plan: Plan, seed=0, lr=4 * 2e-6, dtype=torch.float32, vq=False):
         self.plan = plan
         shapes = param_shapes(plan)
         self.P = {k: v.to(dtype).requires_grad_(True) for k, v in recipe_params(shapes, seed).items()}
         E = encoder4_params(seed)
         self.E = {k: (v.to(dtype).requires_grad_(True) if v.is_floating_point() and 'running' not in k else v)
                   for k, v in E.items()}
+        self.V = {k: v.to(dtype) for k, v in vq_encoder_params(seed).items()} if vq else None
         self.sched = sched_fp32(register_schedule())
         params = list(self.P.values()) + [v for v in self.E.values() if isinstance(v, torch.Tensor)
                                           and v.requires_grad]
         self.opt = torch.optim.AdamW(params, lr=lr)
         self.ema = {k: v.detach().clone() for k, v in self.P.items()}
         self.num_updates = 0
+        self.scale_factor = 1.0
+        self.last = {}
 
-    def step(self, x0, img, t, noise):
+    def load_state(self, unet, cond, exp_avg, exp_avg_sq, step, ema, num_updates):
+        """Start from a given training state (e.g. the HIP trainer's after its warm-up):
+        parameters, AdamW moments (keyed by parameter name, 'cond.' prefix for Encoder4),
+        the AdamW step count, the EMA shadow and LitEma.num_updates."""
+        with torch.no_grad():
+            for k, p in self.P.items():
+                p.copy_(unet[k])
+            for k, p in self.E.items():
+                if k in cond and isinstance(p, torch.Tensor):
+                    p.copy_(cond[k])
+        for name, p in list(self.P.items()) + [('cond.' + k, v) for k, v in self.E.items()]:
+            if isinstance(p, torch.Tensor) and p.requires_grad:
+                self.opt.state[p] = {'step': torch.tensor(float(step)), 'exp_avg': exp_avg[name].clone(),
+                                     'exp_avg_sq': exp_avg_sq[name].clone()}
+        self.ema = {k: v.detach().clone() for k, v in ema.items()}
+        self.num_updates = int(num_updates)
+
+    def step(self, x0, img, t, noise, seed=None):
+        """One step; ``seed``: an upstream gradient for the model output to backpropagate
+        instead of d loss / d eps (the L1 seed sign(eps - noise)/N is discontinuous, so a
+        checker shares the seed the device computed)."""
         self.opt.zero_grad(set_to_none=True)
         c = encoder4_forward(self.E, img)
         x_noisy = q_sample(self.sched, x0, t, noise)
         out = unet_forward(self.P, self.plan, x_noisy, t, [c])
-        loss, _ = p_losses_from_output(self.sched, out, noise, t)
-        loss.backward()
+        loss, ld = p_losses_from_output(self.sched, out, noise, t)
+        if seed is None:
+            loss.backward()
+        else:
+            out.backward(seed)
         self.opt.step()
         with torch.no_grad():
             self.ema, self.num_updates = ema_update(self.ema, {k: v.detach() for k, v in self.P.items()},
                                                     self.num_updates)
+        self.last = dict(eps=out.detach(), x0=x0, loss=loss.detach())
         return loss.detach()
+
+    def encode_images(self, img):
+        """get_input (ddpm_enc.py:780-784): z = scale_factor * VQ.encode(img), no grad."""
+        with torch.no_grad():
+            return self.scale_factor * vq_encode(self.V, img)
+
+    def step_images(self, img, t, noise, seed=None):
+        return self.step(self.encode_images(img), img, t, noise, seed=seed)

@@ -87,27 +87,105 @@ def test_training_gradients_match_oracle(ldm):
         r = rel(unet[n].grad, P[n].grad)
         print(n, r)
         assert r < 5e-2, n
-    # Encoder4's trunk runs in bf16 with ReLU masks: near-zero pre-activations flip (see
-    # test_encoder4_trunk_hip), hence the looser bound on its first conv
+    # Encoder4's trunk forward runs on split-bf16 operands (cond.py): same 5e-2 bound
     cond = dict(ldm.cond_stage_model.named_parameters())
-    for n, tol in [("encoder.0.weight", 0.2), ("encoder.16.weight", 5e-2), ("net.3.4.weight", 5e-2)]:
+    for n, tol in [("encoder.0.weight", 5e-2), ("encoder.16.weight", 5e-2), ("net.3.4.weight", 5e-2)]:
         r = rel(cond[n].grad, E[n].grad)
         print("cond", n, r)
         assert r < tol, n
 
 
+def _ref_noise(steps=10, shape=(2, 3, 16, 16)):
+    """The reference's eta > 0 noise stream as tools/gen_golden.py drew it: torch.manual_seed(1234),
+    then one CPU torch.randn(x.shape) per step (ddim.py:201 noise_like)."""
+    torch.manual_seed(1234)
+    return torch.stack([torch.randn(shape) for _ in range(steps)])
+
+
 @pytest.mark.parametrize("graph", [False, True])
-def test_ddim_matches_reference(ldm, golden_dir, graph):
+@pytest.mark.parametrize("eta", [0, 1])
+def test_ddim_matches_reference(ldm, golden_dir, graph, eta):
+    """DDIM S=10 vs the reference's own samples (ddim.npz); eta = 1 with the reference's noise
+    stream injected through normals_sequence."""
     from encdiff_amd.ldm.models.diffusion.ddim import DDIMSampler
     fx = np.load(os.path.join(golden_dir, "ddim.npz"))
     cond = torch.tensor(fx["cond"]).cuda()
     s = DDIMSampler(ldm, use_graph=graph)
     with torch.no_grad():
-        out, inter = s.sample(10, 2, (3, 16, 16), cond, eta=0.0, verbose=False, x_T=torch.tensor(fx["xT"]).cuda())
-    r = rel(out, fx["samples_eta0"])
-    print("ddim eta0 graph=%s rel-L2" % graph, r)
-    assert r < 3e-2
+        out, inter = s.sample(10, 2, (3, 16, 16), cond, eta=float(eta), verbose=False,
+                              x_T=torch.tensor(fx["xT"]).cuda(), normals_sequence=_ref_noise().cuda())
+    r = rel(out, fx[f"samples_eta{eta}"])
+    rp = rel(inter["pred_x0"][-1], fx[f"pred_x0_last_eta{eta}"])
+    print(f"ddim eta{eta} graph={graph} rel-L2 samples {r:.3e} pred_x0 {rp:.3e}")
+    assert r < 3e-2 and rp < 3e-2
     assert len(inter["x_inter"]) >= 2
+
+
+def test_ddim_sampler_reuse(ldm, golden_dir):
+    """One sampler, several sample() calls (the captured loop must not keep reading a
+    previous call's schedule tables): eta 0 -> 1 -> 0 and a new x_T / conditioning, each equal to a
+    fresh eager run; a second call with the same inputs is bitwise identical."""
+    from encdiff_amd.ldm.models.diffusion.ddim import DDIMSampler
+    fx = np.load(os.path.join(golden_dir, "ddim.npz"))
+    cond = torch.tensor(fx["cond"]).cuda()
+    xT = torch.tensor(fx["xT"]).cuda()
+    nz = _ref_noise().cuda()
+    s = DDIMSampler(ldm, use_graph=True)
+    with torch.no_grad():
+        outs = []
+        for eta, c, x in ((0.0, cond, xT), (1.0, cond, xT), (0.0, cond.flip(0), xT * 0.5), (0.0, cond, xT)):
+            o, _ = s.sample(10, 2, (3, 16, 16), c, eta=eta, verbose=False, x_T=x, normals_sequence=nz)
+            e, _ = DDIMSampler(ldm, use_graph=False).sample(10, 2, (3, 16, 16), c, eta=eta, verbose=False, x_T=x,
+                                                              normals_sequence=nz)
+            r = rel(o, e)
+            print("reuse eta", eta, r)
+            assert r < 1e-5
+            outs.append(o)
+    assert torch.equal(outs[0], outs[3])
+    assert rel(outs[0], fx["samples_eta0"]) < 3e-2 and rel(outs[1], fx["samples_eta1"]) < 3e-2
+
+
+def test_ema_scope_uses_ema_weights(ldm):
+    """Inside ema_scope the UNet must run on the EMA weights (the bf16 packs were
+    refreshed only on master._version, which EMA copy_to/restore never bump)."""
+    ldm.setup_hip_training()
+    unet = ldm.model.diffusion_model
+    x = torch.randn(2, 3, 16, 16, device="cuda")
+    t = torch.tensor([10, 600], device="cuda")
+    c = torch.randn(2, 320, device="cuda") * 0.5
+    with torch.no_grad():
+        base = ldm.apply_model(x, t, c).clone()
+        saved = [p.detach().clone() for p in ldm.model.parameters()]
+        ema = ldm._arena.ema
+        ema.copy_(ldm._arena.master[: ema.numel()] * 0.9)   # EMA shadow != training weights
+        with ldm.ema_scope():
+            inside = ldm.apply_model(x, t, c).clone()
+            # reference: the same model with the parameters set to the shadow explicitly
+            want = [p.detach().clone() for p in ldm.model.parameters()]
+        after = ldm.apply_model(x, t, c).clone()
+        for p, w in zip(ldm.model.parameters(), want):
+            p.data.copy_(w)
+        ldm._arena.mark_dirty()
+        explicit = ldm.apply_model(x, t, c).clone()
+        for p, w in zip(ldm.model.parameters(), saved):
+            p.data.copy_(w)
+        ldm._arena.mark_dirty()
+        ema.copy_(ldm._arena.master[: ema.numel()])
+    assert torch.equal(after, base), "restore did not bring back the training weights"
+    assert torch.equal(inside, explicit), "ema_scope sampled with stale (non-EMA) weights"
+    assert rel(inside, base) > 1e-3
+    # load_state_dict after binding refreshes the packs too
+    sd = {k: v.clone() for k, v in unet.state_dict().items()}
+    with torch.no_grad():
+        k0 = "out.2.bias"
+        orig = sd[k0].clone()
+        sd[k0] = orig + 0.25
+        unet.load_state_dict(sd)
+        moved = ldm.apply_model(x, t, c).clone()
+        sd[k0] = orig
+        unet.load_state_dict(sd)
+        back = ldm.apply_model(x, t, c).clone()
+    assert rel(moved, base) > 1e-3 and torch.equal(back, base)
 
 
 def test_vq_encoder_hip():
@@ -162,12 +240,11 @@ def test_encoder4_trunk_hip():
     r = rel(u.detach(), u_ref.detach())
     print("u rel-L2", r)
     assert r < 3e-2
-    # ReLU masks are evaluated on bf16 activations: the ~1% of near-zero pre-activations whose
-    # sign differs from the fp32 reference each pass a full upstream gradient, which shows as
-    # ~10% rel-L2 on random-init gradients (the kernels themselves are pinned to 1e-2 in
-    # test_gpu_ops.py).  Gradients must agree to 0.2 rel-L2 and cos > 0.98; conv biases that
-    # feed a BatchNorm have zero true gradient: their bf16 residue is measured against the
-    # following BN's beta gradient (same scale).
+    # The forward runs on split-bf16 operands with fp32 pre-BatchNorm tensors (cond.py), so the
+    # ReLU masks match the fp32 reference's up to a few near-zero values; the backward is bf16.
+    # Gradients must agree to 5e-2 rel-L2 and cos > 0.998; conv biases that feed a BatchNorm
+    # have zero true gradient: their bf16 residue is measured against the following BN's beta
+    # gradient (same scale).
     got = dict(enc.named_parameters())
     pre_bn_bias = {"encoder.0.bias": "encoder.1.bias", "encoder.3.bias": "encoder.4.bias",
                    "encoder.6.bias": "encoder.7.bias", "encoder.8.bias": "encoder.9.bias",
@@ -184,13 +261,79 @@ def test_encoder4_trunk_hip():
             continue
         e, cos = rel(g, gr), torch.nn.functional.cosine_similarity(g, gr, dim=0).item()
         print(n, e, cos)
-        assert e < 0.2 and cos > 0.98, n
+        assert e < 5e-2 and cos > 0.998, n
     for (n, b), (_, b_ref) in zip(enc.named_buffers(), ref.named_buffers()):
         if "running" in n:
             assert rel(b, b_ref) < 2e-2, n
+        if "num_batches_tracked" in n:
+            assert int(b) == int(b_ref), n
     # two identical steps give bitwise identical gradients (deterministic BN folds)
     g1 = ldm._arena.grad.clone()
     ldm._arena.zero_grad()
     u = enc.encoding(x)
     (u * proj).sum().backward()
     assert torch.equal(g1, ldm._arena.grad)
+
+
+def test_validation_encoding_pass(ldm):
+    """Batched validation encoding pass (ddpm_enc.py:377-390): HBM-resident
+    uint8 images -> fused gather/normalise -> HIP Encoder4 trunk in eval mode (running BatchNorm
+    statistics) -> Linear -> warp, vs the oracle's eval-mode Encoder4 on the same images."""
+    from oracle import encdiff_oracle as O
+    g = torch.Generator().manual_seed(9)
+    n = 300
+    u8 = torch.randint(0, 256, (n, 64, 64, 3), generator=g, dtype=torch.uint8)
+    enc = ldm.cond_stage_model
+    ldm.setup_hip_training()
+    E = {k: (v.detach().cpu().clone()) for k, v in enc.state_dict().items()}
+    with torch.no_grad():  # non-trivial running statistics (as after training)
+        for k in E:
+            if k.endswith("running_mean"):
+                E[k] = torch.randn(E[k].shape, generator=g) * 0.1
+            elif k.endswith("running_var"):
+                E[k] = torch.rand(E[k].shape, generator=g) + 0.5
+        for k, b in enc.named_buffers():
+            if "running" in k:
+                b.copy_(E[k])
+    codes, toks = ldm.encode_dataset(u8.cuda(), chunk=128)
+    img = O.images_to_input(u8, torch.arange(n))
+    with torch.no_grad():
+        c_ref, u_ref = O.encoder4_forward(E, img, train=False, return_u=True)
+    r_u, r_c = rel(codes, u_ref), rel(toks.reshape(n, -1), c_ref)
+    print(f"validation pass: codes rel-L2 {r_u:.3e}, tokens {r_c:.3e}")
+    assert codes.shape == (n, 20) and toks.shape == (n, 20, 16)
+    assert r_u < 3e-2 and r_c < 3e-2
+    # validation_step / on_validation_epoch_end collect the same arrays batch by batch
+    for s0 in range(0, n, 128):
+        ldm.validation_step({"image": (img[s0:s0 + 128].permute(0, 2, 3, 1)).cuda()}, s0 // 128)
+    sc, outs = ldm.on_validation_epoch_end()
+    assert sc.shape == (n, 20) and outs.shape == (n, 20, 16)
+    assert rel(sc, codes) < 1e-5 and rel(outs, toks) < 1e-5
+
+
+def test_log_images_swap_one_batch(ldm):
+    """log_images(sample_swap=True) (ddpm_enc.py:1522-1535): the latent_unit swapped
+    conditionings are sampled as ONE (latent_unit * N) DDIM batch; row block cdx must equal the
+    reference's cdx-th separate call (same x_T rows), here run eagerly at batch N."""
+    from encdiff_amd.ldm.models.diffusion.ddim import DDIMSampler
+    ldm.setup_hip_training()
+    N, S = 4, 10
+    g = torch.Generator().manual_seed(4)
+    img = (torch.rand(N, 3, 64, 64, generator=g) * 2 - 1).cuda()
+    with torch.no_grad():
+        _, orc = ldm.encode_concepts(img)
+        xT = torch.randn(20 * N, 3, 16, 16, generator=g).cuda()
+        both = ldm.sample_swap(orc, N, ddim_steps=S, eta=0.0, x_T=xT)
+        for cdx in (0, 7, 19):
+            sc = orc.clone()
+            sc[:, cdx] = sc[0, cdx][None].repeat(N)
+            cond = ldm.cond_stage_model.warp(sc).reshape(N, -1)
+            one, _ = DDIMSampler(ldm, use_graph=False).sample(S, N, (3, 16, 16), cond, eta=0.0, verbose=False,
+                                                              x_T=xT[cdx * N:(cdx + 1) * N])
+            r = rel(both[cdx * N:(cdx + 1) * N], one)
+            print("swap row", cdx, r)
+            assert r < 1e-2
+        log = ldm.log_images({"image": img.permute(0, 2, 3, 1)}, N=N, ddim_steps=S, ddim_eta=0.0, sample_swap=True,
+                             plot_diffusion_rows=False)
+    assert log["samples_swapping"].shape == (20 * N, 3, 64, 64)
+    assert torch.isfinite(log["samples_swapping"]).all() and torch.isfinite(log["samples"]).all()

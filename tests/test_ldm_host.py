@@ -84,3 +84,72 @@ def test_reference_yaml_drops_in():
     # the data section's target also resolves (main.DataModuleFromConfig)
     from ldm.util import get_obj_from_str
     assert get_obj_from_str(cfg["data"]["target"]) is not None
+
+
+def _ref_layout_state_dict(golden_dir, seed=7):
+    """A Lightning-style checkpoint in the REFERENCE key layout (1862 keys and shapes recorded
+    from the reference model, latent_diffusion_state_dict_shapes.json), filled with seeded
+    values -- what a reference training run's .ckpt holds (ddpm_enc.py:204-220 loads it)."""
+    ref = json.load(open(os.path.join(golden_dir, "latent_diffusion_state_dict_shapes.json")))
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for k, shp in ref.items():
+        if k.endswith("num_batches_tracked") or k.endswith("num_updates"):
+            sd[k] = torch.tensor(5, dtype=torch.long if k.endswith("tracked") else torch.int)
+        else:
+            sd[k] = torch.randn(shp, generator=g) * 0.02
+    return sd
+
+
+def test_ckpt_roundtrip_init_from_ckpt(ldm, golden_dir, tmp_path):
+    """Reference-layout .ckpt {'state_dict', 'epoch', 'global_step'} -> init_from_ckpt
+    (strict=False, weights_only load): every key lands, values bitwise; then the build's own
+    state_dict saved the same way loads back into a fresh model (reference pattern:
+    test_ckpt_and_gradient.py:232-264)."""
+    from ldm.util import instantiate_from_config
+    sd = _ref_layout_state_dict(golden_dir)
+    path = tmp_path / "ref.ckpt"
+    torch.save({"state_dict": sd, "epoch": 3, "global_step": 11250}, path)
+    torch.manual_seed(1)
+    m = instantiate_from_config(model_config("shapes3d"))
+    missing, unexpected = m.init_from_ckpt(str(path))
+    assert not missing and not unexpected, (missing[:5], unexpected[:5])
+    got = m.state_dict()
+    for k, v in sd.items():
+        assert torch.equal(got[k].to(v.dtype), v), k
+    # ignore_keys drops a prefix (the rest loads, the ignored part keeps its init)
+    torch.manual_seed(2)
+    m2 = instantiate_from_config(model_config("shapes3d"))
+    before = m2.state_dict()["cond_stage_model.encoder.0.weight"].clone()
+    missing, _ = m2.init_from_ckpt(str(path), ignore_keys=["cond_stage_model."])
+    assert missing and all(k.startswith("cond_stage_model.") for k in missing)
+    assert torch.equal(m2.state_dict()["cond_stage_model.encoder.0.weight"], before)
+    assert torch.equal(m2.state_dict()["model.diffusion_model.out.2.weight"], sd["model.diffusion_model.out.2.weight"])
+    # build -> ckpt -> build
+    path2 = tmp_path / "mine.ckpt"
+    torch.save({"state_dict": m.state_dict(), "epoch": 4, "global_step": 15000}, path2)
+    torch.manual_seed(3)
+    m3 = instantiate_from_config(model_config("shapes3d"))
+    missing, unexpected = m3.init_from_ckpt(str(path2))
+    assert not missing and not unexpected
+    for k, v in m.state_dict().items():
+        assert torch.equal(m3.state_dict()[k], v), k
+
+
+def test_ckpt_pre_mcl_strict_false(ldm, golden_dir, tmp_path):
+    """strict=False tolerance as the reference relies on it (test_ckpt_and_gradient.py:232-264:
+    a checkpoint from before a module was added, or with extra keys, still loads): drop the
+    EMA keys and add a foreign one."""
+    from ldm.util import instantiate_from_config
+    sd = _ref_layout_state_dict(golden_dir, seed=8)
+    dropped = [k for k in sd if k.startswith("model_ema.")]
+    for k in dropped:
+        del sd[k]
+    sd["mcl_head.proj.weight"] = torch.zeros(4, 4)
+    path = tmp_path / "old.ckpt"
+    torch.save({"state_dict": sd}, path)
+    m = instantiate_from_config(model_config("shapes3d"))
+    missing, unexpected = m.init_from_ckpt(str(path))
+    assert set(missing) == set(dropped) and unexpected == ["mcl_head.proj.weight"]
+    assert torch.equal(m.state_dict()["model.diffusion_model.time_embed.0.weight"],
+                       sd["model.diffusion_model.time_embed.0.weight"])

@@ -116,3 +116,11 @@ def test_ema_adamw_lr(golden_dir):
         np.testing.assert_allclose(shadow[n].numpy(), fx["ema." + n.replace(".", "")], rtol=1e-5, atol=1e-7)
     for n, f in zip(fx["lr_n"], fx["lr_f"]):
         assert abs(O.lambda_linear_schedule(int(n)) - f) < 1e-12
+
+
+def test_vq_encoder_matches_reference(golden_dir):
+    """Oracle VQ first-stage encode (quant_conv(Encoder(x)), autoencoder.py:313-316) vs the
+    reference's own encode of the same recipe weights and images (p_losses.npz: vq_z)."""
+    fx = np.load(os.path.join(golden_dir, "p_losses.npz"))
+    z = O.vq_encode(O.vq_encoder_params(), torch.tensor(fx["img"]))
+    assert rel_l2(z, fx["vq_z"]) < 1e-5
