@@ -71,7 +71,8 @@ class AttnArgs(C.Structure):
                 ("q", vp), ("ldq", C.c_long), ("k", vp), ("ldk", C.c_long), ("v", vp), ("ldv", C.c_long),
                 ("o", vp), ("ldo", C.c_long), ("lse", vp),
                 ("d_o", vp), ("lddo", C.c_long), ("dq", vp), ("lddq", C.c_long),
-                ("dk", vp), ("lddk", C.c_long), ("dv", vp), ("lddv", C.c_long)]
+                ("dk", vp), ("lddk", C.c_long), ("dv", vp), ("lddv", C.c_long), ("fp8_qk", C.c_int),
+                ("pad_", C.c_int)]
 
 
 class EwArgs(C.Structure):

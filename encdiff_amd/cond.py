@@ -2,7 +2,7 @@
 
 Encoder4.encoder (openaimodel_enc.py:996-1012) is
 
-    Conv2d(3, d, 4, 2, 1)  BN ReLU      64x64 -> 32x32
+    Conv2d(3, d, 4, 2, 1)  BN ReLU      64x64 -> 32x32   (image_size 128: one more [Conv BN ReLU])
     Conv2d(d, d, 4, 2, 1)  BN ReLU            -> 16x16
     Conv2d(d, d, 4, 2, 1)  BN                 ->  8x8
     Conv2d(d, d, 4, 2, 1)  BN ReLU            ->  4x4
@@ -62,6 +62,33 @@ class _Conv:
 class Encoder4TrunkExecutor:
     """Binds Encoder4.encoder (all but View + Linear) to the parameter arena."""
 
+    @staticmethod
+    def layout(enc):
+        """Walk Encoder4.encoder (openaimodel_enc.py:996-1013; any number of stride-2 stages,
+        see Encoder4's image_size): [(conv idx, bn idx, relu)] for the Conv2d(k4, s2, p1) stages,
+        [(res idx, post-bn idx or None)] for the two EncResBlocks, the Linear's index."""
+        mods = list(enc.encoder)
+        stages, res, lin = [], [], None
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            if isinstance(m, torch.nn.Conv2d):
+                assert m.kernel_size == (4, 4) and m.stride == (2, 2) and isinstance(mods[i + 1], torch.nn.BatchNorm2d)
+                relu = i + 2 < len(mods) and isinstance(mods[i + 2], torch.nn.ReLU)
+                stages.append((i, i + 1, relu))
+                i += 3 if relu else 2
+            elif type(m).__name__ == "EncResBlock":
+                post = i + 1 if isinstance(mods[i + 1], torch.nn.BatchNorm2d) else None
+                res.append((i, post))
+                i += 3 if post is not None else 1
+            elif isinstance(m, torch.nn.Linear):
+                lin = i
+                i += 1
+            else:
+                i += 1
+        assert len(res) == 2 and lin == len(mods) - 1 and len(stages) >= 2, "Encoder4 trunk layout"
+        return stages, res, lin
+
     def __init__(self, enc, arena, prefix: str):
         seq = enc.encoder
         self.enc = enc
@@ -69,22 +96,21 @@ class Encoder4TrunkExecutor:
         self.prefix = prefix
         self.dev = arena.device
         mods = list(seq)
-        conv_idx = [0, 3, 6, 8]
-        bn_idx = [1, 4, 7, 9]
-        relu_after = [True, True, False, True]
+        stages, res, lin = self.layout(enc)
         self.d = mods[0].weight.shape[0]
         self.cin_img = mods[0].weight.shape[1]
-        assert mods[0].kernel_size == (4, 4) and self.cin_img <= 8, "Encoder4 trunk layout"
-        hs = [32, 16, 8, 4]
-        self.convs = [_Conv(f"encoder.{i}", mods[i], h, True) for i, h in zip(conv_idx, hs)]
-        self.bns = [(f"encoder.{i}", mods[i], r) for i, r in zip(bn_idx, relu_after)]
+        assert self.cin_img <= 8, "Encoder4 trunk layout"
+        self.img = 4 << len(stages)  # input resolution: every stage halves, the last output is 4x4
+        hs = [self.img >> (k + 1) for k in range(len(stages))]
+        self.convs = [_Conv(f"encoder.{ci}", mods[ci], h, True) for (ci, _, _), h in zip(stages, hs)]
+        self.bns = [(f"encoder.{bi}", mods[bi], r) for _, bi, r in stages]
         self.res = []
-        for ri, bi in ((11, 12), (14, None)):
+        for ri, bi in res:
             rb = mods[ri]
             c3, bnm, c1 = rb.convs[1], rb.convs[2], rb.convs[4]
             self.res.append(dict(prefix=f"encoder.{ri}.convs.", conv3=c3, bn=bnm, conv1=c1,
                                  post_bn=(f"encoder.{bi}", mods[bi]) if bi is not None else None))
-        self.flat = mods[16]
+        self.flat = mods[lin]
         pk = PackTable(arena)
         a = arena
         c0 = self.convs[0]
@@ -125,11 +151,14 @@ class Encoder4TrunkExecutor:
     def Graw(self, local):
         return self.arena.raw(self.arena.grad, self.pn(local))
 
-    @staticmethod
-    def channels_last_names(enc, prefix: str) -> List[str]:
-        """Conv weights the arena stores [co][kh][kw][ci] (the GEMM B layout)."""
-        out = [prefix + f"encoder.{i}.weight" for i in (3, 6, 8)]
-        out += [prefix + f"encoder.{ri}.convs.1.weight" for ri in (11, 14)]
+    @classmethod
+    def channels_last_names(cls, enc, prefix: str) -> List[str]:
+        """Conv weights the arena stores [co][kh][kw][ci] (the GEMM B layout): every stride-2
+        conv but the first (image channels padded to 8 in its own pack) and the EncResBlocks'
+        3x3 convs."""
+        stages, res, _ = cls.layout(enc)
+        out = [prefix + f"encoder.{ci}.weight" for ci, _, _ in stages[1:]]
+        out += [prefix + f"encoder.{ri}.convs.1.weight" for ri, _ in res]
         return out
 
     def _bn_state(self, B, key, rows, c):
@@ -149,11 +178,11 @@ class Encoder4TrunkExecutor:
         d = self.d
         # forward GEMM operands are split-bf16 rows [hi | lo | hi]; pre-BatchNorm tensors (conv
         # outputs, residual sums) are fp32 (see the module doc)
-        b = dict(x0=t(B * 64 * 64, 24))
+        b = dict(x0=t(B * self.img * self.img, 24))
         for i, c in enumerate(self.convs):
             n = B * c.hout * c.hout
             b[f"c{i}"], b[f"dc{i}"], b[f"da{i}"] = t(n, d, F32), t(n, d), t(n, d)
-            if i < 3:
+            if i < len(self.convs) - 1:
                 b[f"a{i}"] = t(n, 3 * d)
         n4 = B * 16
         for j in range(2):
@@ -216,13 +245,14 @@ class Encoder4TrunkExecutor:
     def forward(self, img: torch.Tensor, train: bool = True) -> torch.Tensor:
         """img fp32 NCHW (B, 3, 64, 64) -> trunk output fp32 (B, d*16) in NCHW-flatten order.
         train=False: BatchNorm with the running statistics (eval mode; no backward)."""
-        assert img.is_cuda and img.dtype == F32 and img.shape[1:] == (self.cin_img, 64, 64), \
-            "HIP Encoder4 trunk: fp32 (B, 3, 64, 64) device input"
+        assert img.is_cuda and img.dtype == F32 and img.shape[1:] == (self.cin_img, self.img, self.img), \
+            f"HIP Encoder4 trunk: fp32 (B, {self.cin_img}, {self.img}, {self.img}) device input"
         B = img.shape[0]
         b = self._bind(B)
         img = img.contiguous()
         d = self.d
-        L.check(L.lib.encdiff_nchw_to_rows_split3(img.data_ptr(), B, self.cin_img, 64 * 64, 8, b["x0"].data_ptr(), 24,
+        L.check(L.lib.encdiff_nchw_to_rows_split3(img.data_ptr(), B, self.cin_img, self.img * self.img, 8,
+                                                  b["x0"].data_ptr(), 24,
                                                   ops._s()), "encdiff_nchw_to_rows_split3")
         bn = self._bn_fwd if train else self._bn_eval
         x = b["x0"]
@@ -231,7 +261,7 @@ class Encoder4TrunkExecutor:
             w = self.pack.view("c0x3" if i == 0 else c.name + "x3")
             ops.conv4x4s2_fwd(x, g, x.shape[1], w, b[f"c{i}"], bias=self.P(c.name + ".bias"), out_f32=True)
             key, mod, relu = self.bns[i]
-            y = b[f"a{i}"] if i < 3 else b["R0"][:, 3 * d:]  # the last one feeds res block 0
+            y = b[f"a{i}"] if i < len(self.convs) - 1 else b["R0"][:, 3 * d:]  # the last one feeds res block 0
             bn(B, key, mod, b[f"c{i}"], y, relu)
             x = y
         g4 = Geom(B, 4, 4)
@@ -276,7 +306,7 @@ class Encoder4TrunkExecutor:
             ops.conv3x3_bwd_cl(b[f"dt{j}"], g4, self.pack.view(p + "1"), R[:, 3 * d:4 * d], d,
                                self.Graw(p + "1.weight"), b[f"dh{j}"], self.G(p + "1.bias"), resid=dh)
             dh = b[f"dh{j}"]
-        for i in (3, 2, 1, 0):
+        for i in range(len(self.convs) - 1, -1, -1):
             c = self.convs[i]
             key, mod, relu = self.bns[i]
             self._bn_bwd(B, key, mod, b[f"c{i}"], dh, b[f"dc{i}"], relu)

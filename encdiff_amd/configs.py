@@ -42,12 +42,29 @@ SHAPES3D = {
 }
 SHAPES3D_BATCH = 128  # data.params.batch_size
 
+# BASELINE.json configs[4] -- builder-defined (the reference has no CelebA config; SURVEY.md §8(d)
+# config 5): 128x128 images -> VQ-f4 latent (B, 3, 32, 32), wider UNet (model_channels 128) and
+# 40 concept tokens; Encoder4 with one more stride-2 stage (image_size=128) so its trunk still
+# ends on 4x4; the S = 1024 level-0 self-attention runs its forward on fp8 (e4m3) MFMA
+# (UNetModel attn_fp8_min_tokens).
+CELEBA128 = copy.deepcopy(SHAPES3D)
+_c = CELEBA128["params"]
+_c["image_size"] = 32
+_c["eval_name"] = "celeba"
+_c["unet_config"]["params"].update(image_size=32, model_channels=128, latent_unit=40, attn_fp8_min_tokens=1024)
+_c["first_stage_config"]["params"]["ddconfig"]["resolution"] = 128
+_c["first_stage_config"]["params"]["disentangled_dim"] = 40
+_c["cond_stage_config"]["params"].update(latent_unit=40, image_size=128)
+CELEBA128_BATCH = 128
+
 
 def model_config(name: str = "shapes3d") -> dict:
     if name in ("shapes3d", "mpi3d", "cars3d"):
         cfg = copy.deepcopy(SHAPES3D)
         cfg["params"]["eval_name"] = name
         return cfg
+    if name == "celeba128":
+        return copy.deepcopy(CELEBA128)
     raise KeyError(name)
 
 

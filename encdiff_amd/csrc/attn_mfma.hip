@@ -1,16 +1,30 @@
-// attn_mfma.hip -- MFMA attention for the SpatialTransformer heads (attention.py:170-193).
+// attn_mfma.hip -- MFMA attention for the SpatialTransformer heads (attention.py:170-193)
+// and the VQ encoder's single-head AttnBlock (model.py:178-200, forward only).
 //
-// v_mfma_f32_16x16x16_bf16 (K = 16) tiles; head dims 8/16/32 are zero-padded to 16/16/32.
-// Forward: per wave a 16-query tile; S^T = K Q^T is computed "swapped" so each lane holds
-// 4 consecutive keys of ONE query: the row max / sum of the online softmax are in-register
-// plus two cross-lane xor-shuffles, and the bf16 P is already the B operand of
-// O^T = V^T P^T (no LDS round trip for P).  K and V of the block's heads live in LDS
-// row-major; the V^T operand is read transposed (ds_read_b64_tr_b16).
+// v_mfma_f32_16x16x16_bf16 (K = 16) tiles; head dims 8/16/32/64/128, 8 zero-padded to 16.
+// Forward: per wave a pair of 16-query tiles; S^T = K Q^T is computed "swapped" so each lane
+// holds 4 consecutive keys of ONE query: the row max of the online softmax is in-register plus
+// two cross-lane xor-shuffles, and the bf16 P is already the B operand of O^T = V^T P^T (no
+// LDS round trip for P).  K and V of the block's heads live in LDS row-major; the V^T operand
+// is read transposed (ds_read_b64_tr_b16).
+//
+// The kernels are VALU-bound (exp / max / convert per score; the QK^T and PV MFMAs are a few
+// percent of the issue slots even at dh = 8, where K is half padding), so the work per score is
+// what is trimmed: the softmax scale is folded into the exp's FMA (max over raw scores), and at
+// dh = 8 the softmax denominator comes out of the PV MFMA for free -- V^T's first padding row
+// is all ones, so O^T row 8 accumulates sum_k p under the same online rescaling.
+//
 // Backward (recompute from LSE, no score matrix in HBM): phase A -- waves own key tiles and
-// accumulate dK^T, dV^T over all query tiles; phase B -- waves own query tiles and
-// accumulate dQ^T over all key tiles.  Q, K, V, dO are staged row-major in LDS once per
-// (image, head group) -- the Q^T, K^T, dO^T operands are transposed reads of them -- and
-// rowsum(dO * O) is computed while staging.
+// accumulate dK^T, dV^T over all query tiles, computing dS = P (dP - D); phase B -- waves own
+// query tiles and accumulate dQ^T = K^T dS^T over all key tiles.  When a head group's dS fits
+// the workgroup's LDS (S <= 256) phase A leaves dS^T there and phase B is MFMAs only (no
+// second exp pass); otherwise phase B recomputes it.  Q, K, V, dO are staged row-major in LDS
+// once per (image, head group) -- unpadded at dh = 8 -- the Q^T, K^T, dO^T operands are
+// transposed reads of them, and rowsum(dO * O) is computed while staging.
+//
+// F8 (configs[4]'s S = 1024 level): the scores Q K^T come from v_mfma_f32_16x16x32_fp8_fp8
+// on OCP e4m3 operands (Q, K rounded to e4m3; the same scores in the backward's recompute);
+// softmax, P V and every gradient product stay bf16 / fp32.
 #include "common.h"
 
 namespace {
@@ -24,7 +38,9 @@ ED_DEV s4 ld4(const bf16_t* p) { return *(const s4*)p; }
 // Transposed MFMA operand from a row-major LDS tile [rows][ld]: lane (l16, g) receives
 // t[r0 + 4g + i][c0 + l16], i = 0..3 -- the A (or B) fragment whose k runs along the tile's
 // rows -- via ds_read_b64_tr_b16: lane (tq, tp) = (l16 >> 2, l16 & 3) addresses row
-// r0 + 4g + tq, columns c0 + 4tp .. +3.  Needs every lane of the wave active.
+// r0 + 4g + tq, columns c0 + 4tp .. +3.  Needs every lane of the wave active.  With a row pitch
+// narrower than 16 (dh = 8 staging) lanes l16 >= 8 read the next row: those land in output rows
+// (head-dim rows >= dh) that are never stored.
 typedef __attribute__((address_space(3))) s4 lds_s4;
 ED_DEV s4 ldtr(const bf16_t* t, int ld, int r0, int c0, int l16, int g) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(t + (r0 + 4 * g + (l16 >> 2)) * ld + c0 + 4 * (l16 & 3)));
@@ -34,10 +50,30 @@ ED_DEV s4 pack4(float a, float b, float c, float d) {
   return __builtin_bit_cast(s4, u);
 }
 
+// ---- fp8 (OCP e4m3) score fragments: lane (g, l16) holds elements 8g .. 8g+7 of row l16 ----
+ED_DEV v4f mma8(long a, long b, const v4f& c) { return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0); }
+ED_DEV long to_fp8x8(const uint4& u) {
+  float f[8];
+  unpack8(u, f);
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+  return (long)(((unsigned long)(unsigned)hi << 32) | (unsigned)lo);
+}
+// k-step kc (32 head-dim elements) of row `row` of a bf16 row-major tile with pitch ld
+template <int DH>
+ED_DEV long frag8(const bf16_t* t, int ld, int row, int kc, int g) {
+  const int d0 = kc * 32 + 8 * g;
+  if (d0 >= DH) return 0;
+  return to_fp8x8(*(const uint4*)(t + row * ld + d0));
+}
+
 // Stage one tensor (rows [S][DH] of head h of image b, row stride ld) for the hpb heads
 // bh0 .. bh0+hpb-1 of the workgroup into LDS row-major [SP][DP] per head (rm + hl * rm_hs),
-// zero padding.  Loads are issued U at a time before their LDS writes.
-template <int DH, int DP, int U>
+// zero padding (ONES: column DH of every valid row is 1.0 -- the forward's V denominator row).
+// Loads are issued U at a time before their LDS writes.
+template <int DH, int DP, int U, bool ONES = false>
 ED_DEV void stage_heads_u(const bf16_t* __restrict__ base, long ld, int S, int SP, int H, int bh0, int hpb,
                           bf16_t* rm, int rm_hs) {
   constexpr int CH = DP / 8;
@@ -57,6 +93,7 @@ ED_DEV void stage_heads_u(const bf16_t* __restrict__ base, long ld, int S, int S
         const int bh = bh0 + hl[u], b = bh / H, h = bh - b * H;
         v[u] = *(const uint4*)(base + ((long)b * S + r[u]) * ld + h * DH + c8[u]);
       }
+      if (ONES && e < total && r[u] < S && c8[u] == DH) v[u].x = 0x3F80u;  // bf16 1.0 in column DH
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -65,30 +102,32 @@ ED_DEV void stage_heads_u(const bf16_t* __restrict__ base, long ld, int S, int S
     }
   }
 }
-template <int DH, int DP>
+template <int DH, int DP, bool ONES = false>
 ED_DEV void stage_heads(const bf16_t* __restrict__ base, long ld, int S, int SP, int H, int bh0, int hpb,
                         bf16_t* rm, int rm_hs) {
   // several heads (short sequences): 4 chunks per thread in flight; one long head: the
   // plain loop measured faster (fewer live registers in the 2-workgroup-per-CU kernels)
-  if (hpb > 1) stage_heads_u<DH, DP, 4>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs);
-  else stage_heads_u<DH, DP, 1>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs);
+  if (hpb > 1) stage_heads_u<DH, DP, 4, ONES>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs);
+  else stage_heads_u<DH, DP, 1, ONES>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs);
 }
 
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
-// Forward.  A wave task is a PAIR of 16-query tiles of one head: the K and V^T fragments
-// read from LDS serve both, and the two online-softmax chains are independent.  Keys are
-// consumed 32 at a time (two MFMA tiles) per softmax update, halving the max / rescale
-// work per score; scores live in the log2 domain (scale * log2 e folded, raw v_exp_f32 --
-// arguments are <= 0, underflow to 0 is the correct limit).  MASK: key count not a
-// multiple of 32 (keys past SK get -inf).
 ED_DEV float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-template <int DH, bool MASK>
+// Forward.  A wave task is a PAIR of 16-query tiles of one head: the K and V^T fragments
+// read from LDS serve both, and the two online-softmax chains are independent.  Keys are
+// consumed 32 at a time (two MFMA tiles) per softmax update; the running max is kept in the
+// log2 domain (scale * log2 e) and p = exp2(s * scale * log2e - m) is one FMA + a raw
+// v_exp_f32 (arguments <= 0, underflow to 0 is the correct limit).  MASK: key count not a
+// multiple of 32 (keys past SK get -inf).
+template <int DH, bool MASK, bool F8>
 __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, int hpb) {
   constexpr int DP = DH < 16 ? 16 : DH;
   constexpr int KC = DP / 16;
+  constexpr bool ONES = DH == 8;   // denominator from the PV MFMA (V^T row 8 = 1)
+  constexpr int KC8 = (DH + 31) / 32;  // fp8 score k-steps
   extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
   const int H = p.heads, SQ = p.sq, SK = p.sk;
   const int SKP = (SK + 31) & ~31;
@@ -98,7 +137,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
   bf16_t* Ks = sm;                        // [hpb][SKP][DP]
   bf16_t* Vs = sm + hpb * SKP * DP;       // [hpb][SKP][DP], read transposed (ds_read_b64_tr_b16)
   stage_heads<DH, DP>((const bf16_t*)p.k, p.ldk, SK, SKP, H, bh0, hpb, Ks, SKP * DP);
-  stage_heads<DH, DP>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, Vs, SKP * DP);
+  stage_heads<DH, DP, ONES>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, Vs, SKP * DP);
   __syncthreads();
   const int qtiles = (SQ + 15) >> 4, npairs = (qtiles + 1) >> 1;
   const float sl2 = p.scale * LOG2E;
@@ -108,16 +147,25 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
     const bf16_t* kb = Ks + hl * SKP * DP;
     const bf16_t* vb = Vs + hl * SKP * DP;
     s4 qf[2][KC];
+    long qf8[2][KC8];
     int q[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       q[u] = (2 * qp + u) * 16 + l16;
       const bool qv = q[u] < SQ;
       const bf16_t* qp_ = (const bf16_t*)p.q + ((long)b * SQ + q[u]) * p.ldq + h * DH;
+      if constexpr (F8) {
 #pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        const int d0 = kc * 16 + 4 * g;
-        qf[u][kc] = (qv && d0 < DH) ? ld4(qp_ + d0) : (s4){0, 0, 0, 0};
+        for (int kc = 0; kc < KC8; ++kc) {
+          const int d0 = kc * 32 + 8 * g;
+          qf8[u][kc] = (qv && d0 < DH) ? to_fp8x8(*(const uint4*)(qp_ + d0)) : 0;
+        }
+      } else {
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          const int d0 = kc * 16 + 4 * g;
+          qf[u][kc] = (qv && d0 < DH) ? ld4(qp_ + d0) : (s4){0, 0, 0, 0};
+        }
       }
     }
     float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
@@ -128,10 +176,17 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
       for (int dt = 0; dt < KC; ++dt) o[u][dt] = (v4f){0.f, 0.f, 0.f, 0.f};
     for (int k0 = 0; k0 < SKP; k0 += 32) {
       s4 kf[2][KC];
+      long kf8[2][KC8];
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t) {
+        if constexpr (F8) {
 #pragma unroll
-        for (int kc = 0; kc < KC; ++kc) kf[t][kc] = ld4(kb + (k0 + t * 16 + l16) * DP + kc * 16 + 4 * g);
+          for (int kc = 0; kc < KC8; ++kc) kf8[t][kc] = frag8<DH>(kb, DP, k0 + t * 16 + l16, kc, g);
+        } else {
+#pragma unroll
+          for (int kc = 0; kc < KC; ++kc) kf[t][kc] = ld4(kb + (k0 + t * 16 + l16) * DP + kc * 16 + 4 * g);
+        }
+      }
       s4 pf[2][2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -139,23 +194,33 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           v4f sc = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (F8) {
 #pragma unroll
-          for (int kc = 0; kc < KC; ++kc) sc = mma(kf[t][kc], qf[u][kc], sc);
+            for (int kc = 0; kc < KC8; ++kc) sc = mma8(kf8[t][kc], qf8[u][kc], sc);
+          } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            sv[4 * t + i] = (!MASK || k0 + t * 16 + 4 * g + i < SK) ? sc[i] * sl2 : -INFINITY;
+            for (int kc = 0; kc < KC; ++kc) sc = mma(kf[t][kc], qf[u][kc], sc);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sv[4 * t + i] = (!MASK || k0 + t * 16 + 4 * g + i < SK) ? sc[i] : -INFINITY;
         }
+        // max over raw scores (the scale is positive), the log2-domain max = that * sl2
         float tmax = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
                            fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])));
         tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
         tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-        const float mn = fmaxf(m[u], tmax);
+        const float mn = fmaxf(m[u], tmax * sl2);
         const float alpha = ex2(m[u] - mn);
         m[u] = mn;
-        float ls = 0.f, pv[8];
+        float pv[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { pv[i] = ex2(sv[i] - mn); ls += pv[i]; }
-        l[u] = l[u] * alpha + ls;
+        for (int i = 0; i < 8; ++i) pv[i] = ex2(__builtin_fmaf(sv[i], sl2, -mn));
+        if constexpr (!ONES) {
+          float ls = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) ls += pv[i];
+          l[u] = l[u] * alpha + ls;
+        }
 #pragma unroll
         for (int dt = 0; dt < KC; ++dt) o[u][dt] *= alpha;
         pf[u][0] = pack4(pv[0], pv[1], pv[2], pv[3]);
@@ -172,9 +237,15 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      float lu = l[u];
-      lu += __shfl_xor(lu, 16, 64);
-      lu += __shfl_xor(lu, 32, 64);
+      float lu;
+      if constexpr (ONES) {
+        // O^T row 8 (= g 2, register 0) is sum_k p for query l16: broadcast from lane 32 + l16
+        lu = __shfl(o[u][0][0], 32 + l16, 64);
+      } else {
+        lu = l[u];
+        lu += __shfl_xor(lu, 16, 64);
+        lu += __shfl_xor(lu, 32, 64);
+      }
       const float inv = 1.f / lu;
       if (q[u] < SQ) {
         bf16_t* op = (bf16_t*)p.o + ((long)b * SQ + q[u]) * p.ldo + h * DH;
@@ -200,29 +271,37 @@ __device__ __host__ inline int attn_qsplit(int ktiles, int hpb) {
   return t >= 4 ? 1 : (t >= 2 ? 2 : 4);
 }
 
-template <int DH, bool MASK>
-__global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, int hpb) {
-  constexpr int DP = DH < 16 ? 16 : DH;
+// dS^T row pitch in LDS: +16 elements (32 B) per row so the transposed reads of 8 consecutive
+// rows fall on different banks
+__device__ __host__ inline int ds_pitch(int sqp) { return sqp + 16; }
+
+template <int DH, bool MASK, bool F8>
+__global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, int hpb, int dsl) {
+  constexpr int DP = DH < 16 ? 16 : DH;   // MFMA k extent of the head dim
+  constexpr int RP = DH < 16 ? 8 : DH;    // LDS row pitch (dh = 8 staged unpadded)
   constexpr int KC = DP / 16;
+  constexpr int KC8 = (DH + 31) / 32;
   extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
   const int H = p.heads, SQ = p.sq, SK = p.sk;
   const int SQP = (SQ + 15) & ~15, SKP = (SK + 15) & ~15;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const int bh0 = blockIdx.x * hpb;
-  // per head, row-major: Q, dO [SQP][DP]; K, V [SKP][DP]; lse2, D [SQP].  The transposed
-  // operands (Q^T, dO^T, K^T) are read with ds_read_b64_tr_b16 instead of being stored.
-  const int QE = SQP * DP, KE = SKP * DP;
+  // per head, row-major: Q, dO [SQP][RP]; K, V [SKP][RP]; lse2, D [SQP]; (dsl) dS^T [SKP][SQP+16].
+  // The transposed operands (Q^T, dO^T, K^T, dS^T) are read with ds_read_b64_tr_b16.
+  const int QE = SQP * RP, KE = SKP * RP;
   const int oG = QE, oK = 2 * QE, oV = oK + KE;
   const int per_head = oV + KE;
   float* fls = (float*)(sm + hpb * per_head);
+  const int DSP = ds_pitch(SQP);
+  bf16_t* dS = (bf16_t*)(fls + hpb * 2 * SQP);  // [hpb][SKP][DSP] when dsl
   const int qtiles = SQP >> 4, ktiles = SKP >> 4;
   const int QS = attn_qsplit(ktiles, hpb);
-  float* red = fls + hpb * 2 * SQP;  // phase-A partials [task][2][16*DP lanes-major] when QS > 1
-  stage_heads<DH, DP>((const bf16_t*)p.q, p.ldq, SQ, SQP, H, bh0, hpb, sm, per_head);
-  stage_heads<DH, DP>((const bf16_t*)p.d_o, p.lddo, SQ, SQP, H, bh0, hpb, sm + oG, per_head);
-  stage_heads<DH, DP>((const bf16_t*)p.k, p.ldk, SK, SKP, H, bh0, hpb, sm + oK, per_head);
-  stage_heads<DH, DP>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, sm + oV, per_head);
+  float* red = (float*)(dS + (dsl ? hpb * SKP * DSP : 0));  // phase-A partials [task][2][16*DP] when QS > 1
+  stage_heads<DH, RP>((const bf16_t*)p.q, p.ldq, SQ, SQP, H, bh0, hpb, sm, per_head);
+  stage_heads<DH, RP>((const bf16_t*)p.d_o, p.lddo, SQ, SQP, H, bh0, hpb, sm + oG, per_head);
+  stage_heads<DH, RP>((const bf16_t*)p.k, p.ldk, SK, SKP, H, bh0, hpb, sm + oK, per_head);
+  stage_heads<DH, RP>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, sm + oV, per_head);
   // lse (log2 domain) and D = rowsum(dO * O) per query: 4 rows per thread in flight
   for (int e0 = tid; e0 < hpb * SQP; e0 += 256 * 4) {
     float lse[4], D[4];
@@ -257,6 +336,10 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
   }
   __syncthreads();
   const float scale = p.scale, sl2 = p.scale * LOG2E;
+  // row fragment (A or B operand with k = head dim) of a row-major staged tile
+  auto rowf = [&](const bf16_t* t, int row, int kc) -> s4 {
+    return (DH < 16 && g >= 2) ? (s4){0, 0, 0, 0} : ld4(t + row * RP + kc * 16 + 4 * g);
+  };
   // ---- phase A: dK, dV (task = key tile x query slice; query tiles in pairs) ----------
   const int ntA = hpb * ktiles * QS;
   for (int task = wave; task < ntA; task += 4) {
@@ -268,13 +351,19 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
     const bf16_t *Ks = base + oK, *Vs = base + oV;
     const float* lse = fls + hl * 2 * SQP;
     const float* Dv = lse + SQP;
+    bf16_t* dSh = dS + hl * SKP * DSP;
     const int key = kt * 16 + l16;
     const bool kv = key < SK;
     s4 kf[KC], vf[KC];
+    long kf8[KC8];
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
-      kf[kc] = ld4(Ks + key * DP + kc * 16 + 4 * g);
-      vf[kc] = ld4(Vs + key * DP + kc * 16 + 4 * g);
+      kf[kc] = rowf(Ks, key, kc);
+      vf[kc] = rowf(Vs, key, kc);
+    }
+    if constexpr (F8) {
+#pragma unroll
+      for (int kc = 0; kc < KC8; ++kc) kf8[kc] = frag8<DH>(Ks, RP, key, kc, g);
     }
     v4f dk[2][KC], dv[2][KC];
 #pragma unroll
@@ -285,24 +374,29 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
     // without a partial last step they are straight-line code the compiler interleaves
     auto qstep = [&](const int qt, const int u) {
         v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (F8) {
+#pragma unroll
+          for (int kc = 0; kc < KC8; ++kc) s = mma8(frag8<DH>(Qs, RP, qt * 16 + l16, kc, g), kf8[kc], s);
+        }
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
-          s = mma(ld4(Qs + (qt * 16 + l16) * DP + kc * 16 + 4 * g), kf[kc], s);
-          dp = mma(ld4(Gs + (qt * 16 + l16) * DP + kc * 16 + 4 * g), vf[kc], dp);
+          if constexpr (!F8) s = mma(rowf(Qs, qt * 16 + l16, kc), kf[kc], s);
+          dp = mma(rowf(Gs, qt * 16 + l16, kc), vf[kc], dp);
         }
         float pv[4], ds[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int q = qt * 16 + 4 * g + i;
-          pv[i] = (!MASK || (kv && q < SQ)) ? ex2(s[i] * sl2 - lse[q]) : 0.f;
+          pv[i] = (!MASK || (kv && q < SQ)) ? ex2(__builtin_fmaf(s[i], sl2, -lse[q])) : 0.f;
           ds[i] = pv[i] * (dp[i] - Dv[q]);
         }
         const s4 pf = pack4(pv[0], pv[1], pv[2], pv[3]);
         const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);
+        if (dsl) *(s4*)(dSh + key * DSP + qt * 16 + 4 * g) = df;  // dS^T[key][q .. q+3] for phase B
 #pragma unroll
         for (int dt = 0; dt < KC; ++dt) {
-          dv[u][dt] = mma(ldtr(Gs, DP, qt * 16, dt * 16, l16, g), pf, dv[u][dt]);  // dO^T fragment
-          dk[u][dt] = mma(ldtr(Qs, DP, qt * 16, dt * 16, l16, g), df, dk[u][dt]);  // Q^T fragment
+          dv[u][dt] = mma(ldtr(Gs, RP, qt * 16, dt * 16, l16, g), pf, dv[u][dt]);  // dO^T fragment
+          dk[u][dt] = mma(ldtr(Qs, RP, qt * 16, dt * 16, l16, g), df, dk[u][dt]);  // Q^T fragment
         }
     };
     if (qtiles % (2 * QS) == 0) {
@@ -345,8 +439,8 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
       }
     }
   }
+  if (QS > 1 || dsl) __syncthreads();
   if (QS > 1) {
-    __syncthreads();
     // one wave per (head, key tile) adds its QS slices in order and writes dK, dV
     for (int t = wave; t < hpb * ktiles; t += 4) {
       const int hl = t / ktiles, kt = t - hl * ktiles;
@@ -389,49 +483,69 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
     const bf16_t *Ks = base + oK, *Vs = base + oV;
     const float* lse = fls + hl * 2 * SQP;
     const float* Dv = lse + SQP;
+    const bf16_t* dSh = dS + hl * SKP * DSP;
     const int q = qt * 16 + l16;
     const bool qv = q < SQ;
-    const float lq = lse[q], Dq = Dv[q];
-    s4 qf[KC], gf[KC];
-#pragma unroll
-    for (int kc = 0; kc < KC; ++kc) {
-      qf[kc] = ld4(Qs + q * DP + kc * 16 + 4 * g);
-      gf[kc] = ld4(Gs + q * DP + kc * 16 + 4 * g);
-    }
     v4f dq[2][KC];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int dt = 0; dt < KC; ++dt) dq[u][dt] = (v4f){0.f, 0.f, 0.f, 0.f};
-    auto kstep = [&](const int kt, const int u) {
+    if (dsl) {  // dS^T from phase A: MFMAs only
+      auto kstep = [&](const int kt, const int u) {
+        const s4 df = ldtr(dSh, DSP, kt * 16, qt * 16, l16, g);  // dS^T[key 4g+i][query l16]
+#pragma unroll
+        for (int dt = 0; dt < KC; ++dt)
+          dq[u][dt] = mma(ldtr(Ks, RP, kt * 16, dt * 16, l16, g), df, dq[u][dt]);  // K^T fragment
+      };
+      int kt0 = 0;
+      for (; kt0 + 1 < ktiles; kt0 += 2) {
+        kstep(kt0, 0);
+        kstep(kt0 + 1, 1);
+      }
+      if (kt0 < ktiles) kstep(kt0, 0);
+    } else {
+      const float lq = lse[q], Dq = Dv[q];
+      s4 qf[KC], gf[KC];
+      long qf8[KC8];
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        qf[kc] = rowf(Qs, q, kc);
+        gf[kc] = rowf(Gs, q, kc);
+      }
+      if constexpr (F8) {
+#pragma unroll
+        for (int kc = 0; kc < KC8; ++kc) qf8[kc] = frag8<DH>(Qs, RP, q, kc, g);
+      }
+      auto kstep = [&](const int kt, const int u) {
         v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (F8) {
+#pragma unroll
+          for (int kc = 0; kc < KC8; ++kc) st = mma8(frag8<DH>(Ks, RP, kt * 16 + l16, kc, g), qf8[kc], st);
+        }
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
-          st = mma(ld4(Ks + (kt * 16 + l16) * DP + kc * 16 + 4 * g), qf[kc], st);
-          dpt = mma(ld4(Vs + (kt * 16 + l16) * DP + kc * 16 + 4 * g), gf[kc], dpt);
+          if constexpr (!F8) st = mma(rowf(Ks, kt * 16 + l16, kc), qf[kc], st);
+          dpt = mma(rowf(Vs, kt * 16 + l16, kc), gf[kc], dpt);
         }
         float ds[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int key = kt * 16 + 4 * g + i;
-          const float pr = (!MASK || (qv && key < SK)) ? ex2(st[i] * sl2 - lq) : 0.f;
+          const float pr = (!MASK || (qv && key < SK)) ? ex2(__builtin_fmaf(st[i], sl2, -lq)) : 0.f;
           ds[i] = pr * (dpt[i] - Dq);
         }
         const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);
 #pragma unroll
         for (int dt = 0; dt < KC; ++dt)
-          dq[u][dt] = mma(ldtr(Ks, DP, kt * 16, dt * 16, l16, g), df, dq[u][dt]);  // K^T fragment
-    };
-    if ((ktiles & 1) == 0) {
-      for (int kt0 = 0; kt0 < ktiles; kt0 += 2) {
+          dq[u][dt] = mma(ldtr(Ks, RP, kt * 16, dt * 16, l16, g), df, dq[u][dt]);  // K^T fragment
+      };
+      int kt0 = 0;
+      for (; kt0 + 1 < ktiles; kt0 += 2) {
         kstep(kt0, 0);
         kstep(kt0 + 1, 1);
       }
-    } else {
-      for (int kt0 = 0; kt0 < ktiles; kt0 += 2) {
-        kstep(kt0, 0);
-        if (kt0 + 1 < ktiles) kstep(kt0 + 1, 1);
-      }
+      if (kt0 < ktiles) kstep(kt0, 0);
     }
     if (qv) {
       bf16_t* dqp = (bf16_t*)p.dq + ((long)b * SQ + q) * p.lddq + h * DH;
@@ -456,7 +570,7 @@ int mfma_hpb(const EncdiffAttnArgs& a) {
   return hpb;
 }
 
-template <int DH>
+template <int DH, bool F8>
 int launch_mfma_fwd(const EncdiffAttnArgs& a, hipStream_t s) {
   constexpr int DP = DH < 16 ? 16 : DH;
   const int hpb = mfma_hpb(a);
@@ -465,54 +579,69 @@ int launch_mfma_fwd(const EncdiffAttnArgs& a, hipStream_t s) {
   const size_t lds = (size_t)hpb * 2 * SKP * DP * sizeof(bf16_t);
   if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
   const bool mask = a.sk % 32 != 0;
-  const void* fn = mask ? (const void*)attn_fwd_mfma<DH, true> : (const void*)attn_fwd_mfma<DH, false>;
-  static const hipError_t attr0 = hipFuncSetAttribute((const void*)attn_fwd_mfma<DH, false>,
+  static const hipError_t attr0 = hipFuncSetAttribute((const void*)attn_fwd_mfma<DH, false, F8>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  static const hipError_t attr1 = hipFuncSetAttribute((const void*)attn_fwd_mfma<DH, true>,
+  static const hipError_t attr1 = hipFuncSetAttribute((const void*)attn_fwd_mfma<DH, true, F8>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)attr0; (void)attr1; (void)fn;
-  if (mask) hipLaunchKernelGGL((attn_fwd_mfma<DH, true>), dim3(nblk), dim3(256), lds, s, a, hpb);
-  else hipLaunchKernelGGL((attn_fwd_mfma<DH, false>), dim3(nblk), dim3(256), lds, s, a, hpb);
+  (void)attr0; (void)attr1;
+  if (mask) hipLaunchKernelGGL((attn_fwd_mfma<DH, true, F8>), dim3(nblk), dim3(256), lds, s, a, hpb);
+  else hipLaunchKernelGGL((attn_fwd_mfma<DH, false, F8>), dim3(nblk), dim3(256), lds, s, a, hpb);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
 
-template <int DH>
+template <int DH, bool F8>
 int launch_mfma_bwd(const EncdiffAttnArgs& a, hipStream_t s) {
   constexpr int DP = DH < 16 ? 16 : DH;
+  constexpr int RP = DH < 16 ? 8 : DH;
   const int hpb = mfma_hpb(a);
   const int SQP = (a.sq + 15) & ~15, SKP = (a.sk + 15) & ~15;
   const int nblk = a.batch * a.heads / hpb;
   const int QS = attn_qsplit(SKP / 16, hpb);
   const size_t red = QS > 1 ? (size_t)hpb * (SKP / 16) * QS * 2 * 16 * DP * sizeof(float) : 0;
-  const size_t lds =
-      (size_t)hpb * ((2 * SQP + 2 * SKP) * DP * sizeof(bf16_t) + 2 * SQP * sizeof(float)) + red;
+  const size_t base = (size_t)hpb * ((2 * SQP + 2 * SKP) * RP * sizeof(bf16_t) + 2 * SQP * sizeof(float)) + red;
+  const size_t dsz = (size_t)hpb * SKP * ds_pitch(SQP) * sizeof(bf16_t);
+  const int dsl = base + dsz <= 160 * 1024 ? 1 : 0;  // dS^T kept in LDS for phase B
+  const size_t lds = base + (dsl ? dsz : 0);
   if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
-  static const hipError_t attr0 = hipFuncSetAttribute((const void*)attn_bwd_mfma<DH, false>,
+  static const hipError_t attr0 = hipFuncSetAttribute((const void*)attn_bwd_mfma<DH, false, F8>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  static const hipError_t attr1 = hipFuncSetAttribute((const void*)attn_bwd_mfma<DH, true>,
+  static const hipError_t attr1 = hipFuncSetAttribute((const void*)attn_bwd_mfma<DH, true, F8>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)attr0; (void)attr1;
-  if (a.sq % 16 || a.sk % 16) hipLaunchKernelGGL((attn_bwd_mfma<DH, true>), dim3(nblk), dim3(256), lds, s, a, hpb);
-  else hipLaunchKernelGGL((attn_bwd_mfma<DH, false>), dim3(nblk), dim3(256), lds, s, a, hpb);
+  if (a.sq % 16 || a.sk % 16)
+    hipLaunchKernelGGL((attn_bwd_mfma<DH, true, F8>), dim3(nblk), dim3(256), lds, s, a, hpb, dsl);
+  else hipLaunchKernelGGL((attn_bwd_mfma<DH, false, F8>), dim3(nblk), dim3(256), lds, s, a, hpb, dsl);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
 
-}  // namespace
-
-// used by attn.hip's dispatcher
-int encdiff_attention_mfma(const EncdiffAttnArgs* a, bool bwd, void* stream) {
-  if (a->batch * a->heads % mfma_hpb(*a)) return ENCDIFF_ERR_SHAPE;
-  hipStream_t s = (hipStream_t)stream;
-  switch (a->dh) {
-    case 8: return bwd ? launch_mfma_bwd<8>(*a, s) : launch_mfma_fwd<8>(*a, s);
-    case 16: return bwd ? launch_mfma_bwd<16>(*a, s) : launch_mfma_fwd<16>(*a, s);
-    case 32: return bwd ? launch_mfma_bwd<32>(*a, s) : launch_mfma_fwd<32>(*a, s);
+template <bool F8>
+int dispatch_dh(const EncdiffAttnArgs& a, bool bwd, hipStream_t s) {
+  switch (a.dh) {
+    case 8: return bwd ? launch_mfma_bwd<8, F8>(a, s) : launch_mfma_fwd<8, F8>(a, s);
+    case 16: return bwd ? launch_mfma_bwd<16, F8>(a, s) : launch_mfma_fwd<16, F8>(a, s);
+    case 32: return bwd ? launch_mfma_bwd<32, F8>(a, s) : launch_mfma_fwd<32, F8>(a, s);
     // wider UNets (configs[4], model_channels=128: C=512 over 8 heads at the 8x8 / 4x4 levels)
-    case 64: return bwd ? launch_mfma_bwd<64>(*a, s) : launch_mfma_fwd<64>(*a, s);
-    case 128:  // single-head AttnBlock of the VQ encoder (model.py AttnBlock): forward only (frozen)
-      return bwd ? ENCDIFF_ERR_UNSUPPORTED : launch_mfma_fwd<128>(*a, s);
+    case 64: return bwd ? launch_mfma_bwd<64, F8>(a, s) : launch_mfma_fwd<64, F8>(a, s);
     default: return ENCDIFF_ERR_UNSUPPORTED;
   }
 }
+
+int attn_dispatch(const EncdiffAttnArgs* a, bool bwd, void* stream) {
+  if (!a || !a->q || !a->k || !a->v || !a->o) return ENCDIFF_ERR_ARG;
+  if (bwd && (!a->d_o || !a->dq || !a->dk || !a->dv || !a->lse)) return ENCDIFF_ERR_ARG;
+  if (a->batch <= 0 || a->heads <= 0 || a->sq <= 0 || a->sk <= 0 || a->dh % 8) return ENCDIFF_ERR_SHAPE;
+  if (a->batch * a->heads % mfma_hpb(*a)) return ENCDIFF_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  if (a->dh == 128) {  // single-head AttnBlock of the VQ encoder (model.py AttnBlock): forward only (frozen)
+    if (bwd || a->fp8_qk) return ENCDIFF_ERR_UNSUPPORTED;
+    return launch_mfma_fwd<128, false>(*a, s);
+  }
+  return a->fp8_qk ? dispatch_dh<true>(*a, bwd, s) : dispatch_dh<false>(*a, bwd, s);
+}
+
+}  // namespace
+
+extern "C" int encdiff_attention_fwd(const EncdiffAttnArgs* a, void* stream) { return attn_dispatch(a, false, stream); }
+extern "C" int encdiff_attention_bwd(const EncdiffAttnArgs* a, void* stream) { return attn_dispatch(a, true, stream); }

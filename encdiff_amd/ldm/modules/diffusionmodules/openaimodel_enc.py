@@ -92,7 +92,7 @@ class UNetModel(nn.Module):
                  dims=2, num_classes=None, use_checkpoint=False, use_fp16=False, num_heads=-1,
                  num_head_channels=-1, num_heads_upsample=-1, use_scale_shift_norm=False, resblock_updown=False,
                  use_new_attention_order=False, use_spatial_transformer=False, transformer_depth=1,
-                 context_dim=None, n_embed=None, legacy=True):
+                 context_dim=None, n_embed=None, legacy=True, attn_fp8_min_tokens=None):
         super().__init__()
         given = dict(dims=dims, num_classes=num_classes, use_fp16=use_fp16, num_head_channels=num_head_channels,
                      transformer_depth=transformer_depth, use_spatial_transformer=use_spatial_transformer,
@@ -119,7 +119,9 @@ class UNetModel(nn.Module):
         cfg = dict(image_size=image_size, in_channels=in_channels, out_channels=out_channels,
                    model_channels=model_channels, attention_resolutions=self.attention_resolutions,
                    num_res_blocks=num_res_blocks, channel_mult=self.channel_mult, num_heads=num_heads,
-                   context_dim=context_dim, latent_unit=latent_unit)
+                   context_dim=context_dim, latent_unit=latent_unit, attn_fp8_min_tokens=attn_fp8_min_tokens)
+        # attn_fp8_min_tokens (builder extension for configs[4], not a reference kwarg): self-attention
+        # over >= that many tokens computes its scores on fp8 (e4m3) MFMA
         self._spec = UNetSpec.from_config(cfg)
         ted = model_channels * 4
         self.time_embed = nn.Sequential(nn.Linear(model_channels, ted), nn.SiLU(), nn.Linear(ted, ted))
@@ -248,23 +250,43 @@ class _WarpFn(torch.autograd.Function):
         return du, None
 
 
+def encoder4_stages(image_size: int) -> int:
+    """Stride-2 stages taking an image_size^2 input down to the 4x4 grid the trunk ends on."""
+    n, s = 0, image_size
+    while s > 4:
+        s //= 2
+        n += 1
+    if 4 << n != image_size or n < 2:
+        raise ValueError(f"Encoder4 needs a power-of-two image_size >= 16, got {image_size}")
+    return n
+
+
 class Encoder4(nn.Module):
     """openaimodel_enc.py:991-1041: image -> latent_unit scalars -> per-unit MLP warp
-    to context_dim-d concept tokens, concatenated to (B, latent_unit*context_dim)."""
+    to context_dim-d concept tokens, concatenated to (B, latent_unit*context_dim).
 
-    def __init__(self, d, context_dim, latent_unit, bn=True, num_channels=3):
+    ``image_size`` (builder extension, default 64 = the reference exactly): the reference
+    hard-codes four Conv2d(k4, s2, p1) stages, i.e. a 64x64 input, and View((-1, 128*4*4))
+    (:1012-1013).  Other power-of-two sizes get one [Conv, BN, ReLU] stage per extra halving,
+    inserted after the first (configs[4]: 128x128 CelebA -> five stages), so the trunk still ends
+    on the 4x4 grid the flatten + Linear(d*16, latent_unit) expects; the second-to-last stage keeps
+    the reference's BN-without-ReLU.  image_size=64 reproduces the reference module, indices and
+    state_dict keys unchanged."""
+
+    def __init__(self, d, context_dim, latent_unit, bn=True, num_channels=3, image_size=64):
         super().__init__()
         self.context_dim = context_dim
         self.latent_unit = latent_unit
-        self.encoder = nn.Sequential(
-            nn.Conv2d(num_channels, d, 4, 2, 1), nn.BatchNorm2d(d), nn.ReLU(True),
-            nn.Conv2d(d, d, 4, 2, 1), nn.BatchNorm2d(d), nn.ReLU(True),
-            nn.Conv2d(d, d, 4, 2, 1), nn.BatchNorm2d(d),
-            nn.Conv2d(d, d, 4, 2, 1), nn.BatchNorm2d(d), nn.ReLU(True),
-            EncResBlock(d, d, bn=bn), nn.BatchNorm2d(d), nn.ReLU(True),
-            EncResBlock(d, d, bn=bn),
-            View((-1, 128 * 4 * 4)),
-            nn.Linear(2048, latent_unit))
+        self.image_size = image_size
+        n = encoder4_stages(image_size)
+        layers = []
+        for st in range(n):
+            layers += [nn.Conv2d(num_channels if st == 0 else d, d, 4, 2, 1), nn.BatchNorm2d(d)]
+            if st != n - 2:
+                layers.append(nn.ReLU(True))
+        layers += [EncResBlock(d, d, bn=bn), nn.BatchNorm2d(d), nn.ReLU(True), EncResBlock(d, d, bn=bn),
+                   View((-1, d * 4 * 4)), nn.Linear(d * 16, latent_unit)]
+        self.encoder = nn.Sequential(*layers)
         self.net = nn.ModuleList([nn.Sequential(nn.Linear(1, 64), nn.ELU(True), nn.Linear(64, 128), nn.ELU(True),
                                                 nn.Linear(128, context_dim)) for _ in range(latent_unit)])
         self._warp_bind = None

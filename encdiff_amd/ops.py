@@ -468,18 +468,19 @@ def layernorm_bwd(x, gamma, stats, dy, dx, dgamma_part, dbeta_part, accumulate=F
 
 
 # ------------------------------------------------------------------ attention
-def attention_fwd(q, k, v, o, lse, batch, heads, sq, sk, dh):
+def attention_fwd(q, k, v, o, lse, batch, heads, sq, sk, dh, fp8=False):
+    """fp8: scores on fp8 (e4m3) MFMA (configs[4]'s long-sequence level)."""
     a = L.AttnArgs(batch=batch, heads=heads, sq=sq, sk=sk, dh=dh, scale=dh ** -0.5,
                    q=_p(q), ldq=_ld(q), k=_p(k), ldk=_ld(k), v=_p(v), ldv=_ld(v), o=_p(o), ldo=_ld(o),
-                   lse=_p(lse))
+                   lse=_p(lse), fp8_qk=int(fp8))
     check(lib.encdiff_attention_fwd(C.byref(a), _s()), "encdiff_attention_fwd")
 
 
-def attention_bwd(q, k, v, o, lse, d_o, dq, dk, dv, batch, heads, sq, sk, dh):
+def attention_bwd(q, k, v, o, lse, d_o, dq, dk, dv, batch, heads, sq, sk, dh, fp8=False):
     a = L.AttnArgs(batch=batch, heads=heads, sq=sq, sk=sk, dh=dh, scale=dh ** -0.5,
                    q=_p(q), ldq=_ld(q), k=_p(k), ldk=_ld(k), v=_p(v), ldv=_ld(v), o=_p(o), ldo=_ld(o),
                    lse=_p(lse), d_o=_p(d_o), lddo=_ld(d_o), dq=_p(dq), lddq=_ld(dq), dk=_p(dk), lddk=_ld(dk),
-                   dv=_p(dv), lddv=_ld(dv))
+                   dv=_p(dv), lddv=_ld(dv), fp8_qk=int(fp8))
     check(lib.encdiff_attention_bwd(C.byref(a), _s()), "encdiff_attention_bwd")
 
 

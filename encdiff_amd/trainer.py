@@ -62,10 +62,13 @@ class HipTrainer:
         self._split_lo: Optional[int] = None
         self._split_checked = False
         self._g_rest = None
-        if data is None:  # synthetic uint8 images of the Shapes3D shape/size, resident in HBM
-            data = ImagePool.synthetic(pool_size, batch_size, self.dev, seed=seed, rank=self.rank, world=self.world)
+        # image resolution: the latent size times the first stage's downsampling (VQ-f4: x4)
+        self.res = ldm.image_size * (2 ** getattr(ldm, "num_downs", 2))
+        if data is None:  # synthetic uint8 images of the dataset's shape, resident in HBM
+            data = ImagePool.synthetic(pool_size, batch_size, self.dev, h=self.res, w=self.res, seed=seed,
+                                       rank=self.rank, world=self.world)
         self.data = data
-        self.img = torch.empty(batch_size, 3, 64, 64, device=self.dev)
+        self.img = torch.empty(batch_size, 3, self.res, self.res, device=self.dev)
         self.loss_buf = torch.zeros(4, device=self.dev)
         self.graph = graph
         self._feed = None  # test hook: batch, t and noise from static buffers (enable_feed)
@@ -78,12 +81,12 @@ class HipTrainer:
     # ---------------------------------------------------------------- test hook
     def enable_feed(self):
         """Parity-test hook (call before capture): the step reads its image batch, timesteps
-        and noise from static buffers -- ``feed_img`` (B, 3, 64, 64) fp32, ``feed_t`` (B,)
+        and noise from static buffers -- ``feed_img`` (B, 3, res, res) fp32, ``feed_t`` (B,)
         int64, ``feed_noise`` like z -- instead of the image pool and the RNG.  The captured
         graph reads them on every replay, so a checker writes a step's inputs and replays the
         same graph the benchmark times."""
         z_shape = (self.B, self.ldm.channels, self.ldm.image_size, self.ldm.image_size)
-        self._feed = dict(img=torch.zeros(self.B, 3, 64, 64, device=self.dev),
+        self._feed = dict(img=torch.zeros(self.B, 3, self.res, self.res, device=self.dev),
                           t=torch.zeros(self.B, dtype=torch.long, device=self.dev),
                           noise=torch.zeros(z_shape, device=self.dev))
         return self._feed
@@ -141,7 +144,8 @@ class HipTrainer:
         if any(lo <= o < a.ema_numel and not ex._early_final(n) for n, (o, _) in a.offsets.items()):
             return
         self._split_lo = lo
-        self.buckets = GradBuckets(a.grad, [0, lo, a.ema_numel, a.numel], self.buckets.group)
+        self.buckets = GradBuckets(a.grad, [0, lo, a.ema_numel, a.numel], self.buckets.group,
+                                   self.buckets.grad_dtype)
 
     def _unet_rest(self):
         self.unet._ex.backward_rest()

@@ -61,6 +61,7 @@ class STSpec:
     dh: int
     h: int
     kv_off: int = 0
+    fp8: bool = False  # self-attention scores on fp8 MFMA (UNetModel attn_fp8_min_tokens)
 
 
 @dataclass
@@ -103,8 +104,11 @@ class UNetSpec:
             s.res.append(r)
             return r
 
+        fp8_min = cfg.get("attn_fp8_min_tokens") or 0
+
         def st(prefix, c, hh):
-            t = STSpec(prefix, c, heads, c // heads, hh, kv_off=s.kv_total)
+            t = STSpec(prefix, c, heads, c // heads, hh, kv_off=s.kv_total,
+                       fp8=bool(fp8_min) and hh * hh >= fp8_min)
             s.kv_total += 2 * c
             s.sts.append(t)
             return t
@@ -543,7 +547,7 @@ class UNetExecutor:
                           self.P(tb + "norm1.bias"), S["n1"], S["s1"], LN_EPS, bias=self.P(s.prefix + "proj_in.bias"))
         ops.linear_fwd(S["n1"], self.W(s.prefix + "qkv"), S["qkv"])
         q, k, v = S["qkv"][:, :c], S["qkv"][:, c:2 * c], S["qkv"][:, 2 * c:]
-        ops.attention_fwd(q, k, v, S["o1"], S["lse1"], B, s.heads, ntok, ntok, s.dh)
+        ops.attention_fwd(q, k, v, S["o1"], S["lse1"], B, s.heads, ntok, ntok, s.dh, fp8=s.fp8)
         # cross-attention to the concept tokens (norm2 in the to_out epilogue)
         ops.linear_fwd_ln(S["o1"], self.W(tb + "attn1.to_out.0.weight"), S["t1"], self.P(tb + "norm2.weight"),
                           self.P(tb + "norm2.bias"), S["n2"], S["s2"], LN_EPS,
@@ -826,7 +830,7 @@ class UNetExecutor:
                        self.G(tb + "attn1.to_out.0.weight"), self.G(tb + "attn1.to_out.0.bias"))
         qkv, dqkv = S["qkv"], S["d_qkv"]
         ops.attention_bwd(qkv[:, :c], qkv[:, c:2 * c], qkv[:, 2 * c:], S["o1"], S["lse1"], d_o, dqkv[:, :c],
-                          dqkv[:, c:2 * c], dqkv[:, 2 * c:], B, s.heads, ntok, ntok, s.dh)
+                          dqkv[:, c:2 * c], dqkv[:, 2 * c:], B, s.heads, ntok, ntok, s.dh, fp8=s.fp8)
         ops.linear_bwd(dqkv, self.W(s.prefix + "qkv"), S["n1"], d_n, self.qkv_grad[s.prefix])
         dg, db = self.ln.parts(tb + "norm1.weight", c)
         d_t0 = S["d_t0"]

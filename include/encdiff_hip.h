@@ -214,6 +214,8 @@ int encdiff_layernorm_bwd(const EncdiffLayerNormArgs* args, void* stream);
  * softmax(q k^T * dh^-0.5) v per head, q/k/v/o as [rows][ld] with head h at
  * columns [h*dh, (h+1)*dh) ('b n (h d)', attention.py:170-193).  Self-attention
  * (keys = the same tokens) and cross-attention to the concept tokens (keys = 20).
+ * dh in {8, 16, 32, 64} (fwd + bwd), 128 (fwd only: the VQ encoder's AttnBlock);
+ * ENCDIFF_ERR_SHAPE when a head group's K/V tiles exceed one workgroup's LDS.
  */
 typedef struct EncdiffAttnArgs {
   int batch, heads, sq, sk, dh;
@@ -227,6 +229,8 @@ typedef struct EncdiffAttnArgs {
   void* dq; long lddq;
   void* dk; long lddk;
   void* dv; long lddv;
+  int fp8_qk, pad_;          /* 1: scores Q K^T on fp8 (OCP e4m3) MFMA, fwd and bwd recompute;
+                                softmax, P V and the gradient products stay bf16 / fp32 */
 } EncdiffAttnArgs;
 
 int encdiff_attention_fwd(const EncdiffAttnArgs* args, void* stream);

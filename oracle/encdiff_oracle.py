@@ -46,6 +46,7 @@ class Layer:
     updown: str = ''     # '' | 'down' | 'up'
     heads: int = 0
     dh: int = 0
+    fp8_min_tokens: int = 0  # st: self-attention scores in e4m3 from this many tokens (configs[4])
 
 
 @dataclass
@@ -65,6 +66,7 @@ def build_plan(cfg: dict = SHAPES3D_UNET) -> Plan:
     attn = cfg['attention_resolutions']
     nrb = cfg['num_res_blocks']
     mult = cfg['channel_mult']
+    f8 = cfg.get('attn_fp8_min_tokens') or 0
     p = Plan(cfg=cfg)
     p.input_blocks.append([Layer('conv', cfg['in_channels'], mc)])
     chans = [mc]
@@ -74,14 +76,14 @@ def build_plan(cfg: dict = SHAPES3D_UNET) -> Plan:
             blk = [Layer('res', ch, m * mc)]
             ch = m * mc
             if ds in attn:
-                blk.append(Layer('st', ch, ch, heads=heads, dh=ch // heads))
+                blk.append(Layer('st', ch, ch, heads=heads, dh=ch // heads, fp8_min_tokens=f8))
             p.input_blocks.append(blk)
             chans.append(ch)
         if level != len(mult) - 1:
             p.input_blocks.append([Layer('res', ch, ch, updown='down')])
             chans.append(ch)
             ds *= 2
-    p.middle = [Layer('res', ch, ch), Layer('st', ch, ch, heads=heads, dh=ch // heads),
+    p.middle = [Layer('res', ch, ch), Layer('st', ch, ch, heads=heads, dh=ch // heads, fp8_min_tokens=f8),
                 Layer('res', ch, ch)]
     for level, m in list(enumerate(mult))[::-1]:
         for i in range(nrb + 1):
@@ -89,7 +91,7 @@ def build_plan(cfg: dict = SHAPES3D_UNET) -> Plan:
             blk = [Layer('res', ch + ich, mc * m)]
             ch = mc * m
             if ds in attn:
-                blk.append(Layer('st', ch, ch, heads=heads, dh=ch // heads))
+                blk.append(Layer('st', ch, ch, heads=heads, dh=ch // heads, fp8_min_tokens=f8))
             if level and i == nrb:
                 blk.append(Layer('res', ch, ch, updown='up'))
                 ds //= 2
@@ -211,8 +213,26 @@ def resblock(P, pre, L: Layer, x, emb):
     return x + h
 
 
-def cross_attention(P, pre, x, ctx, heads):
-    """attention.py:170-193: q,k,v no bias; softmax(q k^T * dh^-0.5) v; to_out."""
+class _FP8Scores(torch.autograd.Function):
+    """q k^T with q, k rounded to OCP e4m3 (torch.float8_e4m3fn) -- the builder's configs[4]
+    fp8 self-attention scores (no reference counterpart: the reference is fp32).  The backward
+    uses the unrounded q, k, as the HIP kernel's dQ = dS K and dK = dS^T Q products do."""
+
+    @staticmethod
+    def forward(ctx, q, k):
+        ctx.save_for_backward(q, k)
+        e4 = torch.float8_e4m3fn
+        return torch.einsum('bid,bjd->bij', q.to(e4).float(), k.to(e4).float())
+
+    @staticmethod
+    def backward(ctx, g):
+        q, k = ctx.saved_tensors
+        return torch.einsum('bij,bjd->bid', g, k), torch.einsum('bij,bid->bjd', g, q)
+
+
+def cross_attention(P, pre, x, ctx, heads, fp8=False):
+    """attention.py:170-193: q,k,v no bias; softmax(q k^T * dh^-0.5) v; to_out.
+    fp8: scores from e4m3-rounded q, k (configs[4]'s long-sequence self-attention)."""
     q = F.linear(x, P[pre + 'to_q.weight'])
     c = x if ctx is None else ctx
     k = F.linear(c, P[pre + 'to_k.weight'])
@@ -223,7 +243,7 @@ def cross_attention(P, pre, x, ctx, heads):
     def split(t):  # 'b n (h d) -> (b h) n d'
         return t.reshape(t.shape[0], t.shape[1], heads, dh).permute(0, 2, 1, 3).reshape(-1, t.shape[1], dh)
     q, k, v = split(q), split(k), split(v)
-    sim = torch.einsum('bid,bjd->bij', q, k) * (dh ** -0.5)
+    sim = (_FP8Scores.apply(q, k) if fp8 else torch.einsum('bid,bjd->bij', q, k)) * (dh ** -0.5)
     attn = sim.softmax(dim=-1)
     out = torch.einsum('bij,bjd->bid', attn, v)
     out = out.reshape(b, heads, n, dh).permute(0, 2, 1, 3).reshape(b, n, inner)
@@ -239,7 +259,8 @@ def spatial_transformer(P, pre, L: Layer, x, ctx):
     x = x.permute(0, 2, 3, 1).reshape(b, hh * ww, c)
     t = pre + 'transformer_blocks.0.'
     ln = lambda y, n: F.layer_norm(y, (c,), P[t + n + '.weight'], P[t + n + '.bias'], 1e-5)
-    x = cross_attention(P, t + 'attn1.', ln(x, 'norm1'), None, L.heads) + x
+    fp8_min = L.fp8_min_tokens
+    x = cross_attention(P, t + 'attn1.', ln(x, 'norm1'), None, L.heads, fp8=bool(fp8_min) and hh * ww >= fp8_min) + x
     x = cross_attention(P, t + 'attn2.', ln(x, 'norm2'), ctx, L.heads) + x
     y = F.linear(ln(x, 'norm3'), P[t + 'ff.net.0.proj.weight'], P[t + 'ff.net.0.proj.bias'])
     a, g = y.chunk(2, dim=-1)
@@ -439,23 +460,45 @@ def lambda_linear_schedule(n, warm_up_steps=(10000,), f_start=(1e-6,), f_max=(1.
 # Concept-token encoder Encoder4 (openaimodel_enc.py:969-1049), functional.
 # ----------------------------------------------------------------------------
 
-def encoder4_shapes(d=128, context_dim=16, latent_unit=20, num_channels=3):
+def encoder4_layout(image_size=64):
+    """Indices of Encoder4.encoder (openaimodel_enc.py:996-1013): the stride-2 stages as
+    (conv, bn, relu), the two EncResBlocks with their following BN (or None), the Linear.
+    The reference is image_size 64 (four stages); the builder's 128x128 variant (configs[4])
+    inserts one more [Conv, BN, ReLU] stage after the first (Encoder4 image_size in the build)."""
+    n, sz = 0, image_size
+    while sz > 4:
+        sz //= 2
+        n += 1
+    stages, i = [], 0
+    for st in range(n):
+        relu = st != n - 2
+        stages.append((i, i + 1, relu))
+        i += 3 if relu else 2
+    res = [(i, i + 1), (i + 3, None)]
+    return stages, res, i + 5
+
+
+def encoder4_shapes(d=128, context_dim=16, latent_unit=20, num_channels=3, image_size=64):
     S = {}
     e = 'encoder.'
-    S[e + '0.weight'] = (d, num_channels, 4, 4); S[e + '0.bias'] = (d,)
-    for i in (3, 6, 8):
-        S[e + f'{i}.weight'] = (d, d, 4, 4); S[e + f'{i}.bias'] = (d,)
-    for i in (1, 4, 7, 9, 12):
+    stages, res, lin = encoder4_layout(image_size)
+
+    def bn(i):
         for n, sh in (('weight', (d,)), ('bias', (d,)), ('running_mean', (d,)), ('running_var', (d,)),
                       ('num_batches_tracked', ())):
             S[e + f'{i}.{n}'] = sh
-    for i in (11, 14):
-        S[e + f'{i}.convs.1.weight'] = (d, d, 3, 3); S[e + f'{i}.convs.1.bias'] = (d,)
+    for k, (ci, bi, _) in enumerate(stages):
+        S[e + f'{ci}.weight'] = (d, num_channels if k == 0 else d, 4, 4); S[e + f'{ci}.bias'] = (d,)
+        bn(bi)
+    for ri, bi in res:
+        S[e + f'{ri}.convs.1.weight'] = (d, d, 3, 3); S[e + f'{ri}.convs.1.bias'] = (d,)
         for n, sh in (('weight', (d,)), ('bias', (d,)), ('running_mean', (d,)), ('running_var', (d,)),
                       ('num_batches_tracked', ())):
-            S[e + f'{i}.convs.2.{n}'] = sh
-        S[e + f'{i}.convs.4.weight'] = (d, d, 1, 1); S[e + f'{i}.convs.4.bias'] = (d,)
-    S[e + '16.weight'] = (latent_unit, 2048); S[e + '16.bias'] = (latent_unit,)
+            S[e + f'{ri}.convs.2.{n}'] = sh
+        S[e + f'{ri}.convs.4.weight'] = (d, d, 1, 1); S[e + f'{ri}.convs.4.bias'] = (d,)
+        if bi is not None:
+            bn(bi)
+    S[e + f'{lin}.weight'] = (latent_unit, d * 16); S[e + f'{lin}.bias'] = (latent_unit,)
     for u in range(latent_unit):
         S[f'net.{u}.0.weight'] = (64, 1); S[f'net.{u}.0.bias'] = (64,)
         S[f'net.{u}.2.weight'] = (128, 64); S[f'net.{u}.2.bias'] = (128,)
@@ -480,8 +523,10 @@ def encoder4_params(seed=0, **kw):
 
 def encoder4_forward(P, x, latent_unit=20, train=True, return_u=False):
     """openaimodel_enc.py:996-1031 (BatchNorm in train mode uses batch stats, eval mode the
-    running statistics).  return_u: also the scalar codes u = encoding(x) (:1034-1035)."""
+    running statistics).  return_u: also the scalar codes u = encoding(x) (:1034-1035).
+    The stage count follows the input resolution (reference: 64x64, four stages)."""
     e = 'encoder.'
+    stages, res, lin = encoder4_layout(x.shape[-1])
 
     def bn(h, i):
         return F.batch_norm(h, P[e + f'{i}.running_mean'].clone(), P[e + f'{i}.running_var'].clone(),
@@ -500,15 +545,17 @@ def encoder4_forward(P, x, latent_unit=20, train=True, return_u=False):
         y = F.conv2d(y, P[e + f'{i}.convs.4.weight'], P[e + f'{i}.convs.4.bias'])
         return h + y
 
-    h = F.relu(bn(conv(x, 0), 1))
-    h = F.relu(bn(conv(h, 3), 4))
-    h = bn(conv(h, 6), 7)
-    h = F.relu(bn(conv(h, 8), 9))
-    h = encres(h, 11)
-    h = F.relu(bn(h, 12))
-    h = encres(h, 14)
-    h = h.reshape(-1, 128 * 4 * 4)
-    u = F.linear(h, P[e + '16.weight'], P[e + '16.bias'])
+    h = x
+    for ci, bi, relu in stages:
+        h = bn(conv(h, ci), bi)
+        if relu:
+            h = F.relu(h)
+    (r0, b0), (r1, _) = res
+    h = F.relu(bn(encres(h, r0), b0))
+    h = encres(h, r1)
+    d = h.shape[1]
+    h = h.reshape(-1, d * 4 * 4)
+    u = F.linear(h, P[e + f'{lin}.weight'], P[e + f'{lin}.bias'])
     outs = []
     for i in range(latent_unit):
         y = u[:, i][:, None]
@@ -653,11 +700,12 @@ class OracleTrainer:
     x0 (the frozen VQ encode skipped); ``step_images`` runs the VQ encode of the images
     first, as the reference's get_input does.  Encoder4 is included (training-mode BN)."""
 
-    def __init__(self, plan: Plan, seed=0, lr=4 * 2e-6, dtype=torch.float32, vq=False):
+    def __init__(self, plan: Plan, seed=0, lr=4 * 2e-6, dtype=torch.float32, vq=False, image_size=64):
         self.plan = plan
         shapes = param_shapes(plan)
         self.P = {k: v.to(dtype).requires_grad_(True) for k, v in recipe_params(shapes, seed).items()}
-        E = encoder4_params(seed)
+        self.lu = plan.cfg['latent_unit']
+        E = encoder4_params(seed, latent_unit=self.lu, context_dim=plan.cfg['context_dim'], image_size=image_size)
         self.E = {k: (v.to(dtype).requires_grad_(True) if v.is_floating_point() and 'running' not in k else v)
                   for k, v in E.items()}
         self.V = {k: v.to(dtype) for k, v in vq_encoder_params(seed).items()} if vq else None
@@ -692,7 +740,7 @@ class OracleTrainer:
         instead of d loss / d eps (the L1 seed sign(eps - noise)/N is discontinuous, so a
         checker shares the seed the device computed)."""
         self.opt.zero_grad(set_to_none=True)
-        c = encoder4_forward(self.E, img)
+        c = encoder4_forward(self.E, img, latent_unit=self.lu)
         x_noisy = q_sample(self.sched, x0, t, noise)
         out = unet_forward(self.P, self.plan, x_noisy, t, [c])
         loss, ld = p_losses_from_output(self.sched, out, noise, t)

@@ -53,6 +53,16 @@ def _worker(rank, world, port, outdir):
         b.finish(0, w0)
         b.finish(1, w1)
         res["bucket_err"] = float((ar.grad - full).abs().max())
+        # 1b. the same in the bf16 wire format: mean within bf16 rounding, equal on all ranks
+        ar.grad.copy_(torch.randn(1000, generator=torch.Generator().manual_seed(dp.rank_seed(99, rank))))
+        full = ar.grad.clone()
+        dist.all_reduce(full)
+        full /= world
+        b16 = dp.GradBuckets.from_arena(ar, grad_dtype=torch.bfloat16)
+        assert b16.wire(0).dtype == torch.bfloat16 and ar.grad.dtype == torch.float32
+        b16.allreduce_all()
+        res["bf16_rel"] = float((ar.grad - full).norm() / full.norm())
+        res["bf16_vals"] = ar.grad.clone()
         # 2. DP gradient of a mean loss over per-rank halves == full-batch gradient
         torch.manual_seed(0)
         lin = torch.nn.Linear(16, 8)
@@ -106,7 +116,9 @@ def test_gloo_world2():
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_worker, args=(world, _free_port(), d), nprocs=world, start_method="spawn", join=True)
         res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    assert torch.equal(res[0]["bf16_vals"], res[1]["bf16_vals"])
     for r in res:
+        assert r["bf16_rel"] < 1e-2
         assert r["bucket_err"] < 1e-6
         assert r["dp_grad_err"] < 1e-6
         assert r["opt_rank_diff"] == 0.0

@@ -1,0 +1,56 @@
+"""Data-parallel training step on the GPU: 2 gloo ranks sharing the card run
+the benchmark's HipTrainer (graph-captured step, split backward, bucketed gradient all-reduce on
+the side stream) for 2 eager + 3 replayed steps; the result must equal the step's definition
+run in one process -- per-rank fwd+bwd at batch 32, gradients averaged, one AdamW + EMA update
+(tools/dp_check.py).  Reference: Lightning DDP mean all-reduce (main_val.py:643-666), no SyncBN.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(cmd, log):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", ENCDIFF_DIST_BACKEND="gloo")
+    with open(log, "w") as fh:
+        r = subprocess.run(cmd, cwd=REPO, env=env, stdout=fh, stderr=subprocess.STDOUT, timeout=420)
+    out = open(log).read()
+    assert r.returncode == 0, out[-3000:]
+    return out
+
+
+def test_dp_two_ranks_equal_single_process_definition(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    out = str(tmp_path / "dp.pt")
+    tool = os.path.join(REPO, "tools", "dp_check.py")
+    log = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", "29617", tool, "--mode", "dp", "--out", out],
+               str(tmp_path / "dp.log"))
+    print(log[-400:])
+    assert "ranks_equal=True" in log
+    _run([sys.executable, tool, "--mode", "w1", "--out", out + ".w1"], str(tmp_path / "w1.log"))
+    r0 = torch.load(out + ".rank0", weights_only=True)
+    r1 = torch.load(out + ".rank1", weights_only=True)
+    w1 = torch.load(out + ".w1", weights_only=True)
+    assert r0["split_lo"] is not None, "the split backward (output-block bucket overlap) did not engage"
+    for k in sorted(w1["grads"]):
+        g, gw = r0["grads"][k].double(), w1["grads"][k].double()
+        worst = sorted(((((g[o:o + n] - gw[o:o + n]).norm() / gw[o:o + n].norm().clamp_min(1e-30)).item(), name)
+                        for name, (o, sh) in w1["names"].items() for n in [int(torch.Size(sh).numel())]),
+                       reverse=True)[:6]
+        print(f"step {k}: exchanged gradient vs definition rel-L2 {((g - gw).norm() / gw.norm()).item():.3e} "
+              f"bitwise={torch.equal(r0['grads'][k], w1['grads'][k])} worst {worst}")
+    for k in ("master", "exp_avg", "exp_avg_sq", "ema"):
+        assert torch.equal(r0[k], r1[k]), f"ranks differ in {k}"
+        d = (r0[k].double() - w1[k].double())
+        rel = (d.norm() / w1[k].double().norm()).item()
+        print(f"{k}: DP vs definition max-abs {d.abs().max().item():.3e} rel-L2 {rel:.3e} "
+              f"bitwise={torch.equal(r0[k], w1[k])}")
+        assert rel < 1e-6, k

@@ -281,6 +281,19 @@ def test_layernorm(O, rows, C):
                                                     (2, 8, 1024, 1024, 16, False), (4, 8, 64, 64, 64, False),
                                                     (4, 8, 16, 40, 64, True)])
 def test_attention(O, B, heads, sq, sk, dh, cross):
+    _attention_case(O, B, heads, sq, sk, dh, cross, fp8=False)
+
+
+@pytest.mark.parametrize("B,heads,sq,sk,dh,cross", [(2, 8, 1024, 1024, 16, False), (4, 8, 256, 256, 32, False),
+                                                    (4, 8, 64, 64, 64, False), (4, 8, 256, 20, 16, True)])
+def test_attention_fp8_scores(O, B, heads, sq, sk, dh, cross):
+    """fp8 (OCP e4m3) QK^T (configs[4]'s S = 1024 level): vs a torch fp32 reference whose scores
+    use q, k rounded to float8_e4m3fn and whose gradient products use the bf16 q, k (what the
+    kernel computes), plus the distance to plain bf16 attention."""
+    _attention_case(O, B, heads, sq, sk, dh, cross, fp8=True)
+
+
+def _attention_case(O, B, heads, sq, sk, dh, cross, fp8):
     torch.manual_seed(5)
     C = heads * dh
     if cross:
@@ -292,21 +305,40 @@ def test_attention(O, B, heads, sq, sk, dh, cross):
         q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
     o = torch.empty(B * sq, C, device=dev, dtype=torch.bfloat16)
     lse = torch.empty(B * heads, sq, device=dev)
-    O.attention_fwd(q, k, v, o, lse, B, heads, sq, sk, dh)
+    O.attention_fwd(q, k, v, o, lse, B, heads, sq, sk, dh, fp8=fp8)
 
     def split(t, s):
         return t.float().reshape(B, s, heads, dh).permute(0, 2, 1, 3).reshape(B * heads, s, dh)
+
+    def merge(t, s):
+        return t.reshape(B, heads, s, dh).permute(0, 2, 1, 3).reshape(B * s, C)
+    d_o = bf(B * sq, C)
+    dq = torch.empty_like(o)
+    dkv = torch.empty(B * sk, 2 * C, device=dev, dtype=torch.bfloat16)
+    O.attention_bwd(q, k, v, o, lse, d_o, dq, dkv[:, :C], dkv[:, C:], B, heads, sq, sk, dh, fp8=fp8)
+    if fp8:
+        qs, ks, vs, gs = split(q, sq), split(k, sk), split(v, sk), split(d_o, sq)
+        e4 = torch.float8_e4m3fn
+        att = (qs.to(e4).float() @ ks.to(e4).float().transpose(1, 2) * dh ** -0.5).softmax(-1)
+        ref = att @ vs
+        dp = gs @ vs.transpose(1, 2)
+        dsc = att * (dp - (dp * att).sum(-1, keepdim=True))
+        want = dict(dq=dsc @ ks * dh ** -0.5, dk=dsc.transpose(1, 2) @ qs * dh ** -0.5, dv=att.transpose(1, 2) @ gs)
+        plain = (qs @ ks.transpose(1, 2) * dh ** -0.5).softmax(-1) @ vs
+        print(f"fp8 scores: out rel-L2 vs e4m3 reference {rel(o, merge(ref, sq)):.3e}, vs bf16 attention "
+              f"{rel(o, merge(plain, sq)):.3e}")
+        assert rel(o, merge(ref, sq)) < 1e-2
+        assert rel(split(dq, sq), want["dq"]) < 2e-2
+        assert rel(split(dkv[:, :C], sk), want["dk"]) < 2e-2
+        assert rel(split(dkv[:, C:], sk), want["dv"]) < 2e-2
+        return
     qr, kr, vr = (split(q, sq).requires_grad_(True), split(k, sk).requires_grad_(True),
                   split(v, sk).requires_grad_(True))
     att = (qr @ kr.transpose(1, 2) * dh ** -0.5).softmax(-1)
     ref = att @ vr
-    refm = ref.reshape(B, heads, sq, dh).permute(0, 2, 1, 3).reshape(B * sq, C)
+    refm = merge(ref, sq)
     assert rel(o, refm) < 1e-2
-    d_o = bf(B * sq, C)
     refm.backward(d_o.float())
-    dq = torch.empty_like(o)
-    dkv = torch.empty(B * sk, 2 * C, device=dev, dtype=torch.bfloat16)
-    O.attention_bwd(q, k, v, o, lse, d_o, dq, dkv[:, :C], dkv[:, C:], B, heads, sq, sk, dh)
     assert rel(split(dq, sq), qr.grad) < 2e-2
     assert rel(split(dkv[:, :C], sk), kr.grad) < 2e-2
     assert rel(split(dkv[:, C:], sk), vr.grad) < 2e-2
