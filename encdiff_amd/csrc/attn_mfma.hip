@@ -75,7 +75,7 @@ ED_DEV long frag8(const bf16_t* t, int ld, int row, int kc, int g) {
 // Loads are issued U at a time before their LDS writes.
 template <int DH, int DP, int U, bool ONES = false>
 ED_DEV void stage_heads_u(const bf16_t* __restrict__ base, long ld, int S, int SP, int H, int bh0, int hpb,
-                          bf16_t* rm, int rm_hs) {
+                          bf16_t* rm, int rm_hs, int r0 = 0) {
   constexpr int CH = DP / 8;
   const int ph = SP * CH, total = hpb * ph;
   for (int e0 = threadIdx.x; e0 < total; e0 += 256 * U) {
@@ -89,11 +89,11 @@ ED_DEV void stage_heads_u(const bf16_t* __restrict__ base, long ld, int S, int S
       r[u] = t / CH;
       c8[u] = (t - r[u] * CH) * 8;
       v[u] = (uint4){0u, 0u, 0u, 0u};
-      if (e < total && r[u] < S && c8[u] < DH) {
+      if (e < total && r0 + r[u] < S && c8[u] < DH) {
         const int bh = bh0 + hl[u], b = bh / H, h = bh - b * H;
-        v[u] = *(const uint4*)(base + ((long)b * S + r[u]) * ld + h * DH + c8[u]);
+        v[u] = *(const uint4*)(base + ((long)b * S + r0 + r[u]) * ld + h * DH + c8[u]);
       }
-      if (ONES && e < total && r[u] < S && c8[u] == DH) v[u].x = 0x3F80u;  // bf16 1.0 in column DH
+      if (ONES && e < total && r0 + r[u] < S && c8[u] == DH) v[u].x = 0x3F80u;  // bf16 1.0 in column DH
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -104,11 +104,11 @@ ED_DEV void stage_heads_u(const bf16_t* __restrict__ base, long ld, int S, int S
 }
 template <int DH, int DP, bool ONES = false>
 ED_DEV void stage_heads(const bf16_t* __restrict__ base, long ld, int S, int SP, int H, int bh0, int hpb,
-                        bf16_t* rm, int rm_hs) {
+                        bf16_t* rm, int rm_hs, int r0 = 0) {
   // several heads (short sequences): 4 chunks per thread in flight; one long head: the
   // plain loop measured faster (fewer live registers in the 2-workgroup-per-CU kernels)
-  if (hpb > 1) stage_heads_u<DH, DP, 4, ONES>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs);
-  else stage_heads_u<DH, DP, 1, ONES>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs);
+  if (hpb > 1) stage_heads_u<DH, DP, 4, ONES>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs, r0);
+  else stage_heads_u<DH, DP, 1, ONES>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs, r0);
 }
 
 constexpr float LOG2E = 1.4426950408889634f;
@@ -123,7 +123,7 @@ ED_DEV float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 // v_exp_f32 (arguments <= 0, underflow to 0 is the correct limit).  MASK: key count not a
 // multiple of 32 (keys past SK get -inf).
 template <int DH, bool MASK, bool F8>
-__global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, int hpb) {
+__global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, int hpb, int kch) {
   constexpr int DP = DH < 16 ? 16 : DH;
   constexpr int KC = DP / 16;
   constexpr bool ONES = DH == 8;   // denominator from the PV MFMA (V^T row 8 = 1)
@@ -134,21 +134,23 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const int bh0 = blockIdx.x * hpb;
-  bf16_t* Ks = sm;                        // [hpb][SKP][DP]
-  bf16_t* Vs = sm + hpb * SKP * DP;       // [hpb][SKP][DP], read transposed (ds_read_b64_tr_b16)
-  stage_heads<DH, DP>((const bf16_t*)p.k, p.ldk, SK, SKP, H, bh0, hpb, Ks, SKP * DP);
-  stage_heads<DH, DP, ONES>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, Vs, SKP * DP);
-  __syncthreads();
+  const int KR = kch < SKP ? kch : SKP;  // key rows resident in LDS at a time
+  bf16_t* Ks = sm;                        // [hpb][KR][DP]
+  bf16_t* Vs = sm + hpb * KR * DP;        // [hpb][KR][DP], read transposed (ds_read_b64_tr_b16)
   const int qtiles = (SQ + 15) >> 4, npairs = (qtiles + 1) >> 1;
   const float sl2 = p.scale * LOG2E;
-  for (int task = wave; task < hpb * npairs; task += 4) {
-    const int hl = task / npairs, qp = task - hl * npairs;
-    const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
-    const bf16_t* kb = Ks + hl * SKP * DP;
-    const bf16_t* vb = Vs + hl * SKP * DP;
-    s4 qf[2][KC];
-    long qf8[2][KC8];
-    int q[2];
+  // per-task state: a pair of 16-query tiles of head hl
+  int hl = 0, b = 0, h = 0, q[2];
+  s4 qf[2][KC];
+  long qf8[2][KC8];
+  float m[2], l[2];
+  v4f o[2][KC];
+  auto init = [&](int task) {
+    hl = task / npairs;
+    const int qp = task - hl * npairs;
+    const int bh = bh0 + hl;
+    b = bh / H;
+    h = bh - b * H;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       q[u] = (2 * qp + u) * 16 + l16;
@@ -167,14 +169,17 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
           qf[u][kc] = (qv && d0 < DH) ? ld4(qp_ + d0) : (s4){0, 0, 0, 0};
         }
       }
-    }
-    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-    v4f o[2][KC];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
+      m[u] = -INFINITY;
+      l[u] = 0.f;
 #pragma unroll
       for (int dt = 0; dt < KC; ++dt) o[u][dt] = (v4f){0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < SKP; k0 += 32) {
+    }
+  };
+  // keys [kbase, kbase + klen) of the task's head, staged at local rows 0 .. klen-1
+  auto consume = [&](int kbase, int klen) {
+    const bf16_t* kb = Ks + hl * KR * DP;
+    const bf16_t* vb = Vs + hl * KR * DP;
+    for (int k0 = 0; k0 < klen; k0 += 32) {
       s4 kf[2][KC];
       long kf8[2][KC8];
 #pragma unroll
@@ -202,7 +207,8 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
             for (int kc = 0; kc < KC; ++kc) sc = mma(kf[t][kc], qf[u][kc], sc);
           }
 #pragma unroll
-          for (int i = 0; i < 4; ++i) sv[4 * t + i] = (!MASK || k0 + t * 16 + 4 * g + i < SK) ? sc[i] : -INFINITY;
+          for (int i = 0; i < 4; ++i)
+            sv[4 * t + i] = (!MASK || kbase + k0 + t * 16 + 4 * g + i < SK) ? sc[i] : -INFINITY;
         }
         // max over raw scores (the scale is positive), the log2-domain max = that * sl2
         float tmax = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
@@ -235,6 +241,8 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
           o[1][dt] = mma(vf, pf[1][t], o[1][dt]);
         }
     }
+  };
+  auto finish = [&]() {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       float lu;
@@ -259,10 +267,36 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
             *(uint2*)(op + d0) = w;
           }
         }
-        if (g == 0 && p.lse) p.lse[(long)bh * SQ + q[u]] = (m[u] + __log2f(lu)) * LN2;  // natural-log LSE
+        if (g == 0 && p.lse) p.lse[(long)(bh0 + hl) * SQ + q[u]] = (m[u] + __log2f(lu)) * LN2;  // natural-log LSE
       }
     }
+  };
+  if (KR == SKP) {  // every head's K / V resident: waves loop over their tasks
+    stage_heads<DH, DP>((const bf16_t*)p.k, p.ldk, SK, SKP, H, bh0, hpb, Ks, SKP * DP);
+    stage_heads<DH, DP, ONES>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, Vs, SKP * DP);
+    __syncthreads();
+    for (int task = wave; task < hpb * npairs; task += 4) {
+      init(task);
+      consume(0, SKP);
+      finish();
+    }
+    return;
   }
+  // K / V longer than the LDS budget (one head per workgroup, hpb == 1): blockIdx.y picks four
+  // query-tile pairs, one per wave, whose online softmax runs over key chunks of KR rows
+  // streamed through LDS (every wave reaches every barrier)
+  const int task = blockIdx.y * 4 + wave;
+  const bool active = task < npairs;
+  init(active ? task : 0);
+  for (int c0 = 0; c0 < SKP; c0 += KR) {
+    const int klen = SKP - c0 < KR ? SKP - c0 : KR;
+    __syncthreads();  // the previous chunk is consumed
+    stage_heads<DH, DP>((const bf16_t*)p.k, p.ldk, SK, klen, H, bh0, 1, Ks, KR * DP, c0);
+    stage_heads<DH, DP, ONES>((const bf16_t*)p.v, p.ldv, SK, klen, H, bh0, 1, Vs, KR * DP, c0);
+    __syncthreads();
+    if (active) consume(c0, klen);
+  }
+  if (active) finish();
 }
 
 // q-split of phase A: enough (key tile, query slice) tasks for the 4 waves
@@ -573,19 +607,29 @@ int mfma_hpb(const EncdiffAttnArgs& a) {
 template <int DH, bool F8>
 int launch_mfma_fwd(const EncdiffAttnArgs& a, hipStream_t s) {
   constexpr int DP = DH < 16 ? 16 : DH;
-  const int hpb = mfma_hpb(a);
+  int hpb = mfma_hpb(a);
   const int SKP = (a.sk + 31) & ~31;
-  const int nblk = a.batch * a.heads / hpb;
-  const size_t lds = (size_t)hpb * 2 * SKP * DP * sizeof(bf16_t);
-  if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
+  size_t lds = (size_t)hpb * 2 * SKP * DP * sizeof(bf16_t);
+  int kch = SKP, nqb = 1;
+  if (lds > 160 * 1024) {
+    // K / V of a head exceed LDS (the VQ AttnBlock at 32x32 = 1024 tokens, dh 128): one head per
+    // workgroup, key chunks of <= 64 KB streamed, query tiles split over blockIdx.y
+    hpb = 1;
+    kch = (int)((64 * 1024) / (2 * DP * sizeof(bf16_t))) & ~31;
+    if (kch < 32) return ENCDIFF_ERR_SHAPE;
+    const int npairs = (((a.sq + 15) >> 4) + 1) >> 1;
+    nqb = (npairs + 3) / 4;
+    lds = (size_t)2 * kch * DP * sizeof(bf16_t);
+  }
+  const dim3 grid(a.batch * a.heads / hpb, nqb);
   const bool mask = a.sk % 32 != 0;
   static const hipError_t attr0 = hipFuncSetAttribute((const void*)attn_fwd_mfma<DH, false, F8>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   static const hipError_t attr1 = hipFuncSetAttribute((const void*)attn_fwd_mfma<DH, true, F8>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)attr0; (void)attr1;
-  if (mask) hipLaunchKernelGGL((attn_fwd_mfma<DH, true, F8>), dim3(nblk), dim3(256), lds, s, a, hpb);
-  else hipLaunchKernelGGL((attn_fwd_mfma<DH, false, F8>), dim3(nblk), dim3(256), lds, s, a, hpb);
+  if (mask) hipLaunchKernelGGL((attn_fwd_mfma<DH, true, F8>), grid, dim3(256), lds, s, a, hpb, kch);
+  else hipLaunchKernelGGL((attn_fwd_mfma<DH, false, F8>), grid, dim3(256), lds, s, a, hpb, kch);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }

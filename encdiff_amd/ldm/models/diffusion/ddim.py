@@ -25,7 +25,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from encdiff_amd import ops
+from encdiff_amd import ops, torch_ops  # noqa: F401  (torch_ops registers torch.ops.encdiff.*)
 from ...modules.diffusionmodules.util import make_ddim_sampling_parameters, make_ddim_timesteps, noise_like
 
 GRAPH_MAX_STEPS = 256  # longer loops replay a one-step graph (device step index)
@@ -168,15 +168,12 @@ class DDIMSampler(object):
             noise = torch.nn.functional.dropout(noise, p=noise_dropout)
         x = x.float().contiguous()
         e_t = e_t.float().contiguous()
-        x_prev = torch.empty_like(x)
-        pred_x0 = torch.empty_like(x)
         if quantize_denoised:
             pred_x0 = (x - s1 * e_t) / np.sqrt(a_t)
             pred_x0, _, _ = self.model.first_stage_model.quantize(pred_x0)
             x_prev = np.sqrt(a_prev) * pred_x0 + np.sqrt(1. - a_prev - sigma ** 2) * e_t + sigma * noise
             return x_prev, pred_x0
-        ops.ddim_step(x, e_t, noise.float().contiguous(), a_t, a_prev, sigma, s1, x_prev, pred_x0)
-        return x_prev, pred_x0
+        return torch.ops.encdiff.ddim_step(x, e_t, noise, a_t, a_prev, sigma, s1)
 
     # ------------------------------------------------------------ captured loops
     def _entry(self, kind, cond, img, total, log_every_t):

@@ -25,7 +25,7 @@ import numpy as np
 import torch
 from torch import nn
 
-from encdiff_amd import ops
+from encdiff_amd import ops, torch_ops  # noqa: F401  (torch_ops registers torch.ops.encdiff.*)
 from ...util import count_params, default, exists, instantiate_from_config
 from ...modules.diffusionmodules.util import extract_into_tensor, make_beta_schedule
 from ...modules.ema import LitEma
@@ -46,9 +46,7 @@ class _PLossFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pred, noise, t, lvlb, l_simple_weight):
-        out2 = torch.empty(2, device=pred.device, dtype=torch.float32)
-        seed = torch.empty_like(pred, dtype=torch.float32)
-        ops.l1_loss(pred.float().contiguous(), noise.float().contiguous(), t, lvlb, out2, seed, l_simple_weight)
+        out2, seed = torch.ops.encdiff.l1_loss(pred, noise, t, lvlb, float(l_simple_weight))
         ctx.save_for_backward(seed)
         ctx.mark_non_differentiable(out2)
         return out2[0].clone(), out2[1].clone()
@@ -245,10 +243,8 @@ class DDPM(nn.Module):
         noise = default(noise, lambda: torch.randn_like(x_start))
         if not x_start.is_cuda:
             raise RuntimeError("q_sample runs on the HIP path")
-        out = torch.empty_like(x_start, dtype=torch.float32)
-        ops.q_sample(x_start.float().contiguous(), noise.float().contiguous(), t, self.sqrt_alphas_cumprod,
-                     self.sqrt_one_minus_alphas_cumprod, out)
-        return out
+        return torch.ops.encdiff.q_sample(x_start, noise, t, self.sqrt_alphas_cumprod,
+                                          self.sqrt_one_minus_alphas_cumprod)
 
     def get_loss(self, pred, target, mean=True):
         if self.loss_type == "l1":

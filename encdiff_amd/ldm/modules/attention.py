@@ -40,7 +40,10 @@ class FeedForward(nn.Module):
 
 
 class CrossAttention(nn.Module):
-    """attention.py:152-193: q/k/v without bias, to_out Linear + Dropout."""
+    """attention.py:152-193: q/k/v without bias, to_out Linear + Dropout.  Inside the UNet the
+    executor runs it; called on its own (a HIP tensor) the attention core is
+    torch.ops.encdiff.attention_fwd (MFMA flash attention, autograd through
+    encdiff::attention_bwd) between bf16 projections."""
 
     def __init__(self, query_dim, context_dim=None, heads=8, dim_head=64, dropout=0.0):
         super().__init__()
@@ -54,7 +57,19 @@ class CrossAttention(nn.Module):
         self.to_out = nn.Sequential(nn.Linear(inner, query_dim), nn.Dropout(dropout))
 
     def forward(self, x, context=None, mask=None):
-        _hip_only("CrossAttention")
+        if mask is not None:
+            raise NotImplementedError("attention masks are not used by EncDiff (attention.py:185-188 unused)")
+        if not x.is_cuda:
+            raise RuntimeError("CrossAttention runs on the MI355X HIP path only (no CPU fallback)")
+        import torch.nn.functional as F
+        import encdiff_amd.torch_ops  # noqa: F401  (registers torch.ops.encdiff.*)
+        c = x if context is None else context
+        bf = torch.bfloat16
+        q = F.linear(x.to(bf), self.to_q.weight.to(bf))
+        k = F.linear(c.to(bf), self.to_k.weight.to(bf))
+        v = F.linear(c.to(bf), self.to_v.weight.to(bf))
+        o, _ = torch.ops.encdiff.attention_fwd(q.contiguous(), k.contiguous(), v.contiguous(), self.heads, False)
+        return self.to_out(o.to(x.dtype))
 
 
 class BasicTransformerBlock(nn.Module):

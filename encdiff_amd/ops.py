@@ -235,12 +235,20 @@ def linear_fwd_ln(x, w, out, gamma, beta, y, stats, eps, bias=None, resid=None):
     the GEMM epilogue when the planned tile spans the row, else the LayerNorm kernel."""
     M, K = x.shape
     N = w.shape[0]
-    if not LN_FUSED or N > 128 or N % 8 or M < 8192:  # small (sampling) batches keep split-K
+    if not LN_FUSED or N > 128 or N % 8:
         linear_fwd(x, w, out, bias=bias, resid=resid)
         layernorm_fwd(out, gamma, beta, y, stats, eps)
         return
     tile, _ = plan(M, N, K, L.OPA_ROWK, L.OPB_ROWK, L.OUT_BF16)
-    if _TILE_BN.get(tile, 64) < N:  # forcing a wider tile (fewer workgroups) measured slower
+    if M < 8192:
+        # small (sampling) batches: a launch saved outweighs the tile choice -- force a tile that
+        # spans the row (split-K 1; these GEMMs have K = C <= 512, a few k-tiles)
+        if K > 512:
+            linear_fwd(x, w, out, bias=bias, resid=resid)
+            layernorm_fwd(out, gamma, beta, y, stats, eps)
+            return
+        tile = 3 if N > 64 else 4
+    elif _TILE_BN.get(tile, 64) < N:  # at training batch sizes forcing a wider tile measured slower
         linear_fwd(x, w, out, bias=bias, resid=resid)
         layernorm_fwd(out, gamma, beta, y, stats, eps)
         return

@@ -65,3 +65,25 @@ def test_product_path_has_no_oracle_or_fallback():
             if f.endswith(".py"):
                 txt = open(os.path.join(root, f)).read()
                 assert "from oracle" not in txt and "import oracle" not in txt, f
+
+
+def test_torch_library_ops_registered():
+    """The reference-API modules call torch.ops.encdiff.* (SURVEY §8(b)); their fake kernels
+    propagate shapes without a device, and the real ones refuse CPU tensors (no fallback)."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    import encdiff_amd.torch_ops  # noqa: F401
+    for name in ("q_sample", "l1_loss", "ddim_step", "attention_fwd", "attention_bwd"):
+        assert hasattr(torch.ops.encdiff, name), name
+    with FakeTensorMode():
+        x = torch.empty(4, 3, 16, 16)
+        t = torch.empty(4, dtype=torch.long)
+        assert torch.ops.encdiff.q_sample(x, x, t, torch.empty(1000), torch.empty(1000)).shape == x.shape
+        out2, seed = torch.ops.encdiff.l1_loss(x, x, t, torch.empty(1000), 1.0)
+        assert out2.shape == (2,) and seed.shape == x.shape
+        q = torch.empty(2, 256, 64, dtype=torch.bfloat16)
+        o, lse = torch.ops.encdiff.attention_fwd(q, q, q, 8, False)
+        assert o.shape == q.shape and lse.shape == (16, 256)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        torch.ops.encdiff.q_sample(torch.zeros(1, 3, 4, 4), torch.zeros(1, 3, 4, 4), torch.zeros(1, dtype=torch.long),
+                                   torch.zeros(1000), torch.zeros(1000))

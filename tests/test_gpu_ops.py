@@ -838,3 +838,24 @@ def test_linear_layernorm_fused(O, M, C, resid):
     assert (res[0][1].float() - res[1][1].float()).abs().max().item() < 0.05
     ref = F.layer_norm(res[0][0].float(), (C,), gam, bet, 1e-5)
     assert rel(res[0][1], ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,heads,sq,dh", [(2, 1, 1024, 128), (2, 1, 4096, 128), (2, 2, 2048, 64)])
+def test_attention_fwd_streamed_kv(O, B, heads, sq, dh):
+    """Heads whose K / V exceed one workgroup's LDS (the VQ AttnBlock of configs[4]'s 128x128
+    first stage: 1024 tokens, dh 128) stream K / V through LDS in chunks with the query tiles
+    split over workgroups; forward vs torch fp32 softmax attention."""
+    torch.manual_seed(8)
+    C = heads * dh
+    qkv = bf(B * sq, 3 * C)
+    q, k, v = qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:]
+    o = torch.empty(B * sq, C, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * heads, sq, device=dev)
+    O.attention_fwd(q, k, v, o, lse, B, heads, sq, sq, dh)
+
+    def split(t):
+        return t.float().reshape(B, sq, heads, dh).permute(0, 2, 1, 3).reshape(B * heads, sq, dh)
+    s = split(q) @ split(k).transpose(1, 2) * dh ** -0.5
+    ref = (s.softmax(-1) @ split(v)).reshape(B, heads, sq, dh).permute(0, 2, 1, 3).reshape(B * sq, C)
+    assert rel(o, ref) < 1e-2
+    assert rel(lse, torch.logsumexp(s, -1)) < 1e-4
