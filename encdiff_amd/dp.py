@@ -69,6 +69,7 @@ class GradBuckets:
         # bf16 wire format: one staging buffer covering the whole arena (bucket views into it)
         self._wire = torch.empty(flat.numel(), dtype=grad_dtype, device=flat.device) \
             if grad_dtype != flat.dtype and self.world > 1 else None
+        self.record = None  # tools/dp_check.py: {bucket: clone of what this rank sends}
 
     @classmethod
     def from_arena(cls, arena, group=None, grad_dtype=None) -> "GradBuckets":
@@ -96,6 +97,8 @@ class GradBuckets:
             return None
         op = dist.ReduceOp.AVG if self.native_avg else dist.ReduceOp.SUM
         w = self.wire(i)
+        if self.record is not None:
+            self.record[i] = self.view(i).clone()
         if self._wire is not None:
             w.copy_(self.view(i))  # fp32 -> bf16 on the calling (comm) stream
         return dist.all_reduce(w, op=op, group=self.group, async_op=async_op)

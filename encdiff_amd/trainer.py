@@ -144,8 +144,10 @@ class HipTrainer:
         if any(lo <= o < a.ema_numel and not ex._early_final(n) for n, (o, _) in a.offsets.items()):
             return
         self._split_lo = lo
+        rec = self.buckets.record
         self.buckets = GradBuckets(a.grad, [0, lo, a.ema_numel, a.numel], self.buckets.group,
                                    self.buckets.grad_dtype)
+        self.buckets.record = rec
 
     def _unet_rest(self):
         self.unet._ex.backward_rest()

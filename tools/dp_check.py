@@ -81,18 +81,23 @@ def main():
         f = tr.enable_feed()
         feed(f, rank, -1, B)
         tr.init_scale_factor()  # rank 0's batch, broadcast
-        grads = {}
+        grads, local = {}, {}
         for k in range(args.warmup):
             feed(f, rank, k, B)
+            tr.buckets.record = {}
             tr.step_eager()
             grads[k] = tr.arena.grad.cpu().clone()  # the exchanged (averaged) gradient of step k
+            rec = tr.buckets.record
+            local[k] = torch.cat([rec[i] for i in sorted(rec)]).cpu()  # what this rank sent
+            tr.buckets.record = None
         tr.capture(warmup=0)
         for k in range(args.warmup, args.warmup + args.steps):
             feed(f, rank, k, B)
             tr.step()
             grads[k] = tr.arena.grad.cpu().clone()
         torch.cuda.synchronize()
-        d = save(tr, args.out + f".rank{rank}", dict(split_lo=tr._split_lo, loss=tr.loss(), grads=grads))
+        d = save(tr, args.out + f".rank{rank}", dict(split_lo=tr._split_lo, loss=tr.loss(), grads=grads,
+                                                        local=local))
         digests = [None] * W
         dist.all_gather_object(digests, d)
         if rank == 0:
@@ -107,20 +112,21 @@ def main():
     a = tr.arena
     feed(f, 0, -1, B)
     tr.init_scale_factor()
-    grads = {}
+    grads, local = {}, {}
     for k in range(args.warmup + args.steps):
         tr.opt.stage_hyper()
         acc = torch.zeros_like(a.grad)
         for r in range(W):
             feed(f, r, k, B)
             tr._fwd_bwd()   # zeroes the arena gradient, then UNet + Encoder4 backward
+            local[(k, r)] = a.grad.cpu().clone()
             acc += a.grad
         a.grad.copy_(acc / W)  # the gloo exchange: sum over ranks, then / world
         grads[k] = a.grad.cpu().clone()
         tr.opt.launch()
         tr._post()
     torch.cuda.synchronize()
-    save(tr, args.out, dict(grads=grads, names={n: a.offsets[n] for n in a.names}))
+    save(tr, args.out, dict(grads=grads, local=local, names={n: a.offsets[n] for n in a.names}))
     print("w1: done", flush=True)
 
 
