@@ -34,8 +34,12 @@ def _headers():
     return hs
 
 
+# per-file extra flags: the attention kernels' softmax max trees need no NaN canonicalisation
+FILE_FLAGS = {"attn_mfma.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]}
+
+
 def _compile(src: str, obj: str, verbose: bool):
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

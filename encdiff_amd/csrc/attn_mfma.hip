@@ -27,6 +27,9 @@
 // softmax, P V and every gradient product stay bf16 / fp32.
 #include "common.h"
 
+// Built with -fno-honor-nans -mno-amdgpu-ieee (build.py): no v_max canonicalisation of MFMA
+// results in the softmax max trees (scores are finite; masked keys are -inf, never NaN).
+
 namespace {
 
 typedef short s4 __attribute__((ext_vector_type(4)));
@@ -111,40 +114,104 @@ ED_DEV void stage_heads(const bf16_t* __restrict__ base, long ld, int S, int SP,
   else stage_heads_u<DH, DP, 1, ONES>(base, ld, S, SP, H, bh0, hpb, rm, rm_hs, r0);
 }
 
+// K and V of the workgroup's heads in ONE pass (2*U loads per thread in flight): the forward's
+// staging is one global round trip
+template <int DH, int DP, int U, bool ONES>
+ED_DEV void stage_kv_u(const bf16_t* __restrict__ kb, long ldk, const bf16_t* __restrict__ vb, long ldv, int S, int SP,
+                       int H, int bh0, int hpb, bf16_t* ks, bf16_t* vs, int hs, int r0) {
+  constexpr int CH = DP / 8;
+  const int ph = SP * CH, total = hpb * ph;
+  for (int e0 = threadIdx.x; e0 < total; e0 += 256 * U) {
+    uint4 kv[U], vv[U];
+    int off[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * 256;
+      const int hl = hpb == 1 ? 0 : e / ph;
+      const int t = e - hl * ph, r = t / CH, c8 = (t - r * CH) * 8;
+      off[u] = hl * hs + r * DP + c8;
+      kv[u] = (uint4){0u, 0u, 0u, 0u};
+      vv[u] = kv[u];
+      if (e < total && r0 + r < S && c8 < DH) {
+        const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
+        kv[u] = *(const uint4*)(kb + ((long)b * S + r0 + r) * ldk + h * DH + c8);
+        vv[u] = *(const uint4*)(vb + ((long)b * S + r0 + r) * ldv + h * DH + c8);
+      }
+      if (ONES && e < total && r0 + r < S && c8 == DH) vv[u].x = 0x3F80u;  // bf16 1.0 in column DH
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (e0 + u * 256 >= total) break;
+      *(uint4*)(ks + off[u]) = kv[u];
+      *(uint4*)(vs + off[u]) = vv[u];
+    }
+  }
+}
+
+// Workgroup -> head-group index, XCD-aware: workgroup i runs on XCD i % 8, so consecutive head
+// groups (the heads of one image share every 128-B row of the fused q / k / v projection) are
+// given to consecutive workgroups OF ONE XCD and each row is fetched into one L2, not eight.
+// Bijective when the grid is a multiple of 8 (else identity).
+ED_DEV int xcd_group(int i, int n) { return (n & 7) ? i : (i & 7) * (n >> 3) + (i >> 3); }
+
+// Cross-row reductions of the 4 lane rows (lane = 16 * g + l16) by the gfx950 permlane swaps
+// (VALU, no LDS round trip as ds_bpermute): each returns the pair {v, v of lane ^ 16 / ^ 32}.
+ED_DEV float max_x16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+ED_DEV float max_x32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+ED_DEV float sum_x16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+ED_DEV float sum_x32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
 ED_DEV float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// Forward.  A wave task is a PAIR of 16-query tiles of one head: the K and V^T fragments
+__host__ __device__ constexpr int fwd_tiles_per_task(int dh) { return dh == 8 ? 4 : 2; }
+
+// Forward.  A wave task is a PAIR (dh 8: four) of 16-query tiles of one head: the K and V^T fragments
 // read from LDS serve both, and the two online-softmax chains are independent.  Keys are
 // consumed 32 at a time (two MFMA tiles) per softmax update; the running max is kept in the
 // log2 domain (scale * log2 e) and p = exp2(s * scale * log2e - m) is one FMA + a raw
 // v_exp_f32 (arguments <= 0, underflow to 0 is the correct limit).  MASK: key count not a
 // multiple of 32 (keys past SK get -inf).
-template <int DH, bool MASK, bool F8>
+template <int DH, bool MASK, bool F8, int SC = 0>
 __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, int hpb, int kch) {
   constexpr int DP = DH < 16 ? 16 : DH;
   constexpr int KC = DP / 16;
   constexpr bool ONES = DH == 8;   // denominator from the PV MFMA (V^T row 8 = 1)
   constexpr int KC8 = (DH + 31) / 32;  // fp8 score k-steps
   extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
-  const int H = p.heads, SQ = p.sq, SK = p.sk;
+  // SC > 0: sq == sk == SC, one head per workgroup, K / V resident (compile-time loop bounds)
+  const int H = p.heads, SQ = SC ? SC : p.sq, SK = SC ? SC : p.sk;
+  if (SC) { hpb = 1; kch = (SC + 31) & ~31; }
   const int SKP = (SK + 31) & ~31;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
-  const int bh0 = blockIdx.x * hpb;
+  const int bh0 = xcd_group(blockIdx.x, gridDim.x) * hpb;
   const int KR = kch < SKP ? kch : SKP;  // key rows resident in LDS at a time
   bf16_t* Ks = sm;                        // [hpb][KR][DP]
   bf16_t* Vs = sm + hpb * KR * DP;        // [hpb][KR][DP], read transposed (ds_read_b64_tr_b16)
-  const int qtiles = (SQ + 15) >> 4, npairs = (qtiles + 1) >> 1;
+  constexpr int NT = fwd_tiles_per_task(DH);  // 16-query tiles per wave task (independent chains)
+  const int qtiles = (SQ + 15) >> 4, npairs = (qtiles + NT - 1) / NT;
   const float sl2 = p.scale * LOG2E;
   // per-task state: a pair of 16-query tiles of head hl
-  int hl = 0, b = 0, h = 0, q[2];
-  s4 qf[2][KC];
-  long qf8[2][KC8];
-  float m[2], l[2];
-  v4f o[2][KC];
+  int hl = 0, b = 0, h = 0, q[NT];
+  s4 qf[NT][KC];
+  long qf8[NT][KC8];
+  float m[NT], l[NT];
+  v4f o[NT][KC];
   auto init = [&](int task) {
     hl = task / npairs;
     const int qp = task - hl * npairs;
@@ -152,8 +219,8 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
     b = bh / H;
     h = bh - b * H;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      q[u] = (2 * qp + u) * 16 + l16;
+    for (int u = 0; u < NT; ++u) {
+      q[u] = (NT * qp + u) * 16 + l16;
       const bool qv = q[u] < SQ;
       const bf16_t* qp_ = (const bf16_t*)p.q + ((long)b * SQ + q[u]) * p.ldq + h * DH;
       if constexpr (F8) {
@@ -179,6 +246,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
   auto consume = [&](int kbase, int klen) {
     const bf16_t* kb = Ks + hl * KR * DP;
     const bf16_t* vb = Vs + hl * KR * DP;
+#pragma unroll 2
     for (int k0 = 0; k0 < klen; k0 += 32) {
       s4 kf[2][KC];
       long kf8[2][KC8];
@@ -192,9 +260,9 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
           for (int kc = 0; kc < KC; ++kc) kf[t][kc] = ld4(kb + (k0 + t * 16 + l16) * DP + kc * 16 + 4 * g);
         }
       }
-      s4 pf[2][2];
+      s4 pf[NT][2];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < NT; ++u) {
         float sv[8];
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -213,8 +281,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
         // max over raw scores (the scale is positive), the log2-domain max = that * sl2
         float tmax = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
                            fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])));
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        tmax = max_x32(max_x16(tmax));
         const float mn = fmaxf(m[u], tmax * sl2);
         const float alpha = ex2(m[u] - mn);
         m[u] = mn;
@@ -237,22 +304,21 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const s4 vf = ldtr(vb, DP, k0 + t * 16, dt * 16, l16, g);  // V^T fragment
-          o[0][dt] = mma(vf, pf[0][t], o[0][dt]);
-          o[1][dt] = mma(vf, pf[1][t], o[1][dt]);
+#pragma unroll
+          for (int u = 0; u < NT; ++u) o[u][dt] = mma(vf, pf[u][t], o[u][dt]);
         }
     }
   };
   auto finish = [&]() {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NT; ++u) {
       float lu;
       if constexpr (ONES) {
         // O^T row 8 (= g 2, register 0) is sum_k p for query l16: broadcast from lane 32 + l16
         lu = __shfl(o[u][0][0], 32 + l16, 64);
       } else {
         lu = l[u];
-        lu += __shfl_xor(lu, 16, 64);
-        lu += __shfl_xor(lu, 32, 64);
+        lu = sum_x32(sum_x16(lu));
       }
       const float inv = 1.f / lu;
       if (q[u] < SQ) {
@@ -272,11 +338,13 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
     }
   };
   if (KR == SKP) {  // every head's K / V resident: waves loop over their tasks
-    stage_heads<DH, DP>((const bf16_t*)p.k, p.ldk, SK, SKP, H, bh0, hpb, Ks, SKP * DP);
-    stage_heads<DH, DP, ONES>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, Vs, SKP * DP);
+    // the first task's Q loads are issued with the K / V staging loads (one round trip)
+    if (wave < hpb * npairs) init(wave);
+    stage_kv_u<DH, DP, 2, ONES>((const bf16_t*)p.k, p.ldk, (const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, Ks, Vs,
+                                SKP * DP, 0);
     __syncthreads();
     for (int task = wave; task < hpb * npairs; task += 4) {
-      init(task);
+      if (task != wave) init(task);
       consume(0, SKP);
       finish();
     }
@@ -309,18 +377,37 @@ __device__ __host__ inline int attn_qsplit(int ktiles, int hpb) {
 // rows fall on different banks
 __device__ __host__ inline int ds_pitch(int sqp) { return sqp + 16; }
 
-template <int DH, bool MASK, bool F8>
-__global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, int hpb, int dsl) {
+// split: phase A (dK, dV) and phase B (dQ, scores recomputed) run in two workgroups of their own
+// (twice the workgroups per CU to hide each wave's LDS -> MFMA -> exp chains); both stage the
+// head group.  The pair and consecutive head groups stay on one XCD (workgroup i runs on XCD i % 8).
+template <int DH, bool MASK, bool F8, int SC = 0>
+__global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, int hpb, int dsl, int split) {
   constexpr int DP = DH < 16 ? 16 : DH;   // MFMA k extent of the head dim
   constexpr int RP = DH < 16 ? 8 : DH;    // LDS row pitch (dh = 8 staged unpadded)
   constexpr int KC = DP / 16;
   constexpr int KC8 = (DH + 31) / 32;
   extern __shared__ __attribute__((aligned(16))) bf16_t sm[];
-  const int H = p.heads, SQ = p.sq, SK = p.sk;
+  // SC > 0: sq == sk == SC and one head per workgroup known at compile time
+  const int H = p.heads, SQ = SC ? SC : p.sq, SK = SC ? SC : p.sk;
+  if (SC) hpb = 1;
   const int SQP = (SQ + 15) & ~15, SKP = (SK + 15) & ~15;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
-  const int bh0 = blockIdx.x * hpb;
+  int grp = blockIdx.x, part = -1;  // part: -1 both phases, 0 phase A only, 1 phase B only
+  if (split) {
+    const int n = gridDim.x;
+    if (n & 15) {
+      grp = blockIdx.x >> 1;
+      part = blockIdx.x & 1;
+    } else {
+      const int s = blockIdx.x >> 3;
+      grp = (blockIdx.x & 7) * (n >> 4) + (s >> 1);
+      part = s & 1;
+    }
+  } else {
+    grp = xcd_group(blockIdx.x, gridDim.x);
+  }
+  const int bh0 = grp * hpb;
   // per head, row-major: Q, dO [SQP][RP]; K, V [SKP][RP]; lse2, D [SQP]; (dsl) dS^T [SKP][SQP+16].
   // The transposed operands (Q^T, dO^T, K^T, dS^T) are read with ds_read_b64_tr_b16.
   const int QE = SQP * RP, KE = SKP * RP;
@@ -332,39 +419,52 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
   const int qtiles = SQP >> 4, ktiles = SKP >> 4;
   const int QS = attn_qsplit(ktiles, hpb);
   float* red = (float*)(dS + (dsl ? hpb * SKP * DSP : 0));  // phase-A partials [task][2][16*DP] when QS > 1
-  stage_heads<DH, RP>((const bf16_t*)p.q, p.ldq, SQ, SQP, H, bh0, hpb, sm, per_head);
-  stage_heads<DH, RP>((const bf16_t*)p.d_o, p.lddo, SQ, SQP, H, bh0, hpb, sm + oG, per_head);
-  stage_heads<DH, RP>((const bf16_t*)p.k, p.ldk, SK, SKP, H, bh0, hpb, sm + oK, per_head);
-  stage_heads<DH, RP>((const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, sm + oV, per_head);
-  // lse (log2 domain) and D = rowsum(dO * O) per query: 4 rows per thread in flight
-  for (int e0 = tid; e0 < hpb * SQP; e0 += 256 * 4) {
-    float lse[4], D[4];
+  // ONE staging pass, every load of a thread's chunk in flight together: Q, dO, O (query rows),
+  // K, V (key rows), lse; D = rowsum(dO * O) summed over the row's CH chunk lanes by xor-shuffles
+  {
+    constexpr int CH = RP / 8;
+    const int nq = hpb * SQP * CH, nk = hpb * SKP * CH, n = nq > nk ? nq : nk;
+    for (int e0 = 0; e0 < n; e0 += 256) {
+      const int e = e0 + tid;
+      const uint4 z = {0u, 0u, 0u, 0u};
+      uint4 qv = z, gv = z, ov = z, kv = z, vv = z;
+      float lq = 0.f;
+      const int hq = e / (SQP * CH), tq = e - hq * SQP * CH, rq = tq / CH, cq = (tq - rq * CH) * 8;
+      const int hk = e / (SKP * CH), tk = e - hk * SKP * CH, rk = tk / CH, ck = (tk - rk * CH) * 8;
+      if (e < nq && rq < SQ && cq < DH) {
+        const int bh = bh0 + hq, b = bh / H, h = bh - b * H;
+        const long row = (long)b * SQ + rq;
+        qv = *(const uint4*)((const bf16_t*)p.q + row * p.ldq + h * DH + cq);
+        gv = *(const uint4*)((const bf16_t*)p.d_o + row * p.lddo + h * DH + cq);
+        ov = *(const uint4*)((const bf16_t*)p.o + row * p.ldo + h * DH + cq);
+        lq = p.lse[(long)bh * SQ + rq] * LOG2E;
+      }
+      if (e < nk && rk < SK && ck < DH) {
+        const int bh = bh0 + hk, b = bh / H, h = bh - b * H;
+        const long row = (long)b * SK + rk;
+        kv = *(const uint4*)((const bf16_t*)p.k + row * p.ldk + h * DH + ck);
+        vv = *(const uint4*)((const bf16_t*)p.v + row * p.ldv + h * DH + ck);
+      }
+      float a[8], c[8], d = 0.f;
+      unpack8(ov, a);
+      unpack8(gv, c);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * 256, hl = e / SQP, q = e - hl * SQP;
-      lse[u] = 0.f;
-      D[u] = 0.f;
-      if (e < hpb * SQP && q < SQ) {
-        const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
-        lse[u] = p.lse[(long)bh * SQ + q] * LOG2E;
-        const bf16_t* op = (const bf16_t*)p.o + ((long)b * SQ + q) * p.ldo + h * DH;
-        const bf16_t* gp = (const bf16_t*)p.d_o + ((long)b * SQ + q) * p.lddo + h * DH;
+      for (int k = 0; k < 8; ++k) d += a[k] * c[k];
 #pragma unroll
-        for (int d = 0; d < DH; d += 8) {
-          float a[8], c[8];
-          unpack8(*(const uint4*)(op + d), a);
-          unpack8(*(const uint4*)(gp + d), c);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) D[u] += a[k] * c[k];
+      for (int s = 1; s < CH; s <<= 1) d += __shfl_xor(d, s, 64);
+      if (e < nq) {
+        bf16_t* hb = sm + hq * per_head + rq * RP + cq;
+        *(uint4*)hb = qv;
+        *(uint4*)(hb + oG) = gv;
+        if (cq == 0) {
+          fls[hq * 2 * SQP + rq] = lq;
+          fls[hq * 2 * SQP + SQP + rq] = d;
         }
       }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * 256, hl = e / SQP, q = e - hl * SQP;
-      if (e < hpb * SQP) {
-        fls[hl * 2 * SQP + q] = lse[u];
-        fls[hl * 2 * SQP + SQP + q] = D[u];
+      if (e < nk) {
+        bf16_t* hb = sm + hk * per_head + rk * RP + ck;
+        *(uint4*)(hb + oK) = kv;
+        *(uint4*)(hb + oV) = vv;
       }
     }
   }
@@ -372,10 +472,135 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
   const float scale = p.scale, sl2 = p.scale * LOG2E;
   // row fragment (A or B operand with k = head dim) of a row-major staged tile
   auto rowf = [&](const bf16_t* t, int row, int kc) -> s4 {
-    return (DH < 16 && g >= 2) ? (s4){0, 0, 0, 0} : ld4(t + row * RP + kc * 16 + 4 * g);
+    // dh 8 (unpadded rows): lanes g >= 2 hold the zero k = 8..15 half of the fragment; their load
+    // stays inside the row and is discarded by a select (no exec-mask branch)
+    const s4 v = ld4(t + row * RP + kc * 16 + 4 * (DH < 16 ? (g & 1) : g));
+    return (DH < 16 && g >= 2) ? (s4){0, 0, 0, 0} : v;
   };
+  if (dsl > 1) {
+    // Key chunks of dsl keys (one head, host-checked: hpb 1, <= 16 query tiles): phase A on the
+    // chunk's key tiles leaves the chunk's dS^T in LDS, phase B adds the chunk's share of dQ^T
+    // into registers kept across chunks (each wave owns query tiles wave, wave + 4, ...).  No
+    // score is computed twice, and the small dS^T buffer keeps three workgroups per CU.
+    const int KCH = dsl;
+    const bf16_t *Qs = sm, *Gs = sm + oG, *Ks = sm + oK, *Vs = sm + oV;
+    const float* lse = fls;
+    const float* Dv = fls + SQP;
+    const int b = bh0 / H, h = bh0 - b * H;
+    v4f dq[4][KC];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int dt = 0; dt < KC; ++dt) dq[j][dt] = (v4f){0.f, 0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < SKP; c0 += KCH) {
+      const int nkt = (SKP - c0 < KCH ? SKP - c0 : KCH) >> 4;
+      for (int t = wave; t < nkt; t += 4) {
+        const int key = c0 + t * 16 + l16;
+        const bool kv = key < SK;
+        s4 kf[KC], vf[KC];
+        long kf8[KC8];
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          kf[kc] = rowf(Ks, key, kc);
+          vf[kc] = rowf(Vs, key, kc);
+        }
+        if constexpr (F8) {
+#pragma unroll
+          for (int kc = 0; kc < KC8; ++kc) kf8[kc] = frag8<DH>(Ks, RP, key, kc, g);
+        }
+        v4f dk[2][KC], dv[2][KC];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int dt = 0; dt < KC; ++dt) { dk[u][dt] = (v4f){0.f, 0.f, 0.f, 0.f}; dv[u][dt] = dk[u][dt]; }
+        auto qstep = [&](const int qt, const int u) {
+          v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (F8) {
+#pragma unroll
+            for (int kc = 0; kc < KC8; ++kc) s = mma8(frag8<DH>(Qs, RP, qt * 16 + l16, kc, g), kf8[kc], s);
+          }
+#pragma unroll
+          for (int kc = 0; kc < KC; ++kc) {
+            if constexpr (!F8) s = mma(rowf(Qs, qt * 16 + l16, kc), kf[kc], s);
+            dp = mma(rowf(Gs, qt * 16 + l16, kc), vf[kc], dp);
+          }
+          float pv[4], ds[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int q = qt * 16 + 4 * g + i;
+            pv[i] = (!MASK || (kv && q < SQ)) ? ex2(__builtin_fmaf(s[i], sl2, -lse[q])) : 0.f;
+            ds[i] = pv[i] * (dp[i] - Dv[q]);
+          }
+          const s4 pf = pack4(pv[0], pv[1], pv[2], pv[3]);
+          const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);
+          *(s4*)(dS + (t * 16 + l16) * DSP + qt * 16 + 4 * g) = df;
+#pragma unroll
+          for (int dt = 0; dt < KC; ++dt) {
+            dv[u][dt] = mma(ldtr(Gs, RP, qt * 16, dt * 16, l16, g), pf, dv[u][dt]);
+            dk[u][dt] = mma(ldtr(Qs, RP, qt * 16, dt * 16, l16, g), df, dk[u][dt]);
+          }
+        };
+        int qt0 = 0;
+#pragma unroll 4
+        for (; qt0 + 1 < qtiles; qt0 += 2) {
+          qstep(qt0, 0);
+          qstep(qt0 + 1, 1);
+        }
+        if (qt0 < qtiles) qstep(qt0, 0);
+        if (kv) {
+          bf16_t* dkp = (bf16_t*)p.dk + ((long)b * SK + key) * p.lddk + h * DH;
+          bf16_t* dvp = (bf16_t*)p.dv + ((long)b * SK + key) * p.lddv + h * DH;
+#pragma unroll
+          for (int dt = 0; dt < KC; ++dt) {
+            const int d0 = dt * 16 + 4 * g;
+            if (d0 < DH) {
+              const v4f a = dk[0][dt] + dk[1][dt], c = dv[0][dt] + dv[1][dt];
+              uint2 w;
+              w.x = pack2(a[0] * scale, a[1] * scale);
+              w.y = pack2(a[2] * scale, a[3] * scale);
+              *(uint2*)(dkp + d0) = w;
+              w.x = pack2(c[0], c[1]);
+              w.y = pack2(c[2], c[3]);
+              *(uint2*)(dvp + d0) = w;
+            }
+          }
+        }
+      }
+      __syncthreads();  // the chunk's dS^T is complete
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int qt = wave + 4 * j;
+        if (qt < qtiles) {
+          for (int t = 0; t < nkt; ++t) {
+            const s4 df = ldtr(dS, DSP, t * 16, qt * 16, l16, g);
+#pragma unroll
+            for (int dt = 0; dt < KC; ++dt) dq[j][dt] = mma(ldtr(Ks, RP, c0 + t * 16, dt * 16, l16, g), df, dq[j][dt]);
+          }
+        }
+      }
+      __syncthreads();  // dS^T is rewritten by the next chunk
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = (wave + 4 * j) * 16 + l16;
+      if (wave + 4 * j < qtiles && q < SQ) {
+        bf16_t* dqp = (bf16_t*)p.dq + ((long)b * SQ + q) * p.lddq + h * DH;
+#pragma unroll
+        for (int dt = 0; dt < KC; ++dt) {
+          const int d0 = dt * 16 + 4 * g;
+          if (d0 < DH) {
+            uint2 w;
+            w.x = pack2(dq[j][dt][0] * scale, dq[j][dt][1] * scale);
+            w.y = pack2(dq[j][dt][2] * scale, dq[j][dt][3] * scale);
+            *(uint2*)(dqp + d0) = w;
+          }
+        }
+      }
+    }
+    return;
+  }
   // ---- phase A: dK, dV (task = key tile x query slice; query tiles in pairs) ----------
-  const int ntA = hpb * ktiles * QS;
+  const int ntA = part == 1 ? 0 : hpb * ktiles * QS;
   for (int task = wave; task < ntA; task += 4) {
     const int hl = task / (ktiles * QS), rem = task - hl * ktiles * QS;
     const int kt = rem / QS, qs = rem - kt * QS;
@@ -434,6 +659,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
         }
     };
     if (qtiles % (2 * QS) == 0) {
+#pragma unroll
       for (int qt0 = qs; qt0 < qtiles; qt0 += 2 * QS) {
         qstep(qt0, 0);
         qstep(qt0 + QS, 1);
@@ -474,7 +700,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
     }
   }
   if (QS > 1 || dsl) __syncthreads();
-  if (QS > 1) {
+  if (QS > 1 && part != 1) {
     // one wave per (head, key tile) adds its QS slices in order and writes dK, dV
     for (int t = wave; t < hpb * ktiles; t += 4) {
       const int hl = t / ktiles, kt = t - hl * ktiles;
@@ -509,7 +735,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
     }
   }
   // ---- phase B: dQ (waves own query tiles; key tiles in pairs) ----------------------
-  for (int task = wave; task < hpb * qtiles; task += 4) {
+  for (int task = wave; task < (part == 0 ? 0 : hpb * qtiles); task += 4) {
     const int hl = task / qtiles, qt = task - hl * qtiles;
     const int bh = bh0 + hl, b = bh / H, h = bh - b * H;
     const bf16_t* base = sm + hl * per_head;
@@ -533,6 +759,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
           dq[u][dt] = mma(ldtr(Ks, RP, kt * 16, dt * 16, l16, g), df, dq[u][dt]);  // K^T fragment
       };
       int kt0 = 0;
+#pragma unroll
       for (; kt0 + 1 < ktiles; kt0 += 2) {
         kstep(kt0, 0);
         kstep(kt0 + 1, 1);
@@ -575,6 +802,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
           dq[u][dt] = mma(ldtr(Ks, RP, kt * 16, dt * 16, l16, g), df, dq[u][dt]);  // K^T fragment
       };
       int kt0 = 0;
+#pragma unroll
       for (; kt0 + 1 < ktiles; kt0 += 2) {
         kstep(kt0, 0);
         kstep(kt0 + 1, 1);
@@ -617,7 +845,8 @@ int launch_mfma_fwd(const EncdiffAttnArgs& a, hipStream_t s) {
     hpb = 1;
     kch = (int)((64 * 1024) / (2 * DP * sizeof(bf16_t))) & ~31;
     if (kch < 32) return ENCDIFF_ERR_SHAPE;
-    const int npairs = (((a.sq + 15) >> 4) + 1) >> 1;
+    constexpr int NT = fwd_tiles_per_task(DH);
+    const int npairs = (((a.sq + 15) >> 4) + NT - 1) / NT;
     nqb = (npairs + 3) / 4;
     lds = (size_t)2 * kch * DP * sizeof(bf16_t);
   }
@@ -628,6 +857,16 @@ int launch_mfma_fwd(const EncdiffAttnArgs& a, hipStream_t s) {
   static const hipError_t attr1 = hipFuncSetAttribute((const void*)attn_fwd_mfma<DH, true, F8>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)attr0; (void)attr1;
+  if constexpr (DH == 8 && !F8) {
+    if (a.sq == 256 && a.sk == 256 && hpb == 1 && nqb == 1) {  // level-0 self-attention of the UNet
+      static const hipError_t attr2 = hipFuncSetAttribute((const void*)attn_fwd_mfma<DH, false, F8, 256>,
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)attr2;
+      hipLaunchKernelGGL((attn_fwd_mfma<DH, false, F8, 256>), grid, dim3(256), lds, s, a, hpb, kch);
+      ED_CHECK_LAUNCH();
+      return ENCDIFF_OK;
+    }
+  }
   if (mask) hipLaunchKernelGGL((attn_fwd_mfma<DH, true, F8>), grid, dim3(256), lds, s, a, hpb, kch);
   else hipLaunchKernelGGL((attn_fwd_mfma<DH, false, F8>), grid, dim3(256), lds, s, a, hpb, kch);
   ED_CHECK_LAUNCH();
@@ -645,17 +884,52 @@ int launch_mfma_bwd(const EncdiffAttnArgs& a, hipStream_t s) {
   const size_t red = QS > 1 ? (size_t)hpb * (SKP / 16) * QS * 2 * 16 * DP * sizeof(float) : 0;
   const size_t base = (size_t)hpb * ((2 * SQP + 2 * SKP) * RP * sizeof(bf16_t) + 2 * SQP * sizeof(float)) + red;
   const size_t dsz = (size_t)hpb * SKP * ds_pitch(SQP) * sizeof(bf16_t);
-  const int dsl = base + dsz <= 160 * 1024 ? 1 : 0;  // dS^T kept in LDS for phase B
-  const size_t lds = base + (dsl ? dsz : 0);
+  // dS^T kept in LDS for phase B (no second exp sweep) only while >= 3 workgroups fit a CU: at
+  // one workgroup per CU (S = 256: 157 KB) every wave's LDS -> MFMA -> exp chain is exposed
+  static const long dsl_max = [] {
+    const char* e = getenv("ENCDIFF_ATTN_DSL_MAX");  // tuning knob (bytes)
+    return e ? atol(e) : 52L * 1024;
+  }();
+  int dsl = (long)(base + dsz) <= dsl_max ? 1 : 0;
+  size_t lds = base + (dsl ? dsz : 0);
+  static const int kch_env = [] {
+    const char* e = getenv("ENCDIFF_ATTN_KCHUNK");  // tuning knob (keys per dS^T chunk, 0: off)
+    return e ? atoi(e) : 64;
+  }();
+  if (!dsl && kch_env >= 16 && hpb == 1 && QS == 1 && SQP <= 256 && SKP > kch_env) {
+    const size_t csz = (size_t)kch_env * ds_pitch(SQP) * sizeof(bf16_t);
+    if ((long)(base + csz) <= dsl_max + 4096) {
+      dsl = kch_env & ~15;
+      lds = base + csz;
+    }
+  }
   if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
   static const hipError_t attr0 = hipFuncSetAttribute((const void*)attn_bwd_mfma<DH, false, F8>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   static const hipError_t attr1 = hipFuncSetAttribute((const void*)attn_bwd_mfma<DH, true, F8>,
                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)attr0; (void)attr1;
+  // phase B recomputes the scores: optionally in workgroups of its own (measured: 59 -> 62 us at
+  // S = 256 dh 8, B = 128 -- the workgroups already fill the CUs; kept as a knob)
+  static const int split_env = [] {
+    const char* e = getenv("ENCDIFF_ATTN_SPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  const int split = (dsl || !split_env) ? 0 : 1;  // (dsl > 1: chunked dS^T, one workgroup per head)
+  const dim3 grid(nblk * (split ? 2 : 1));
+  if constexpr (DH == 8 && !F8) {
+    if (a.sq == 256 && a.sk == 256 && hpb == 1 && dsl != 1) {  // level-0 self-attention of the UNet
+      static const hipError_t attr2 = hipFuncSetAttribute((const void*)attn_bwd_mfma<DH, false, F8, 256>,
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)attr2;
+      hipLaunchKernelGGL((attn_bwd_mfma<DH, false, F8, 256>), grid, dim3(256), lds, s, a, hpb, dsl, split);
+      ED_CHECK_LAUNCH();
+      return ENCDIFF_OK;
+    }
+  }
   if (a.sq % 16 || a.sk % 16)
-    hipLaunchKernelGGL((attn_bwd_mfma<DH, true, F8>), dim3(nblk), dim3(256), lds, s, a, hpb, dsl);
-  else hipLaunchKernelGGL((attn_bwd_mfma<DH, false, F8>), dim3(nblk), dim3(256), lds, s, a, hpb, dsl);
+    hipLaunchKernelGGL((attn_bwd_mfma<DH, true, F8>), grid, dim3(256), lds, s, a, hpb, dsl, split);
+  else hipLaunchKernelGGL((attn_bwd_mfma<DH, false, F8>), grid, dim3(256), lds, s, a, hpb, dsl, split);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }

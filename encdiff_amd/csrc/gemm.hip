@@ -24,6 +24,9 @@ enum { A_ROWK = ENCDIFF_OPA_ROWK, A_IM2COL = ENCDIFF_OPA_IM2COL, A_ROWM = ENCDIF
 enum { B_ROWK = ENCDIFF_OPB_ROWK, B_ROWN = ENCDIFF_OPB_ROWN, B_CONVD = ENCDIFF_OPB_CONV_DGRAD,
        B_IM2COL = ENCDIFF_OPB_IM2COL };
 
+// internal A mode (tiles >= 16): implicit im2col read from a per-workgroup halo image in LDS
+enum { A_HALO = 16 };
+
 template <int AM> struct AKInner { static constexpr bool v = AM != A_ROWM; };
 template <int BMd> struct BKInner { static constexpr bool v = BMd == B_ROWK; };
 
@@ -39,8 +42,9 @@ struct TileShape {
   static constexpr int ELEMS = ROWS * KB;
   static constexpr int CHUNKS = ROWS * KB / 8;  // 16-byte chunks per tile
   static constexpr int PER_THREAD = CHUNKS / 256;
-  // swizzle mask: 16 rows of a 256-byte k-inner row (KB = 128) spread over all 64 banks
-  static constexpr int SWM = (KINNER && KB >= 128) ? 15 : 7;
+  // swizzle mask: 16 rows of a 256-byte k-inner row (KB = 128) spread over all 64 banks;
+  // a 4-slot k-outer row (32 columns) swizzles within its 4 slots
+  static constexpr int SWM = (KINNER && KB >= 128) ? 15 : (SLOTS < 8 ? SLOTS - 1 : 7);
 };
 ED_DEV int swz(int row, int slot, int mask = 7) { return slot ^ (row & mask); }
 
@@ -57,11 +61,28 @@ struct FDiv {
 };
 ED_DEV uint32_t fdiv(uint32_t n, const FDiv& f) { return (uint32_t)(((unsigned long long)n * f.mul) >> 40); }
 
+// Halo tiles (A_HALO): a workgroup's BM output pixels are R whole rows of one image (or NI
+// whole images); every conv-input pixel their taps reach -- an (hr x hc) window per image, all
+// cin channels -- is staged into LDS ONCE by LDS-DMA, so the K loop streams only weights and the
+// im2col operand is read from L2 once instead of once per tap.  Conv-input coordinate of halo
+// pixel (hy, hx): (s*y0 + off + hy, off + hx), bounds (lh, lw); source pixel = coordinate >> ush
+// (nearest-up) of an (hs x ws) image.  16-byte chunk c of halo pixel p sits at LDS slot
+// c ^ ((p >> xsh) & xmsk): the 16 pixels an MFMA fragment read touches land on distinct banks.
+struct HaloGeom {
+  int hr, hc, ni;      // halo rows / cols per image, images per tile
+  int s, off, kt;      // conv-input stride, window origin offset, taps per dimension
+  int lh, lw, ush, hs, ws;
+  int ch, xsh, xmsk;   // 16-B chunks per pixel (cin / 8), bank swizzle
+  int npix, chunks;    // halo pixels, chunks rounded up to 256 (one per thread per DMA round)
+  FDiv fch, fimg, fhc; // / ch, / (hr * hc), / hc
+};
+
 struct GemmAux {
   FDiv cin;   // A/B im2col: k (or n) -> (tap, channel)
   FDiv cout;  // B_CONVD: k -> (tap, co)
   FDiv hw;    // pixel -> (image, in-image index)
   FDiv w;     // in-image index -> (y, x)
+  HaloGeom halo;
 };
 
 // Implicit im2col, branch-free.  The launch's resample mode is folded into uniform
@@ -133,13 +154,15 @@ struct Gemm {
   using TB = TileShape<BN, BKI, KB>;
   static constexpr int TM = BM / 32;  // 16x16 MFMA tiles per wave along M
   static constexpr int TN = BN / 32;
-  static constexpr int STAGE = TA::ELEMS + TB::ELEMS;  // elements per LDS stage
+  static constexpr bool HALO = AM == A_HALO;
+  static constexpr int ASTAGE = HALO ? 0 : TA::ELEMS;  // halo mode: the ring holds B only
+  static constexpr int STAGE = ASTAGE + TB::ELEMS;     // elements per LDS stage
   // LDS ring depth.  Measured on the step's GEMMs: 3-4 stages for every GEMM (one or two
   // workgroups per CU) lost 7% overall against 2 stages with up to five resident workgroups
   // per CU hiding the load latency instead; the deeper rings are tile choices of their own
   // (tiles 5, 6) that the measured table picks per problem.
   static constexpr int NSTAGE = NS;
-  static constexpr int LPS = TA::PER_THREAD + TB::PER_THREAD;  // LDS-DMA loads per thread per stage
+  static constexpr int LPS = (HALO ? 0 : TA::PER_THREAD) + TB::PER_THREAD;  // LDS-DMA loads per thread per stage
   // the staging ring, reused by the fp32 epilogue tile [BM][BN + 4]
   static constexpr int LDS_BYTES =
       (NSTAGE * STAGE * 2 > BM * (BN + 4) * 4) ? NSTAGE * STAGE * 2 : BM * (BN + 4) * 4;
@@ -205,12 +228,33 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   auto gcol = [&](int c) -> int {
     return c < BN / 2 ? by * (BN / 2) + c : (p.N >> 1) + by * (BN / 2) + c - BN / 2;
   };
+  // halo mode: the window sits at the LDS base, the B ring behind it
+  bf16_t* ring = smem;
+  if constexpr (G::HALO) ring = smem + aux.halo.chunks * 8;
+  auto stage_halo = [&]() {
+    const HaloGeom& h = aux.halo;
+    const uint32_t b0 = fdiv((uint32_t)m0, aux.hw);
+    const uint32_t y0 = fdiv((uint32_t)m0 - b0 * aux.hw.d, aux.w);  // 0 when the tile holds whole images
+    const int cy0 = h.s * (int)y0 + h.off;
+    for (int c = tid; c < h.chunks; c += 256) {
+      const uint32_t px = fdiv((uint32_t)c, h.fch);
+      const int gch = (c - (int)(px * (uint32_t)h.ch)) ^ ((int)(px >> h.xsh) & h.xmsk);
+      const uint32_t j = fdiv(px, h.fimg);
+      const uint32_t r = px - j * h.fimg.d;
+      const uint32_t hy = fdiv(r, h.fhc);
+      const int cy = cy0 + (int)hy, cx = h.off + (int)(r - hy * (uint32_t)h.hc);
+      const bool ok = (int)px < h.npix && (unsigned)cy < (unsigned)h.lh && (unsigned)cx < (unsigned)h.lw;
+      const uint32_t row = ((b0 + j) * (uint32_t)h.hs + (uint32_t)(cy >> h.ush)) * (uint32_t)h.ws + (uint32_t)(cx >> h.ush);
+      const void* src = ok ? (const void*)(A + (size_t)row * p.conv.ld_src + gch * 8) : (const void*)&g_zero16;
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(smem + (c & ~63) * 8), 16, 0, 0);
+    }
+  };
   auto stage = [&](bf16_t* s, int kt) {
     const int k0 = kt * BK;
     bf16_t* sa = s;
-    bf16_t* sb = s + TA::ELEMS;
+    bf16_t* sb = s + G::ASTAGE;
 #pragma unroll
-    for (int i = 0; i < TA::PER_THREAD; ++i) {
+    for (int i = 0; i < (G::HALO ? 0 : TA::PER_THREAD); ++i) {
       const int c = tid + 256 * i;               // LDS chunk position (lane-linear)
       const int row = c / TA::SLOTS, slot = c % TA::SLOTS;
       const int gs = swz(row, slot, TA::SWM);     // global chunk held at this slot
@@ -308,20 +352,43 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   auto frag_kinner = [&](const bf16_t* s, int row, int kk, int mask) -> v8bf {
     return *(const v8bf*)(s + row * BK + swz(row, kk * 4 + g4, mask) * 8);
   };
-  auto frag_kouter = [&](const bf16_t* s, int ld, int colbase, int kk) -> v8bf {
+  auto frag_kouter = [&](const bf16_t* s, int ld, int colbase, int kk, int mask) -> v8bf {
     // rows k = kk*32 + g4*8 + tq (+4): 4 bf16 at column colbase + 4*tp, swizzled chunk
     typedef __attribute__((address_space(3))) v4s lds_v4s;
     const int r0 = kk * 32 + g4 * 8 + tq, r1 = r0 + 4;
     const int ch = (colbase >> 3) + (tp >> 1), sub = (tp & 1) * 4;
-    v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(s + r0 * ld + swz(r0, ch) * 8 + sub));
-    v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(s + r1 * ld + swz(r1, ch) * 8 + sub));
+    v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(s + r0 * ld + swz(r0, ch, mask) * 8 + sub));
+    v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(s + r1 * ld + swz(r1, ch, mask) * 8 + sub));
     v8s r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(v8bf, r);
   };
 
-  auto compute = [&](const bf16_t* s) {
+  // halo mode: window pixel of each of this lane's fragment rows at tap (0, 0)
+  uint32_t hpb[TM];
+  if constexpr (G::HALO) {
+    const HaloGeom& h = aux.halo;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const uint32_t m = (uint32_t)(wr + 16 * i + l16);
+      const uint32_t j = fdiv(m, aux.hw), rr = m - j * aux.hw.d;
+      const uint32_t ry = fdiv(rr, aux.w), rx = rr - ry * aux.w.d;
+      hpb[i] = j * h.fimg.d + (uint32_t)h.s * (ry * (uint32_t)h.hc + rx);
+    }
+  }
+  auto frag_halo = [&](int kt, int kk, int i) -> v8bf {
+    const HaloGeom& h = aux.halo;
+    uint32_t k = (uint32_t)(kt * BK + kk * 32 + g4 * 8);
+    if (k >= (uint32_t)p.K) k = 0;  // tail of the last k-tile: B is zero there, keep A finite
+    const uint32_t tap = fdiv(k, aux.cin), ci = k - tap * (uint32_t)p.conv.cin;
+    const uint32_t ty = h.kt == 4 ? tap >> 2 : (tap * 11u) >> 5;
+    const uint32_t hp = hpb[i] + ty * (uint32_t)h.hc + (tap - (uint32_t)h.kt * ty);
+    const uint32_t slot = (ci >> 3) ^ ((hp >> h.xsh) & (uint32_t)h.xmsk);
+    return *(const v8bf*)(smem + (hp * (uint32_t)h.ch + slot) * 8);
+  };
+
+  auto compute = [&](const bf16_t* s, int kt) {
     const bf16_t* sa = s;
-    const bf16_t* sb = s + TA::ELEMS;
+    const bf16_t* sb = s + G::ASTAGE;
     if (do_bgrad) {
       // BM columns x BK rows; 256 threads -> 256/BM row-groups
       constexpr int RG = 256 / BM;
@@ -335,13 +402,14 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       v8bf af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        if constexpr (AKI) af[i] = frag_kinner(sa, wr + 16 * i + l16, kk, TA::SWM);
-        else af[i] = frag_kouter(sa, TA::LD, wr + 16 * i, kk);
+        if constexpr (G::HALO) af[i] = frag_halo(kt, kk, i);
+        else if constexpr (AKI) af[i] = frag_kinner(sa, wr + 16 * i + l16, kk, TA::SWM);
+        else af[i] = frag_kouter(sa, TA::LD, wr + 16 * i, kk, TA::SWM);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         if constexpr (BKI) bfr[j] = frag_kinner(sb, wc + 16 * j + l16, kk, TB::SWM);
-        else bfr[j] = frag_kouter(sb, TB::LD, wc + 16 * j, kk);
+        else bfr[j] = frag_kouter(sb, TB::LD, wc + 16 * j, kk, TB::SWM);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -359,15 +427,17 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   constexpr int D = G::NSTAGE;
   static_assert(D - 2 <= 2, "vm_wait_stages covers up to two stages ahead");
   if (nkt > 0) {
+    // halo mode: the window's DMAs are issued first, so the wait for ring tile 0 covers them
+    if constexpr (G::HALO) stage_halo();
 #pragma unroll
     for (int st = 0; st < D - 1; ++st)
-      if (st < nkt) stage(smem + st * G::STAGE, kt_begin + st);
+      if (st < nkt) stage(ring + st * G::STAGE, kt_begin + st);
     int rd = 0, wr = D - 1;  // ring slots of the tile read now / the tile issued next
     for (int it = 0; it < nkt; ++it) {
       vm_wait_stages<G::LPS>(min(D - 2, nkt - 1 - it));
       asm volatile("s_barrier" ::: "memory");  // (asm: the compiler may not move LDS-DMA issue across it)
-      if (it + D - 1 < nkt) stage(smem + wr * G::STAGE, kt_begin + it + D - 1);
-      compute(smem + rd * G::STAGE);
+      if (it + D - 1 < nkt) stage(ring + wr * G::STAGE, kt_begin + it + D - 1);
+      compute(ring + rd * G::STAGE, kt_begin + it);
       // this wave's fragment reads of slot rd retire before it reaches the next barrier
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       rd = rd + 1 == D ? 0 : rd + 1;
@@ -830,8 +900,51 @@ hipError_t launch_t(const EncdiffGemmArgs& p, const GemmAux& aux, hipStream_t s)
   return hipGetLastError();
 }
 
+// halo tiles: ids 16.. (tile_halo_bm / tile_halo_bn), 3-deep B ring, window + ring in dynamic LDS
+constexpr int HALO_NS = 3;
+constexpr int HALO_LDS_MAX = 156 * 1024;  // 160 KiB less the paired kernel's static finalize scratch
+__host__ __device__ constexpr int halo_bm(int t) {
+  return t == 16 ? 64 : t == 17 ? 128 : t == 18 ? 128 : t == 19 ? 256 : t == 20 ? 128 : t == 21 ? 256 : t == 22 ? 64 : 64;
+}
+__host__ __device__ constexpr int halo_bn(int t) {
+  return t == 16 ? 64 : t == 17 ? 64 : t == 18 ? 128 : t == 19 ? 32 : t == 20 ? 32 : t == 21 ? 64 : t == 22 ? 128 : 32;
+}
+inline size_t halo_lds_bytes(const HaloGeom& h, int bm, int bn) {
+  const size_t win = (size_t)h.chunks * 16 + (size_t)HALO_NS * bn * BK * 2;
+  const size_t epi = (size_t)bm * (bn + 4) * 4;
+  return win > epi ? win : epi;
+}
+
+template <int BM, int BN, int BMD>
+hipError_t launch_halo_t(const EncdiffGemmArgs& p, const GemmAux& aux, hipStream_t s) {
+  static const hipError_t attr_ok = hipFuncSetAttribute(
+      (const void*)gemm_kernel<BM, BN, A_HALO, BMD, HALO_NS, BK>, hipFuncAttributeMaxDynamicSharedMemorySize, HALO_LDS_MAX);
+  if (attr_ok != hipSuccess) return attr_ok;
+  dim3 grid(p.M / BM, (p.N + BN - 1) / BN, 1);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, A_HALO, BMD, HALO_NS, BK>), grid, dim3(256), halo_lds_bytes(aux.halo, BM, BN), s,
+                     p, aux);
+  return hipGetLastError();
+}
+
+template <int BMD>
+hipError_t launch_halo(const EncdiffGemmArgs& p, const GemmAux& aux, int tile, hipStream_t s) {
+  switch (tile) {
+    case 16: return launch_halo_t<64, 64, BMD>(p, aux, s);
+    case 17: return launch_halo_t<128, 64, BMD>(p, aux, s);
+    case 18: return launch_halo_t<128, 128, BMD>(p, aux, s);
+    case 19: return launch_halo_t<256, 32, BMD>(p, aux, s);
+    case 20: return launch_halo_t<128, 32, BMD>(p, aux, s);
+    case 21: return launch_halo_t<256, 64, BMD>(p, aux, s);
+    case 22: return launch_halo_t<64, 128, BMD>(p, aux, s);
+    default: return launch_halo_t<64, 32, BMD>(p, aux, s);
+  }
+}
+
 template <int AM, int BMD>
 hipError_t launch_modes(const EncdiffGemmArgs& p, const GemmAux& aux, int tile, hipStream_t s) {
+  if constexpr (AM == A_IM2COL && (BMD == B_ROWK || BMD == B_CONVD)) {
+    if (tile >= 16) return launch_halo<BMD>(p, aux, tile, s);
+  }
   switch (tile) {
     case 1: return launch_t<128, 128, AM, BMD>(p, aux, s);
     case 2: return launch_t<128, 64, AM, BMD>(p, aux, s);
@@ -862,6 +975,60 @@ int pick_tile(const EncdiffGemmArgs& p) {
   if (bm == 128) return 2;
   if (bn == 128) return 3;
   return 4;
+}
+
+int gcd_i(int a, int b) { return b ? gcd_i(b, a % b) : a; }
+
+// Halo-tile eligibility and geometry (tiles 16..23): implicit-im2col A of a 3x3 (pad 1, optional
+// nearest-up), VQ stride-2 or Encoder4 k4 s2 conv forward, or a plain 3x3 input gradient;
+// BM pixels = whole rows of one image or whole images; window + B ring within 160 KiB of LDS.
+int prepare_halo(const EncdiffGemmArgs& p, int tile, HaloGeom& h) {
+  if (tile > 23 || p.a_mode != ENCDIFF_OPA_IM2COL) return ENCDIFF_ERR_UNSUPPORTED;
+  const int rs = p.conv.resample;
+  if (p.b_mode == ENCDIFF_OPB_ROWK) {
+    if (rs != ENCDIFF_RESAMPLE_NONE && rs != ENCDIFF_RESAMPLE_UP2 && rs != ENCDIFF_RESAMPLE_STRIDE2 &&
+        rs != ENCDIFF_RESAMPLE_K4S2)
+      return ENCDIFF_ERR_UNSUPPORTED;
+  } else if (p.b_mode != ENCDIFF_OPB_CONV_DGRAD || rs != ENCDIFF_RESAMPLE_NONE) {
+    return ENCDIFF_ERR_UNSUPPORTED;
+  }
+  if (p.split_k != 1 || p.c_mode == ENCDIFF_OUT_F32_ATOMIC || p.c_mode == ENCDIFF_OUT_F32_ATOMIC_CONVW)
+    return ENCDIFF_ERR_UNSUPPORTED;
+  const int bm = halo_bm(tile), bn = halo_bn(tile);
+  const int H = p.conv.h, W = p.conv.w, HW = H * W, cin = p.conv.cin;
+  if ((long)p.M != (long)p.conv.batch * HW || p.M % bm || bm % W || (HW % bm && bm % HW)) return ENCDIFF_ERR_SHAPE;
+  const bool up = rs == ENCDIFF_RESAMPLE_UP2, s2 = rs == ENCDIFF_RESAMPLE_STRIDE2, k4 = rs == ENCDIFF_RESAMPLE_K4S2;
+  if (up && ((H | W) & 1)) return ENCDIFF_ERR_SHAPE;
+  h.s = (s2 || k4) ? 2 : 1;
+  h.off = s2 ? 0 : -1;
+  h.kt = k4 ? 4 : 3;
+  if (p.K != h.kt * h.kt * cin || cin % 8) return ENCDIFF_ERR_SHAPE;
+  h.lh = h.s * H;
+  h.lw = h.s * W;
+  h.ush = up ? 1 : 0;
+  h.hs = up ? H / 2 : h.lh;
+  h.ws = up ? W / 2 : h.lw;
+  const int rows = bm / W < H ? bm / W : H;
+  h.ni = bm > HW ? bm / HW : 1;
+  h.hr = h.s * (rows - 1) + h.kt;
+  h.hc = h.s * (W - 1) + h.kt;
+  h.ch = cin / 8;
+  h.npix = h.ni * h.hr * h.hc;
+  h.chunks = (h.npix * h.ch + 255) & ~255;
+  // bank swizzle: consecutive pixels advance q 16-B slots in the 16-slot bank row; g pixels share a
+  // slot position, spread them over min(g, largest power of two dividing ch) slots
+  const int q = h.ch % 16, g = q ? gcd_i(q, 16) : 16;
+  int pw = 1;
+  while (pw < 16 && h.ch % (2 * pw) == 0) pw *= 2;
+  h.xmsk = (pw < g ? pw : g) - 1;
+  int xsh = 0;
+  while ((1 << xsh) < 16 / g) ++xsh;
+  h.xsh = xsh;
+  h.fch = make_fdiv(h.ch);
+  h.fimg = make_fdiv(h.hr * h.hc);
+  h.fhc = make_fdiv(h.hc);
+  if (halo_lds_bytes(h, bm, bn) > (size_t)HALO_LDS_MAX) return ENCDIFF_ERR_SHAPE;
+  return ENCDIFF_OK;
 }
 
 // Validated launch plan of one GEMM: the arguments the tile kernel sees (split-K slabs
@@ -914,6 +1081,11 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
     if (fwd && (p.a_mode != ENCDIFF_OPA_ROWK || p.b_mode != ENCDIFF_OPB_ROWK || p.N % 128)) return ENCDIFF_ERR_ARG;
   }
   g.tile = p.tile ? p.tile : pick_tile(p);
+  g.aux.halo = HaloGeom{};
+  if (g.tile >= 16) {
+    const int rc = prepare_halo(p, g.tile, g.aux.halo);
+    if (rc != ENCDIFF_OK) return rc;
+  }
   g.user = p;
   g.ws_path = ws_path;
   if (ws_path) {  // per-split fp32 slabs (plain stores); epilogue in the finalize pass
@@ -973,9 +1145,43 @@ hipError_t launch_pair_t(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGe
   return hipGetLastError();
 }
 
+// paired launch whose input gradient runs on a halo tile: dynamic LDS = the larger of the two
+template <int AM1, int BMD1, int BM2, int BN2, int KB1>
+hipError_t launch_pair_halo_t(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
+  using G1 = Gemm<64, 64, AM1, BMD1, 2, KB1>;
+  auto kern = gemm2_kernel<AM1, BMD1, BM2, BN2, A_HALO, B_CONVD, HALO_NS, BK, KB1>;
+  static const hipError_t attr_ok =
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, HALO_LDS_MAX);
+  if (attr_ok != hipSuccess) return attr_ok;
+  size_t lds = halo_lds_bytes(g2.aux.halo, BM2, BN2);
+  if ((size_t)G1::LDS_BYTES > lds) lds = G1::LDS_BYTES;
+  const int gx1 = (g1.p.M + 63) / 64, gy1 = (g1.p.N + 63) / 64;
+  const int gx2 = g2.p.M / BM2, gy2 = (g2.p.N + BN2 - 1) / BN2;
+  const long nb = (long)gx1 * gy1 * g1.p.split_k + (long)gx2 * gy2 + nf;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), lds, s, g1.p, g1.aux, g2.p, g2.aux, gx1, gy1, gx2, gy2, pf, nf);
+  return hipGetLastError();
+}
+
+template <int AM1, int BMD1, int KB1>
+hipError_t launch_pair_halo(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
+  switch (g2.tile) {
+    case 16: return launch_pair_halo_t<AM1, BMD1, 64, 64, KB1>(g1, g2, pf, nf, s);
+    case 17: return launch_pair_halo_t<AM1, BMD1, 128, 64, KB1>(g1, g2, pf, nf, s);
+    case 18: return launch_pair_halo_t<AM1, BMD1, 128, 128, KB1>(g1, g2, pf, nf, s);
+    case 22: return launch_pair_halo_t<AM1, BMD1, 64, 128, KB1>(g1, g2, pf, nf, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 template <int AM1, int BMD1, int AM2, int BMD2>
 hipError_t launch_pair_tiles(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf,
                              hipStream_t s) {
+  if constexpr (AM2 == A_IM2COL && BMD2 == B_CONVD) {
+    if (g2.tile >= 16) {
+      return g1.tile == 7 ? launch_pair_halo<AM1, BMD1, 128>(g1, g2, pf, nf, s)
+                          : launch_pair_halo<AM1, BMD1, BK>(g1, g2, pf, nf, s);
+    }
+  }
   if (g1.tile == 7) {  // weight gradient with 128-deep k stages (64 KB of LDS): dgrad tile 7 or 64x64
     if (g2.tile == 7) return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 2, 128, 128>(g1, g2, pf, nf, s);
     return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 2, 64, 128>(g1, g2, pf, nf, s);

@@ -84,6 +84,30 @@ MAX_SPLIT = int(os.environ.get("ENCDIFF_MAX_SPLIT", "1024"))  # experiment knob:
 FORCE_TILE = 0  # tests: override the planned tile of every GEMM that does not pass one
 
 
+# halo tiles (gemm.hip tiles 16-23): BM x BN, window staged once per workgroup
+HALO_TILES = {16: (64, 64), 17: (128, 64), 18: (128, 128), 19: (256, 32), 20: (128, 32), 21: (256, 64),
+              22: (64, 128), 23: (64, 32)}
+HALO_LDS_MAX = 156 * 1024  # gemm.hip: 160 KiB less the paired kernel's static scratch
+
+
+def halo_fits(tile, batch, h, w, cin, resample):
+    """Host mirror of gemm.hip prepare_halo's geometry checks: the tile's BM pixels are whole
+    rows of one image (or whole images) and window + 3-deep B ring + epilogue fit the LDS."""
+    if tile not in HALO_TILES or cin % 8 or resample not in (0, 2, 3, 4):
+        return False
+    bm, bn = HALO_TILES[tile]
+    hw = h * w
+    if (batch * hw) % bm or bm % w or (hw % bm and bm % hw) or (resample == 2 and (h | w) & 1):
+        return False
+    s = 2 if resample in (3, 4) else 1
+    kt = 4 if resample == 4 else 3
+    rows = min(h, bm // w)
+    ni = bm // hw if bm > hw else 1
+    npix = ni * (s * (rows - 1) + kt) * (s * (w - 1) + kt)
+    chunks = (npix * (cin // 8) + 255) & ~255
+    return max(chunks * 16 + 3 * bn * 64 * 2, bm * (bn + 4) * 4) <= HALO_LDS_MAX
+
+
 def plan_key(M, N, K, a_mode, b_mode, c_mode, resample=0):
     key = f"{a_mode},{b_mode},{c_mode},{M},{N},{K}"
     return key + (f",r{resample}" if resample else "")

@@ -133,6 +133,80 @@ def test_gemm_tiles(O, tile):
     assert rel(nhwc(dx, g), xin.grad) < 1e-2, tile
 
 
+HALO_TWIN = {16: 4, 17: 2, 18: 1, 22: 3}  # halo tile -> the ring tile of the same BM x BN
+
+
+@pytest.mark.parametrize("tile", [16, 17, 18, 19, 20, 21, 22, 23])
+@pytest.mark.parametrize("B,H,cin,cout,mode", [(4, 16, 64, 64, 0), (4, 8, 128, 96, 0), (2, 16, 192, 64, 0),
+                                               (2, 16, 128, 64, 2), (2, 32, 32, 32, 3), (2, 64, 8, 32, 0),
+                                               (3, 16, 32, 128, 4), (2, 32, 24, 32, 0)])
+def test_conv_halo_tiles(O, tile, B, H, cin, cout, mode):
+    """Halo tiles (16-23): the workgroup's whole conv-input window staged once in LDS.  Forward
+    (3x3 pad 1, nearest-up, VQ stride-2, Encoder4 k4 s2) and the 3x3 input gradient vs torch fp32,
+    and bitwise equal to the LDS-ring tile of the same shape (same k order, same MFMA sequence).
+    Shapes the window does not fit (LDS) or whose tile straddles image rows are refused."""
+    import encdiff_amd._lib as L
+    from encdiff_amd.ops import Geom
+    torch.manual_seed(9)
+    g = Geom(B, H, H)
+    k4 = mode == 4
+    src_h = 2 * H if mode in (3, 4) else (H // 2 if mode == 2 else H)
+    gs = Geom(B, src_h, src_h)
+    T = 16 if k4 else 9
+    x = bf(gs.pixels, cin)
+    wf = bf(cout, T * cin, scale=(T * cin) ** -0.5)
+    kh = 4 if k4 else 3
+    wq = wf.float().reshape(cout, kh, kh, cin).permute(0, 3, 1, 2)
+    bias = torch.randn(cout, device=dev)
+    cg = L.ConvGeom(batch=B, h=H, w=H, cin=cin, resample=mode, ld_src=cin)
+
+    def run(t, c_mode=L.OUT_BF16):
+        out = torch.empty(g.pixels, cout, device=dev, dtype=torch.bfloat16 if c_mode == L.OUT_BF16 else torch.float32)
+        O.gemm(g.pixels, cout, T * cin, x, cin, wf, T * cin, out, cout, a_mode=L.OPA_IM2COL, c_mode=c_mode,
+               conv=cg, bias=bias, split_k=1, tile=t)
+        return out
+    if not O.halo_fits(tile, B, H, H, cin, mode):  # the host mirror and the library agree on refusals
+        with pytest.raises(L.HipError):
+            run(tile)
+        return
+    y = run(tile)
+    xin = nhwc(x, gs)
+    if mode == 2:
+        xin = F.interpolate(xin, scale_factor=2, mode="nearest")
+    if mode == 3:
+        ref = F.conv2d(F.pad(xin, (0, 1, 0, 1)), wq, bias, stride=2)
+    elif mode == 4:
+        ref = F.conv2d(xin, wq, bias, stride=2, padding=1)
+    else:
+        ref = F.conv2d(xin, wq, bias, padding=1)
+    assert rel(nhwc(y, g), ref) < 1e-2
+    y32 = run(tile, L.OUT_F32)
+    assert rel(nhwc(y32, g), ref) < 1e-4
+    if tile in HALO_TWIN:
+        assert torch.equal(y32, run(HALO_TWIN[tile], L.OUT_F32))
+    if mode != 0:
+        return
+    # input gradient: dY im2col through the window, flipped weights
+    dy = bf(g.pixels, cout)
+    cgd = L.ConvGeom(batch=B, h=H, w=H, cin=cout, resample=0, ld_src=cout)
+
+    def drun(t):
+        dx = torch.empty(g.pixels, cin, device=dev)
+        O.gemm(g.pixels, cin, 9 * cout, dy, cout, wf, 9 * cin, dx, cin, a_mode=L.OPA_IM2COL,
+               b_mode=L.OPB_CONV_DGRAD, c_mode=L.OUT_F32, conv=cgd, conv_cout=cout, split_k=1, tile=t)
+        return dx
+    if not O.halo_fits(tile, B, H, H, cout, 0):
+        with pytest.raises(L.HipError):
+            drun(tile)
+        return
+    dx = drun(tile)
+    xr = nhwc(x, gs).requires_grad_(True)
+    F.conv2d(xr, wq, None, padding=1).backward(nhwc(dy, g))
+    assert rel(nhwc(dx, g), xr.grad) < 1e-4
+    if tile in HALO_TWIN:
+        assert torch.equal(dx, drun(HALO_TWIN[tile]))
+
+
 def test_linear_strided_views(O):
     """q/k/v slices of a fused [M][3C] projection output are strided views."""
     torch.manual_seed(1)

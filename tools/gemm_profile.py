@@ -139,8 +139,14 @@ def main():
         # LDS for the larger tile, so the deep-ring / deep-k tiles (5-8) cost the weight-gradient
         # blocks occupancy in the step (this standalone timing cannot see it): not candidates
         dgrad = a.b_mode in (L.OPB_ROWN, L.OPB_CONV_DGRAD) and not wgrad
-        for tile in ((4, 7) if wgrad else ((1, 2, 3, 4) if dgrad else (1, 2, 3, 4, 5, 6, 7, 8))):
-            for split in (1, 2, 4, 8, 16, 32, 64, 128, 256):
+        cands = (4, 7) if wgrad else ((1, 2, 3, 4) if dgrad else (1, 2, 3, 4, 5, 6, 7, 8))
+        if a.a_mode == L.OPA_IM2COL and a.b_mode in (L.OPB_ROWK, L.OPB_CONV_DGRAD):
+            # halo tiles (window staged once; split-K 1); paired input gradients: 16, 17, 18, 22
+            halo = (16, 17, 18, 22) if dgrad else tuple(ops.HALO_TILES)
+            cands += tuple(t for t in halo if ops.halo_fits(t, a.conv.batch, a.conv.h, a.conv.w, a.conv.cin,
+                                                            a.conv.resample))
+        for tile in cands:
+            for split in ((1,) if tile >= 16 else (1, 2, 4, 8, 16, 32, 64, 128, 256)):
                 if split > 1 and a.K // split < 64:
                     continue
                 if wgrad and split > 1 and split * a.M * (a.N + 1) > ops.WS_HALF // 2:
