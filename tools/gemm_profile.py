@@ -25,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--pairs", type=int, default=1, help="choose paired wgrad/dgrad tiles by timing the pair")
     ap.add_argument("--write-table", default="", help="path for the measured (tile, split) table, e.g. "
                     "gpurun_out/gemm_tiles.json (copy it to encdiff_amd/gemm_tiles.json)")
     args = ap.parse_args()
@@ -164,6 +165,73 @@ def main():
         rows.append((k, a.M, a.N, a.K, a.split_k, a.tile, cur, f"{best_tile}/{best_split}", best_t))
         print(f"[{len(rows)}/{len(calls)}] {k} {a.M}x{a.N}x{a.K} r{a.conv.resample}: {cur:.1f} -> "
               f"{best_tile}/{best_split} {best_t:.1f} us", flush=True)
+    # ---- paired backward launches: a layer's weight and input gradient share ONE grid whose
+    # workgroups all get the larger tile's LDS, so the dgrad tile (halo tiles: large LDS) and the
+    # wgrad tile (128-deep k: 64 KB) are chosen together, timing the pair as the step runs it
+    if args.pairs:
+        recs = bench.record_gemms(tr)
+        seen_p = set()
+        orig_pair = L.lib.encdiff_gemm_pair
+
+        def copy_args(a, tile, split, ws_off):
+            a2 = L.GemmArgs()
+            C.memmove(C.byref(a2), C.byref(a), C.sizeof(L.GemmArgs))
+            a2.tile, a2.split_k = tile, split
+            slab = split > 1 and a2.c_mode in (L.OUT_BF16, L.OUT_F32, L.OUT_F32_ACCUM)
+            a2.workspace = ws.data_ptr() + 4 * ws_off if slab else None
+            return a2
+
+        def time_pair(w, d):
+            for _ in range(2):
+                if orig_pair(C.byref(w), C.byref(d), stream) != 0:
+                    return float("inf")
+            gs = torch.cuda.Stream()
+            gs.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=gs):
+                st = C.c_void_p(gs.cuda_stream)
+                for _ in range(args.reps):
+                    orig_pair(C.byref(w), C.byref(d), st)
+            g.replay()
+            torch.cuda.synchronize()
+            s, f = ev(), ev()
+            s.record()
+            g.replay()
+            f.record()
+            torch.cuda.synchronize()
+            return s.elapsed_time(f) / args.reps * 1e3
+
+        key_of = lambda a: ops.plan_key(a.M, a.N, a.K, a.a_mode, a.b_mode, a.c_mode, a.conv.resample)
+        for rec in recs:
+            if rec[0] != "pair_ex":
+                continue
+            w, d = rec[1], rec[2]
+            wk, dk = key_of(w), key_of(d)
+            if (wk, dk) in seen_p or wk not in table or dk not in table:
+                continue
+            seen_p.add((wk, dk))
+            w_split = table[wk][1]
+            conv = d.a_mode == L.OPA_IM2COL
+            dc = {(table[dk][0], table[dk][1])} | {(t, s) for t in (1, 2, 3, 4) for s in (1, 2, 4, 8) if d.K // s >= 64}
+            if conv:
+                dc |= {(t, 1) for t in (16, 17, 18, 22)
+                       if ops.halo_fits(t, d.conv.batch, d.conv.h, d.conv.w, d.conv.cin, d.conv.resample)}
+            best = None
+            for wt in (4, 7):
+                wa = copy_args(w, wt, w_split, 0)
+                for dt, ds_ in sorted(dc):
+                    if ds_ > 1 and ds_ * d.M * (d.N + 1) + ops.ws_floats(wa) > ops.WS_FLOATS:
+                        continue
+                    tt = time_pair(wa, copy_args(d, dt, ds_, ops.ws_floats(wa)))
+                    if best is None or tt < best[0]:
+                        best = (tt, wt, dt, ds_)
+            cur = time_pair(copy_args(w, table[wk][0], w_split, 0),
+                            copy_args(d, table[dk][0], table[dk][1], ops.ws_floats(copy_args(w, table[wk][0], w_split, 0))))
+            print(f"pair {wk} | {dk}: table {table[wk][0]}/{table[dk][0]}x{table[dk][1]} {cur:.1f} us -> "
+                  f"{best[1]}/{best[2]}x{best[3]} {best[0]:.1f} us", flush=True)
+            if best[0] < cur:
+                table[wk] = [best[1], w_split, table[wk][2]]
+                table[dk] = [best[2], best[3], table[dk][2]]
     for cat_name in sorted(tot_cur):
         sel = sorted([r for r in rows if r[0] == cat_name], key=lambda r: -r[6])[:8]
         for r in sel:
