@@ -720,7 +720,7 @@ __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const in
 // gradient (problem 2) share the machine instead of running back to back, each too small
 // to fill 256 CUs; the previous layer's weight-gradient finalize rides along, so neither
 // needs a launch of its own.
-template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2, int KB2, int KB1>
+template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2, int KB2, int KB1, int NS1 = 2>
 __global__ __launch_bounds__(256) void gemm2_kernel(const EncdiffGemmArgs p1, const GemmAux aux1,
                                                     const EncdiffGemmArgs p2, const GemmAux aux2, int gx1,
                                                     int gy1, int gx2, int gy2, const EncdiffGemmArgs pf, int nf) {
@@ -730,7 +730,7 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const EncdiffGemmArgs p1, co
   int i = blockIdx.x;
   if (i < n1) {
     const int bx = i % gx1, t = i / gx1;
-    gemm_tile<64, 64, AM1, BMD1, 2, KB1>(p1, aux1, bx, t % gy1, t / gy1, smem);
+    gemm_tile<64, 64, AM1, BMD1, NS1, KB1>(p1, aux1, bx, t % gy1, t / gy1, smem);
   } else if (i < n1 + n2) {
     i -= n1;
     const int bx = i % gx2, t = i / gx2;
@@ -1129,18 +1129,18 @@ int launch_one(const GemmPlan& g, hipStream_t s) {
   return ENCDIFF_OK;
 }
 
-template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2 = 2, int KB2 = BK, int KB1 = BK>
+template <int AM1, int BMD1, int BM2, int BN2, int AM2, int BMD2, int NS2 = 2, int KB2 = BK, int KB1 = BK, int NS1 = 2>
 hipError_t launch_pair_t(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
-  using G1 = Gemm<64, 64, AM1, BMD1, 2, KB1>;
+  using G1 = Gemm<64, 64, AM1, BMD1, NS1, KB1>;
   using G2 = Gemm<BM2, BN2, AM2, BMD2, NS2, KB2>;
   constexpr size_t lds = G1::LDS_BYTES > G2::LDS_BYTES ? G1::LDS_BYTES : G2::LDS_BYTES;
   static const hipError_t attr_ok = hipFuncSetAttribute(
-      (const void*)gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2, KB2, KB1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (const void*)gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2, KB2, KB1, NS1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr_ok != hipSuccess) return attr_ok;
   const int gx1 = (g1.p.M + 63) / 64, gy1 = (g1.p.N + 63) / 64;
   const int gx2 = (g2.p.M + BM2 - 1) / BM2, gy2 = (g2.p.N + BN2 - 1) / BN2;
   const long nb = (long)gx1 * gy1 * g1.p.split_k + (long)gx2 * gy2 * g2.p.split_k + nf;
-  hipLaunchKernelGGL((gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2, KB2, KB1>), dim3((unsigned)nb), dim3(256), lds, s, g1.p,
+  hipLaunchKernelGGL((gemm2_kernel<AM1, BMD1, BM2, BN2, AM2, BMD2, NS2, KB2, KB1, NS1>), dim3((unsigned)nb), dim3(256), lds, s, g1.p,
                      g1.aux, g2.p, g2.aux, gx1, gy1, gx2, gy2, pf, nf);
   return hipGetLastError();
 }
@@ -1181,6 +1181,9 @@ hipError_t launch_pair_tiles(const GemmPlan& g1, const GemmPlan& g2, const Encdi
       return g1.tile == 7 ? launch_pair_halo<AM1, BMD1, 128>(g1, g2, pf, nf, s)
                           : launch_pair_halo<AM1, BMD1, BK>(g1, g2, pf, nf, s);
     }
+  }
+  if (g1.tile == 5) {  // weight gradient with a 4-deep ring (64 KB of LDS): every k-tile of a short split in flight
+    return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 2, 64, 64, 4>(g1, g2, pf, nf, s);
   }
   if (g1.tile == 7) {  // weight gradient with 128-deep k stages (64 KB of LDS): dgrad tile 7 or 64x64
     if (g2.tile == 7) return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 2, 128, 128>(g1, g2, pf, nf, s);
@@ -1234,7 +1237,7 @@ extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffG
   // both split-K problems need disjoint slabs
   if (g1.ws_path && g2.ws_path && g1.p.workspace == g2.p.workspace) return ENCDIFF_ERR_ARG;
   const bool defer1 = defer && g1.ws_path;
-  if ((!lin && !conv) || (g1.tile != 4 && g1.tile != 7)) {  // pairs the fused kernel does not cover: back to back
+  if ((!lin && !conv) || (g1.tile != 4 && g1.tile != 5 && g1.tile != 7)) {  // pairs the fused kernel does not cover
     if (have_prev && (e = launch_finalize(gp.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
     GemmPlan w = g1;
     w.ws_path = g1.ws_path && !defer1;

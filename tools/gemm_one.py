@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("kind", choices=["conv", "lin", "wgrad"])
+    ap.add_argument("kind", choices=["conv", "lin", "wgrad", "cwgrad"])
     ap.add_argument("--M", type=int, default=32768)
     ap.add_argument("--N", type=int, default=64)
     ap.add_argument("--K", type=int, default=64)
@@ -56,6 +56,18 @@ def main():
 
         def run():
             ops.gemm(a.M, a.N, a.K, x, a.K, w, a.K, y, a.N, **kw)
+    elif a.kind == "cwgrad":  # conv 3x3 weight gradient: M = cout, N = 9 * cin, K = pixels
+        B = a.K // (a.h * a.h)
+        g = Geom(B, a.h, a.h)
+        dy = torch.randn(g.pixels, a.M, device=dev).to(bf)
+        x = torch.randn(g.pixels, a.cin, device=dev).to(bf)
+        dw = torch.zeros(a.M, 9 * a.cin, device=dev)
+        flops = 2.0 * a.M * 9 * a.cin * g.pixels
+
+        def run():
+            ops.gemm(a.M, 9 * a.cin, g.pixels, dy, a.M, x, a.cin, dw, 9 * a.cin, a_mode=L.OPA_ROWM,
+                     b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32_ACCUM, conv=ops._conv_geom(g, a.cin, 0, x), **kw)
+            ops.flush()
     else:
         dy = torch.randn(a.K, a.M, device=dev).to(bf)
         x = torch.randn(a.K, a.N, device=dev).to(bf)
