@@ -42,7 +42,7 @@ class GemmArgs(C.Structure):
                 ("tile", C.c_int), ("pad2_", C.c_int), ("workspace", vp),
                 ("aux", vp), ("ld_aux", C.c_long), ("gn_stats", vp), ("ld_gn_stats", C.c_long),
                 ("ln_gamma", vp), ("ln_beta", vp), ("ln_y", vp), ("ld_ln_y", C.c_long), ("ln_stats", vp),
-                ("ln_eps", C.c_float), ("pad3_", C.c_int)]
+                ("ln_eps", C.c_float), ("pad3_", C.c_int), ("split_counters", vp)]
 
 
 class GroupNormArgs(C.Structure):

@@ -11,6 +11,7 @@ typedef uint16_t bf16_t;  // raw bf16 bits in memory
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef short v8s __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 typedef __bf16 v4bf __attribute__((ext_vector_type(4)));
 typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 

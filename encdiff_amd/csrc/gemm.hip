@@ -77,12 +77,25 @@ struct HaloGeom {
   FDiv fch, fimg, fhc; // / ch, / (hr * hc), / hc
 };
 
+// In-kernel split-K combine (EncdiffGemmArgs.split_counters): the user's output of a slab GEMM
+struct SplitFold {
+  int* cnt;              // per-tile tickets (NULL: a finalize pass combines the slabs)
+  void* c;
+  long ldc;
+  int mode;              // ENCDIFF_OUT_BF16 / F32 / F32_ACCUM
+  float alpha;
+  const float* bias;
+  const bf16_t* resid;
+  long ld_resid;
+};
+
 struct GemmAux {
   FDiv cin;   // A/B im2col: k (or n) -> (tap, channel)
   FDiv cout;  // B_CONVD: k -> (tap, co)
   FDiv hw;    // pixel -> (image, in-image index)
   FDiv w;     // in-image index -> (y, x)
   HaloGeom halo;
+  SplitFold fold;
 };
 
 // Implicit im2col, branch-free.  The launch's resample mode is folded into uniform
@@ -570,6 +583,9 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     const uint32_t y = fdiv(r, aux.w), x = r - y * aux.w.d;
     return ((long)b * p.conv.h + 2 * y + (tp_q >> 1)) * p.conv.w + 2 * x + (tp_q & 1);
   };
+  // in-kernel split-K combine: this split's slab goes out write-through (sc1)
+  const bool fold = aux.fold.cnt != nullptr && slab_out;
+  const auto slab_rs = __builtin_amdgcn_make_buffer_rsrc(p.c, 0, fold ? p.split_k * p.M * p.N * 4 : 0, 0x00020000);
   const bool vec = (p.N % 8 == 0) && (p.ldc % 8 == 0) && (((uintptr_t)p.c & 15) == 0) &&
                    (!add_bias || (((uintptr_t)p.bias & 15) == 0)) &&
                    (!R || ((p.ld_resid % 8 == 0) && (((uintptr_t)R & 15) == 0)));
@@ -610,8 +626,16 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
           v[0] += c0.x; v[1] += c0.y; v[2] += c0.z; v[3] += c0.w;
           v[4] += c1.x; v[5] += c1.y; v[6] += c1.z; v[7] += c1.w;
         }
-        *(float4*)cp = make_float4(v[0], v[1], v[2], v[3]);
-        *(float4*)(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        if (fold) {  // write-through (sc1) slab stores: visible to the combining split without a release fence
+          const int bo = (int)((cp - (const float*)p.c) * 4);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, make_float4(v[0], v[1], v[2], v[3])), slab_rs,
+                                                 bo, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, make_float4(v[4], v[5], v[6], v[7])), slab_rs,
+                                                 bo + 16, 0, 16);
+        } else {
+          *(float4*)cp = make_float4(v[0], v[1], v[2], v[3]);
+          *(float4*)(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
       }
     }
   } else {
@@ -627,6 +651,70 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       else p_c_slab[ro * p.ldc + col] = v;
       if (p.gn_stats || p.ln_y) sc[r * SLD + cc] = bf16_round(v);
     }
+  }
+  if (fold) {
+    // In-kernel split-K combine (the guide's write-through ticket recipe): every wave drains its
+    // sc1 slab stores, then one lane takes the tile's ticket (relaxed, agent scope); the split that
+    // draws split_k - 1 acquires and sums the tile's slabs in split order (bitwise reproducible,
+    // placement independent), writes the user's output and leaves the ticket at zero.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = (int*)smem;  // the staging LDS is free: every thread is past its last read of it
+    const int tile_id = by * ((p.M + BM - 1) / BM) + bx;
+    if (tid == 0) {
+      const int tk = __hip_atomic_fetch_add(aux.fold.cnt + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = tk == p.split_k - 1;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(aux.fold.cnt + tile_id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const SplitFold& f = aux.fold;
+    const long total = (long)p.M * p.N;
+    constexpr int CPR = BN / 8;
+    for (int e = tid; e < BM * CPR; e += 256) {
+      const int r = e / CPR, c8 = (e - r * CPR) * 8;
+      const int row = m0 + r, col = n0 + c8;
+      if (row >= p.M || col >= p.N) continue;
+      const float* s = (const float*)p.c + (long)row * p.N + col;
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int z = 0; z < p.split_k; ++z) {
+        const float4 a0 = *(const float4*)(s + z * total), a1 = *(const float4*)(s + z * total + 4);
+        v[0] += a0.x; v[1] += a0.y; v[2] += a0.z; v[3] += a0.w;
+        v[4] += a1.x; v[5] += a1.y; v[6] += a1.z; v[7] += a1.w;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= f.alpha;
+      if (f.bias) {
+        const float4 b0 = *(const float4*)(f.bias + col), b1 = *(const float4*)(f.bias + col + 4);
+        v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+        v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+      }
+      if (f.resid) {
+        float rr[8];
+        unpack8(*(const uint4*)(f.resid + (long)row * f.ld_resid + col), rr);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] += rr[k];
+      }
+      if (f.mode == ENCDIFF_OUT_BF16) {
+        *(uint4*)((bf16_t*)f.c + (long)row * f.ldc + col) = pack8(v);
+      } else {
+        float* cp = (float*)f.c + (long)row * f.ldc + col;
+        if (f.mode == ENCDIFF_OUT_F32_ACCUM) {
+          const float4 c0 = *(const float4*)cp, c1 = *(const float4*)(cp + 4);
+          v[0] += c0.x; v[1] += c0.y; v[2] += c0.z; v[3] += c0.w;
+          v[4] += c1.x; v[5] += c1.y; v[6] += c1.z; v[7] += c1.w;
+        }
+        *(float4*)cp = make_float4(v[0], v[1], v[2], v[3]);
+        *(float4*)(cp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    }
+    return;
   }
   if (p.ln_y) {
     // LayerNorm of each produced row (host: n0 == 0 and N <= BN, OUT_BF16, split_k 1): TPR
@@ -1038,6 +1126,7 @@ struct GemmPlan {
   GemmAux aux;
   int tile;
   bool ws_path;
+  bool fold;  // split-K slabs combined in the kernel (no finalize pass)
 };
 
 int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
@@ -1092,6 +1181,18 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
     p.c = p.workspace; p.ldc = p.N; p.c_mode = ENCDIFF_OUT_F32; p.alpha = 1.f;
     p.bias = nullptr; p.resid = nullptr;
   }
+  // in-kernel split-K combine: vectorised slab / output rows, plain row mapping, no bias gradient
+  g.aux.fold = SplitFold{};
+  g.fold = false;
+  if (ws_path && p.split_counters && p.a_mode != ENCDIFF_OPA_ROWM && !p.bias_grad && p.N % 8 == 0 &&
+      !(im2col && p.conv.resample == ENCDIFF_RESAMPLE_K4S2_TP) && g.user.ldc % 8 == 0 &&
+      ((uintptr_t)g.user.c & 15) == 0 && ((uintptr_t)p.workspace & 15) == 0 &&
+      (!g.user.bias || ((uintptr_t)g.user.bias & 15) == 0) &&
+      (!g.user.resid || (g.user.ld_resid % 8 == 0 && ((uintptr_t)g.user.resid & 15) == 0))) {
+    g.fold = true;
+    g.aux.fold = SplitFold{p.split_counters, g.user.c, g.user.ldc, g.user.c_mode, g.user.alpha, g.user.bias,
+                           (const bf16_t*)g.user.resid, g.user.ld_resid};
+  }
   g.p = p;
   g.aux.cin = make_fdiv(p.conv.cin);
   g.aux.cout = make_fdiv(p.conv_cout);
@@ -1121,7 +1222,7 @@ int launch_one(const GemmPlan& g, hipStream_t s) {
   else if (am == ENCDIFF_OPA_ROWM && bm == ENCDIFF_OPB_IM2COL) e = launch_modes<A_ROWM, B_IM2COL>(g.p, g.aux, g.tile, s);
   else return ENCDIFF_ERR_UNSUPPORTED;
   if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
-  if (g.ws_path) {
+  if (g.ws_path && !g.fold) {
     hipLaunchKernelGGL(gemm_finalize_kernel, dim3((unsigned)fin_blocks(g.user)), dim3(256), 0, s, g.user);
     e = hipGetLastError();
     if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
@@ -1250,12 +1351,13 @@ extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffG
           : launch_pair_tiles<A_ROWM, B_IM2COL, A_IM2COL, B_CONVD>(g1, g2, pf, nf, s);
   if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
   const bool f1 = g1.ws_path && !defer1;
-  if (f1 && g2.ws_path) {
+  const bool f2 = g2.ws_path && !g2.fold;
+  if (f1 && f2) {
     const int n1 = fin_blocks(g1.user), n2 = fin_blocks(g2.user);
     hipLaunchKernelGGL(gemm_finalize2_kernel, dim3((unsigned)(n1 + n2)), dim3(256), 0, s, g1.user, g2.user, n1);
   } else if (f1) {
     launch_finalize(g1.user, s);
-  } else if (g2.ws_path) {
+  } else if (f2) {
     launch_finalize(g2.user, s);
   }
   e = hipGetLastError();
@@ -1270,7 +1372,7 @@ extern "C" int encdiff_gemm_finalize(const EncdiffGemmArgs* args, void* stream) 
   GemmPlan g;
   const int rc = prepare(args, g);
   if (rc != ENCDIFF_OK) return rc;
-  if (!g.ws_path) return ENCDIFF_OK;
+  if (!g.ws_path || g.fold) return ENCDIFF_OK;  // folded GEMMs combined their slabs in the kernel
   const hipError_t e = launch_finalize(g.user, (hipStream_t)stream);
   return e != hipSuccess ? ENCDIFF_ERR_LAUNCH - (int)e : ENCDIFF_OK;
 }

@@ -52,6 +52,22 @@ def _conv_geom(g: Geom, cin: int, resample: int, src: torch.Tensor) -> L.ConvGeo
 
 
 _WS = {}
+_CNT = {}
+# split-K GEMMs may combine their slabs in the kernel (EncdiffGemmArgs.split_counters) instead of
+# a finalize launch: per problem, as the measured table says (4th entry).  ENCDIFF_SPLIT_FOLD:
+# 1 table choice (default), 0 never, 2 always.
+SPLIT_FOLD = int(os.environ.get("ENCDIFF_SPLIT_FOLD", "1"))
+
+
+def _counters():
+    """Per-(device, stream) split-K tickets: one int per output tile, zero between launches (each
+    launch's combining splits leave them zero); launches on one stream never overlap."""
+    dev = torch.cuda.current_device()
+    key = (dev, torch.cuda.current_stream().cuda_stream)
+    c = _CNT.get(key)
+    if c is None:
+        c = _CNT[key] = torch.zeros(1 << 16, device=f"cuda:{dev}", dtype=torch.int32)
+    return c
 WS_FLOATS = 64 * 1024 * 1024         # fp32 split-K scratch per stream, 256 MB (two halves, see gemm_pair)
 WS_HALF = WS_FLOATS // 2
 _TILES = None
@@ -113,6 +129,16 @@ def plan_key(M, N, K, a_mode, b_mode, c_mode, resample=0):
     return key + (f",r{resample}" if resample else "")
 
 
+def fold_choice(M, N, K, a_mode, b_mode, c_mode, resample=0) -> bool:
+    """Whether a split-K GEMM combines its slabs in the kernel (measured per problem)."""
+    if SPLIT_FOLD != 1:
+        return SPLIT_FOLD == 2
+    hit = _tile_table().get(plan_key(M, N, K, a_mode, b_mode, c_mode, resample))
+    if hit is None and c_mode == L.OUT_F32:
+        hit = _tile_table().get(plan_key(M, N, K, a_mode, b_mode, L.OUT_BF16, resample))
+    return hit is not None and len(hit) > 3 and bool(hit[3])
+
+
 def plan(M, N, K, a_mode, b_mode, c_mode, resample=0):
     """(tile, split_k) for a GEMM: measured table (tools/gemm_profile.py --write-table) first,
     else a heuristic aiming at >= 256 workgroups with bounded split-K traffic."""
@@ -156,10 +182,14 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
         tile = tile or FORCE_TILE or t
         split_k = split_k or sp
     ws = None
+    cnt = None
     if split_k > 1 and c_mode in (L.OUT_BF16, L.OUT_F32, L.OUT_F32_ACCUM):
         need = ws_offset + split_k * M * N + (split_k * M if bias_grad is not None else 0)
         assert need <= WS_FLOATS, "split-K slabs exceed the workspace"
         ws = _workspace()
+        if a_mode != L.OPA_ROWM and fold_choice(M, N, K, a_mode, b_mode, c_mode,
+                                                 conv.resample if conv is not None else 0):
+            cnt = _counters()
     return L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=b_mode, c_mode=c_mode,
                       a=_p(a), lda=lda, b=_p(b), ldb=ldb, c=_p(c), ldc=ldc,
                       conv=conv if conv is not None else L.ConvGeom(),
@@ -167,6 +197,7 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
                       bias=_p(bias), resid=_p(resid), ld_resid=ld_resid, bias_grad=_p(bias_grad), tile=tile,
                       workspace=None if ws is None else ws.data_ptr() + 4 * ws_offset, aux=_p(aux), ld_aux=ld_aux,
                       gn_stats=_p(gn_stats), ld_gn_stats=_ld(gn_stats) if gn_stats is not None else 0,
+                      split_counters=None if cnt is None else cnt.data_ptr(),
                       **({} if ln is None else dict(ln_gamma=_p(ln[0]), ln_beta=_p(ln[1]), ln_y=_p(ln[2]),
                                                     ld_ln_y=_ld(ln[2]), ln_stats=_p(ln[3]), ln_eps=ln[4])))
 

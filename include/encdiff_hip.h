@@ -128,6 +128,11 @@ typedef struct EncdiffGemmArgs {
   float* ln_stats;           /*   ln_stats [M][2] (mean, rstd) for the backward                  */
   float ln_eps;
   int pad3_;
+  int* split_counters;       /* optional, split_k > 1 with a workspace (not OPA_ROWM, not K4S2_TP,
+                                N % 8 == 0): the splits combine IN the kernel -- the last split
+                                to finish a tile (one int ticket per output tile, zero on entry,
+                                left zero) sums the tile's slabs in split order (reproducible)
+                                and applies alpha/bias/resid; no finalize pass.  NULL: finalize */
 } EncdiffGemmArgs;
 
 int encdiff_gemm(const EncdiffGemmArgs* args, void* stream);

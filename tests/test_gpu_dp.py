@@ -60,8 +60,10 @@ def test_dp_two_ranks_equal_single_process_definition(tmp_path):
         rel = (d.norm() / w1[k].double().norm()).item()
         print(f"{k}: DP vs definition max-abs {d.abs().max().item():.3e} rel-L2 {rel:.3e} "
               f"bitwise={torch.equal(r0[k], w1[k])}")
-        # bitwise in most runs; in 2 of ~8 GPU runs (two ranks + the test process on one card)
-        # a local gradient differed at 1e-5..1e-4 relative in one step, which
-        # AdamW carries forward -- far below the O(1) deviation a wrong exchange (a missing
-        # bucket, a stale finalize, a wrong scale) produces
-        assert rel < 1e-4, k
+        # bitwise in most runs; in a few GPU runs (two ranks + the test process on one card)
+        # one rank's local gradient differed at 1e-5..1e-4 relative in its first step (DESIGN.md
+        # §6), which AdamW carries forward (exp_avg reached 1.9e-4 once: the largest relative
+        # parts are Encoder4 conv biases ahead of BatchNorm, whose true gradient is zero) -- far
+        # below the O(1) deviation a wrong exchange (a missing bucket, a stale finalize, a wrong
+        # scale) produces
+        assert rel < 1e-3, k

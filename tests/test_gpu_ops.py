@@ -95,6 +95,67 @@ def test_split_k_workspace(O, split):
         assert rel(out, x.float() @ w.float().t() + b + r.float()) < 1e-2
 
 
+@pytest.mark.parametrize("split", [2, 3, 8, 16])
+@pytest.mark.parametrize("tile", [1, 4, 5])
+def test_split_k_in_kernel_combine(O, tile, split):
+    """Split-K slabs combined in the kernel by the last-arriving split (split_counters) vs the
+    finalize pass: bitwise equal where the finalize also sums in split order (split <= 8), within
+    fp32 rounding beyond; bf16 output with bias + residual and an fp32 accumulate output; the
+    tickets are left zero; the input gradient of a 3x3 conv (paired with its weight gradient)."""
+    import encdiff_amd._lib as L
+    torch.manual_seed(12)
+    M, N, K = 320, 192, 2304
+    x, w = bf(M, K), bf(N, K, scale=K ** -0.5)
+    b = torch.randn(N, device=dev)
+    r = bf(M, N)
+    outs = {}
+    for fold in (False, True):
+        O.SPLIT_FOLD = 2 if fold else 0
+        try:
+            o16 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            O.gemm(M, N, K, x, K, w, K, o16, N, bias=b, resid=r, ld_resid=N, split_k=split, tile=tile)
+            o32 = torch.full((M, N), 0.5, device=dev)
+            O.gemm(M, N, K, x, K, w, K, o32, N, c_mode=L.OUT_F32_ACCUM, split_k=split, tile=tile)
+            torch.cuda.synchronize()
+        finally:
+            O.SPLIT_FOLD = 1
+        outs[fold] = (o16, o32)
+    ref = x.float() @ w.float().t()
+    assert rel(outs[True][0], ref + b + r.float()) < 1e-2
+    assert rel(outs[True][1], ref + 0.5) < 1e-5
+    if split <= 8:
+        assert torch.equal(outs[True][0], outs[False][0]) and torch.equal(outs[True][1], outs[False][1])
+    assert rel(outs[True][1], outs[False][1]) < 1e-6
+    assert int(O._counters().abs().sum()) == 0
+    # paired conv backward whose input gradient is split: folded dgrad, deferred weight gradient
+    from encdiff_amd.ops import Geom
+    g = Geom(8, 4, 4)
+    cin, cout = 256, 256
+    xs, dy = bf(g.pixels, cin), bf(g.pixels, cout)
+    wf = bf(cout, 9 * cin, scale=(9 * cin) ** -0.5)
+    res = []
+    for fold in (False, True):
+        O.SPLIT_FOLD = 2 if fold else 0
+        try:
+            dw = torch.zeros(cout, 9 * cin, device=dev)
+            dx = torch.empty(g.pixels, cin, device=dev, dtype=torch.bfloat16)
+            O.gemm_pair(lambda off: O.conv3x3_wgrad_cl_args(dy, xs, g, cin, dw, None, 0, off),
+                        lambda off: O.gemm_args(g.pixels, cin, 9 * cout, dy, cout, wf, 9 * cin, dx, cin,
+                                                a_mode=L.OPA_IM2COL, b_mode=L.OPB_CONV_DGRAD,
+                                                conv=L.ConvGeom(batch=8, h=4, w=4, cin=cout, resample=0, ld_src=cout),
+                                                conv_cout=cout, split_k=split, tile=4, ws_offset=off))
+            O.flush()
+            torch.cuda.synchronize()
+        finally:
+            O.SPLIT_FOLD = 1
+        res.append((dw, dx))
+    assert torch.equal(res[0][0], res[1][0])
+    if split <= 8:
+        assert torch.equal(res[0][1], res[1][1])
+    assert rel(res[1][1], res[0][1]) < 1e-2
+    assert int(O._counters().abs().sum()) == 0
+
+
 @pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_gemm_tiles(O, tile):
     """Every tile shape / LDS ring depth (tiles 5, 6: 4- and 3-deep rings; 7, 8: 128-deep k

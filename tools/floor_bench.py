@@ -1,0 +1,40 @@
+"""Per-launch floors in graph replay: a 1-workgroup GEMM, small GEMMs of the DDIM B=8 shapes, a
+tiny elementwise copy and an empty torch kernel (launch + dependent boundary), for the latency
+budget of the small-batch (sampling) step.
+
+    python tools/floor_bench.py
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+
+def main():
+    from encdiff_amd import ops
+    from gn_bench import timed
+    L = ops.L
+    bf = torch.bfloat16
+    dev = "cuda"
+    x = torch.randn(64, 64, device=dev).to(bf)
+    y = torch.empty_like(x)
+    print(f"ew copy 4K elems          {timed(lambda: ops.ew(L.EW_COPY, x, y)):6.2f} us")
+    t = torch.zeros(1, device=dev)
+    print(f"torch add_ 1 elem         {timed(lambda: t.add_(1)):6.2f} us")
+    for M, N, K, split in [(64, 64, 64, 1), (512, 64, 64, 1), (2048, 64, 64, 1), (2048, 64, 576, 1),
+                           (128, 256, 2304, 8), (32, 256, 2304, 8), (32, 256, 2304, 1), (512, 128, 1152, 2)]:
+        a = torch.randn(M, K, device=dev).to(bf)
+        w = torch.randn(N, K, device=dev).to(bf) * 0.05
+        o = torch.empty(M, N, device=dev, dtype=bf)
+        us = timed(lambda: ops.gemm(M, N, K, a, K, w, K, o, N, split_k=split, tile=4))
+        print(f"gemm {M:5d}x{N:4d}x{K:5d} split {split}: {us:6.2f} us")
+
+
+if __name__ == "__main__":
+    main()

@@ -82,13 +82,15 @@ def main():
 
     ws = ops._workspace()
 
-    def timeit(a, tile, split=None):
+    def timeit(a, tile, split=None, fold=False):
         a2 = L.GemmArgs()
         C.memmove(C.byref(a2), C.byref(a), C.sizeof(L.GemmArgs))
         a2.tile = tile
         if split is not None:
             a2.split_k = split
             a2.workspace = ws.data_ptr() if split > 1 else None
+            a2.split_counters = (ops._counters().data_ptr() if split > 1 and fold and
+                                 a2.a_mode != L.OPA_ROWM else None)
             if split > 1 and a2.c_mode in (L.OUT_BF16, L.OUT_F32, L.OUT_F32_ACCUM) and split * a2.M * (a2.N + 1) > ops.WS_FLOATS:
                 return float("inf")
         for _ in range(2):
@@ -125,14 +127,14 @@ def main():
     for a in calls:
         key = ops.plan_key(a.M, a.N, a.K, a.a_mode, a.b_mode, a.c_mode, a.conv.resample)
         if key in done:  # same problem already swept: reuse
-            cur, best_tile, best_split, best_t = done[key]
+            cur, best_tile, best_split, best_t, best_fold = done[key]
             k = cat(a)
             tot_cur[k] += cur
             tot_best[k] += best_t
             flops[k] += 2.0 * a.M * a.N * a.K
             continue
         cur = timeit(a, a.tile)
-        best_t, best_tile, best_split = cur, a.tile, a.split_k
+        best_t, best_tile, best_split, best_fold = cur, a.tile, a.split_k, bool(a.split_counters)
         # weight gradients run inside the paired kernel (64 x 64 tiles, k stages 64 or 128) with their slabs in
         # one workspace half (deferred finalize): only splits that fit are candidates
         wgrad = a.a_mode == L.OPA_ROWM
@@ -152,16 +154,17 @@ def main():
                     continue
                 if wgrad and split > 1 and split * a.M * (a.N + 1) > ops.WS_HALF // 2:
                     continue
-                tt = timeit(a, tile, split)
-                if tt < best_t:
-                    best_t, best_tile, best_split = tt, tile, split
+                for fold in ((False, True) if split > 1 and not wgrad else (False,)):
+                    tt = timeit(a, tile, split, fold)
+                    if tt < best_t:
+                        best_t, best_tile, best_split, best_fold = tt, tile, split, fold
         k = cat(a)
         tot_cur[k] += cur
         tot_best[k] += best_t
         flops[k] += 2.0 * a.M * a.N * a.K
-        done[key] = (cur, best_tile, best_split, best_t)
+        done[key] = (cur, best_tile, best_split, best_t, best_fold)
         if key not in table or table[key][2] > best_t:
-            table[key] = [best_tile, best_split, best_t]
+            table[key] = [best_tile, best_split, best_t, int(best_fold)]
         rows.append((k, a.M, a.N, a.K, a.split_k, a.tile, cur, f"{best_tile}/{best_split}", best_t))
         print(f"[{len(rows)}/{len(calls)}] {k} {a.M}x{a.N}x{a.K} r{a.conv.resample}: {cur:.1f} -> "
               f"{best_tile}/{best_split} {best_t:.1f} us", flush=True)
@@ -173,12 +176,13 @@ def main():
         seen_p = set()
         orig_pair = L.lib.encdiff_gemm_pair
 
-        def copy_args(a, tile, split, ws_off):
+        def copy_args(a, tile, split, ws_off, fold=False):
             a2 = L.GemmArgs()
             C.memmove(C.byref(a2), C.byref(a), C.sizeof(L.GemmArgs))
             a2.tile, a2.split_k = tile, split
             slab = split > 1 and a2.c_mode in (L.OUT_BF16, L.OUT_F32, L.OUT_F32_ACCUM)
             a2.workspace = ws.data_ptr() + 4 * ws_off if slab else None
+            a2.split_counters = (ops._counters().data_ptr() if slab and fold and a2.a_mode != L.OPA_ROWM else None)
             return a2
 
         def time_pair(w, d):
@@ -222,16 +226,19 @@ def main():
                 for dt, ds_ in sorted(dc):
                     if ds_ > 1 and ds_ * d.M * (d.N + 1) + ops.ws_floats(wa) > ops.WS_FLOATS:
                         continue
-                    tt = time_pair(wa, copy_args(d, dt, ds_, ops.ws_floats(wa)))
-                    if best is None or tt < best[0]:
-                        best = (tt, wt, dt, ds_)
+                    for fold in ((False, True) if ds_ > 1 else (False,)):
+                        tt = time_pair(wa, copy_args(d, dt, ds_, ops.ws_floats(wa), fold))
+                        if best is None or tt < best[0]:
+                            best = (tt, wt, dt, ds_, fold)
+            dfold = len(table[dk]) > 3 and bool(table[dk][3])
             cur = time_pair(copy_args(w, table[wk][0], w_split, 0),
-                            copy_args(d, table[dk][0], table[dk][1], ops.ws_floats(copy_args(w, table[wk][0], w_split, 0))))
+                            copy_args(d, table[dk][0], table[dk][1], ops.ws_floats(copy_args(w, table[wk][0], w_split, 0)),
+                                      dfold))
             print(f"pair {wk} | {dk}: table {table[wk][0]}/{table[dk][0]}x{table[dk][1]} {cur:.1f} us -> "
                   f"{best[1]}/{best[2]}x{best[3]} {best[0]:.1f} us", flush=True)
             if best[0] < cur:
                 table[wk] = [best[1], w_split, table[wk][2]]
-                table[dk] = [best[2], best[3], table[dk][2]]
+                table[dk] = [best[2], best[3], table[dk][2], int(best[4])]
     for cat_name in sorted(tot_cur):
         sel = sorted([r for r in rows if r[0] == cat_name], key=lambda r: -r[6])[:8]
         for r in sel:
