@@ -25,14 +25,21 @@ constexpr int GN_TILE_FWD = 6144;  // forward: dynamic LDS tile up to 96 KB (the
 // statistics are two-pass (mean, then centred sum of squares).  Loops stay rolled (4-way
 // unrolled) so the kernels are a few hundred instructions: a cold instruction cache is
 // otherwise the dominant latency of these small launches.
+// Workgroup -> (image, slice) index, XCD-aware: workgroup i runs on XCD i % 8, and the slices of
+// one image share every 128-B line of its rows (a slice is a channel range), so consecutive
+// slice indices go to consecutive workgroups OF ONE XCD -- each line is fetched into one L2.
+// Bijective when the grid is a multiple of 8 (else identity).
+ED_DEV int gn_xcd_index(int i, int n) { return (n & 7) ? i : (i & 7) * (n >> 3) + (i >> 3); }
+
 struct GnSlice {
   int S, b, c0, cs, nvc, np, tv, tp, cpg, gs, g0, cb;
   bool active, tiled;
   ED_DEV GnSlice(const EncdiffGroupNormArgs& p, int cs_, int tile_cap = GN_TILE) {
     cs = cs_;
     S = p.c / cs;
-    b = blockIdx.x / S;
-    c0 = (blockIdx.x - b * S) * cs;
+    const int bid = gn_xcd_index(blockIdx.x, gridDim.x);
+    b = bid / S;
+    c0 = (bid - b * S) * cs;
     nvc = cs >> 3;
     np = GN_THREADS / nvc;
     tv = threadIdx.x % nvc;
@@ -405,10 +412,23 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[k][i] = 0.f;
   if (L.active) {
-#pragma unroll 2
-    for (int px = L.tp; px < HW; px += L.np) {
-      const uint4 ux = *(const uint4*)(X + (long)px * p.ldx);
-      const uint4 ud = *(const uint4*)(DY + (long)px * p.lddy);
+    constexpr int U1 = 4;  // rows per batch: every load of a batch issued before the first use
+    for (int px0 = L.tp; px0 < HW; px0 += U1 * L.np) {
+    uint4 bx[U1], bd[U1];
+#pragma unroll
+    for (int u = 0; u < U1; ++u) {
+      const int px = px0 + u * L.np;
+      bx[u] = bd[u] = (uint4){0u, 0u, 0u, 0u};
+      if (px < HW) {
+        bx[u] = *(const uint4*)(X + (long)px * p.ldx);
+        bd[u] = *(const uint4*)(DY + (long)px * p.lddy);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U1; ++u) {
+      const int px = px0 + u * L.np;
+      if (px >= HW) break;
+      const uint4 ux = bx[u], ud = bd[u];
       if (L.tiled) { tx[px * L.nvc + L.tv] = ux; td[px * L.nvc + L.tv] = ud; }
       float v[8], d[8];
       unpack8(ux, v);
@@ -423,6 +443,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
         acc[0][i] += dn; acc[1][i] += dn * xh;
         acc[2][i] += dz; acc[3][i] += dz * n;
       }
+    }
     }
   }
   slice_reduce<4>(acc, L, red, chs);
@@ -624,6 +645,8 @@ int gn_slice(int C, int HW, int cpg, int batch) {
   // tools/gn_bench.py: 8K elements at 16x16, 4K at 8x8, 2K at 4x4, 1K at 2x2
   const int shrink = HW >= 256 ? 1 : (HW >= 64 ? 2 : (HW >= 16 ? 4 : 8));
   const long min_el = (batch >= 64 ? gn_min_slice() : gn_min_slice() / 4) / shrink;
+  // (a smaller slice that fits the backward's LDS tile at 16x16 x 192 channels -- 24 instead of
+  // 48 channels, non-power-of-two lane reduction -- measured slower: 23.4 -> 26.3 us)
   for (int w = unit; w < C; w += unit)
     if (C % w == 0 && (long)w * HW >= min_el) return w;
   return C;
