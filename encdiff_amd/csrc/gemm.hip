@@ -45,6 +45,16 @@ struct TileShape {
   // swizzle mask: 16 rows of a 256-byte k-inner row (KB = 128) spread over all 64 banks;
   // a 4-slot k-outer row (32 columns) swizzles within its 4 slots
   static constexpr int SWM = (KINNER && KB >= 128) ? 15 : (SLOTS < 8 ? SLOTS - 1 : 7);
+  // Bank swizzle (an involution on a row's slots): k-inner rows are read by ds_read_b128 along
+  // rows (slot ^ row); k-outer rows by ds_read_b64_tr_b16, whose 32-lane groups read rows
+  // {r..r+3, r+8..r+11} two slots each -- the XOR keeps each slot pair aligned and gives those
+  // 8 rows distinct bank positions (slot ^ (row & 7) put rows r and r+8 on the same banks: ~half
+  // the weight-gradient tiles' LDS cycles were conflicts)
+  static ED_DEV int sw(int row, int slot) {
+    if constexpr (KINNER || LD < 64) return slot ^ (row & SWM);
+    else if constexpr (LD == 64) return slot ^ ((((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2));
+    else return slot ^ (((row & 3) << 1) | (((row >> 3) & 1) << 3));
+  }
 };
 ED_DEV int swz(int row, int slot, int mask = 7) { return slot ^ (row & mask); }
 
@@ -181,6 +191,18 @@ struct Gemm {
       (NSTAGE * STAGE * 2 > BM * (BN + 4) * 4) ? NSTAGE * STAGE * 2 : BM * (BN + 4) * 4;
 };
 
+// ds_read_b64_tr_b16 as inline asm.  Through the builtin, hipcc cannot tell the transposed read
+// from the LDS-DMA writes still in flight to ANOTHER ring slot and drains them (s_waitcnt
+// vmcnt(0)) before every k-outer fragment read: the next stage's loads then never overlap the
+// current tile's MFMAs in any backward GEMM.  The asm read is waited for explicitly (compute()).
+ED_DEV v4s ds_read_tr16(const bf16_t* p) {
+  typedef __attribute__((address_space(3))) const char lds_char;
+  const uint32_t a = (uint32_t)(uintptr_t)(lds_char*)p;
+  v4s r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
 // Wait until at most N of this thread's vector-memory loads are outstanding (LDS-DMA stages
 // still in flight behind the one about to be read).
 template <int N>
@@ -270,7 +292,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     for (int i = 0; i < (G::HALO ? 0 : TA::PER_THREAD); ++i) {
       const int c = tid + 256 * i;               // LDS chunk position (lane-linear)
       const int row = c / TA::SLOTS, slot = c % TA::SLOTS;
-      const int gs = swz(row, slot, TA::SWM);     // global chunk held at this slot
+      const int gs = TA::sw(row, slot);           // global chunk held at this slot
       bool ok;
       size_t off;
       if constexpr (AKI) {
@@ -308,7 +330,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     for (int i = 0; i < TB::PER_THREAD; ++i) {
       const int c = tid + 256 * i;
       const int row = c / TB::SLOTS, slot = c % TB::SLOTS;
-      const int gs = swz(row, slot, TB::SWM);
+      const int gs = TB::sw(row, slot);
       bool ok;
       size_t off;
       if constexpr (BKI) {  // B_ROWK: Bt[n][k], row = n
@@ -365,13 +387,14 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   auto frag_kinner = [&](const bf16_t* s, int row, int kk, int mask) -> v8bf {
     return *(const v8bf*)(s + row * BK + swz(row, kk * 4 + g4, mask) * 8);
   };
-  auto frag_kouter = [&](const bf16_t* s, int ld, int colbase, int kk, int mask) -> v8bf {
+  auto frag_kouter = [&](auto tile, const bf16_t* s, int colbase, int kk) -> v8bf {
     // rows k = kk*32 + g4*8 + tq (+4): 4 bf16 at column colbase + 4*tp, swizzled chunk
+    using T = decltype(tile);
     typedef __attribute__((address_space(3))) v4s lds_v4s;
     const int r0 = kk * 32 + g4 * 8 + tq, r1 = r0 + 4;
     const int ch = (colbase >> 3) + (tp >> 1), sub = (tp & 1) * 4;
-    v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(s + r0 * ld + swz(r0, ch, mask) * 8 + sub));
-    v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(s + r1 * ld + swz(r1, ch, mask) * 8 + sub));
+    v4s lo = ds_read_tr16(s + r0 * T::LD + T::sw(r0, ch) * 8 + sub);
+    v4s hi = ds_read_tr16(s + r1 * T::LD + T::sw(r1, ch) * 8 + sub);
     v8s r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(v8bf, r);
   };
@@ -408,7 +431,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       const int col = tid % BM, rg = tid / BM;
 #pragma unroll 4
       for (int r = rg * (BK / RG); r < (rg + 1) * (BK / RG); ++r)
-        bsum += bf2f(sa[r * TA::LD + swz(r, col >> 3) * 8 + (col & 7)]);
+        bsum += bf2f(sa[r * TA::LD + TA::sw(r, col >> 3) * 8 + (col & 7)]);
     }
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
@@ -417,12 +440,16 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       for (int i = 0; i < TM; ++i) {
         if constexpr (G::HALO) af[i] = frag_halo(kt, kk, i);
         else if constexpr (AKI) af[i] = frag_kinner(sa, wr + 16 * i + l16, kk, TA::SWM);
-        else af[i] = frag_kouter(sa, TA::LD, wr + 16 * i, kk, TA::SWM);
+        else af[i] = frag_kouter(TA{}, sa, wr + 16 * i, kk);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         if constexpr (BKI) bfr[j] = frag_kinner(sb, wc + 16 * j + l16, kk, TB::SWM);
-        else bfr[j] = frag_kouter(sb, TB::LD, wc + 16 * j, kk, TB::SWM);
+        else bfr[j] = frag_kouter(TB{}, sb, wc + 16 * j, kk);
+      }
+      if constexpr (!AKI || !BKI) {  // asm transposed reads: wait for them before the MFMAs use them
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
