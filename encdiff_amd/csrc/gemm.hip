@@ -284,89 +284,186 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(smem + (c & ~63) * 8), 16, 0, 0);
     }
   };
+  // Staging addresses.  Buffer-resource LDS-DMA with 32-bit byte offsets (host: every operand
+  // spans < 2^31 bytes); a masked chunk (padding tap, tile tail) gets an out-of-range offset and
+  // the DMA writes zeros.  What does not depend on the k-tile is computed once per thread here,
+  // so a chunk costs a few adds and compares per k-tile: the earlier form (64-bit addresses, a
+  // zero-page pointer per masked chunk, the pixel / tap decomposition redone per chunk) issued
+  // 20-30 VALU per 16-byte chunk and left the MFMA pipe idle behind the address arithmetic.
+  constexpr uint32_t OOB = 0x80000000u;
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, 0x7FFFFFF0, 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, 0x7FFFFFF0, 0x00020000);
+  constexpr int APT = G::HALO ? 0 : TA::PER_THREAD, BPT = TB::PER_THREAD;
+  const uint32_t ldsrc2 = (uint32_t)p.conv.ld_src * 2u;
+  // a k-tile of an im2col / flipped-weight operand lies inside one tap: tap and channel base are
+  // uniform per k-tile
+  const bool a_tapk = AM == A_IM2COL && (p.conv.cin % BK) == 0;
+  const bool b_tapk = BMD == B_CONVD && (p.conv_cout % BK) == 0;
+  // weight-gradient im2col operand (k = output pixel): with w | BK and hw | BK or BK | hw, pixel
+  // k0 + r splits into a uniform part of k0 and a per-lane part of r (no per-k-tile division)
+  bool b_pix = false;
+  if constexpr (BMD == B_IM2COL) b_pix = (BK % aux.w.d) == 0 && ((aux.hw.d % BK) == 0 || (BK % aux.hw.d) == 0);
+  uint32_t a_off[APT > 0 ? APT : 1];  // invariant byte offset (OOB: masked row)
+  int a_k[APT > 0 ? APT : 1], a_y[APT > 0 ? APT : 1], a_x[APT > 0 ? APT : 1];
+  uint32_t b_off[BPT], b_n2[BPT];
+  int b_k[BPT], b_ys[BPT];
+  uint32_t b_base[BPT], b_xsh[BPT];
+#pragma unroll
+  for (int i = 0; i < APT; ++i) {
+    const int c = tid + 256 * i;
+    const int row = c / TA::SLOTS, slot = c % TA::SLOTS;
+    const int gs = TA::sw(row, slot);
+    if constexpr (AM == A_ROWK) {
+      const int m = m0 + row;
+      a_k[i] = gs * 8;
+      a_off[i] = m < p.M ? ((uint32_t)m * (uint32_t)p.lda + (uint32_t)(gs * 8)) * 2u : OOB;
+    } else if constexpr (AM == A_ROWM) {
+      const int m = m0 + gs * 8;
+      a_k[i] = row;
+      a_off[i] = m < p.M ? ((uint32_t)row * (uint32_t)p.lda + (uint32_t)m) * 2u : OOB;
+    } else if constexpr (AM == A_IM2COL) {  // this row = output pixel (fixed): source window origin
+      const uint32_t mm0 = (uint32_t)(m0 + row);
+      const bool min = mm0 < (uint32_t)p.M;
+      const uint32_t mm = min ? mm0 - mbase : 0u;
+      const uint32_t bb = fdiv(mm, aux.hw);
+      const uint32_t r = mm - bb * aux.hw.d;
+      const int y = (int)fdiv(r, aux.w), x = (int)(r - (uint32_t)y * aux.w.d);
+      a_k[i] = gs * 8;
+      a_y[i] = min ? md.sy * y + md.oy : (1 << 28);  // out of range: masked row
+      a_x[i] = md.sy * x + md.ox;
+      a_off[i] = bb * (uint32_t)md.hs;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < BPT; ++i) {
+    const int c = tid + 256 * i;
+    const int row = c / TB::SLOTS, slot = c % TB::SLOTS;
+    const int gs = TB::sw(row, slot);
+    if constexpr (BKI) {  // B_ROWK: Bt[n][k], row = n
+      const int n = gfwd ? gcol(row) : n0 + row;
+      b_k[i] = gs * 8;
+      b_off[i] = n < p.N ? ((uint32_t)n * (uint32_t)p.ldb + (uint32_t)(gs * 8)) * 2u : OOB;
+    } else {  // k-outer: row = k, chunk = 8 columns of n
+      const int n = n0 + gs * 8;
+      b_k[i] = row;
+      if constexpr (BMD == B_ROWN || BMD == B_CONVD) {
+        b_off[i] = n < p.N ? ((uint32_t)row * (uint32_t)p.ldb + (uint32_t)n) * 2u : OOB;
+        b_n2[i] = n < p.N ? (uint32_t)n * 2u : OOB;
+      } else {  // B_IM2COL: column n = (tap, ci), invariant; row = pixel offset in the k-tile
+        const uint32_t nn = n < p.N ? (uint32_t)n : 0u;
+        const uint32_t tap = fdiv(nn, aux.cin);
+        const uint32_t ci = nn - tap * (uint32_t)p.conv.cin;
+        int ty, tx;
+        tap_yx(md, tap, ty, tx);
+        b_n2[i] = n < p.N ? ci * 2u : OOB;
+        b_off[i] = (uint32_t)(ty * 16 + tx);  // general path: tap offsets
+        if (b_pix) {
+          const uint32_t bl = fdiv((uint32_t)row, aux.hw), rl = (uint32_t)row - bl * aux.hw.d;
+          const uint32_t yl = fdiv(rl, aux.w), xl = rl - yl * aux.w.d;
+          const int xs = md.sy * (int)xl + tx + md.ox;
+          const bool xok = (unsigned)xs < (unsigned)md.lw && (xs & md.par) == 0 && n < p.N;
+          b_ys[i] = xok ? md.sy * (int)yl + ty + md.oy : (1 << 28);
+          b_base[i] = bl * (uint32_t)md.hs;
+          b_xsh[i] = (uint32_t)(xs >> md.sh);
+        }
+      }
+    }
+  }
   auto stage = [&](bf16_t* s, int kt) {
     const int k0 = kt * BK;
     bf16_t* sa = s;
     bf16_t* sb = s + G::ASTAGE;
-#pragma unroll
-    for (int i = 0; i < (G::HALO ? 0 : TA::PER_THREAD); ++i) {
-      const int c = tid + 256 * i;               // LDS chunk position (lane-linear)
-      const int row = c / TA::SLOTS, slot = c % TA::SLOTS;
-      const int gs = TA::sw(row, slot);           // global chunk held at this slot
-      bool ok;
-      size_t off;
-      if constexpr (AKI) {
-        const int k = k0 + gs * 8;
-        if constexpr (AM == A_ROWK) {
-          const int m = m0 + row;
-          ok = m < p.M && k < p.K;
-          off = (size_t)(ok ? m : 0) * p.lda + (ok ? k : 0);
-        } else {  // IM2COL: this row = output pixel, fixed per (thread, i) only when SLOTS == 8
-          const uint32_t mm0 = (uint32_t)(m0 + row);
-          const bool min = mm0 < (uint32_t)p.M;
-          const uint32_t mm = min ? mm0 - mbase : 0u;
-          const uint32_t bb = fdiv(mm, aux.hw);
-          const uint32_t r = mm - bb * aux.hw.d;
-          const int y = (int)fdiv(r, aux.w), x = (int)(r - (uint32_t)y * aux.w.d);
-          const uint32_t kk = k < p.K ? (uint32_t)k : 0u;
-          const uint32_t tap = fdiv(kk, aux.cin);
-          const uint32_t ch = kk - tap * (uint32_t)p.conv.cin;
-          int ty, tx;
-          tap_yx(md, tap, ty, tx);
-          bool inb;
-          const uint32_t prow = im2col_row(md, bb, y, x, ty, tx, inb);
-          ok = min && k < p.K && inb;
-          off = (size_t)(ok ? prow : 0u) * p.conv.ld_src + (ok ? ch : 0u);
-        }
-      } else {  // A_ROWM: tile [BK][BM], row = k
-        const int k = k0 + row, m = m0 + gs * 8;
-        ok = k < p.K && m < p.M;
-        off = (size_t)(ok ? k : 0) * p.lda + (ok ? m : 0);
+    // uniform per-k-tile values
+    uint32_t a_ch = 0u, b_cv = 0u, b_pb = 0u;
+    int a_ty = 0, a_tx = 0, b_yo = 0;
+    if constexpr (AM == A_IM2COL) {
+      if (a_tapk) {
+        const uint32_t tap = fdiv((uint32_t)k0, aux.cin);
+        a_ch = (uint32_t)k0 - tap * (uint32_t)p.conv.cin;
+        tap_yx(md, tap, a_ty, a_tx);
       }
-      const void* src = ok ? (const void*)(A + off) : (const void*)&g_zero16;
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sa + (c & ~63) * 8), 16, 0, 0);
+    }
+    if constexpr (BMD == B_CONVD) {
+      if (b_tapk) {
+        const uint32_t tap = fdiv((uint32_t)k0, aux.cout);
+        const uint32_t co = (uint32_t)k0 - tap * (uint32_t)p.conv_cout;
+        b_cv = (co * (uint32_t)p.ldb + md.wtap(tap) * (uint32_t)p.N) * 2u;
+      }
+    }
+    if constexpr (BMD == B_IM2COL) {
+      if (b_pix) {
+        const uint32_t bs = fdiv((uint32_t)k0, aux.hw);
+        const uint32_t ys = fdiv((uint32_t)k0 - bs * aux.hw.d, aux.w);
+        b_yo = md.sy * (int)ys;
+        b_pb = bs * (uint32_t)md.hs;
+      }
     }
 #pragma unroll
-    for (int i = 0; i < TB::PER_THREAD; ++i) {
+    for (int i = 0; i < APT; ++i) {
+      const int c = tid + 256 * i;  // LDS chunk position (lane-linear)
+      const int k = k0 + a_k[i];
+      uint32_t vo;
+      if constexpr (AM == A_ROWK) {
+        vo = k < p.K ? a_off[i] + 2u * (uint32_t)k0 : OOB;
+      } else if constexpr (AM == A_ROWM) {
+        vo = k < p.K ? a_off[i] + (uint32_t)k0 * (uint32_t)p.lda * 2u : OOB;
+      } else {  // IM2COL
+        uint32_t ch;
+        int ty, tx;
+        if (a_tapk) {
+          ch = a_ch + (uint32_t)a_k[i];
+          ty = a_ty;
+          tx = a_tx;
+        } else {
+          const uint32_t kk = k < p.K ? (uint32_t)k : 0u;
+          const uint32_t tap = fdiv(kk, aux.cin);
+          ch = kk - tap * (uint32_t)p.conv.cin;
+          tap_yx(md, tap, ty, tx);
+        }
+        const int ys = a_y[i] + ty, xs = a_x[i] + tx;
+        const bool ok = k < p.K && (unsigned)ys < (unsigned)md.lh && (unsigned)xs < (unsigned)md.lw &&
+                        ((ys | xs) & md.par) == 0;
+        const uint32_t prow = (a_off[i] + (uint32_t)(ys >> md.sh)) * (uint32_t)md.ws + (uint32_t)(xs >> md.sh);
+        vo = ok ? prow * ldsrc2 + ch * 2u : OOB;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)(sa + (c & ~63) * 8), 16, vo, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
       const int c = tid + 256 * i;
-      const int row = c / TB::SLOTS, slot = c % TB::SLOTS;
-      const int gs = TB::sw(row, slot);
-      bool ok;
-      size_t off;
-      if constexpr (BKI) {  // B_ROWK: Bt[n][k], row = n
-        const int n = gfwd ? gcol(row) : n0 + row, k = k0 + gs * 8;
-        ok = n < p.N && k < p.K;
-        off = (size_t)(ok ? n : 0) * p.ldb + (ok ? k : 0);
-      } else {  // k-outer: row = k, chunk = 8 columns of n
-        const int k = k0 + row, n = n0 + gs * 8;
-        const bool kn = k < p.K && n < p.N;
-        if constexpr (BMD == B_ROWN) {
-          ok = kn;
-          off = (size_t)(ok ? k : 0) * p.ldb + (ok ? n : 0);
-        } else if constexpr (BMD == B_CONVD) {
-          const uint32_t kk = kn ? (uint32_t)k : 0u;
+      const int k = k0 + b_k[i];
+      uint32_t vo;
+      if constexpr (BKI) {
+        vo = k < p.K ? b_off[i] + 2u * (uint32_t)k0 : OOB;
+      } else if constexpr (BMD == B_ROWN) {
+        vo = k < p.K ? b_off[i] + (uint32_t)k0 * (uint32_t)p.ldb * 2u : OOB;
+      } else if constexpr (BMD == B_CONVD) {
+        if (b_tapk) {
+          vo = k < p.K ? b_off[i] + b_cv : OOB;
+        } else {
+          const uint32_t kk = k < p.K ? (uint32_t)k : 0u;
           const uint32_t tap = fdiv(kk, aux.cout);
           const uint32_t co = kk - tap * (uint32_t)p.conv_cout;
-          ok = kn;
-          off = (size_t)co * p.ldb + (size_t)md.wtap(tap) * p.N + (ok ? n : 0);
-        } else {  // B_IM2COL: row = output pixel k, column n = (tap, ci)
-          const uint32_t kk = kn ? (uint32_t)k : 0u;
+          vo = k < p.K ? b_n2[i] + (co * (uint32_t)p.ldb + md.wtap(tap) * (uint32_t)p.N) * 2u : OOB;
+        }
+      } else {  // B_IM2COL
+        if (b_pix) {
+          const int ys = b_ys[i] + b_yo;
+          const bool ok = k < p.K && (unsigned)ys < (unsigned)md.lh && (ys & md.par) == 0;
+          const uint32_t prow = (b_pb + b_base[i] + (uint32_t)(ys >> md.sh)) * (uint32_t)md.ws + b_xsh[i];
+          vo = ok ? prow * ldsrc2 + b_n2[i] : OOB;
+        } else {
+          const uint32_t kk = k < p.K ? (uint32_t)k : 0u;
           const uint32_t bb = fdiv(kk, aux.hw);
           const uint32_t r = kk - bb * aux.hw.d;
           const int y = (int)fdiv(r, aux.w), x = (int)(r - (uint32_t)y * aux.w.d);
-          const uint32_t nn = kn ? (uint32_t)n : 0u;
-          const uint32_t tap = fdiv(nn, aux.cin);
-          const uint32_t ci = nn - tap * (uint32_t)p.conv.cin;
-          int ty, tx;
-          tap_yx(md, tap, ty, tx);
+          const int ty = (int)(b_off[i] >> 4), tx = (int)(b_off[i] & 15u);
           bool inb;
           const uint32_t prow = im2col_row(md, bb, y, x, ty, tx, inb);
-          ok = kn && inb;
-          off = (size_t)(ok ? prow : 0u) * p.conv.ld_src + (ok ? ci : 0u);
+          vo = (k < p.K && inb) ? prow * ldsrc2 + b_n2[i] : OOB;
         }
       }
-      const void* src = ok ? (const void*)(B + off) : (const void*)&g_zero16;
-      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(sb + (c & ~63) * 8), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_void*)(sb + (c & ~63) * 8), 16, vo, 0, 0, 0);
     }
   };
 
@@ -1182,6 +1279,18 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
     if (p.c_mode == ENCDIFF_OUT_F32_ATOMIC || p.c_mode == ENCDIFF_OUT_F32_ATOMIC_CONVW) return ENCDIFF_ERR_UNSUPPORTED;
   }
   if (p.K >= (1 << 24)) return ENCDIFF_ERR_SHAPE;
+  {  // the staging loads address every operand by 32-bit byte offsets from its base
+    const long src = (long)p.conv.batch * p.conv.h * p.conv.w * 4 * p.conv.ld_src * 2;  // im2col source
+    long ea = 0, eb = 0;
+    if (p.a_mode == ENCDIFF_OPA_ROWK) ea = ((long)(p.M - 1) * p.lda + p.K) * 2;
+    else if (p.a_mode == ENCDIFF_OPA_ROWM) ea = ((long)(p.K - 1) * p.lda + p.M) * 2;
+    else ea = src;
+    if (p.b_mode == ENCDIFF_OPB_ROWK) eb = ((long)(p.N - 1) * p.ldb + p.K) * 2;
+    else if (p.b_mode == ENCDIFF_OPB_ROWN) eb = ((long)(p.K - 1) * p.ldb + p.N) * 2;
+    else if (p.b_mode == ENCDIFF_OPB_CONV_DGRAD) eb = ((long)p.conv_cout * p.ldb + 16L * p.N) * 2;
+    else eb = src;
+    if (ea >= 0x7FFFFFF0L || eb >= 0x7FFFFFF0L) return ENCDIFF_ERR_SHAPE;
+  }
   if (p.bias_grad && p.a_mode != ENCDIFF_OPA_ROWM) return ENCDIFF_ERR_ARG;
   if (p.gn_stats && (p.c_mode != ENCDIFF_OUT_BF16 || p.split_k != 1 || p.M % 64 || p.ld_gn_stats < p.N))
     return ENCDIFF_ERR_ARG;
