@@ -98,6 +98,21 @@ class BatchNormArgs(C.Structure):
                 ("dgamma", vp), ("dbeta", vp), ("y_split", C.c_int), ("pad2_", C.c_int)]
 
 
+class StTailArgs(C.Structure):
+    _fields_ = [("rows", C.c_int), ("c", C.c_int), ("tokens", C.c_int), ("heads", C.c_int), ("n_ctx", C.c_int),
+                ("ln_eps", C.c_float), ("scale", C.c_float), ("pad_", C.c_int),
+                ("o1", vp), ("ld_o1", C.c_long), ("t0", vp), ("ld_t0", C.c_long), ("x", vp), ("ld_x", C.c_long),
+                ("k2", vp), ("v2", vp), ("ld_kv", C.c_long),
+                ("w_out1", vp), ("ld_out1", C.c_long), ("b_out1", vp), ("g2", vp), ("be2", vp),
+                ("w_q2", vp), ("ld_q2", C.c_long), ("w_out2", vp), ("ld_out2", C.c_long), ("b_out2", vp),
+                ("g3", vp), ("be3", vp), ("w_ff1", vp), ("ld_ff1", C.c_long), ("b_ff1", vp),
+                ("w_ff2", vp), ("ld_ff2", C.c_long), ("b_ff2", vp), ("w_po", vp), ("ld_po", C.c_long), ("b_po", vp),
+                ("out", vp), ("ld_out", C.c_long),
+                ("save_t1", vp), ("save_n2", vp), ("save_q2", vp), ("save_o2", vp), ("save_t2", vp),
+                ("save_n3", vp), ("save_f", vp), ("save_a", vp), ("save_t3", vp), ("ld_save", C.c_long),
+                ("save_s2", vp), ("save_s3", vp), ("save_lse2", vp)]
+
+
 class PackJob(C.Structure):
     _fields_ = [("src_off", C.c_longlong), ("dst_off", C.c_longlong), ("rows", C.c_int), ("cols", C.c_int),
                 ("kind", C.c_int), ("cin", C.c_int)]
@@ -137,6 +152,7 @@ _PROTOS = {
     "encdiff_batchnorm_apply": [C.POINTER(BatchNormArgs), vp],
     "encdiff_nchw_to_rows": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_long, vp],
     "encdiff_nchw_to_rows_split3": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_long, vp],
+    "encdiff_st_tail_fwd": [C.POINTER(StTailArgs), vp],
     "encdiff_version": [],
 }
 

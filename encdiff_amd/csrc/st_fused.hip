@@ -1,0 +1,467 @@
+// st_fused.hip -- the row-local tail of a SpatialTransformer block as one kernel.
+//
+// After its self-attention, a SpatialTransformer (attention.py:196-261) only mixes channels of
+// a token row (projections, LayerNorms, GEGLU) or attends to the 20 concept tokens of the row's
+// own image: no row needs another row.  A workgroup therefore keeps R rows resident in LDS --
+// the residual stream in fp32, one bf16 operand buffer for the next MFMA -- and runs
+//   t1 = o1 Wout1^T + b + t0          (attn1.to_out, residual)
+//   n2 = LN2(t1);  q2 = n2 Wq^T        (norm2, attn2.to_q)
+//   o2 = softmax(q2 k2^T * scale) v2   (attn2 over the image's concept tokens)
+//   t2 = o2 Wout2^T + b + t1          (attn2.to_out, residual)
+//   n3 = LN3(t2); [v|g] = n3 W1^T + b; a = v * gelu(g)   (norm3, GEGLU proj, 64-column chunks)
+//   t3 = a W2^T + b + t2              (ff.net.2, residual)
+//   out = t3 Wpo^T + b + x            (proj_out, block residual)
+// with every weight streamed from L2 straight into MFMA B fragments (v_mfma_f32_16x16x32_bf16,
+// 4 waves, each owning a quarter of the output columns for all R rows).  Seven launches of the
+// unfused path (3 GEMM+LN, to_q, cross-attention, GEGLU proj, ff2 + proj_out -- each a few us of
+// launch and load latency at sampling batches) become one.  The training forward additionally
+// writes the activations its backward reads (save_*).
+#include "common.h"
+
+namespace {
+
+template <int C, int RR>
+struct Tail {
+  static constexpr int R = RR;                  // rows per workgroup (64; 32 at C = 256: LDS 108 KiB; 16 for tiny batches)
+  static constexpr int TM = R / 16;             // 16-row MFMA tiles
+  static constexpr int LDT = C + 4;             // fp32 residual-stream row stride (floats)
+  static constexpr int LDX = C + 8;             // bf16 operand row stride (elements): conflict-free b128 reads
+  static constexpr int NT = C / 64;             // 16-column MFMA tiles per wave for N = C
+  static constexpr int HC = 64;                 // GEGLU hidden chunk (columns of a)
+  static constexpr int DH = C / 8;              // head dim (8 heads)
+  static size_t lds_bytes(int nimg, int nctx) {
+    return (size_t)R * LDT * 4 + 2 * (size_t)R * LDX * 2 + (size_t)nimg * 2 * nctx * C * 2;
+  }
+};
+
+// GELU (erf form, F.gelu's default) with a branch-free erf: Abramowitz-Stegun 7.1.26, |error| <=
+// 1.5e-7 -- far below the bf16 rounding of a -- instead of ocml erff's range branches, which made
+// the GEGLU chunk the tail kernel's longest stage.
+ED_DEV float gelu_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * z);
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float erf_abs = 1.f - poly * __expf(-z * z);
+  return 0.5f * x * (1.f + copysignf(erf_abs, x));
+}
+
+// B fragments of W[n0 + 16 j + col][k0 + k] for k < K (lane: column l16, k = kk*32 + g4*8 .. +8)
+template <int NT, int K>
+struct BFrags {
+  v8bf f[K / 32][NT];
+};
+template <int NT, int K>
+ED_DEV void load_b(BFrags<NT, K>& b, const bf16_t* __restrict__ W, long ldw, int n0, int k0, int lane) {
+  const int l16 = lane & 15, g4 = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < K / 32; ++kk)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+      b.f[kk][j] = *(const v8bf*)(W + (long)(n0 + 16 * j + l16) * ldw + k0 + kk * 32 + g4 * 8);
+}
+// acc[i][j] += X[16 i + row][k] * B   (X in LDS, row stride ldx, k < K)
+template <int TM, int NT, int K>
+ED_DEV void mma(v4f (&acc)[TM][NT], const bf16_t* X, int ldx, const BFrags<NT, K>& b, int lane) {
+  const int l16 = lane & 15, g4 = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < K / 32; ++kk) {
+    v8bf af[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = *(const v8bf*)(X + (16 * i + l16) * ldx + kk * 32 + g4 * 8);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], b.f[kk][j], acc[i][j], 0, 0, 0);
+  }
+}
+template <int TM, int NT>
+ED_DEV void zero(v4f (&acc)[TM][NT]) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+}
+// accumulator element (i, j, q): row 16 i + 4 g4 + q, column n0 + 16 j + l16
+template <int TM, int NT>
+ED_DEV void acc_add_tr(const v4f (&acc)[TM][NT], float* Tr, int ldt, const float* __restrict__ bias, int n0, int lane) {
+  const int l16 = lane & 15, g4 = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = n0 + 16 * j + l16;
+    const float bv = bias[col];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Tr[(16 * i + 4 * g4 + q) * ldt + col] += acc[i][j][q] + bv;
+  }
+}
+template <int TM, int NT>
+ED_DEV void acc_store_bf(const v4f (&acc)[TM][NT], bf16_t* X, int ldx, int n0, int lane) {
+  const int l16 = lane & 15, g4 = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) X[(16 * i + 4 * g4 + q) * ldx + n0 + 16 * j + l16] = f2bf(acc[i][j][q]);
+}
+
+// LayerNorm of the R residual rows (fp32, LDS) into the bf16 operand buffer; optional saves.  The
+// statistics are those of the bf16-rounded rows (the tensor the unfused path stores and its
+// LayerNorm backward re-reads); the residual stream itself stays fp32.
+template <int C, int R>
+ED_DEV void ln_rows(const float* Tr, int ldt, bf16_t* X, int ldx, const float* __restrict__ g,
+                    const float* __restrict__ b, float eps, int tid, bf16_t* save_y, long ld_save,
+                    bf16_t* save_x, float* save_s) {
+  // all R rows at once: TPR consecutive lanes per row, each owning float4 chunks k, k + TPR, ...
+  // (a row per wave with 64-lane butterflies serialised R/4 rows of ds_bpermute round trips)
+  constexpr int TPR = 256 / R, NQ = C / (4 * TPR);
+  const int r = tid / TPR, k = tid % TPR;
+  float v[NQ][4], s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const float4 f = *(const float4*)(Tr + r * ldt + 4 * (k + TPR * i));
+    // the stored (bf16) residual, as the unfused path normalises it
+    v[i][0] = bf16_round(f.x); v[i][1] = bf16_round(f.y); v[i][2] = bf16_round(f.z); v[i][3] = bf16_round(f.w);
+    s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  }
+#pragma unroll
+  for (int o = 1; o < TPR; o <<= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s * (1.f / C);
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s2 += (v[i][e] - mean) * (v[i][e] - mean);
+#pragma unroll
+  for (int o = 1; o < TPR; o <<= 1) s2 += __shfl_xor(s2, o, 64);
+  const float rstd = rsqrtf(s2 * (1.f / C) + eps);
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int c = 4 * (k + TPR * i);
+    const float4 gv = make_float4(g[c], g[c + 1], g[c + 2], g[c + 3]);  // fp32 arena: 4-byte alignment only
+    const float4 bv = make_float4(b[c], b[c + 1], b[c + 2], b[c + 3]);
+    const uint2 y = make_uint2(pack2((v[i][0] - mean) * rstd * gv.x + bv.x, (v[i][1] - mean) * rstd * gv.y + bv.y),
+                               pack2((v[i][2] - mean) * rstd * gv.z + bv.z, (v[i][3] - mean) * rstd * gv.w + bv.w));
+    *(uint2*)(X + r * ldx + c) = y;
+    if (save_y) {
+      *(uint2*)(save_y + r * ld_save + c) = y;
+      *(uint2*)(save_x + r * ld_save + c) = make_uint2(pack2(v[i][0], v[i][1]), pack2(v[i][2], v[i][3]));
+    }
+  }
+  if (save_s && k == 0) {
+    save_s[2 * r] = mean;
+    save_s[2 * r + 1] = rstd;
+  }
+}
+
+// copy R rows x C bf16 between global and LDS (16-byte chunks)
+template <int C, int R>
+ED_DEV void rows_to_lds(bf16_t* X, int ldx, const bf16_t* __restrict__ g, long ldg, int tid) {
+  constexpr int CH = C / 8;
+  for (int e = tid; e < R * CH; e += 256) {
+    const int r = e / CH, c8 = (e - r * CH) * 8;
+    *(uint4*)(X + r * ldx + c8) = *(const uint4*)(g + (long)r * ldg + c8);
+  }
+}
+template <int C, int R>
+ED_DEV void rows_to_global(bf16_t* __restrict__ g, long ldg, const bf16_t* X, int ldx, int tid) {
+  constexpr int CH = C / 8;
+  for (int e = tid; e < R * CH; e += 256) {
+    const int r = e / CH, c8 = (e - r * CH) * 8;
+    *(uint4*)(g + (long)r * ldg + c8) = *(const uint4*)(X + r * ldx + c8);
+  }
+}
+
+template <int C, int RR>
+__global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p) {
+  using T = Tail<C, RR>;
+  constexpr int R = T::R, TM = T::TM, NT = T::NT, LDT = T::LDT, LDX = T::LDX, HC = T::HC, DH = T::DH;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  float* Tr = (float*)smem_raw;
+  bf16_t* Xa = (bf16_t*)(Tr + R * LDT);
+  bf16_t* Xb = Xa + R * LDX;
+  bf16_t* KV = Xb + R * LDX;  // [nimg][2][n_ctx][C]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row0 = blockIdx.x * R;
+  const int nctx = p.n_ctx;
+  const int img0 = row0 / p.tokens;
+  const int nimg = R > p.tokens ? R / p.tokens : 1;
+  const bool save = p.save_t1 != nullptr;
+  const int n0 = wave * (C / 4);  // this wave's output columns for N = C
+
+  // Weights.  PRE (c = 64: 128 VGPRs for all of them): every weight fragment of the chain is
+  // loaded here, before anything else, so the chain's stages never wait on L2 / MALL latency.
+  // c = 128: the four projections here, the feed-forward's chunks double-buffered one chunk
+  // ahead; c = 256: each projection while the previous stage runs.
+  constexpr int NCH = 4 * C / HC;  // GEGLU hidden chunks
+  constexpr bool PRE = C == 64;
+  constexpr bool PREP = C <= 128;
+  constexpr int NW = PRE ? NCH : 2;
+  const bf16_t* W1 = (const bf16_t*)p.w_ff1;
+  const bf16_t* W2 = (const bf16_t*)p.w_ff2;
+  const int nc16 = wave * 16;  // this wave's 16 columns of a hidden chunk
+  BFrags<NT, C> wo1, wq, wo2, wpo;
+  BFrags<1, C> wv[NW], wg[NW];
+  BFrags<NT, HC> w2[PRE ? NCH : 1];
+  load_b(wo1, (const bf16_t*)p.w_out1, p.ld_out1, n0, 0, lane);
+  if constexpr (PREP) {
+    load_b(wq, (const bf16_t*)p.w_q2, p.ld_q2, n0, 0, lane);
+    load_b(wo2, (const bf16_t*)p.w_out2, p.ld_out2, n0, 0, lane);
+  }
+  if constexpr (PRE) {
+#pragma unroll
+    for (int ch = 0; ch < NW; ++ch) {
+      load_b(wv[ch], W1, p.ld_ff1, ch * HC + nc16, 0, lane);
+      load_b(wg[ch], W1, p.ld_ff1, 4 * C + ch * HC + nc16, 0, lane);
+      load_b(w2[ch], W2, p.ld_ff2, n0, ch * HC, lane);
+    }
+  }
+  if constexpr (PREP) load_b(wpo, (const bf16_t*)p.w_po, p.ld_po, n0, 0, lane);
+
+  // ---- stage: o1 -> Xa, t0 -> Tr (fp32), the tile's concept-token K / V -> LDS
+  rows_to_lds<C, R>(Xa, LDX, (const bf16_t*)p.o1 + (long)row0 * p.ld_o1, p.ld_o1, tid);
+  {
+    constexpr int CH = C / 8;
+    const bf16_t* t0 = (const bf16_t*)p.t0 + (long)row0 * p.ld_t0;
+    for (int e = tid; e < R * CH; e += 256) {
+      const int r = e / CH, c8 = (e - r * CH) * 8;
+      float f[8];
+      unpack8(*(const uint4*)(t0 + (long)r * p.ld_t0 + c8), f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) Tr[r * LDT + c8 + k] = f[k];
+    }
+    const int nkv = nimg * 2 * nctx * CH;
+    for (int e = tid; e < nkv; e += 256) {
+      const int c8 = (e % CH) * 8, rr = e / CH;  // rr = (i * 2 + kv) * nctx + j
+      const int j = rr % nctx, ikv = rr / nctx, kv = ikv & 1, i = ikv >> 1;
+      const bf16_t* src = (const bf16_t*)(kv ? p.v2 : p.k2) + (long)((img0 + i) * nctx + j) * p.ld_kv + c8;
+      *(uint4*)(KV + (long)rr * C + c8) = *(const uint4*)src;
+    }
+  }
+  __syncthreads();
+
+  v4f acc[TM][NT];
+  // ---- t1 = o1 Wout1^T + b + t0
+  zero(acc);
+  mma(acc, Xa, LDX, wo1, lane);
+  if constexpr (!PREP) load_b(wq, (const bf16_t*)p.w_q2, p.ld_q2, n0, 0, lane);  // next GEMM's weights in flight
+  acc_add_tr(acc, Tr, LDT, p.b_out1, n0, lane);
+  __syncthreads();
+  // ---- n2 = LN2(t1)
+  if (!(p.pad_ & 4))
+  ln_rows<C, R>(Tr, LDT, Xa, LDX, p.g2, p.be2, p.ln_eps, tid,
+                save ? (bf16_t*)p.save_n2 + (long)row0 * p.ld_save : nullptr, p.ld_save,
+                save ? (bf16_t*)p.save_t1 + (long)row0 * p.ld_save : nullptr, save ? p.save_s2 + 2L * row0 : nullptr);
+  __syncthreads();
+  // ---- q2 = n2 Wq^T -> Xb
+  zero(acc);
+  mma(acc, Xa, LDX, wq, lane);
+  if constexpr (!PREP) load_b(wo2, (const bf16_t*)p.w_out2, p.ld_out2, n0, 0, lane);
+  acc_store_bf(acc, Xb, LDX, n0, lane);
+  __syncthreads();
+  if (save) rows_to_global<C, R>((bf16_t*)p.save_q2 + (long)row0 * p.ld_save, p.ld_save, Xb, LDX, tid);
+  // ---- o2 = softmax(q2 k2^T * scale) v2 per (row, head) -> Xa (online softmax over the keys)
+  const int dbg = p.pad_;  // timing experiments only (tools/st_tail_bench.py): bit 0 skips the
+                           // cross-attention, bit 1 the feed-forward, bit 2 the LayerNorms
+  for (int pr = (dbg & 1) ? R * 8 : tid; pr < R * 8; pr += 256) {
+    const int r = pr % R, h = pr / R;
+    const int il = (row0 + r) / p.tokens - img0;
+    float q[DH], o[DH];
+#pragma unroll
+    for (int d8 = 0; d8 < DH; d8 += 8) unpack8(*(const uint4*)(Xb + r * LDX + h * DH + d8), q + d8);
+    const bf16_t* Ks = KV + (long)(il * 2) * nctx * C + h * DH;
+    const bf16_t* Vs = Ks + (long)nctx * C;
+    float m = -INFINITY, l = 0.f;
+#pragma unroll
+    for (int d = 0; d < DH; ++d) o[d] = 0.f;
+    for (int j = 0; j < nctx; ++j) {
+      float kf[DH], vf[DH];
+#pragma unroll
+      for (int d8 = 0; d8 < DH; d8 += 8) {
+        unpack8(*(const uint4*)(Ks + j * C + d8), kf + d8);
+        unpack8(*(const uint4*)(Vs + j * C + d8), vf + d8);
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) s += q[d] * kf[d];
+      s *= p.scale;
+      const float mn = fmaxf(m, s);
+      const float cr = __expf(m - mn), pe = __expf(s - mn);
+      l = l * cr + pe;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) o[d] = o[d] * cr + pe * vf[d];
+      m = mn;
+    }
+    const float il_ = 1.f / l;
+#pragma unroll
+    for (int d8 = 0; d8 < DH; d8 += 8) {
+      float y[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) y[k] = o[d8 + k] * il_;
+      *(uint4*)(Xa + r * LDX + h * DH + d8) = pack8(y);
+    }
+    if (save) p.save_lse2[(long)((img0 + il) * 8 + h) * p.tokens + (row0 + r) % p.tokens] = m + __logf(l);
+  }
+  __syncthreads();
+  if (save) rows_to_global<C, R>((bf16_t*)p.save_o2 + (long)row0 * p.ld_save, p.ld_save, Xa, LDX, tid);
+  // ---- t2 = o2 Wout2^T + b + t1
+  zero(acc);
+  mma(acc, Xa, LDX, wo2, lane);
+  acc_add_tr(acc, Tr, LDT, p.b_out2, n0, lane);
+  __syncthreads();
+  // ---- n3 = LN3(t2)
+  if (!(dbg & 4))
+  ln_rows<C, R>(Tr, LDT, Xa, LDX, p.g3, p.be3, p.ln_eps, tid,
+                save ? (bf16_t*)p.save_n3 + (long)row0 * p.ld_save : nullptr, p.ld_save,
+                save ? (bf16_t*)p.save_t2 + (long)row0 * p.ld_save : nullptr, save ? p.save_s3 + 2L * row0 : nullptr);
+  // ---- GEGLU feed-forward in 64-column chunks of the hidden a; t3 accumulates in registers
+  if constexpr (!PRE) {
+    load_b(wv[0], W1, p.ld_ff1, nc16, 0, lane);
+    load_b(wg[0], W1, p.ld_ff1, 4 * C + nc16, 0, lane);
+  }
+  __syncthreads();
+  v4f acc3[TM][NT];
+  zero(acc3);
+#pragma unroll
+  for (int ch = 0; ch < ((dbg & 2) ? 0 : NCH); ++ch) {
+    const int w = PRE ? ch : (ch & 1);  // static after the full unroll
+    const int w2i = PRE ? ch : 0;
+    if constexpr (!PRE) {
+      // this chunk's ff2 fragments and the next chunk's value / gate fragments are in flight
+      // while this chunk's value / gate GEMMs and GELU run
+      load_b(w2[0], W2, p.ld_ff2, n0, ch * HC, lane);
+      if (ch + 1 < NCH) {
+        load_b(wv[w ^ 1], W1, p.ld_ff1, (ch + 1) * HC + nc16, 0, lane);
+        load_b(wg[w ^ 1], W1, p.ld_ff1, 4 * C + (ch + 1) * HC + nc16, 0, lane);
+      }
+      if (ch + 1 == NCH && !PREP) load_b(wpo, (const bf16_t*)p.w_po, p.ld_po, n0, 0, lane);
+    }
+    v4f av[TM][1], ag[TM][1];
+    zero(av);
+    zero(ag);
+    mma(av, Xa, LDX, wv[w], lane);
+    mma(ag, Xa, LDX, wg[w], lane);
+    {
+      const int l16 = lane & 15, g4 = lane >> 4;
+      const int col = ch * HC + nc16 + l16;  // hidden column
+      const float bvv = p.b_ff1[col], bgg = p.b_ff1[4 * C + col];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 16 * i + 4 * g4 + q;
+          const float fv = av[i][0][q] + bvv, fg = ag[i][0][q] + bgg;
+          const bf16_t fvb = f2bf(fv), fgb = f2bf(fg);
+          // the unfused path stores f in bf16 and forms a from the stored values
+          const float y = bf2f(fvb) * gelu_fast(bf2f(fgb));
+          Xb[r * LDX + nc16 + l16] = f2bf(y);
+          if (save) {
+            bf16_t* f = (bf16_t*)p.save_f + (long)(row0 + r) * (8 * C);
+            f[col] = fvb;
+            f[4 * C + col] = fgb;
+            ((bf16_t*)p.save_a)[(long)(row0 + r) * (4 * C) + col] = f2bf(y);
+          }
+        }
+    }
+    __syncthreads();
+    mma(acc3, Xb, LDX, w2[w2i], lane);
+    __syncthreads();  // Xb is rewritten by the next chunk
+  }
+  // ---- t3 = a W2^T + b + t2;  Xa = bf16(t3);  Tr = x
+  acc_add_tr(acc3, Tr, LDT, p.b_ff2, n0, lane);
+  __syncthreads();
+  {
+    constexpr int CH = C / 8;
+    const bf16_t* xg = (const bf16_t*)p.x + (long)row0 * p.ld_x;
+    for (int e = tid; e < R * CH; e += 256) {
+      const int r = e / CH, c8 = (e - r * CH) * 8;
+      float f[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = Tr[r * LDT + c8 + k];
+      const uint4 t3 = pack8(f);
+      *(uint4*)(Xa + r * LDX + c8) = t3;
+      if (save) *(uint4*)((bf16_t*)p.save_t3 + (long)(row0 + r) * p.ld_save + c8) = t3;
+      unpack8(*(const uint4*)(xg + (long)r * p.ld_x + c8), f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) Tr[r * LDT + c8 + k] = f[k];
+    }
+  }
+  __syncthreads();
+  // ---- out = t3 Wpo^T + b + x
+  zero(acc);
+  mma(acc, Xa, LDX, wpo, lane);
+  acc_add_tr(acc, Tr, LDT, p.b_po, n0, lane);
+  __syncthreads();
+  {
+    constexpr int CH = C / 8;
+    bf16_t* og = (bf16_t*)p.out + (long)row0 * p.ld_out;
+    for (int e = tid; e < R * CH; e += 256) {
+      const int r = e / CH, c8 = (e - r * CH) * 8;
+      float f[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = Tr[r * LDT + c8 + k];
+      *(uint4*)(og + (long)r * p.ld_out + c8) = pack8(f);
+    }
+  }
+}
+
+template <int C, int RR>
+int launch_tail(const EncdiffStTailArgs& p, hipStream_t s) {
+  using T = Tail<C, RR>;
+  if (p.rows % T::R || (T::R % p.tokens && p.tokens % T::R)) return ENCDIFF_ERR_SHAPE;
+  const int nimg = T::R > p.tokens ? T::R / p.tokens : 1;
+  const size_t lds = T::lds_bytes(nimg, p.n_ctx);
+  if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
+  static const hipError_t attr_ok = hipFuncSetAttribute((const void*)st_tail_kernel<C, RR>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr_ok != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)attr_ok;
+  hipLaunchKernelGGL((st_tail_kernel<C, RR>), dim3((unsigned)(p.rows / T::R)), dim3(256), lds, s, p);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
+
+}  // namespace
+
+extern "C" int encdiff_st_tail_fwd(const EncdiffStTailArgs* a, void* stream) {
+  if (!a) return ENCDIFF_ERR_ARG;
+  const EncdiffStTailArgs& p = *a;
+  if (p.heads != 8 || (p.c != 64 && p.c != 128 && p.c != 256)) return ENCDIFF_ERR_UNSUPPORTED;
+  if (p.n_ctx < 1 || p.n_ctx > 64 || p.tokens < 1 || p.rows < 1 || p.rows % p.tokens) return ENCDIFF_ERR_SHAPE;
+  const void* ptrs[] = {p.o1, p.t0, p.x, p.k2, p.v2, p.w_out1, p.w_q2, p.w_out2, p.w_ff1, p.w_ff2, p.w_po, p.out};
+  for (const void* q : ptrs)
+    if (!q || !al16(q)) return ENCDIFF_ERR_ARG;
+  const long lds[] = {p.ld_o1, p.ld_t0, p.ld_x, p.ld_kv, p.ld_out1, p.ld_q2, p.ld_out2, p.ld_ff1, p.ld_ff2, p.ld_po,
+                      p.ld_out};
+  for (long l : lds)
+    if (l % 8) return ENCDIFF_ERR_ARG;
+  if (!p.b_out1 || !p.b_out2 || !p.b_ff1 || !p.b_ff2 || !p.b_po || !p.g2 || !p.be2 || !p.g3 || !p.be3)
+    return ENCDIFF_ERR_ARG;
+  const void* sv[] = {p.save_t1, p.save_n2, p.save_q2, p.save_o2, p.save_t2, p.save_n3, p.save_f, p.save_a,
+                      p.save_t3, p.save_s2, p.save_s3, p.save_lse2};
+  int nsave = 0;
+  for (const void* q : sv) nsave += q != nullptr;
+  if (nsave != 0 && (nsave != 12 || p.ld_save % 8)) return ENCDIFF_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  // row tile: 64 rows (32 at c = 256); 16 when the batch is too small for it or the tile's images'
+  // concept-token K / V would not fit the LDS (the 2x2 middle block: 4 tokens per image)
+  // Few rows (sampling batches): 16-row tiles, so more CUs share the chain (at B = 8 the 64-row
+  // tile ran the c = 64 tail in 27 us on 32 CUs, the 16-row tile in 15 us on 128).
+  const int rdef = p.c == 256 ? 32 : 64;
+  int rc = ENCDIFF_ERR_SHAPE;
+  if (!(p.pad_ & 8) && p.rows / rdef >= 256)  // debug mask bit 3: force the 16-row tile
+  switch (p.c) {
+    case 64: rc = launch_tail<64, 64>(p, s); break;
+    case 128: rc = launch_tail<128, 64>(p, s); break;
+    default: rc = launch_tail<256, 32>(p, s); break;
+  }
+  if (rc != ENCDIFF_ERR_SHAPE) return rc;
+  switch (p.c) {
+    case 64: return launch_tail<64, 16>(p, s);
+    case 128: return launch_tail<128, 16>(p, s);
+    default: return launch_tail<256, 16>(p, s);
+  }
+}

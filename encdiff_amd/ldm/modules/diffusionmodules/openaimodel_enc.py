@@ -189,6 +189,7 @@ class UNetModel(nn.Module):
         c = context[0] if isinstance(context, (list, tuple)) else context
         c = c.reshape(x.shape[0], -1).float()
         ex = self.executor()
+        ex.infer = not torch.is_grad_enabled()  # inference-only fusions (no saved activations)
         if torch.is_grad_enabled():
             self._arena.attach_grads()
         return _UNetFn.apply(x.float(), timesteps.long(), c, ex)

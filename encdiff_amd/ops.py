@@ -547,6 +547,35 @@ def attention_bwd(q, k, v, o, lse, d_o, dq, dk, dv, batch, heads, sq, sk, dh, fp
     check(lib.encdiff_attention_bwd(C.byref(a), _s()), "encdiff_attention_bwd")
 
 
+def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps, save=None) -> bool:
+    """The row-local tail of a SpatialTransformer (attn1.to_out ... proj_out, attention.py:211-215,
+    250-261) as one kernel.  w: dict of the bf16 GEMM weights / fp32 biases and LayerNorm affines
+    (keys out1, b_out1, g2, be2, q2, out2, b_out2, g3, be3, ff1, b_ff1, ff2, b_ff2, po, b_po).
+    save: None (inference) or a dict of the training activations (t1 n2 q2 o2 t2 n3 f a t3 s2 s3
+    lse2).  Returns False when the shape is outside the fused kernel's support (the caller issues
+    the separate launches); any other error raises."""
+    a = L.StTailArgs(rows=rows, c=c, tokens=tokens, heads=heads, n_ctx=n_ctx, ln_eps=ln_eps,
+                     scale=(c // heads) ** -0.5,
+                     o1=_p(o1), ld_o1=_ld(o1), t0=_p(t0), ld_t0=_ld(t0), x=_p(x), ld_x=_ld(x),
+                     k2=_p(k2), v2=_p(v2), ld_kv=_ld(k2),
+                     w_out1=_p(w["out1"]), ld_out1=_ld(w["out1"]), b_out1=_p(w["b_out1"]),
+                     g2=_p(w["g2"]), be2=_p(w["be2"]), w_q2=_p(w["q2"]), ld_q2=_ld(w["q2"]),
+                     w_out2=_p(w["out2"]), ld_out2=_ld(w["out2"]), b_out2=_p(w["b_out2"]),
+                     g3=_p(w["g3"]), be3=_p(w["be3"]), w_ff1=_p(w["ff1"]), ld_ff1=_ld(w["ff1"]),
+                     b_ff1=_p(w["b_ff1"]), w_ff2=_p(w["ff2"]), ld_ff2=_ld(w["ff2"]), b_ff2=_p(w["b_ff2"]),
+                     w_po=_p(w["po"]), ld_po=_ld(w["po"]), b_po=_p(w["b_po"]), out=_p(out), ld_out=_ld(out))
+    if save is not None:
+        for k in ("t1", "n2", "q2", "o2", "t2", "n3", "f", "a", "t3", "s2", "s3", "lse2"):
+            setattr(a, "save_" + k, _p(save[k]))
+        a.ld_save = _ld(save["t1"])
+    rc = lib.encdiff_st_tail_fwd(C.byref(a), _s())
+    if rc in (-2, -3):
+        st_tail_fwd.declined = rc
+        return False
+    check(rc, "encdiff_st_tail_fwd")
+    return True
+
+
 # ------------------------------------------------------------------ elementwise
 def ew(op, x, y, x2=None, rows=None, cols=None, accumulate=False, resample=0, g: Optional[Geom] = None):
     rows = rows if rows is not None else y.shape[0]

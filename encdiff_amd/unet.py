@@ -39,6 +39,12 @@ ST_GN_EPS = 1e-6   # Normalize (attention.py:76-77)
 # GroupNorm kernel, for A/B runs)
 GN_FROM_PRODUCER = os.environ.get("ENCDIFF_GN_FROM_PRODUCER", "1") != "0"
 LN_EPS = 1e-5      # nn.LayerNorm default (attention.py:206-208)
+# the row-local SpatialTransformer tail (attn1.to_out .. proj_out) as one kernel
+# (encdiff_st_tail_fwd) in no-grad forwards (0: the separate launches, for A/B runs)
+ST_TAIL_FUSED = os.environ.get("ENCDIFF_ST_TAIL", "1") != "0"
+# widest level that uses it: at c = 256 one workgroup streams 2.6 MB of weights through one CU
+# (74 us at B = 8 against ~35 us for the separate launches, tools/st_tail_bench.py)
+ST_TAIL_MAXC = int(os.environ.get("ENCDIFF_ST_TAIL_MAXC", "128"))
 
 
 # --------------------------------------------------------------------------- spec
@@ -265,6 +271,7 @@ class UNetExecutor:
         self.B = None
         self._sets: Dict[int, dict] = {}
         self.split_requested = False  # data-parallel trainer: backward(split=True) via autograd
+        self.infer = False  # no backward follows the next forward (UNetModel.forward under no_grad)
         self._base_names = set(self.__dict__) | {"_base_names"}
         self.pack.repack()
 
@@ -548,13 +555,17 @@ class UNetExecutor:
         ops.linear_fwd(S["n1"], self.W(s.prefix + "qkv"), S["qkv"])
         q, k, v = S["qkv"][:, :c], S["qkv"][:, c:2 * c], S["qkv"][:, 2 * c:]
         ops.attention_fwd(q, k, v, S["o1"], S["lse1"], B, s.heads, ntok, ntok, s.dh, fp8=s.fp8)
+        k2 = self.KV[:, s.kv_off:s.kv_off + c]
+        v2 = self.KV[:, s.kv_off + c:s.kv_off + 2 * c]
+        if self.infer and ST_TAIL_FUSED and c <= ST_TAIL_MAXC and self._gst(S["out"]) is None:
+            if ops.st_tail_fwd(S["o1"], S["t0"], x, k2, v2, self._tail_weights(s), S["out"], B * ntok, c, ntok,
+                               s.heads, self.lu, LN_EPS):
+                return S["out"]
         # cross-attention to the concept tokens (norm2 in the to_out epilogue)
         ops.linear_fwd_ln(S["o1"], self.W(tb + "attn1.to_out.0.weight"), S["t1"], self.P(tb + "norm2.weight"),
                           self.P(tb + "norm2.bias"), S["n2"], S["s2"], LN_EPS,
                           bias=self.P(tb + "attn1.to_out.0.bias"), resid=S["t0"])
         ops.linear_fwd(S["n2"], self.W(tb + "attn2.to_q.weight"), S["q2"])
-        k2 = self.KV[:, s.kv_off:s.kv_off + c]
-        v2 = self.KV[:, s.kv_off + c:s.kv_off + 2 * c]
         ops.attention_fwd(S["q2"], k2, v2, S["o2"], S["lse2"], B, s.heads, ntok, self.lu, s.dh)
         # GEGLU feed-forward (norm3 in the to_out epilogue)
         ops.linear_fwd_ln(S["o2"], self.W(tb + "attn2.to_out.0.weight"), S["t2"], self.P(tb + "norm3.weight"),
@@ -567,6 +578,17 @@ class UNetExecutor:
         ops.linear_fwd(S["t3"], self.W(s.prefix + "proj_out.weight"), S["out"], bias=self.P(s.prefix + "proj_out.bias"),
                        resid=x, gn_stats=self._gst(S["out"]))
         return S["out"]
+
+    def _tail_weights(self, s: STSpec):
+        tb = s.prefix + "transformer_blocks.0."
+        W, P = self.W, self.P
+        return dict(out1=W(tb + "attn1.to_out.0.weight"), b_out1=P(tb + "attn1.to_out.0.bias"),
+                    g2=P(tb + "norm2.weight"), be2=P(tb + "norm2.bias"), q2=W(tb + "attn2.to_q.weight"),
+                    out2=W(tb + "attn2.to_out.0.weight"), b_out2=P(tb + "attn2.to_out.0.bias"),
+                    g3=P(tb + "norm3.weight"), be3=P(tb + "norm3.bias"),
+                    ff1=W(tb + "ff.net.0.proj.weight"), b_ff1=P(tb + "ff.net.0.proj.bias"),
+                    ff2=W(tb + "ff.net.2.weight"), b_ff2=P(tb + "ff.net.2.bias"),
+                    po=W(s.prefix + "proj_out.weight"), b_po=P(s.prefix + "proj_out.bias"))
 
     # ---------------------------------------------------------------- backward
     # ---------------------------------------------------------------- split backward (DP)

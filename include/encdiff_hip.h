@@ -437,6 +437,43 @@ int encdiff_nchw_to_rows(const float* x, int batch, int c, int hw, int cpad, voi
 int encdiff_nchw_to_rows_split3(const float* x, int batch, int c, int hw, int cpad, void* y, long ldy,
                                 void* stream);
 
+/* ---------------------------------------------------------------- SpatialTransformer tail
+ * Everything of a SpatialTransformer after its self-attention is row-local (attention.py:211-215,
+ * 250-261): t1 = to_out(o1) + t0; q2 = to_q(LN2(t1)); o2 = softmax(q2 k2^T * scale) v2 over the
+ * image's concept tokens; t2 = to_out(o2) + t1; f = proj(LN3(t2)); a = f_v * gelu(f_g);
+ * t3 = ff2(a) + t2; out = proj_out(t3) + x.  ONE kernel runs the chain for a tile of rows with
+ * the rows resident in LDS (fp32 residual stream) and the weights streamed from L2, instead of
+ * seven launches (GEMMs, cross-attention, LayerNorms).  Weights are the bf16 GEMM operands
+ * [out][in] (row stride ld_*); biases / LayerNorm affine fp32.  The save_* pointers (all NULL or
+ * all set) receive the activations the backward reads (training forward): t1, n2, q2, o2, t2,
+ * n3, f, a, t3 (bf16 [rows][..]), s2 / s3 (fp32 [rows][2] mean, rstd), lse2 (fp32
+ * [batch*heads][tokens], natural-log).  Supported: (c, heads) in {(64, 8), (128, 8), (256, 8)},
+ * n_ctx <= 64, rows a multiple of the row tile (64; 32 at c = 256) and tile / tokens nested;
+ * ENCDIFF_ERR_UNSUPPORTED / _SHAPE otherwise (the caller then issues the separate launches). */
+typedef struct EncdiffStTailArgs {
+  int rows, c, tokens, heads, n_ctx;
+  float ln_eps, scale;
+  int pad_;
+  const void* o1; long ld_o1;   /* self-attention output      */
+  const void* t0; long ld_t0;   /* proj_in output (residual)  */
+  const void* x; long ld_x;     /* block input (residual of proj_out) */
+  const void* k2; const void* v2; long ld_kv;  /* [batch*n_ctx][..] concept-token keys / values */
+  const void* w_out1; long ld_out1; const float* b_out1;
+  const float* g2; const float* be2;
+  const void* w_q2; long ld_q2;
+  const void* w_out2; long ld_out2; const float* b_out2;
+  const float* g3; const float* be3;
+  const void* w_ff1; long ld_ff1; const float* b_ff1;   /* [8c][c]: value rows, then gate rows */
+  const void* w_ff2; long ld_ff2; const float* b_ff2;   /* [c][4c] */
+  const void* w_po; long ld_po; const float* b_po;
+  void* out; long ld_out;
+  void* save_t1; void* save_n2; void* save_q2; void* save_o2; void* save_t2; void* save_n3;
+  void* save_f; void* save_a; void* save_t3; long ld_save; /* ld of the [rows][c] saves (f: 8c, a: 4c dense) */
+  float* save_s2; float* save_s3; float* save_lse2;
+} EncdiffStTailArgs;
+
+int encdiff_st_tail_fwd(const EncdiffStTailArgs* args, void* stream);
+
 /* Library/device information (for tests): returns the number of exported kernels. */
 int encdiff_version(void);
 
