@@ -405,6 +405,36 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
       *(uint4*)(og + (long)r * p.ld_out + c8) = pack8(f);
     }
   }
+  if constexpr (R == 64) {
+    if (p.gn_stats) {
+      // the next GroupNorm's statistics of this 64-row segment (gemm.hip's gn_stats layout): per
+      // column sum and sum of squares of the stored bf16 values, TPC row groups added in order
+      constexpr int TPC = 256 / C, RPG = R / TPC;
+      const int col = tid % C, grp = tid / C;
+      float a = 0.f, q = 0.f;
+#pragma unroll 4
+      for (int r = grp * RPG; r < (grp + 1) * RPG; ++r) {
+        const float v = bf16_round(Tr[r * LDT + col]);
+        a += v;
+        q += v * v;
+      }
+      float* red = (float*)Xa;  // free: the last GEMM read it before the barrier above
+      red[grp * C + col] = a;
+      red[(TPC + grp) * C + col] = q;
+      __syncthreads();
+      if (grp == 0) {
+        float sa = red[col], sq = red[TPC * C + col];
+#pragma unroll
+        for (int g = 1; g < TPC; ++g) {
+          sa += red[g * C + col];
+          sq += red[(TPC + g) * C + col];
+        }
+        const long slot = row0 >> 6;
+        p.gn_stats[(2 * slot) * p.ld_gn_stats + col] = sa;
+        p.gn_stats[(2 * slot + 1) * p.ld_gn_stats + col] = sq;
+      }
+    }
+  }
 }
 
 template <int C, int RR>
@@ -451,14 +481,16 @@ extern "C" int encdiff_st_tail_fwd(const EncdiffStTailArgs* a, void* stream) {
   // Few rows (sampling batches): 16-row tiles, so more CUs share the chain (at B = 8 the 64-row
   // tile ran the c = 64 tail in 27 us on 32 CUs, the 16-row tile in 15 us on 128).
   const int rdef = p.c == 256 ? 32 : 64;
+  if (p.gn_stats && (p.c == 256 || p.rows % 64 || p.ld_gn_stats < p.c)) return ENCDIFF_ERR_SHAPE;
   int rc = ENCDIFF_ERR_SHAPE;
-  if (!(p.pad_ & 8) && p.rows / rdef >= 256)  // debug mask bit 3: force the 16-row tile
+  // debug mask bit 3: force the 16-row tile; producer statistics need one 64-row tile per segment
+  if (p.gn_stats || (!(p.pad_ & 8) && p.rows / rdef >= 256))
   switch (p.c) {
     case 64: rc = launch_tail<64, 64>(p, s); break;
     case 128: rc = launch_tail<128, 64>(p, s); break;
     default: rc = launch_tail<256, 32>(p, s); break;
   }
-  if (rc != ENCDIFF_ERR_SHAPE) return rc;
+  if (rc != ENCDIFF_ERR_SHAPE || p.gn_stats) return rc;
   switch (p.c) {
     case 64: return launch_tail<64, 16>(p, s);
     case 128: return launch_tail<128, 16>(p, s);

@@ -547,7 +547,8 @@ def attention_bwd(q, k, v, o, lse, d_o, dq, dk, dv, batch, heads, sq, sk, dh, fp
     check(lib.encdiff_attention_bwd(C.byref(a), _s()), "encdiff_attention_bwd")
 
 
-def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps, save=None) -> bool:
+def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps, save=None,
+                gn_stats=None) -> bool:
     """The row-local tail of a SpatialTransformer (attn1.to_out ... proj_out, attention.py:211-215,
     250-261) as one kernel.  w: dict of the bf16 GEMM weights / fp32 biases and LayerNorm affines
     (keys out1, b_out1, g2, be2, q2, out2, b_out2, g3, be3, ff1, b_ff1, ff2, b_ff2, po, b_po).
@@ -568,6 +569,8 @@ def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps
         for k in ("t1", "n2", "q2", "o2", "t2", "n3", "f", "a", "t3", "s2", "s3", "lse2"):
             setattr(a, "save_" + k, _p(save[k]))
         a.ld_save = _ld(save["t1"])
+    if gn_stats is not None:  # the next GroupNorm's producer statistics of out
+        a.gn_stats, a.ld_gn_stats = _p(gn_stats), _ld(gn_stats)
     rc = lib.encdiff_st_tail_fwd(C.byref(a), _s())
     if rc in (-2, -3):
         st_tail_fwd.declined = rc

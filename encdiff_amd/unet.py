@@ -45,6 +45,8 @@ ST_TAIL_FUSED = os.environ.get("ENCDIFF_ST_TAIL", "1") != "0"
 # widest level that uses it: at c = 256 one workgroup streams 2.6 MB of weights through one CU
 # (74 us at B = 8 against ~35 us for the separate launches, tools/st_tail_bench.py)
 ST_TAIL_MAXC = int(os.environ.get("ENCDIFF_ST_TAIL_MAXC", "128"))
+# ... also in the training forward, writing the activations the backward reads
+ST_TAIL_TRAIN = os.environ.get("ENCDIFF_ST_TAIL_TRAIN", "1") != "0"
 
 
 # --------------------------------------------------------------------------- spec
@@ -557,9 +559,13 @@ class UNetExecutor:
         ops.attention_fwd(q, k, v, S["o1"], S["lse1"], B, s.heads, ntok, ntok, s.dh, fp8=s.fp8)
         k2 = self.KV[:, s.kv_off:s.kv_off + c]
         v2 = self.KV[:, s.kv_off + c:s.kv_off + 2 * c]
-        if self.infer and ST_TAIL_FUSED and c <= ST_TAIL_MAXC and self._gst(S["out"]) is None:
+        if ST_TAIL_FUSED and c <= ST_TAIL_MAXC and (self.infer or ST_TAIL_TRAIN):
+            save = None if self.infer else {k: S[k] for k in ("t1", "n2", "q2", "o2", "t2", "n3", "f", "a", "t3",
+                                                             "s2", "s3")}
+            if save is not None:
+                save["lse2"] = S["lse2"]
             if ops.st_tail_fwd(S["o1"], S["t0"], x, k2, v2, self._tail_weights(s), S["out"], B * ntok, c, ntok,
-                               s.heads, self.lu, LN_EPS):
+                               s.heads, self.lu, LN_EPS, save=save, gn_stats=self._gst(S["out"])):
                 return S["out"]
         # cross-attention to the concept tokens (norm2 in the to_out epilogue)
         ops.linear_fwd_ln(S["o1"], self.W(tb + "attn1.to_out.0.weight"), S["t1"], self.P(tb + "norm2.weight"),

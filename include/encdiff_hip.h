@@ -470,6 +470,8 @@ typedef struct EncdiffStTailArgs {
   void* save_t1; void* save_n2; void* save_q2; void* save_o2; void* save_t2; void* save_n3;
   void* save_f; void* save_a; void* save_t3; long ld_save; /* ld of the [rows][c] saves (f: 8c, a: 4c dense) */
   float* save_s2; float* save_s3; float* save_lse2;
+  float* gn_stats; long ld_gn_stats;  /* optional: the next GroupNorm's producer statistics of out
+                                         (EncdiffGemmArgs.gn_stats layout; needs rows % 64 == 0) */
 } EncdiffStTailArgs;
 
 int encdiff_st_tail_fwd(const EncdiffStTailArgs* args, void* stream);
