@@ -113,6 +113,15 @@ class StTailArgs(C.Structure):
                 ("save_s2", vp), ("save_s3", vp), ("save_lse2", vp), ("gn_stats", vp), ("ld_gn_stats", C.c_long)]
 
 
+class StHeadArgs(C.Structure):
+    _fields_ = [("rows", C.c_int), ("c", C.c_int), ("tokens", C.c_int), ("pad_", C.c_int),
+                ("gn_eps", C.c_float), ("ln_eps", C.c_float), ("x", vp), ("ld_x", C.c_long),
+                ("gn_in_stats", vp), ("ld_gn_in_stats", C.c_long), ("gn_gamma", vp), ("gn_beta", vp),
+                ("gn", vp), ("ld_gn", C.c_long), ("gn_stats", vp), ("w_in", vp), ("ld_in", C.c_long), ("b_in", vp),
+                ("g1", vp), ("be1", vp), ("w_qkv", vp), ("ld_w_qkv", C.c_long), ("t0", vp), ("ld_t0", C.c_long),
+                ("n1", vp), ("ld_n1", C.c_long), ("s1", vp), ("qkv", vp), ("ld_qkv", C.c_long)]
+
+
 class PackJob(C.Structure):
     _fields_ = [("src_off", C.c_longlong), ("dst_off", C.c_longlong), ("rows", C.c_int), ("cols", C.c_int),
                 ("kind", C.c_int), ("cin", C.c_int)]
@@ -153,6 +162,7 @@ _PROTOS = {
     "encdiff_nchw_to_rows": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_long, vp],
     "encdiff_nchw_to_rows_split3": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_long, vp],
     "encdiff_st_tail_fwd": [C.POINTER(StTailArgs), vp],
+    "encdiff_st_head_fwd": [C.POINTER(StHeadArgs), vp],
     "encdiff_version": [],
 }
 

@@ -452,6 +452,128 @@ int launch_tail(const EncdiffStTailArgs& p, hipStream_t s) {
   return ENCDIFF_OK;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// The head: gn = GroupNorm(x) (from producer segment sums) or read, t0 = proj_in(gn) + b,
+// n1 = LN1(t0), qkv = n1 Wqkv^T -- row-local once the GroupNorm statistics are known.
+template <int C, int RR>
+__global__ __launch_bounds__(256) void st_head_kernel(const EncdiffStHeadArgs p) {
+  constexpr int R = RR, TM = R / 16, NT = C / 64, NT3 = 3 * C / 64, LDT = C + 4, LDX = C + 8, LDQ = 3 * C + 8;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  float* Tr = (float*)smem_raw;
+  bf16_t* Xa = (bf16_t*)(Tr + R * LDT);
+  bf16_t* Xq = Xa + R * LDX;                          // [R][3C] qkv staging
+  float* gms = (float*)(Xq + R * LDQ);                // [nimg][32][2] GroupNorm mean, rstd
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row0 = blockIdx.x * R;
+  const int img0 = row0 / p.tokens;
+  const int nimg = R > p.tokens ? R / p.tokens : 1;
+  const int n0 = wave * (C / 4), n03 = wave * (3 * C / 4);
+  BFrags<NT, C> win;
+  BFrags<NT3, C> wq;
+  load_b(win, (const bf16_t*)p.w_in, p.ld_in, n0, 0, lane);
+  load_b(wq, (const bf16_t*)p.w_qkv, p.ld_w_qkv, n03, 0, lane);
+  constexpr int CH = C / 8;
+  if (p.gn_in_stats) {
+    // per (image, group) statistics from the producer's 64-row segment sums (as gn_fwd_stats_kernel)
+    constexpr int cpg = C / 32;
+    const int nseg = p.tokens >> 6;
+    if (tid < nimg * 32) {
+      const int i = tid >> 5, g = tid & 31;
+      float a = 0.f, q = 0.f;
+      for (int sg = 0; sg < nseg; ++sg) {
+        const float* st = p.gn_in_stats + 2 * ((long)(img0 + i) * nseg + sg) * p.ld_gn_in_stats + g * cpg;
+        for (int c = 0; c < cpg; ++c) {
+          a += st[c];
+          q += st[p.ld_gn_in_stats + c];
+        }
+      }
+      const float inv_n = 1.f / ((float)p.tokens * cpg);
+      const float mean = a * inv_n;
+      const float rstd = rsqrtf(fmaxf(q * inv_n - mean * mean, 0.f) + p.gn_eps);
+      gms[2 * tid] = mean;
+      gms[2 * tid + 1] = rstd;
+      if (p.gn_stats && (row0 + i * p.tokens) % p.tokens == 0) {  // this block holds the image's first row
+        p.gn_stats[2 * ((long)(img0 + i) * 32 + g)] = mean;
+        p.gn_stats[2 * ((long)(img0 + i) * 32 + g) + 1] = rstd;
+      }
+    }
+    __syncthreads();
+    const bf16_t* xg = (const bf16_t*)p.x + (long)row0 * p.ld_x;
+    bf16_t* gg = (bf16_t*)p.gn + (long)row0 * p.ld_gn;
+    for (int e = tid; e < R * CH; e += 256) {
+      const int r = e / CH, c8 = (e - r * CH) * 8, i = (row0 + r) / p.tokens - img0;
+      float v[8];
+      unpack8(*(const uint4*)(xg + (long)r * p.ld_x + c8), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = c8 + k, g = c / cpg;
+        const float a = gms[2 * (i * 32 + g) + 1] * p.gn_gamma[c];
+        v[k] = v[k] * a + (p.gn_beta[c] - gms[2 * (i * 32 + g)] * a);
+      }
+      const uint4 y = pack8(v);
+      *(uint4*)(Xa + r * LDX + c8) = y;
+      *(uint4*)(gg + (long)r * p.ld_gn + c8) = y;
+    }
+  } else {
+    rows_to_lds<C, R>(Xa, LDX, (const bf16_t*)p.gn + (long)row0 * p.ld_gn, p.ld_gn, tid);
+  }
+  __syncthreads();
+  // ---- t0 = gn Win^T + b  (fp32 stream in Tr, bf16 t0 out)
+  v4f acc[TM][NT];
+  zero(acc);
+  mma(acc, Xa, LDX, win, lane);
+  {
+    const int l16 = lane & 15, g4 = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int col = n0 + 16 * j + l16;
+      const float bv = p.b_in[col];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Tr[(16 * i + 4 * g4 + q) * LDT + col] = acc[i][j][q] + bv;
+    }
+  }
+  __syncthreads();
+  // ---- n1 = LN1(t0) -> Xa (t0 saved as its bf16 rounding, which the LayerNorm reads)
+  ln_rows<C, R>(Tr, LDT, Xa, LDX, p.g1, p.be1, p.ln_eps, tid, p.n1 ? (bf16_t*)p.n1 + (long)row0 * p.ld_n1 : nullptr,
+                p.ld_n1, p.n1 ? (bf16_t*)p.t0 + (long)row0 * p.ld_t0 : nullptr, p.s1 ? p.s1 + 2L * row0 : nullptr);
+  if (!p.n1) {  // inference: t0 is still the tail's residual input
+    bf16_t* tg = (bf16_t*)p.t0 + (long)row0 * p.ld_t0;
+    for (int e = tid; e < R * CH; e += 256) {
+      const int r = e / CH, c8 = (e - r * CH) * 8;
+      float f[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = Tr[r * LDT + c8 + k];
+      *(uint4*)(tg + (long)r * p.ld_t0 + c8) = pack8(f);
+    }
+  }
+  __syncthreads();
+  // ---- qkv = n1 Wqkv^T  (staged through LDS for 16-byte stores)
+  v4f aq[TM][NT3];
+  zero(aq);
+  mma(aq, Xa, LDX, wq, lane);
+  acc_store_bf(aq, Xq, LDQ, n03, lane);
+  __syncthreads();
+  rows_to_global<3 * C, R>((bf16_t*)p.qkv + (long)row0 * p.ld_qkv, p.ld_qkv, Xq, LDQ, tid);
+}
+
+template <int C, int RR>
+int launch_head(const EncdiffStHeadArgs& p, hipStream_t s) {
+  constexpr int R = RR;
+  if (p.rows % R || (R % p.tokens && p.tokens % R)) return ENCDIFF_ERR_SHAPE;
+  const int nimg = R > p.tokens ? R / p.tokens : 1;
+  const size_t lds = (size_t)R * (C + 4) * 4 + (size_t)R * (C + 8) * 2 + (size_t)R * (3 * C + 8) * 2 + nimg * 64 * 4;
+  if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
+  static const hipError_t attr_ok = hipFuncSetAttribute((const void*)st_head_kernel<C, RR>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr_ok != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)attr_ok;
+  hipLaunchKernelGGL((st_head_kernel<C, RR>), dim3((unsigned)(p.rows / R)), dim3(256), lds, s, p);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
 bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
 }  // namespace
@@ -496,4 +618,27 @@ extern "C" int encdiff_st_tail_fwd(const EncdiffStTailArgs* a, void* stream) {
     case 128: return launch_tail<128, 16>(p, s);
     default: return launch_tail<256, 16>(p, s);
   }
+}
+
+extern "C" int encdiff_st_head_fwd(const EncdiffStHeadArgs* a, void* stream) {
+  if (!a) return ENCDIFF_ERR_ARG;
+  const EncdiffStHeadArgs& p = *a;
+  if (p.c != 64 && p.c != 128) return ENCDIFF_ERR_UNSUPPORTED;
+  if (p.tokens < 1 || p.rows < 1 || p.rows % p.tokens) return ENCDIFF_ERR_SHAPE;
+  if (p.gn_in_stats && (p.tokens % 64 || p.ld_gn_in_stats < p.c || !p.x || !al16(p.x) || p.ld_x % 8))
+    return ENCDIFF_ERR_SHAPE;
+  const void* ptrs[] = {p.gn, p.w_in, p.w_qkv, p.t0, p.qkv};
+  for (const void* q : ptrs)
+    if (!q || !al16(q)) return ENCDIFF_ERR_ARG;
+  const long lds[] = {p.ld_gn, p.ld_in, p.ld_w_qkv, p.ld_t0, p.ld_qkv};
+  for (long l : lds)
+    if (l % 8) return ENCDIFF_ERR_ARG;
+  if (!p.b_in || !p.g1 || !p.be1 || (p.gn_in_stats && (!p.gn_gamma || !p.gn_beta))) return ENCDIFF_ERR_ARG;
+  if ((p.n1 != nullptr) != (p.s1 != nullptr) || (p.n1 && p.ld_n1 % 8)) return ENCDIFF_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  // 64-row tiles at training batches, 16 rows when that leaves most CUs idle (sampling)
+  const bool big = p.rows / 64 >= 256;
+  int rc = big ? (p.c == 64 ? launch_head<64, 64>(p, s) : launch_head<128, 64>(p, s)) : ENCDIFF_ERR_SHAPE;
+  if (rc != ENCDIFF_ERR_SHAPE) return rc;
+  return p.c == 64 ? launch_head<64, 16>(p, s) : launch_head<128, 16>(p, s);
 }

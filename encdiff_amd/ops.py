@@ -579,6 +579,27 @@ def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps
     return True
 
 
+def st_head_fwd(x, gn, w_in, b_in, g1, be1, w_qkv, t0, qkv, rows, c, tokens, gn_eps, ln_eps, in_stats=None,
+                gn_gamma=None, gn_beta=None, gn_stats=None, n1=None, s1=None) -> bool:
+    """The row-local head of a SpatialTransformer (attention.py:250-254, 211) as one kernel:
+    gn = GroupNorm32(x) from the producer's segment sums `in_stats` (else `gn` is read, already
+    computed), t0 = proj_in(gn), n1 = LN1(t0) (saved with s1 when given), qkv = n1 Wqkv^T.
+    Returns False outside the kernel's support (the caller issues the separate launches)."""
+    a = L.StHeadArgs(rows=rows, c=c, tokens=tokens, gn_eps=gn_eps, ln_eps=ln_eps, x=_p(x), ld_x=_ld(x),
+                     gn=_p(gn), ld_gn=_ld(gn), w_in=_p(w_in), ld_in=_ld(w_in), b_in=_p(b_in), g1=_p(g1), be1=_p(be1),
+                     w_qkv=_p(w_qkv), ld_w_qkv=_ld(w_qkv), t0=_p(t0), ld_t0=_ld(t0), qkv=_p(qkv), ld_qkv=_ld(qkv))
+    if in_stats is not None:
+        a.gn_in_stats, a.ld_gn_in_stats = _p(in_stats), _ld(in_stats)
+        a.gn_gamma, a.gn_beta, a.gn_stats = _p(gn_gamma), _p(gn_beta), _p(gn_stats)
+    if n1 is not None:
+        a.n1, a.ld_n1, a.s1 = _p(n1), _ld(n1), _p(s1)
+    rc = lib.encdiff_st_head_fwd(C.byref(a), _s())
+    if rc in (-2, -3):
+        return False
+    check(rc, "encdiff_st_head_fwd")
+    return True
+
+
 # ------------------------------------------------------------------ elementwise
 def ew(op, x, y, x2=None, rows=None, cols=None, accumulate=False, resample=0, g: Optional[Geom] = None):
     rows = rows if rows is not None else y.shape[0]

@@ -549,12 +549,25 @@ class UNetExecutor:
         g = Geom(B, s.h, s.h)
         tb = s.prefix + "transformer_blocks.0."
         ntok = s.h * s.h
-        ops.groupnorm_fwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["gn"], S["stg"],
-                          ST_GN_EPS, False, in_stats=self._gst(x))
-        # proj_in, then norm1 in its epilogue (self-attention input)
-        ops.linear_fwd_ln(S["gn"], self.W(s.prefix + "proj_in.weight"), S["t0"], self.P(tb + "norm1.weight"),
-                          self.P(tb + "norm1.bias"), S["n1"], S["s1"], LN_EPS, bias=self.P(s.prefix + "proj_in.bias"))
-        ops.linear_fwd(S["n1"], self.W(s.prefix + "qkv"), S["qkv"])
+        fused = ST_TAIL_FUSED and c <= ST_TAIL_MAXC and (self.infer or ST_TAIL_TRAIN)
+        in_st = self._gst(x)
+        if fused and in_st is None:  # no producer statistics: the GroupNorm kernel reduces them
+            ops.groupnorm_fwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["gn"],
+                              S["stg"], ST_GN_EPS, False)
+        # GroupNorm (from producer statistics) + proj_in + norm1 + q/k/v as one kernel
+        if not (fused and ops.st_head_fwd(
+                x, S["gn"], self.W(s.prefix + "proj_in.weight"), self.P(s.prefix + "proj_in.bias"),
+                self.P(tb + "norm1.weight"), self.P(tb + "norm1.bias"), self.W(s.prefix + "qkv"), S["t0"], S["qkv"],
+                B * ntok, c, ntok, ST_GN_EPS, LN_EPS, in_stats=in_st, gn_gamma=self.P(s.prefix + "norm.weight"),
+                gn_beta=self.P(s.prefix + "norm.bias"), gn_stats=S["stg"], n1=None if self.infer else S["n1"],
+                s1=None if self.infer else S["s1"])):
+            if not fused or in_st is not None:
+                ops.groupnorm_fwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["gn"],
+                                  S["stg"], ST_GN_EPS, False, in_stats=in_st)
+            # proj_in, then norm1 in its epilogue (self-attention input)
+            ops.linear_fwd_ln(S["gn"], self.W(s.prefix + "proj_in.weight"), S["t0"], self.P(tb + "norm1.weight"),
+                              self.P(tb + "norm1.bias"), S["n1"], S["s1"], LN_EPS, bias=self.P(s.prefix + "proj_in.bias"))
+            ops.linear_fwd(S["n1"], self.W(s.prefix + "qkv"), S["qkv"])
         q, k, v = S["qkv"][:, :c], S["qkv"][:, c:2 * c], S["qkv"][:, 2 * c:]
         ops.attention_fwd(q, k, v, S["o1"], S["lse1"], B, s.heads, ntok, ntok, s.dh, fp8=s.fp8)
         k2 = self.KV[:, s.kv_off:s.kv_off + c]

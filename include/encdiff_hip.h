@@ -476,6 +476,30 @@ typedef struct EncdiffStTailArgs {
 
 int encdiff_st_tail_fwd(const EncdiffStTailArgs* args, void* stream);
 
+/* The row-local head of a SpatialTransformer (attention.py:250-254, 211): gn = GroupNorm32(x)
+ * (from the producer's segment sums gn_in_stats, EncdiffGemmArgs.gn_stats layout, when given --
+ * then gn and the per-(image, group) mean / rstd gn_stats are written; else gn is read, computed
+ * by encdiff_groupnorm_fwd), t0 = proj_in(gn), n1 = LN1(t0), qkv = n1 [Wq; Wk; Wv]^T, as one kernel
+ * (c in {64, 128}).  n1 / s1 optional (training saves).  Replaces up to three launches. */
+typedef struct EncdiffStHeadArgs {
+  int rows, c, tokens, pad_;
+  float gn_eps, ln_eps;
+  const void* x; long ld_x;
+  const float* gn_in_stats; long ld_gn_in_stats;
+  const float* gn_gamma; const float* gn_beta;
+  void* gn; long ld_gn;
+  float* gn_stats;                  /* [batch][32][2] (with gn_in_stats) */
+  const void* w_in; long ld_in; const float* b_in;
+  const float* g1; const float* be1;
+  const void* w_qkv; long ld_w_qkv; /* [3c][c] */
+  void* t0; long ld_t0;
+  void* n1; long ld_n1;
+  float* s1;                        /* [rows][2] mean, rstd */
+  void* qkv; long ld_qkv;
+} EncdiffStHeadArgs;
+
+int encdiff_st_head_fwd(const EncdiffStHeadArgs* args, void* stream);
+
 /* Library/device information (for tests): returns the number of exported kernels. */
 int encdiff_version(void);
 

@@ -32,7 +32,7 @@ STRUCTS = {
     "EncdiffConvGeom": "ConvGeom", "EncdiffGemmArgs": "GemmArgs", "EncdiffGroupNormArgs": "GroupNormArgs",
     "EncdiffLayerNormArgs": "LayerNormArgs", "EncdiffAttnArgs": "AttnArgs", "EncdiffEwArgs": "EwArgs",
     "EncdiffSmallConvArgs": "SmallConvArgs", "EncdiffPackJob": "PackJob", "EncdiffBatchNormArgs": "BatchNormArgs",
-    "EncdiffStTailArgs": "StTailArgs",
+    "EncdiffStTailArgs": "StTailArgs", "EncdiffStHeadArgs": "StHeadArgs",
 }
 
 

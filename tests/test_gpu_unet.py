@@ -130,7 +130,7 @@ def test_unet_split_backward_bitwise(unet):
 
 
 def test_st_tail_fused_inference(unet, golden_dir):
-    """No-grad forwards run each SpatialTransformer's row-local tail (attn1.to_out .. proj_out,
+    """No-grad forwards run each SpatialTransformer's row-local head (proj_in, norm1, q/k/v) and tail (attn1.to_out .. proj_out,
     attention.py:211-215, 250-261) as ONE kernel (encdiff_st_tail_fwd).  It must match the
     reference fixture like the unfused path (eps rel-L2 <= 3e-2, max-abs <= 6e-2), agree with
     the separate launches within the same bound, and actually run for every transformer at B=4 and B=8."""
@@ -147,6 +147,14 @@ def test_st_tail_fused_inference(unet, golden_dir):
             print("fused tail declined: rows, c, tokens, heads, n_ctx =", a[7:12])
         return ok
     ops.st_tail_fwd = counted
+    heads = []
+    orig_head = ops.st_head_fwd
+
+    def counted_head(*a, **k):
+        ok = orig_head(*a, **k)
+        heads.append(ok)
+        return ok
+    ops.st_head_fwd = counted_head
     maxc = U.ST_TAIL_MAXC
     U.ST_TAIL_MAXC = 256  # every width the kernel supports (the default leaves c = 256 unfused)
     try:
@@ -159,6 +167,7 @@ def test_st_tail_fused_inference(unet, golden_dir):
                 t = torch.randint(0, 1000, (B,), generator=g).cuda()
                 ctx = (torch.randn(B, 320, generator=g) * 0.5).cuda()
             calls.clear()
+            heads.clear()
             with torch.no_grad():
                 U.ST_TAIL_FUSED = True
                 e_f = unet(x, t, context=[ctx]).float().cpu()
@@ -166,6 +175,7 @@ def test_st_tail_fused_inference(unet, golden_dir):
                 U.ST_TAIL_FUSED = False
                 e_u = unet(x, t, context=[ctx]).float().cpu()
             assert n_st == 16 and all(calls[:n_st]), calls
+            assert sum(heads) == 10, heads  # the fused head runs at c in {64, 128}
             ref = torch.tensor(fx["eps"]) if B == 4 else O.unet_forward(
                 O.recipe_params(O.param_shapes(O.build_plan())), O.build_plan(), x.cpu(), t.cpu(), [ctx.cpu()])
             r_ref, r_unf = rel(e_f, ref), rel(e_f, e_u)
@@ -177,5 +187,6 @@ def test_st_tail_fused_inference(unet, golden_dir):
             assert r_unf < EPS_TOL
     finally:
         ops.st_tail_fwd = orig
+        ops.st_head_fwd = orig_head
         U.ST_TAIL_FUSED = True
         U.ST_TAIL_MAXC = maxc
