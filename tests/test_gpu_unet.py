@@ -5,7 +5,7 @@ Pinned two ways:
      (fp32, CPU) on name-seeded weights (tools/gen_golden.py);
   2. against the CPU oracle (oracle/encdiff_oracle.py) on fresh seeded inputs.
 Tolerance (bf16 activations / fp32 accumulation vs an fp32 reference, stated in
-north_star terms): eps rel-L2 <= 3e-2; gradients rel-L2 <= 5e-2.
+north_star terms): eps rel-L2 <= 3e-2 and max-abs <= 6e-2; gradients rel-L2 <= 5e-2.
 """
 import os
 
@@ -16,6 +16,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 EPS_TOL = 3e-2
+MAXABS_TOL = 6e-2  # bf16 acceptance is rel-L2 <= 3e-2 AND max-abs <= 6e-2
 GRAD_TOL = 5e-2
 
 
@@ -45,8 +46,9 @@ def test_unet_matches_reference_fixture(unet, golden_dir):
     unet._arena.zero_grad()
     eps = unet(x, t, context=[ctx])
     e = rel(eps.detach(), fx["eps"])
-    print("eps rel-L2 vs reference:", e)
-    assert e < EPS_TOL
+    mab = (eps.detach().cpu() - torch.tensor(fx["eps"])).abs().max().item()
+    print("eps rel-L2 vs reference:", e, "max-abs", mab)
+    assert e < EPS_TOL and mab < MAXABS_TOL
     eps.backward(torch.tensor(fx["gout"]).cuda())
     d = rel(ctx.grad, fx["dctx"])
     print("d(context) rel-L2:", d)
@@ -71,8 +73,9 @@ def test_unet_matches_oracle_b16(unet):
         ref = O.unet_forward(P, O.build_plan(), x, t, [ctx])
         out = unet(x.cuda(), t.cuda(), context=[ctx.cuda()])
     e = rel(out, ref)
-    print("eps rel-L2 vs oracle (B=16):", e)
-    assert e < EPS_TOL
+    mab = (out.cpu() - ref).abs().max().item()
+    print("eps rel-L2 vs oracle (B=16):", e, "max-abs", mab)
+    assert e < EPS_TOL and mab < MAXABS_TOL
 
 
 def test_unet_deterministic(unet):
