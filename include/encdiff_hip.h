@@ -453,7 +453,7 @@ int encdiff_nchw_to_rows_split3(const float* x, int batch, int c, int hw, int cp
 typedef struct EncdiffStTailArgs {
   int rows, c, tokens, heads, n_ctx;
   float ln_eps, scale;
-  int pad_;
+  int pad_;                     /* 0; timing experiments only (tools/st_tail_bench.py): stage mask */
   const void* o1; long ld_o1;   /* self-attention output      */
   const void* t0; long ld_t0;   /* proj_in output (residual)  */
   const void* x; long ld_x;     /* block input (residual of proj_out) */
