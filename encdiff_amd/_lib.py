@@ -110,7 +110,8 @@ class StTailArgs(C.Structure):
                 ("out", vp), ("ld_out", C.c_long),
                 ("save_t1", vp), ("save_n2", vp), ("save_q2", vp), ("save_o2", vp), ("save_t2", vp),
                 ("save_n3", vp), ("save_f", vp), ("save_a", vp), ("save_t3", vp), ("ld_save", C.c_long),
-                ("save_s2", vp), ("save_s3", vp), ("save_lse2", vp), ("gn_stats", vp), ("ld_gn_stats", C.c_long)]
+                ("save_s2", vp), ("save_s3", vp), ("save_lse2", vp), ("gn_stats", vp), ("ld_gn_stats", C.c_long),
+                ("gn_stats_add", C.c_int), ("pad2_", C.c_int)]
 
 
 class StHeadArgs(C.Structure):

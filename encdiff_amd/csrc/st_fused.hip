@@ -405,10 +405,12 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
       *(uint4*)(og + (long)r * p.ld_out + c8) = pack8(f);
     }
   }
-  if constexpr (R == 64) {
+  if constexpr (R == 64 || R == 32) {
     if (p.gn_stats) {
       // the next GroupNorm's statistics of this 64-row segment (gemm.hip's gn_stats layout): per
-      // column sum and sum of squares of the stored bf16 values, TPC row groups added in order
+      // column sum and sum of squares of the stored bf16 values, TPC row groups added in order;
+      // a 32-row tile adds its half of the segment into the zeroed slot (gn_stats_add: with two
+      // addends 0 + a + b has the same bits in either order)
       constexpr int TPC = 256 / C, RPG = R / TPC;
       const int col = tid % C, grp = tid / C;
       float a = 0.f, q = 0.f;
@@ -430,8 +432,13 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
           sq += red[(TPC + g) * C + col];
         }
         const long slot = row0 >> 6;
-        p.gn_stats[(2 * slot) * p.ld_gn_stats + col] = sa;
-        p.gn_stats[(2 * slot + 1) * p.ld_gn_stats + col] = sq;
+        if constexpr (R == 64) {
+          p.gn_stats[(2 * slot) * p.ld_gn_stats + col] = sa;
+          p.gn_stats[(2 * slot + 1) * p.ld_gn_stats + col] = sq;
+        } else {
+          atomicAdd(p.gn_stats + (2 * slot) * p.ld_gn_stats + col, sa);
+          atomicAdd(p.gn_stats + (2 * slot + 1) * p.ld_gn_stats + col, sq);
+        }
       }
     }
   }
@@ -606,6 +613,8 @@ extern "C" int encdiff_st_tail_fwd(const EncdiffStTailArgs* a, void* stream) {
   if (p.gn_stats && (p.c == 256 || p.rows % 64 || p.ld_gn_stats < p.c)) return ENCDIFF_ERR_SHAPE;
   int rc = ENCDIFF_ERR_SHAPE;
   // debug mask bit 3: force the 16-row tile; producer statistics need one 64-row tile per segment
+  if (p.gn_stats && p.gn_stats_add && p.c == 128 && p.rows / 64 < 256)
+    return launch_tail<128, 32>(p, s);  // 8x8 level at B = 128: 256 workgroups instead of 128
   if (p.gn_stats || (!(p.pad_ & 8) && p.rows / rdef >= 256))
   switch (p.c) {
     case 64: rc = launch_tail<64, 64>(p, s); break;

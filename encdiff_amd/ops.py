@@ -547,6 +547,9 @@ def attention_bwd(q, k, v, o, lse, d_o, dq, dk, dv, batch, heads, sq, sk, dh, fp
     check(lib.encdiff_attention_bwd(C.byref(a), _s()), "encdiff_attention_bwd")
 
 
+ST_TAIL_STATS_ADD = os.environ.get("ENCDIFF_ST_TAIL_STATS_ADD", "1") != "0"
+
+
 def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps, save=None,
                 gn_stats=None) -> bool:
     """The row-local tail of a SpatialTransformer (attn1.to_out ... proj_out, attention.py:211-215,
@@ -571,6 +574,10 @@ def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps
         a.ld_save = _ld(save["t1"])
     if gn_stats is not None:  # the next GroupNorm's producer statistics of out
         a.gn_stats, a.ld_gn_stats = _p(gn_stats), _ld(gn_stats)
+        if c == 128 and rows // 64 < 256 and ST_TAIL_STATS_ADD:
+            # two 32-row tiles per 64-row segment add into the zeroed slots (twice the workgroups)
+            gn_stats[:, :c].zero_()  # only this tensor's columns (the view may span a concat's other producer)
+            a.gn_stats_add = 1
     rc = lib.encdiff_st_tail_fwd(C.byref(a), _s())
     if rc in (-2, -3):
         st_tail_fwd.declined = rc

@@ -472,6 +472,11 @@ typedef struct EncdiffStTailArgs {
   float* save_s2; float* save_s3; float* save_lse2;
   float* gn_stats; long ld_gn_stats;  /* optional: the next GroupNorm's producer statistics of out
                                          (EncdiffGemmArgs.gn_stats layout; needs rows % 64 == 0) */
+  int gn_stats_add;                   /* 1: gn_stats is zeroed by the caller and two 32-row tiles
+                                         add their halves of a segment atomically (0 + a + b: the
+                                         same bits in either order) -- twice the workgroups when a
+                                         64-row tile would leave CUs idle; 0: written by one tile */
+  int pad2_;
 } EncdiffStTailArgs;
 
 int encdiff_st_tail_fwd(const EncdiffStTailArgs* args, void* stream);
