@@ -109,13 +109,13 @@ ED_DEV void acc_store_bf(const v4f (&acc)[TM][NT], bf16_t* X, int ldx, int n0, i
 // LayerNorm of the R residual rows (fp32, LDS) into the bf16 operand buffer; optional saves.  The
 // statistics are those of the bf16-rounded rows (the tensor the unfused path stores and its
 // LayerNorm backward re-reads); the residual stream itself stays fp32.
-template <int C, int R>
+template <int C, int R, int NTH = 256>
 ED_DEV void ln_rows(const float* Tr, int ldt, bf16_t* X, int ldx, const float* __restrict__ g,
                     const float* __restrict__ b, float eps, int tid, bf16_t* save_y, long ld_save,
                     bf16_t* save_x, float* save_s) {
   // all R rows at once: TPR consecutive lanes per row, each owning float4 chunks k, k + TPR, ...
   // (a row per wave with 64-lane butterflies serialised R/4 rows of ds_bpermute round trips)
-  constexpr int TPR = 256 / R, NQ = C / (4 * TPR);
+  constexpr int TPR = NTH / R, NQ = C / (4 * TPR);
   const int r = tid / TPR, k = tid % TPR;
   float v[NQ][4], s = 0.f;
 #pragma unroll
@@ -156,27 +156,30 @@ ED_DEV void ln_rows(const float* Tr, int ldt, bf16_t* X, int ldx, const float* _
 }
 
 // copy R rows x C bf16 between global and LDS (16-byte chunks)
-template <int C, int R>
+template <int C, int R, int NTH = 256>
 ED_DEV void rows_to_lds(bf16_t* X, int ldx, const bf16_t* __restrict__ g, long ldg, int tid) {
   constexpr int CH = C / 8;
-  for (int e = tid; e < R * CH; e += 256) {
+  for (int e = tid; e < R * CH; e += NTH) {
     const int r = e / CH, c8 = (e - r * CH) * 8;
     *(uint4*)(X + r * ldx + c8) = *(const uint4*)(g + (long)r * ldg + c8);
   }
 }
-template <int C, int R>
+template <int C, int R, int NTH = 256>
 ED_DEV void rows_to_global(bf16_t* __restrict__ g, long ldg, const bf16_t* X, int ldx, int tid) {
   constexpr int CH = C / 8;
-  for (int e = tid; e < R * CH; e += 256) {
+  for (int e = tid; e < R * CH; e += NTH) {
     const int r = e / CH, c8 = (e - r * CH) * 8;
     *(uint4*)(g + (long)r * ldg + c8) = *(const uint4*)(X + r * ldx + c8);
   }
 }
 
-template <int C, int RR>
-__global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p) {
+template <int C, int RR, int NWV>
+__global__ __launch_bounds__(64 * NWV) void st_tail_kernel(const EncdiffStTailArgs p) {
   using T = Tail<C, RR>;
-  constexpr int R = T::R, TM = T::TM, NT = T::NT, LDT = T::LDT, LDX = T::LDX, HC = T::HC, DH = T::DH;
+  // NWV waves: each owns C / NWV output columns of every GEMM and 16 columns of each hidden chunk
+  // (8 waves at c = 128: two waves per SIMD hide each other's latencies)
+  constexpr int NTH = 64 * NWV, NT = C / (16 * NWV), HC = 16 * NWV;
+  constexpr int R = T::R, TM = T::TM, LDT = T::LDT, LDX = T::LDX, DH = T::DH;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   float* Tr = (float*)smem_raw;
   bf16_t* Xa = (bf16_t*)(Tr + R * LDT);
@@ -189,14 +192,14 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
   const int img0 = row0 / p.tokens;
   const int nimg = R > p.tokens ? R / p.tokens : 1;
   const bool save = p.save_t1 != nullptr;
-  const int n0 = wave * (C / 4);  // this wave's output columns for N = C
+  const int n0 = wave * (C / NWV);  // this wave's output columns for N = C
 
   // Weights.  PRE (c = 64: 128 VGPRs for all of them): every weight fragment of the chain is
   // loaded here, before anything else, so the chain's stages never wait on L2 / MALL latency.
   // c = 128: the four projections here, the feed-forward's chunks double-buffered one chunk
   // ahead; c = 256: each projection while the previous stage runs.
   constexpr int NCH = 4 * C / HC;  // GEGLU hidden chunks
-  constexpr bool PRE = C == 64;
+  constexpr bool PRE = C == 64 && NWV == 4;
   constexpr bool PREP = C <= 128;
   constexpr int NW = PRE ? NCH : 2;
   const bf16_t* W1 = (const bf16_t*)p.w_ff1;
@@ -221,11 +224,11 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
   if constexpr (PREP) load_b(wpo, (const bf16_t*)p.w_po, p.ld_po, n0, 0, lane);
 
   // ---- stage: o1 -> Xa, t0 -> Tr (fp32), the tile's concept-token K / V -> LDS
-  rows_to_lds<C, R>(Xa, LDX, (const bf16_t*)p.o1 + (long)row0 * p.ld_o1, p.ld_o1, tid);
+  rows_to_lds<C, R, NTH>(Xa, LDX, (const bf16_t*)p.o1 + (long)row0 * p.ld_o1, p.ld_o1, tid);
   {
     constexpr int CH = C / 8;
     const bf16_t* t0 = (const bf16_t*)p.t0 + (long)row0 * p.ld_t0;
-    for (int e = tid; e < R * CH; e += 256) {
+    for (int e = tid; e < R * CH; e += NTH) {
       const int r = e / CH, c8 = (e - r * CH) * 8;
       float f[8];
       unpack8(*(const uint4*)(t0 + (long)r * p.ld_t0 + c8), f);
@@ -233,7 +236,7 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
       for (int k = 0; k < 8; ++k) Tr[r * LDT + c8 + k] = f[k];
     }
     const int nkv = nimg * 2 * nctx * CH;
-    for (int e = tid; e < nkv; e += 256) {
+    for (int e = tid; e < nkv; e += NTH) {
       const int c8 = (e % CH) * 8, rr = e / CH;  // rr = (i * 2 + kv) * nctx + j
       const int j = rr % nctx, ikv = rr / nctx, kv = ikv & 1, i = ikv >> 1;
       const bf16_t* src = (const bf16_t*)(kv ? p.v2 : p.k2) + (long)((img0 + i) * nctx + j) * p.ld_kv + c8;
@@ -251,7 +254,7 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
   __syncthreads();
   // ---- n2 = LN2(t1)
   if (!(p.pad_ & 4))
-  ln_rows<C, R>(Tr, LDT, Xa, LDX, p.g2, p.be2, p.ln_eps, tid,
+  ln_rows<C, R, NTH>(Tr, LDT, Xa, LDX, p.g2, p.be2, p.ln_eps, tid,
                 save ? (bf16_t*)p.save_n2 + (long)row0 * p.ld_save : nullptr, p.ld_save,
                 save ? (bf16_t*)p.save_t1 + (long)row0 * p.ld_save : nullptr, save ? p.save_s2 + 2L * row0 : nullptr);
   __syncthreads();
@@ -261,11 +264,11 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
   if constexpr (!PREP) load_b(wo2, (const bf16_t*)p.w_out2, p.ld_out2, n0, 0, lane);
   acc_store_bf(acc, Xb, LDX, n0, lane);
   __syncthreads();
-  if (save) rows_to_global<C, R>((bf16_t*)p.save_q2 + (long)row0 * p.ld_save, p.ld_save, Xb, LDX, tid);
+  if (save) rows_to_global<C, R, NTH>((bf16_t*)p.save_q2 + (long)row0 * p.ld_save, p.ld_save, Xb, LDX, tid);
   // ---- o2 = softmax(q2 k2^T * scale) v2 per (row, head) -> Xa (online softmax over the keys)
   const int dbg = p.pad_;  // timing experiments only (tools/st_tail_bench.py): bit 0 skips the
                            // cross-attention, bit 1 the feed-forward, bit 2 the LayerNorms
-  for (int pr = (dbg & 1) ? R * 8 : tid; pr < R * 8; pr += 256) {
+  for (int pr = (dbg & 1) ? R * 8 : tid; pr < R * 8; pr += NTH) {
     const int r = pr % R, h = pr / R;
     const int il = (row0 + r) / p.tokens - img0;
     float q[DH], o[DH];
@@ -305,7 +308,7 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
     if (save) p.save_lse2[(long)((img0 + il) * 8 + h) * p.tokens + (row0 + r) % p.tokens] = m + __logf(l);
   }
   __syncthreads();
-  if (save) rows_to_global<C, R>((bf16_t*)p.save_o2 + (long)row0 * p.ld_save, p.ld_save, Xa, LDX, tid);
+  if (save) rows_to_global<C, R, NTH>((bf16_t*)p.save_o2 + (long)row0 * p.ld_save, p.ld_save, Xa, LDX, tid);
   // ---- t2 = o2 Wout2^T + b + t1
   zero(acc);
   mma(acc, Xa, LDX, wo2, lane);
@@ -313,7 +316,7 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
   __syncthreads();
   // ---- n3 = LN3(t2)
   if (!(dbg & 4))
-  ln_rows<C, R>(Tr, LDT, Xa, LDX, p.g3, p.be3, p.ln_eps, tid,
+  ln_rows<C, R, NTH>(Tr, LDT, Xa, LDX, p.g3, p.be3, p.ln_eps, tid,
                 save ? (bf16_t*)p.save_n3 + (long)row0 * p.ld_save : nullptr, p.ld_save,
                 save ? (bf16_t*)p.save_t2 + (long)row0 * p.ld_save : nullptr, save ? p.save_s3 + 2L * row0 : nullptr);
   // ---- GEGLU feed-forward in 64-column chunks of the hidden a; t3 accumulates in registers
@@ -375,7 +378,7 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
   {
     constexpr int CH = C / 8;
     const bf16_t* xg = (const bf16_t*)p.x + (long)row0 * p.ld_x;
-    for (int e = tid; e < R * CH; e += 256) {
+    for (int e = tid; e < R * CH; e += NTH) {
       const int r = e / CH, c8 = (e - r * CH) * 8;
       float f[8];
 #pragma unroll
@@ -397,7 +400,7 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
   {
     constexpr int CH = C / 8;
     bf16_t* og = (bf16_t*)p.out + (long)row0 * p.ld_out;
-    for (int e = tid; e < R * CH; e += 256) {
+    for (int e = tid; e < R * CH; e += NTH) {
       const int r = e / CH, c8 = (e - r * CH) * 8;
       float f[8];
 #pragma unroll
@@ -411,7 +414,7 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
       // column sum and sum of squares of the stored bf16 values, TPC row groups added in order;
       // a 32-row tile adds its half of the segment into the zeroed slot (gn_stats_add: with two
       // addends 0 + a + b has the same bits in either order)
-      constexpr int TPC = 256 / C, RPG = R / TPC;
+      constexpr int TPC = NTH / C, RPG = R / TPC;
       const int col = tid % C, grp = tid / C;
       float a = 0.f, q = 0.f;
 #pragma unroll 4
@@ -444,19 +447,29 @@ __global__ __launch_bounds__(256) void st_tail_kernel(const EncdiffStTailArgs p)
   }
 }
 
-template <int C, int RR>
-int launch_tail(const EncdiffStTailArgs& p, hipStream_t s) {
+template <int C, int RR, int NWV>
+int launch_tail_w(const EncdiffStTailArgs& p, hipStream_t s) {
   using T = Tail<C, RR>;
   if (p.rows % T::R || (T::R % p.tokens && p.tokens % T::R)) return ENCDIFF_ERR_SHAPE;
   const int nimg = T::R > p.tokens ? T::R / p.tokens : 1;
   const size_t lds = T::lds_bytes(nimg, p.n_ctx);
   if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
-  static const hipError_t attr_ok = hipFuncSetAttribute((const void*)st_tail_kernel<C, RR>,
+  static const hipError_t attr_ok = hipFuncSetAttribute((const void*)st_tail_kernel<C, RR, NWV>,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr_ok != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)attr_ok;
-  hipLaunchKernelGGL((st_tail_kernel<C, RR>), dim3((unsigned)(p.rows / T::R)), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((st_tail_kernel<C, RR, NWV>), dim3((unsigned)(p.rows / T::R)), dim3(64 * NWV), lds, s, p);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
+}
+
+// c = 128 with few workgroups (sampling batches): 8 waves per workgroup, two per SIMD hiding each
+// other's latencies (B = 8: 24.7 -> 23.3 us); with >= 256 workgroups 4 waves (B = 128: 39 vs 47 us)
+template <int C, int RR>
+int launch_tail(const EncdiffStTailArgs& p, hipStream_t s) {
+  if constexpr (C == 128) {
+    if (p.rows / RR < 256) return launch_tail_w<C, RR, 8>(p, s);
+  }
+  return launch_tail_w<C, RR, 4>(p, s);
 }
 
 

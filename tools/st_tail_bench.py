@@ -18,12 +18,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--eager", action="store_true", help="5 eager launches per case (PMC runs), no timing")
+    ap.add_argument("--only", type=int, default=0, help="only this channel count")
     a = ap.parse_args()
     from encdiff_amd import _lib as L
     from encdiff_amd import ops
     dev = "cuda"
     bf = torch.bfloat16
     for c, hw in ((64, 256), (128, 64), (256, 16)):
+        if a.only and c != a.only:
+            continue
         rows = a.batch * hw
         r = lambda *s: (torch.randn(*s, device=dev) * 0.5).to(bf)  # noqa: E731
         o1, t0, x, out = r(rows, c), r(rows, c), r(rows, c), torch.empty(rows, c, device=dev, dtype=bf)
@@ -33,7 +37,7 @@ def main():
             w[k] = torch.zeros(8 * c if k == "b_ff1" else c, device=dev)
         w["g2"] = torch.ones(c, device=dev)
         w["g3"] = torch.ones(c, device=dev)
-        for dbg in (0, 1, 2, 4, 7, 8, 15):
+        for dbg in ((0,) if a.eager else (0, 1, 2, 4, 7, 8, 15)):
             orig = L.lib.encdiff_st_tail_fwd
 
             def f(argp, s, dbg=dbg):
@@ -43,6 +47,11 @@ def main():
             try:
                 run = lambda: ops.st_tail_fwd(o1, t0, x, kv[:, :c], kv[:, c:], w, out, rows, c, hw, 8, 20, 1e-5)  # noqa
                 run()
+                if a.eager:
+                    for _ in range(5):
+                        run()
+                    torch.cuda.synchronize()
+                    continue
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
                     for _ in range(a.reps):
