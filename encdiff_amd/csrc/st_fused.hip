@@ -268,7 +268,12 @@ __global__ __launch_bounds__(64 * NWV) void st_tail_kernel(const EncdiffStTailAr
   // ---- o2 = softmax(q2 k2^T * scale) v2 per (row, head) -> Xa (online softmax over the keys)
   const int dbg = p.pad_;  // timing experiments only (tools/st_tail_bench.py): bit 0 skips the
                            // cross-attention, bit 1 the feed-forward, bit 2 the LayerNorms
-  for (int pr = (dbg & 1) ? R * 8 : tid; pr < R * 8; pr += NTH) {
+  // SPL lanes per (row, head) pair when the workgroup has lanes to spare (sampling tiles): each
+  // takes every SPL-th key, the partial softmax states (m, l, o) are merged by lane shuffles
+  constexpr int NPR = R * 8;
+  constexpr int SPL = NTH / NPR >= 4 ? 4 : (NTH / NPR >= 2 ? 2 : 1);
+  const int part = tid % SPL;
+  for (int pr = (dbg & 1) ? NPR : tid / SPL; pr < NPR; pr += NTH / SPL) {
     const int r = pr % R, h = pr / R;
     const int il = (row0 + r) / p.tokens - img0;
     float q[DH], o[DH];
@@ -279,7 +284,7 @@ __global__ __launch_bounds__(64 * NWV) void st_tail_kernel(const EncdiffStTailAr
     float m = -INFINITY, l = 0.f;
 #pragma unroll
     for (int d = 0; d < DH; ++d) o[d] = 0.f;
-    for (int j = 0; j < nctx; ++j) {
+    for (int j = part; j < nctx; j += SPL) {
       float kf[DH], vf[DH];
 #pragma unroll
       for (int d8 = 0; d8 < DH; d8 += 8) {
@@ -297,15 +302,29 @@ __global__ __launch_bounds__(64 * NWV) void st_tail_kernel(const EncdiffStTailAr
       for (int d = 0; d < DH; ++d) o[d] = o[d] * cr + pe * vf[d];
       m = mn;
     }
-    const float il_ = 1.f / l;
+    if constexpr (SPL > 1) {
 #pragma unroll
-    for (int d8 = 0; d8 < DH; d8 += 8) {
-      float y[8];
+      for (int off = 1; off < SPL; off <<= 1) {
+        const float m2 = __shfl_xor(m, off, 64), l2 = __shfl_xor(l, off, 64);
+        const float mx = fmaxf(m, m2);
+        const float a = mx == -INFINITY ? 0.f : __expf(m - mx), b = mx == -INFINITY ? 0.f : __expf(m2 - mx);
+        l = l * a + l2 * b;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) y[k] = o[d8 + k] * il_;
-      *(uint4*)(Xa + r * LDX + h * DH + d8) = pack8(y);
+        for (int d = 0; d < DH; ++d) o[d] = o[d] * a + __shfl_xor(o[d], off, 64) * b;
+        m = mx;
+      }
     }
-    if (save) p.save_lse2[(long)((img0 + il) * 8 + h) * p.tokens + (row0 + r) % p.tokens] = m + __logf(l);
+    if (part == 0) {
+      const float il_ = 1.f / l;
+#pragma unroll
+      for (int d8 = 0; d8 < DH; d8 += 8) {
+        float y[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) y[k] = o[d8 + k] * il_;
+        *(uint4*)(Xa + r * LDX + h * DH + d8) = pack8(y);
+      }
+      if (save) p.save_lse2[(long)((img0 + il) * 8 + h) * p.tokens + (row0 + r) % p.tokens] = m + __logf(l);
+    }
   }
   __syncthreads();
   if (save) rows_to_global<C, R, NTH>((bf16_t*)p.save_o2 + (long)row0 * p.ld_save, p.ld_save, Xa, LDX, tid);
