@@ -150,6 +150,7 @@ _PROTOS = {
     "encdiff_adamw_ema": [vp, vp, vp, vp, vp, C.c_longlong, vp, C.c_longlong, vp],
     "encdiff_pack_weights": [vp, vp, vp, C.c_int, vp],
     "encdiff_reduce_partials": [vp, C.c_long, C.c_int, C.c_int, vp, vp, vp],
+    "encdiff_grad_fold": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp],
     "encdiff_encoder_warp_fwd": [vp, C.c_long, C.c_int, C.c_int, vp, C.c_long, C.c_int, vp, C.c_long, vp],
     "encdiff_encoder_warp_bwd": [vp, C.c_long, C.c_int, C.c_int, vp, C.c_long, C.c_int, vp, C.c_long, vp, C.c_long,
                                  vp, vp, vp],

@@ -137,6 +137,31 @@ class Encoder4TrunkExecutor:
         pk.repack()
         self.pack = pk
         self._bufs: Dict[int, dict] = {}
+        self._nbt = None
+        self._bind_counters()
+
+    def _bind_counters(self):
+        """The trunk's BatchNorm2d.num_batches_tracked buffers become views of ONE int64 tensor, so
+        a training forward advances all of them with one launch (BatchNorm2d.train() semantics,
+        state_dict parity) instead of one torch kernel per module.  Rebound if the module moved
+        its buffers (e.g. .to())."""
+        mods = [m for _, m, _ in self.bns] + [r["bn"] for r in self.res] + \
+               [r["post_bn"][1] for r in self.res if r["post_bn"] is not None]
+        mods = [m for m in mods if m.num_batches_tracked is not None]
+        if not mods:
+            return
+        shared = torch.stack([m.num_batches_tracked.detach().to(self.dev) for m in mods])
+        for i, m in enumerate(mods):
+            m._buffers["num_batches_tracked"] = shared[i]
+        self._nbt, self._nbt_mods = shared, mods
+
+    def _count_batch(self):
+        if self._nbt is None:
+            return
+        m0 = self._nbt_mods[0]
+        if m0.num_batches_tracked.data_ptr() != self._nbt.data_ptr():
+            self._bind_counters()
+        self._nbt.add_(1)
 
     # ------------------------------------------------------------ helpers
     def pn(self, local: str) -> str:
@@ -210,8 +235,6 @@ class Encoder4TrunkExecutor:
                             running_var=mod.running_var.data_ptr() if mod.training else None,
                             partials=st["part"].data_ptr(), counter=st["counter"].data_ptr())
         L.check(L.lib.encdiff_batchnorm_fwd(C.byref(a), ops._s()), "encdiff_batchnorm_fwd")
-        if mod.training and mod.num_batches_tracked is not None:
-            mod.num_batches_tracked.add_(1)  # as BatchNorm2d.train() does (state_dict parity)
 
     def _bn_bwd(self, B, key, mod, x, dy, dx, relu):
         st = self._bn_state(B, key, x.shape[0], x.shape[1])
@@ -277,6 +300,8 @@ class Encoder4TrunkExecutor:
             if r["post_bn"] is not None:
                 key, mod = r["post_bn"]
                 bn(B, key, mod, b[f"r{j}"], b[f"R{j + 1}"][:, 3 * d:], True)
+        if train and self.enc.training:
+            self._count_batch()  # num_batches_tracked += 1 of every trunk BatchNorm2d (one launch)
         flat = b["flat"]
         flat.view(B, d, 4, 4).copy_(b["r1"].view(B, 4, 4, d).permute(0, 3, 1, 2))
         return flat
@@ -319,9 +344,8 @@ class Encoder4TrunkExecutor:
                          conv=L.ConvGeom(batch=B, h=c.hout, w=c.hout, cin=8, resample=L.RESAMPLE_K4S2,
                                          ld_src=x.stride(0)),
                          bias_grad=self.G(c.name + ".bias"))
-                gw = self.G(c.name + ".weight").view(c.cout, self.cin_img, 16)
-                gw.add_(b["dw0"].view(c.cout, 16, 8)[:, :, :self.cin_img].permute(0, 2, 1))
                 ops.flush()
+                ops.grad_fold(b["dw0"], c.cout, self.cin_img, 8, 16, self.G(c.name + ".weight"))
                 break
             x = b[f"a{i - 1}"][:, :d]  # the hi block of the split operand
             ops.conv4x4s2_bwd_cl(dy, g, self.pack.view(c.name), x, c.cin, self.Graw(c.name + ".weight"),

@@ -769,6 +769,32 @@ extern "C" int encdiff_pack_weights(const float* src, void* dst, const EncdiffPa
   return ENCDIFF_OK;
 }
 
+// conv weight-gradient fold (see encdiff_grad_fold): one thread per arena weight
+__global__ __launch_bounds__(256) void grad_fold_kernel(const float* dw, int co, int cin, int cpad, int taps, float* db,
+                                                        float* gw, float* gb) {
+  const int n = co * cin * taps;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    const int o = i / (cin * taps), r = i - o * cin * taps, c = r / taps, t = r - c * taps;
+    gw[i] += dw[((long)o * taps + t) * cpad + c];
+  }
+  if (db && blockIdx.x == 0 && threadIdx.x < co) {
+    gb[threadIdx.x] += db[threadIdx.x];
+    db[threadIdx.x] = 0.f;
+  }
+}
+
+extern "C" int encdiff_grad_fold(const float* dw, int co, int cin, int cpad, int taps, float* db, float* gw, float* gb,
+                                 void* stream) {
+  if (!dw || !gw || (db && !gb) || co <= 0 || cin <= 0 || cin > cpad || taps <= 0 || co > 256)
+    return ENCDIFF_ERR_ARG;
+  const int n = co * cin * taps;
+  hipLaunchKernelGGL(grad_fold_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, dw, co, cin, cpad,
+                     taps, db, gw, gb);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
 extern "C" int encdiff_reduce_partials(const float* part, long ld, int rows, int cols, const int* idx, float* grad,
                                        void* stream) {
   if (!part || !idx || !grad || cols <= 0) return ENCDIFF_ERR_ARG;

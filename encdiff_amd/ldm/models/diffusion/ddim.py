@@ -14,11 +14,16 @@ schedule coefficients are kernel arguments of the unrolled steps.  Loops longer 
 ``GRAPH_MAX_STEPS`` capture one step (coefficients and timestep looked up at a device step
 index) and replay it S times.
 
-Noise: the S draws of a loop are generated up front as one (S, *x.shape) table
-(one launch); ``normals_sequence`` (the reference's kwarg, unused there) injects a given
-table instead -- step i (in loop order, i = 0 .. S-1) adds sigma_i * normals_sequence[i] --
-which is how the eta > 0 trajectory is pinned against the reference's CPU noise stream.
+Noise: with eta > 0 each captured step draws its N(0, I) row inside the graph (torch's
+graph-safe Philox stream advances on every replay), so a loop holds one step's noise, not an
+(S, *x.shape) table.  ``normals_sequence`` (the reference's kwarg, unused there) injects a
+given table instead -- step i (in loop order, i = 0 .. S-1) adds sigma_i * normals_sequence[i]
+-- which is how the eta > 0 trajectory is pinned against the reference's CPU noise stream.
 At eta == 0 sigma is 0 for every step and no noise is drawn.
+
+Before a replay the model's bf16 weight packs are refreshed if the parameters changed in
+place since the capture (LatentDiffusion.refresh_hip_weights): a sampler captured outside
+ema_scope() samples with the EMA weights inside it.
 """
 from __future__ import annotations
 
@@ -176,9 +181,12 @@ class DDIMSampler(object):
         return torch.ops.encdiff.ddim_step(x, e_t, noise, a_t, a_prev, sigma, s1)
 
     # ------------------------------------------------------------ captured loops
-    def _entry(self, kind, cond, img, total, log_every_t):
-        """Cache entry (static input / output buffers) of a captured loop."""
-        key = (kind, tuple(img.shape), total, self._sched_key, tuple(cond.shape), cond.dtype, log_every_t)
+    def _entry(self, kind, cond, img, total, log_every_t, injected):
+        """Cache entry (static input / output buffers) of a captured loop.  ``injected``: the
+        noise comes from a caller's normals_sequence table (else drawn inside the graph)."""
+        injected = bool(injected and self.ddim_eta)
+        key = (kind, tuple(img.shape), total, self._sched_key, tuple(cond.shape), cond.dtype, log_every_t,
+               injected)
         st = self._graphs.get(key)
         if st is None:
             dev = img.device
@@ -187,26 +195,28 @@ class DDIMSampler(object):
                       cond=torch.empty_like(cond), logs=logs,
                       log_x=torch.empty(len(logs), *img.shape, device=dev),
                       log_px0=torch.empty(len(logs), *img.shape, device=dev),
-                      noise=torch.zeros((total if self.ddim_eta else 1), *img.shape, device=dev),
-                      graph=None)
+                      noise=torch.zeros((total if injected else 1), *img.shape, device=dev),
+                      draw=bool(self.ddim_eta) and not injected, graph=None)
             self._graphs[key] = st
         st["cond"].copy_(cond)
         st["x"].copy_(img)
         return st
 
     def _fill_noise(self, st, normals_sequence, total):
-        if not self.ddim_eta:
-            return  # sigma == 0 at every step: the noise term vanishes
-        if normals_sequence is not None:
+        if self.ddim_eta and normals_sequence is not None:  # injected table (else: in-graph draws)
             st["noise"].copy_(normals_sequence[:total])
-        else:
-            st["noise"].normal_()
+
+    def _refresh(self):
+        f = getattr(self.model, "refresh_hip_weights", None)
+        if f is not None:
+            f()
 
     def _loop_graph(self, cond, img, total, log_every_t, intermediates, normals_sequence):
         """The whole loop as one HIP graph (unrolled: step i's coefficients and timestep are
         kernel arguments / a static timestep row)."""
-        st = self._entry("loop", cond, img, total, log_every_t)
+        st = self._entry("loop", cond, img, total, log_every_t, normals_sequence is not None)
         self._fill_noise(st, normals_sequence, total)
+        self._refresh()
         if st["graph"] is None:
             b = img.shape[0]
             steps = np.flip(self.ddim_timesteps)
@@ -238,6 +248,8 @@ class DDIMSampler(object):
             e_t = self.model.apply_model(x, st["ts"][i], st["cond"])
             a_t, a_prev = float(self.ddim_alphas[index]), float(self.ddim_alphas_prev[index])
             sigma, s1 = float(self.ddim_sigmas[index]), float(self.ddim_sqrt_one_minus_alphas[index])
+            if st["draw"]:
+                st["noise"][0].normal_()
             ops.ddim_step(x, e_t.float().contiguous(), st["noise"][i if noise_n > 1 else 0], a_t, a_prev, sigma, s1,
                           xn, st["px0"])
             x, xn = xn, x
@@ -250,8 +262,9 @@ class DDIMSampler(object):
     def _step_graph(self, cond, img, total, log_every_t, intermediates, normals_sequence):
         """Loops longer than GRAPH_MAX_STEPS: one captured step (coefficients, timestep and
         noise row looked up at a device step index), replayed S times."""
-        st = self._entry("step", cond, img, total, log_every_t)
+        st = self._entry("step", cond, img, total, log_every_t, normals_sequence is not None)
         self._fill_noise(st, normals_sequence, total)
+        self._refresh()
         b = img.shape[0]
         if st["graph"] is None:
             dev = img.device
@@ -289,6 +302,8 @@ class DDIMSampler(object):
             z = st["zrow"]
         else:
             z = st["noise"][0]
+            if st["draw"]:
+                z.normal_()
         ops.ddim_step_indexed(st["x"], e_t.float().contiguous(), z, self._coef, idx, st["x2"], st["px0"],
                               advance=True)
         st["x"].copy_(st["x2"])

@@ -219,6 +219,19 @@ class DDPM(nn.Module):
                 self.model_ema.restore(self.model.parameters())
                 self._weights_changed()
 
+    def refresh_hip_weights(self):
+        """Bring the bf16 weight packs up to date with the fp32 parameters before a captured
+        graph is replayed: a replay skips UNetModel.executor() / Encoder4._encode, where the
+        eager path checks for in-place parameter changes (EMA swap, load_state_dict, arena
+        writes).  Host-side version checks; a repack launch only when something changed."""
+        unet = self.model.diffusion_model
+        if getattr(unet, "_arena", None) is not None:
+            unet.executor()
+        cs = self.cond_stage_model
+        tr = getattr(cs, "_trunk", None)
+        if tr is not None and (tr.arena.master._version, tr.arena.gen) != cs._trunk_version:
+            cs.repack_hip()
+
     def _weights_changed(self):
         """Parameters were rewritten through their .data views (EMA swap): the UNet's bf16
         weight packs must be refreshed before the next forward."""
@@ -505,11 +518,19 @@ class LatentDiffusion(DDPM):
         return opt
 
     # ------------------------------------------------------------ sampling
+    def ddim_sampler(self):
+        """One DDIMSampler per model: its captured loop graphs (keyed by batch shape, S, eta,
+        log_every_t) are reused by every later log_images / sample_log / sample_swap call."""
+        s = getattr(self, "_ddim_sampler", None)
+        if s is None:
+            s = self._ddim_sampler = DDIMSampler(self)
+        return s
+
     @torch.no_grad()
     def sample_log(self, cond, batch_size, ddim, ddim_steps, **kwargs):
         if not ddim:
             raise NotImplementedError("ancestral p_sample loop is not on the EncDiff path; use ddim=True")
-        sampler = DDIMSampler(self)
+        sampler = self.ddim_sampler()
         shape = (self.channels, self.image_size, self.image_size)
         return sampler.sample(ddim_steps, batch_size, shape, cond, verbose=False, **kwargs)
 
@@ -531,7 +552,7 @@ class LatentDiffusion(DDPM):
         sc[idx, :, idx] = orc[0][:, None].expand(lu, n)       # unit cdx <- image 0's unit cdx
         cond = self.cond_stage_model.warp(sc.reshape(lu * n, lu))
         shape = (self.channels, self.image_size, self.image_size)
-        sampler = DDIMSampler(self)
+        sampler = self.ddim_sampler()
         samples, _ = sampler.sample(ddim_steps, lu * n, shape, cond.reshape(lu * n, -1), eta=eta, verbose=False,
                                     x_T=x_T, normals_sequence=normals_sequence)
         return samples

@@ -51,38 +51,55 @@ def _conv_geom(g: Geom, cin: int, resample: int, src: torch.Tensor) -> L.ConvGeo
     return L.ConvGeom(batch=g.batch, h=g.h, w=g.w, cin=cin, resample=resample, ld_src=_ld(src))
 
 
-_WS = {}
-_CNT = {}
+_SCRATCH = {}
+_RETIRED = []  # outgrown scratch stays allocated: graphs captured earlier still address it
 # split-K GEMMs may combine their slabs in the kernel (EncdiffGemmArgs.split_counters) instead of
 # a finalize launch: per problem, as the measured table says (4th entry).  ENCDIFF_SPLIT_FOLD:
 # 1 table choice (default), 0 never, 2 always.
 SPLIT_FOLD = int(os.environ.get("ENCDIFF_SPLIT_FOLD", "1"))
-
-
-def _counters():
-    """Per-(device, stream) split-K tickets: one int per output tile, zero between launches (each
-    launch's combining splits leave them zero); launches on one stream never overlap."""
-    dev = torch.cuda.current_device()
-    key = (dev, torch.cuda.current_stream().cuda_stream)
-    c = _CNT.get(key)
-    if c is None:
-        c = _CNT[key] = torch.zeros(1 << 16, device=f"cuda:{dev}", dtype=torch.int32)
-    return c
-WS_FLOATS = 64 * 1024 * 1024         # fp32 split-K scratch per stream, 256 MB (two halves, see gemm_pair)
+WS_FLOATS = 64 * 1024 * 1024         # fp32 split-K scratch per device, 256 MB (two halves, see gemm_pair)
 WS_HALF = WS_FLOATS // 2
+COUNTERS = 1 << 16                   # split-K tickets per device (one int per output tile)
 _TILES = None
 _TILE_SHAPES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64)}
 
 
-def _workspace():
-    """Split-K slab scratch, one per (device, stream): GEMMs enqueued on different streams
-    (the executor's weight-gradient side stream) may run concurrently."""
-    dev = torch.cuda.current_device()
-    key = (dev, torch.cuda.current_stream().cuda_stream)
-    ws = _WS.get(key)
-    if ws is None:
-        ws = _WS[key] = torch.zeros(WS_FLOATS, device=f"cuda:{dev}", dtype=torch.float32)
-    return ws
+def scratch(name, numel, dtype=torch.float32, device=None):
+    """Library scratch owned by this module, ONE per (device, name), allocated outside any graph
+    capture and never freed.  Captured graphs hold these addresses, so they must not come from a
+    graph's private memory pool (a pool dies with its graph; the old per-stream keying handed a
+    dead graph's workspace to a later capture on a recycled stream handle).  Sharing one scratch
+    per device is correct because every launch that uses it is ordered on one stream at a time:
+    the executors issue GEMMs on the current stream only, and captured graphs are replayed one
+    after another, never concurrently (the DP exchange stream runs collectives only)."""
+    dev = torch.cuda.current_device() if device is None else device
+    key = (dev, name)
+    t = _SCRATCH.get(key)
+    if t is None or t.numel() < numel:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(f"encdiff scratch '{name}' first needed inside a graph capture: run an eager "
+                               f"step (or ops.ensure_scratch()) before capturing")
+        if t is not None:
+            _RETIRED.append(t)
+        t = _SCRATCH[key] = torch.zeros(numel, device=f"cuda:{dev}", dtype=dtype)
+    return t
+
+
+def ensure_scratch(device=None):
+    """Allocate the GEMM scratch now (executors call this at bind time, outside capture)."""
+    _workspace(device)
+    _counters(device)
+
+
+def _counters(device=None):
+    """Split-K tickets: one int per output tile, zero between launches (each launch's
+    combining splits leave them zero)."""
+    return scratch("split_counters", COUNTERS, torch.int32, device)
+
+
+def _workspace(device=None):
+    """Split-K slab scratch (fp32)."""
+    return scratch("splitk_ws", WS_FLOATS, torch.float32, device)
 
 
 def _tile_table():
@@ -187,8 +204,10 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
         need = ws_offset + split_k * M * N + (split_k * M if bias_grad is not None else 0)
         assert need <= WS_FLOATS, "split-K slabs exceed the workspace"
         ws = _workspace()
-        if a_mode != L.OPA_ROWM and fold_choice(M, N, K, a_mode, b_mode, c_mode,
-                                                 conv.resample if conv is not None else 0):
+        # the in-kernel combine indexes one ticket per output tile: only when every tile shape
+        # (>= 32 x 32) stays within the ticket array
+        if (a_mode != L.OPA_ROWM and math.ceil(M / 32) * math.ceil(N / 32) <= COUNTERS and
+                fold_choice(M, N, K, a_mode, b_mode, c_mode, conv.resample if conv is not None else 0)):
             cnt = _counters()
     return L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=b_mode, c_mode=c_mode,
                       a=_p(a), lda=lda, b=_p(b), ldb=ldb, c=_p(c), ldc=ldc,
@@ -691,20 +710,14 @@ def q_sample(x0, eps, t, sqrt_ac, sqrt_1mac, xt):
                                _s()), "encdiff_q_sample")
 
 
-_L1_SCRATCH = {}
-
-
 def l1_loss(pred, eps, t, lvlb, out2, grad=None, l_simple_weight=1.0):
     """out2 = (loss, loss_vlb); grad = the L1 seed.  Per-sample partials and the last-block
-    ticket live in a per-(device, stream, batch) scratch (stream-ordered reuse is safe)."""
+    ticket live in the device's library scratch (see `scratch`; the ticket returns to zero)."""
     b = pred.shape[0]
-    key = (pred.device.index, torch.cuda.current_stream().cuda_stream, b)
-    sc = _L1_SCRATCH.get(key)
-    if sc is None:
-        sc = _L1_SCRATCH[key] = (torch.empty(b, device=pred.device, dtype=torch.float32),
-                                 torch.zeros(1, device=pred.device, dtype=torch.int32))
+    part = scratch("l1_partials", b, torch.float32, pred.device.index)
+    tick = scratch("l1_ticket", 1, torch.int32, pred.device.index)
     check(lib.encdiff_l1_loss(_p(pred), _p(eps), _p(t), _p(lvlb), b, pred.numel() // b, l_simple_weight,
-                              _p(out2), _p(grad), _p(sc[0]), _p(sc[1]), _s()), "encdiff_l1_loss")
+                              _p(out2), _p(grad), _p(part), _p(tick), _s()), "encdiff_l1_loss")
 
 
 def ddim_step(x, e, noise, a_t, a_prev, sigma, s1, x_prev, pred_x0=None):
@@ -733,6 +746,13 @@ def pack_weights(src_f32, dst_bf16, jobs_dev, njobs):
     check(lib.encdiff_pack_weights(_p(src_f32), _p(dst_bf16), _p(jobs_dev), njobs, _s()), "encdiff_pack_weights")
 
 
+def grad_fold(dw, co, cin, cpad, taps, gw, db=None, gb=None):
+    """gw[o][c][t] += dw[o][t][c] (dw rows [taps][cpad]); gb += db, db zeroed (encdiff_grad_fold)."""
+    assert dw.dtype == F32 and gw.dtype == F32 and gw.is_contiguous() and gw.numel() == co * cin * taps
+    assert dw.is_contiguous() and dw.numel() >= co * taps * cpad
+    check(lib.encdiff_grad_fold(_p(dw), co, cin, cpad, taps, _p(db), _p(gw), _p(gb), _s()), "encdiff_grad_fold")
+
+
 def reduce_partials(part, ld, rows, cols, col_index, grad):
     check(lib.encdiff_reduce_partials(_p(part), ld, rows, cols, _p(col_index), _p(grad), _s()),
           "encdiff_reduce_partials")
@@ -758,6 +778,7 @@ def encoder_warp_fwd(u, params, unit_stride, units, context_dim, out):
 
 
 _WARP_SCRATCH = {}
+_RETIRED = []  # outgrown scratch stays allocated: graphs captured earlier still address it
 
 
 def encoder_warp_bwd(u, params, unit_stride, units, context_dim, dout, du, grads):

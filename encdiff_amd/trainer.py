@@ -243,6 +243,9 @@ class HipTrainer:
         if self._g_fb is None:
             return self.step_eager()
         self.opt.stage_hyper()
+        # a replay skips the eager paths' weight-version checks: repack the bf16 weights if the
+        # parameters were changed in place since the last step (e.g. after an EMA scope)
+        self.ldm.refresh_hip_weights()
         self._g_fb.replay()
         if self.world > 1:
             self._exchange(self._g_cond.replay, self._g_rest.replay if self._g_rest is not None else None)

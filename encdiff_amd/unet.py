@@ -307,6 +307,7 @@ class UNetExecutor:
         if B in self._sets:
             self.__dict__.update(self._sets[B])
             return
+        ops.ensure_scratch(self.dev.index if self.dev.index is not None else None)
         sp = self.spec
         self._split = False  # split_plan() not computed for this batch size yet
         self._cont = None
@@ -364,6 +365,7 @@ class UNetExecutor:
         self.dw_in = t(self.mc, 72, F32)     # input conv weight gradient, GEMM layout
         self.deps8 = t(g0.pixels, 8)         # d eps as channel-padded bf16 rows
         self.dw_out = t(8, 9 * sp.out_ch, F32)
+        self.db_out = torch.zeros(8, device=self.dev, dtype=F32)  # bias-gradient accumulator (left zero)
         self.a_out = t(g0.pixels, sp.out_ch)
         self.st_out = t(B, 64, F32)
         self.d_aout = t(g0.pixels, sp.out_ch)
@@ -693,12 +695,14 @@ class UNetExecutor:
         ops.small_conv_out_bwd(self.a_out, g0, self.P("out.2.weight"), d_eps, self.d_aout, None, None)
         ops.nchw_to_rows(d_eps, 8, self.deps8)
         co = d_eps.shape[1]
+        # bias gradient = column sums of the padded d eps rows (the GEMM's bias-gradient
+        # accumulator db_out, emptied by the fold)
         ops.gemm(8, 9 * sp.out_ch, g0.pixels, self.deps8, 8, self.a_out, self.a_out.stride(0), self.dw_out,
                  9 * sp.out_ch, a_mode=L.OPA_ROWM, b_mode=L.OPB_IM2COL, c_mode=L.OUT_F32,
                  conv=L.ConvGeom(batch=B, h=self.H, w=self.H, cin=sp.out_ch, resample=0,
-                                 ld_src=self.a_out.stride(0)))
-        self.G("out.2.weight").view(co, sp.out_ch, 9).add_(self.dw_out.view(8, 9, sp.out_ch)[:co].permute(0, 2, 1))
-        self.G("out.2.bias").add_(d_eps.sum((0, 2, 3)))
+                                 ld_src=self.a_out.stride(0)), bias_grad=self.db_out)
+        ops.grad_fold(self.dw_out, co, sp.out_ch, sp.out_ch, 9, self.G("out.2.weight"), self.db_out,
+                      self.G("out.2.bias"))
         dg, db = self.gn.parts("out.0.weight", sp.out_ch)
         ops.groupnorm_bwd(self._h_last, g0, self.P("out.0.weight"), self.P("out.0.bias"), self.st_out, GN_EPS, True,
                           self.d_aout, self.d_hlast, dg, db, ld_part=self.gn.ld)
@@ -755,8 +759,7 @@ class UNetExecutor:
                  conv=L.ConvGeom(batch=B, h=self.H, w=self.H, cin=8, resample=0, ld_src=8),
                  bias_grad=self.G("input_blocks.0.0.bias"))
         cin0 = self._x.shape[1]
-        self.G("input_blocks.0.0.weight").view(self.mc, cin0, 9).add_(
-            self.dw_in.view(self.mc, 9, 8)[:, :, :cin0].permute(0, 2, 1))
+        ops.grad_fold(self.dw_in, self.mc, cin0, 8, 9, self.G("input_blocks.0.0.weight"))
         # batched emb_layers backward -> time MLP
         ops.ew(L.EW_F32_TO_BF16, self.dE, self.dE16)
         ops.linear_bwd(self.dE16, self.W("emb_all"), self.emb_s, self.d_emb_s, self.emb_w_grad, self.emb_bias_grad)

@@ -362,6 +362,16 @@ int encdiff_pack_weights(const float* src, void* dst_bf16, const EncdiffPackJob*
 int encdiff_reduce_partials(const float* part, long ld, int rows, int cols, const int* col_index,
                             float* grad, void* stream);
 
+/* Fold a channel-padded conv weight gradient into the arena (the GEMM-computed weight gradient of
+ * a conv whose narrow side is padded to `cpad` channels, openaimodel_enc.py:687 out conv and :521
+ * input conv, Encoder4's first Conv2d :1002):
+ *   gw[o][c][t] += dw[o][t][c],  o < co, c < cin <= cpad, t < taps   (dw rows: [taps][cpad])
+ *   gb[o] += db[o]; db[o] = 0   (when db != NULL: a GEMM bias-gradient accumulator, left zero
+ *                                for the next step -- graph-replay safe, no memset)
+ * One launch; replaces torch permute/add and reduction kernels in the captured step. */
+int encdiff_grad_fold(const float* dw, int co, int cin, int cpad, int taps, float* db, float* gw, float* gb,
+                      void* stream);
+
 /* ---------------------------------------------------------------- input path
  * GPU-resident dataset: uint8 images [n_images][h][w][c] (Shapes3D layout, disdata.py:45-97)
  * stay in HBM; one launch gathers a batch and applies ToTensor + Normalize(0.5, 0.5)

@@ -399,19 +399,25 @@ def ddim_step(x, e_t, a_t, a_prev, sigma_t, sqrt_one_minus_at, noise):
     return x_prev, pred_x0
 
 
-def ddim_sample(eps_fn, x_T, S, eta, alphas_cumprod32, noise_fn=torch.randn):
-    """ddim.py:114-166: iterate flip(timesteps); index = S - i - 1."""
+def ddim_sample(eps_fn, x_T, S, eta, alphas_cumprod32, noise_fn=torch.randn, log_every_t=None):
+    """ddim.py:114-166: iterate flip(timesteps); index = S - i - 1.  With ``log_every_t`` also
+    returns the reference's intermediates dict (x_inter / pred_x0 logged at index %
+    log_every_t == 0 or index == S - 1, after x_T itself; ddim.py:132-166)."""
     d = ddim_schedule(alphas_cumprod32, S, eta)
     x = x_T
     b = x.shape[0]
+    inter = {'x_inter': [x_T], 'pred_x0': [x_T]}
     for i, step in enumerate(np.flip(d['timesteps'])):
         index = S - i - 1
         ts = torch.full((b,), int(step), dtype=torch.long)
         e_t = eps_fn(x, ts)
         noise = noise_fn(x.shape)
-        x, _ = ddim_step(x, e_t, d['alphas'][index], d['alphas_prev'][index], d['sigmas'][index],
-                         d['sqrt_one_minus_alphas'][index], noise)
-    return x
+        x, px0 = ddim_step(x, e_t, d['alphas'][index], d['alphas_prev'][index], d['sigmas'][index],
+                           d['sqrt_one_minus_alphas'][index], noise)
+        if log_every_t and (index % log_every_t == 0 or index == S - 1):
+            inter['x_inter'].append(x)
+            inter['pred_x0'].append(px0)
+    return (x, inter) if log_every_t else x
 
 
 # ----------------------------------------------------------------------------
@@ -556,14 +562,20 @@ def encoder4_forward(P, x, latent_unit=20, train=True, return_u=False):
     d = h.shape[1]
     h = h.reshape(-1, d * 4 * 4)
     u = F.linear(h, P[e + f'{lin}.weight'], P[e + f'{lin}.bias'])
+    c = encoder4_warp(P, u, latent_unit)
+    return (c, u) if return_u else c
+
+
+def encoder4_warp(P, u, latent_unit=20):
+    """Encoder4.warp (openaimodel_enc.py:1037-1041): unit i's scalar code through its own
+    Linear(1, 64) ELU Linear(64, 128) ELU Linear(128, context_dim); tokens concatenated."""
     outs = []
     for i in range(latent_unit):
         y = u[:, i][:, None]
         y = F.elu(F.linear(y, P[f'net.{i}.0.weight'], P[f'net.{i}.0.bias']))
         y = F.elu(F.linear(y, P[f'net.{i}.2.weight'], P[f'net.{i}.2.bias']))
         outs.append(F.linear(y, P[f'net.{i}.4.weight'], P[f'net.{i}.4.bias']))
-    c = torch.cat(outs, dim=1)
-    return (c, u) if return_u else c
+    return torch.cat(outs, dim=1)
 
 
 # ----------------------------------------------------------------------------

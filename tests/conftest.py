@@ -15,3 +15,17 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(REPO, "tests", "golden")
+
+
+# The benchmarked objects run first, so a failure elsewhere under `-x` cannot hide their
+# evidence: the configs[1] / configs[3] graph step, configs[4], then the model-level tests,
+# and the per-op suite (many small cases) last.
+_ORDER = ["test_gpu_trainer.py", "test_gpu_config4.py", "test_gpu_ldm.py", "test_gpu_unet.py",
+          "test_gpu_unet_wide.py", "test_gpu_fp32.py", "test_gpu_dp.py", "test_gpu_ops.py"]
+
+
+def pytest_collection_modifyitems(session, config, items):
+    def rank(item):
+        name = os.path.basename(str(item.fspath))
+        return _ORDER.index(name) if name in _ORDER else len(_ORDER) - 1
+    items.sort(key=rank)  # stable: the order inside a file is kept

@@ -314,29 +314,128 @@ def test_validation_encoding_pass(ldm):
     assert rel(sc, codes) < 1e-5 and rel(outs, toks) < 1e-5
 
 
-def test_log_images_swap_one_batch(ldm):
+def test_log_images_swap_matches_oracle(ldm):
     """log_images(sample_swap=True) (ddpm_enc.py:1522-1535): the latent_unit swapped
-    conditionings are sampled as ONE (latent_unit * N) DDIM batch; row block cdx must equal the
-    reference's cdx-th separate call (same x_T rows), here run eagerly at batch N."""
-    from encdiff_amd.ldm.models.diffusion.ddim import DDIMSampler
+    conditionings are sampled as ONE (latent_unit * N) DDIM batch.  Row block cdx is checked
+    against the ORACLE: the reference's cdx-th call restated on the CPU -- unit cdx of every
+    code replaced by image 0's, warped to tokens by the oracle's Encoder4.warp, DDIM sampled
+    from the same x_T rows (ddim.py:114-207)."""
+    from oracle import encdiff_oracle as O
     ldm.setup_hip_training()
     N, S = 4, 10
     g = torch.Generator().manual_seed(4)
     img = (torch.rand(N, 3, 64, 64, generator=g) * 2 - 1).cuda()
+    plan = O.build_plan()
+    P = O.recipe_params(O.param_shapes(plan))
+    E = {k: v.detach().cpu() for k, v in ldm.cond_stage_model.state_dict().items()}
+    ac32 = O.sched_fp32(O.register_schedule())["alphas_cumprod"]
     with torch.no_grad():
         _, orc = ldm.encode_concepts(img)
         xT = torch.randn(20 * N, 3, 16, 16, generator=g).cuda()
         both = ldm.sample_swap(orc, N, ddim_steps=S, eta=0.0, x_T=xT)
         for cdx in (0, 7, 19):
-            sc = orc.clone()
-            sc[:, cdx] = sc[0, cdx][None].repeat(N)
-            cond = ldm.cond_stage_model.warp(sc).reshape(N, -1)
-            one, _ = DDIMSampler(ldm, use_graph=False).sample(S, N, (3, 16, 16), cond, eta=0.0, verbose=False,
-                                                              x_T=xT[cdx * N:(cdx + 1) * N])
-            r = rel(both[cdx * N:(cdx + 1) * N], one)
-            print("swap row", cdx, r)
-            assert r < 1e-2
+            sc = orc.detach().cpu().clone()
+            sc[:, cdx] = sc[0, cdx]
+            cond = O.encoder4_warp(E, sc, 20)
+            want = O.ddim_sample(lambda x, ts: O.unet_forward(P, plan, x, ts, [cond]),
+                                 xT[cdx * N:(cdx + 1) * N].cpu(), S, 0.0, ac32)
+            r = rel(both[cdx * N:(cdx + 1) * N], want)
+            print("swap row block", cdx, "vs oracle", r)
+            assert r < 3e-2
         log = ldm.log_images({"image": img.permute(0, 2, 3, 1)}, N=N, ddim_steps=S, ddim_eta=0.0, sample_swap=True,
                              plot_diffusion_rows=False)
     assert log["samples_swapping"].shape == (20 * N, 3, 64, 64)
     assert torch.isfinite(log["samples_swapping"]).all() and torch.isfinite(log["samples"]).all()
+    # the second log_images call reuses the model's sampler and its captured loop graphs
+    sampler = ldm.ddim_sampler()
+    n_graphs = len(sampler._graphs)
+    with torch.no_grad():
+        ldm.log_images({"image": img.permute(0, 2, 3, 1)}, N=N, ddim_steps=S, ddim_eta=0.0, sample_swap=True,
+                       plot_diffusion_rows=False)
+    assert ldm.ddim_sampler() is sampler and len(sampler._graphs) == n_graphs
+
+
+@pytest.mark.parametrize("path", ["loop", "step"])
+@pytest.mark.parametrize("eta", [0, 1])
+def test_ddim_s200_matches_reference(ldm, golden_dir, eta, path, monkeypatch):
+    """DDIM at the reference's log_images length (ddpm_enc.py:1474: ddim_steps=200,
+    ddim_eta=1.) vs the reference's own samples and logged intermediates (ddim_s200.npz), the
+    eta = 1 noise stream injected; "loop" = the whole 200-step loop as one graph, "step" = the
+    one-step graph replayed 200 times (the path of loops longer than GRAPH_MAX_STEPS)."""
+    from encdiff_amd.ldm.models.diffusion import ddim as D
+    fx = np.load(os.path.join(golden_dir, "ddim_s200.npz"))
+    if path == "step":
+        monkeypatch.setattr(D, "GRAPH_MAX_STEPS", 64)
+    cond = torch.tensor(fx["cond"]).cuda()
+    s = D.DDIMSampler(ldm, use_graph=True)
+    with torch.no_grad():
+        out, inter = s.sample(200, 2, (3, 16, 16), cond, eta=float(eta), verbose=False,
+                              x_T=torch.tensor(fx["xT"]).cuda(), normals_sequence=_ref_noise(200).cuda())
+    assert any(k[0] == path for k in s._graphs), "the sampler did not take the expected graph path"
+    r = rel(out, fx[f"samples_eta{eta}"])
+    xi = torch.stack([v.cpu() for v in inter["x_inter"]])
+    px = torch.stack([v.cpu() for v in inter["pred_x0"]])
+    assert xi.shape == fx[f"x_inter_eta{eta}"].shape
+    ri, rp = rel(xi, fx[f"x_inter_eta{eta}"]), rel(px, fx[f"pred_x0_eta{eta}"])
+    print(f"ddim S=200 eta{eta} {path}: samples rel-L2 {r:.3e}, x_inter {ri:.3e}, pred_x0 {rp:.3e}")
+    assert r < 3e-2 and ri < 3e-2 and rp < 3e-2
+
+
+def test_ddim_b128_matches_oracle(ldm):
+    """The bench's B = 128 eta = 1 sampling line: the no-grad B >= 64 UNet forward (sampling
+    tiles, fused transformer tails, GroupNorm from producer statistics) vs the oracle, eps of
+    one forward and a 4-step eta = 1 trajectory with injected noise."""
+    from oracle import encdiff_oracle as O
+    from encdiff_amd.ldm.models.diffusion.ddim import DDIMSampler
+    B, S = 128, 4
+    g = torch.Generator().manual_seed(128)
+    plan = O.build_plan()
+    P = O.recipe_params(O.param_shapes(plan))
+    cond = torch.randn(B, 320, generator=g) * 0.5
+    x = torch.randn(B, 3, 16, 16, generator=g)
+    t = torch.randint(0, 1000, (B,), generator=g)
+    ldm.eval()
+    with torch.no_grad():
+        eps = ldm.apply_model(x.cuda(), t.cuda(), cond.cuda()).cpu()
+        want = O.unet_forward(P, plan, x, t, [cond])
+    e_rel, e_max = rel(eps, want), (eps - want).abs().max().item()
+    print(f"B=128 no-grad eps rel-L2 {e_rel:.3e} max-abs {e_max:.3e}")
+    assert e_rel < 3e-2 and e_max < 6e-2
+    nz = torch.randn(S, B, 3, 16, 16, generator=g)
+    ac32 = O.sched_fp32(O.register_schedule())["alphas_cumprod"]
+    with torch.no_grad():
+        out, _ = DDIMSampler(ldm).sample(S, B, (3, 16, 16), cond.cuda(), eta=1.0, verbose=False, x_T=x.cuda(),
+                                         normals_sequence=nz.cuda())
+        it = iter(nz)
+        ref = O.ddim_sample(lambda xx, ts: O.unet_forward(P, plan, xx, ts, [cond]), x, S, 1.0, ac32,
+                            noise_fn=lambda shape: next(it))
+    r = rel(out, ref)
+    print(f"B=128 eta=1 S={S} samples rel-L2 {r:.3e}")
+    assert r < 3e-2
+    ldm.train()
+
+
+def test_captured_graphs_follow_ema_scope(ldm):
+    """a DDIM loop graph captured OUTSIDE ema_scope() must sample with the EMA
+    weights when replayed INSIDE it (the replay refreshes stale bf16 packs), and the training
+    graph replayed after the scope must run on the restored training weights."""
+    from encdiff_amd.ldm.models.diffusion.ddim import DDIMSampler
+    ldm.setup_hip_training()
+    x = torch.randn(2, 3, 16, 16, device="cuda")
+    c = torch.randn(2, 320, device="cuda") * 0.5
+    a = ldm._arena
+    s = DDIMSampler(ldm)
+    with torch.no_grad():
+        base = s.sample(5, 2, (3, 16, 16), c, eta=0.0, verbose=False, x_T=x)[0].clone()  # captures
+        saved = a.master.clone()
+        a.ema.copy_(a.master[: a.ema.numel()] * 0.9)      # EMA shadow != training weights
+        with ldm.ema_scope():
+            inside = s.sample(5, 2, (3, 16, 16), c, eta=0.0, verbose=False, x_T=x)[0].clone()
+            explicit = DDIMSampler(ldm, use_graph=False).sample(5, 2, (3, 16, 16), c, eta=0.0, verbose=False,
+                                                                x_T=x)[0].clone()
+        after = s.sample(5, 2, (3, 16, 16), c, eta=0.0, verbose=False, x_T=x)[0].clone()
+        a.ema.copy_(saved[: a.ema.numel()])
+    assert torch.equal(a.master, saved)
+    print("graph inside ema_scope vs eager", rel(inside, explicit), "vs base", rel(inside, base))
+    assert rel(inside, explicit) < 1e-5 and rel(inside, base) > 1e-3
+    assert torch.equal(after, base)

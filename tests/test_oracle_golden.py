@@ -124,3 +124,21 @@ def test_vq_encoder_matches_reference(golden_dir):
     fx = np.load(os.path.join(golden_dir, "p_losses.npz"))
     z = O.vq_encode(O.vq_encoder_params(), torch.tensor(fx["img"]))
     assert rel_l2(z, fx["vq_z"]) < 1e-5
+
+
+@pytest.mark.parametrize("eta", [0, 1])
+def test_ddim_sampling_s200(plan, golden_dir, eta):
+    """The reference's log_images length (ddpm_enc.py:1474: ddim_steps=200, ddim_eta=1.): oracle
+    samples and the logged intermediates vs the reference's own (ddim_s200.npz)."""
+    fx = np.load(os.path.join(golden_dir, "ddim_s200.npz"))
+    P = O.recipe_params(O.param_shapes(plan))
+    cond = torch.tensor(fx["cond"])
+    ac32 = O.sched_fp32(O.register_schedule())["alphas_cumprod"]
+    torch.manual_seed(1234)
+    with torch.no_grad():
+        xs, inter = O.ddim_sample(lambda x, ts: O.unet_forward(P, plan, x, ts, [cond]), torch.tensor(fx["xT"]),
+                                  200, float(eta), ac32, log_every_t=100)
+    assert rel_l2(xs, fx[f"samples_eta{eta}"]) < 1e-4
+    assert len(inter["x_inter"]) == fx[f"x_inter_eta{eta}"].shape[0]
+    assert rel_l2(torch.stack(inter["x_inter"]), fx[f"x_inter_eta{eta}"]) < 1e-4
+    assert rel_l2(torch.stack(inter["pred_x0"]), fx[f"pred_x0_eta{eta}"]) < 1e-4

@@ -113,7 +113,32 @@ def set_recipe(module: nn.Module, prefix: str, seed=0):
             p.copy_(O.recipe_tensor(prefix + n, tuple(p.shape), seed))
 
 
+def ddim_long(ldm, cond, S=200):
+    """DDIM at the reference's log_images workload length (ddpm_enc.py:1474: ddim_steps=200,
+    ddim_eta=1.), B = 2, eta in {0, 1}; the eta = 1 noise stream is torch.manual_seed(1234)
+    then one CPU torch.randn(x.shape) per step (ddim.py:201 noise_like), as tests/test_gpu_ldm.py
+    regenerates it.  Also the logged intermediates (log_every_t = 100 -> S/100 + 1 entries)."""
+    from ldm.models.diffusion.ddim import DDIMSampler
+    DDIMSampler.register_buffer = lambda self, name, attr: setattr(self, name, attr)
+    res = {}
+    for eta in (0.0, 1.0):
+        sampler = DDIMSampler(ldm)
+        xT = torch.randn(2, 3, 16, 16, generator=torch.Generator().manual_seed(5))
+        torch.manual_seed(1234)
+        with torch.no_grad():
+            samples, inter = sampler.sample(S, 2, (3, 16, 16), cond[:2], eta=eta, verbose=False, x_T=xT)
+        res['xT'] = xT.numpy()
+        res[f'samples_eta{int(eta)}'] = samples.numpy()
+        res[f'x_inter_eta{int(eta)}'] = torch.stack(inter['x_inter']).numpy()
+        res[f'pred_x0_eta{int(eta)}'] = torch.stack(inter['pred_x0']).numpy()
+    res['cond'] = cond[:2].numpy()
+    res['S'] = np.array(S)
+    np.savez_compressed(os.path.join(OUT, f'ddim_s{S}.npz'), **res)
+    print(f'ddim S={S} written')
+
+
 def main():
+    only_ddim_long = '--only-ddim-long' in sys.argv
     install_shims()
     torch.set_num_threads(8)
     os.makedirs(OUT, exist_ok=True)
@@ -126,6 +151,8 @@ def main():
     cfg = load_yaml_cfg()
     up = cfg['model']['params']['unet_config']['params']
 
+    if only_ddim_long:
+        return ddim_only(cfg)
     # ---------------- full UNet fwd + bwd, B=4 --------------------------------
     unet = UNetModel(**up)
     set_recipe(unet, '')
@@ -234,6 +261,7 @@ def main():
         res[f'pred_x0_last_eta{int(eta)}'] = inter['pred_x0'][-1].numpy()
     res['cond'] = cond[:2].numpy()
     np.savez_compressed(os.path.join(OUT, 'ddim.npz'), **res)
+    ddim_long(ldm, cond)
 
     # ---------------- EMA + AdamW + LR schedule -------------------------------
     small = nn.Sequential(nn.Linear(8, 16), nn.SiLU(), nn.Linear(16, 4))
@@ -261,6 +289,39 @@ def main():
     e['lr_f'] = np.array([sched(int(n)) for n in ns], dtype=np.float64)
     np.savez_compressed(os.path.join(OUT, 'ema_adamw_lr.npz'), **e)
     print('fixtures written to', OUT)
+
+
+def build_ldm(cfg):
+    """The reference LatentDiffusion of the Shapes3D config with recipe weights (as main())."""
+    from ldm.models.diffusion.ddpm_enc import LatentDiffusion
+    fsc = to_attr(json.loads(json.dumps(cfg['model']['params']['first_stage_config'])))
+    fsc['params'].pop('ckpt_path', None)
+    kwargs = {k: v for k, v in cfg['model']['params'].items()
+              if k not in ('first_stage_config', 'cond_stage_config', 'unet_config', 'scheduler_config',
+                           'eval_name', 'monitor')}
+    ldm = LatentDiffusion(first_stage_config=fsc, cond_stage_config=cfg['model']['params']['cond_stage_config'],
+                          unet_config=cfg['model']['params']['unet_config'], **kwargs)
+    set_recipe(ldm.model.diffusion_model, '')
+    set_recipe(ldm.cond_stage_model, 'cond.')
+    set_recipe(ldm.first_stage_model, 'vq.')
+    ldm.eval()
+    return ldm
+
+
+def ddim_only(cfg):
+    """--only-ddim-long: rebuild the p_losses conditioning exactly as main() does and write
+    ddim_s200.npz only (the other fixtures untouched)."""
+    ldm = build_ldm(cfg)
+    g = torch.Generator().manual_seed(11)
+    torch.randn(4, 3, 16, 16, generator=g)                 # x0 (same draw order as main())
+    img = torch.rand(4, 3, 64, 64, generator=g) * 2 - 1
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    with torch.no_grad():
+        ldm.cond_stage_model.train()
+        cond = ldm.get_learned_conditioning(img)
+    ref = np.load(os.path.join(OUT, 'ddim.npz'))['cond']
+    assert np.array_equal(cond[:2].numpy(), ref), 'conditioning differs from ddim.npz'
+    ddim_long(ldm, cond)
 
 
 if __name__ == '__main__':
