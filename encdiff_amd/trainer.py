@@ -261,6 +261,13 @@ class HipTrainer:
     def loss(self):
         return float(self.loss_buf[0])
 
+    def eps(self):
+        """The denoiser output of the last step (the executor's buffer set of this batch size;
+        a forward at another batch size in between, e.g. sampling, swaps the executor's set)."""
+        ex = self.unet._ex
+        ex.bind(self.B)
+        return ex.eps
+
 
 def time_steps(trainer: HipTrainer, steps: int) -> float:
     """Barrier + sync on both sides; returns the wall time of exactly `steps` steps."""

@@ -139,7 +139,7 @@ class GraphStepCheck:
         cond_before = {n: self._view(a.master, "cond_stage_model." + n) for n in cnames}
         tr.step()  # graph replay: the benchmarked step
         torch.cuda.synchronize()
-        eps = tr.unet._ex.eps.detach().cpu().clone()
+        eps = tr.eps().detach().cpu().clone()
         loss = tr.loss()
         seed = torch.sign(eps - noise) / eps.numel()
         o_before = {n: p.detach().clone() for n, p in orc.P.items()}
