@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("ENCDIFF_LIB", os.path.join(HERE, "libencdiff_hip.so")
 # enums (mirror include/encdiff_hip.h)
 OPA_ROWK, OPA_IM2COL, OPA_ROWM = 0, 1, 2
 OPB_ROWK, OPB_ROWN, OPB_CONV_DGRAD, OPB_IM2COL = 0, 1, 2, 3
+DT_BF16, DT_F32 = 0, 1  # EncdiffGemmArgs / GroupNorm / LayerNorm / Attn / Ew .dtype
 OUT_BF16, OUT_F32, OUT_F32_ATOMIC, OUT_F32_ATOMIC_CONVW, OUT_F32_ACCUM, OUT_BF16_GEGLU, OUT_BF16_GEGLU_BWD = \
     0, 1, 2, 3, 4, 5, 6
 RESAMPLE_NONE, RESAMPLE_DOWN2, RESAMPLE_UP2, RESAMPLE_STRIDE2, RESAMPLE_K4S2, RESAMPLE_K4S2_T, RESAMPLE_K4S2_TP = \
@@ -39,7 +40,7 @@ class GemmArgs(C.Structure):
                 ("conv", ConvGeom), ("conv_cout", C.c_int), ("convw_cin", C.c_int),
                 ("alpha", C.c_float), ("split_k", C.c_int),
                 ("bias", vp), ("resid", vp), ("ld_resid", C.c_long), ("bias_grad", vp),
-                ("tile", C.c_int), ("pad2_", C.c_int), ("workspace", vp),
+                ("tile", C.c_int), ("dtype", C.c_int), ("workspace", vp),
                 ("aux", vp), ("ld_aux", C.c_long), ("gn_stats", vp), ("ld_gn_stats", C.c_long),
                 ("ln_gamma", vp), ("ln_beta", vp), ("ln_y", vp), ("ld_ln_y", C.c_long), ("ln_stats", vp),
                 ("ln_eps", C.c_float), ("pad3_", C.c_int), ("split_counters", vp)]
@@ -51,7 +52,7 @@ class GroupNormArgs(C.Structure):
                 ("x", vp), ("ldx", C.c_long), ("gamma", vp), ("beta", vp),
                 ("film", vp), ("ld_film", C.c_long), ("y", vp), ("ldy", C.c_long), ("stats", vp),
                 ("dy", vp), ("lddy", C.c_long), ("dx", vp), ("lddx", C.c_long),
-                ("accumulate_dx", C.c_int), ("pad_", C.c_int),
+                ("accumulate_dx", C.c_int), ("dtype", C.c_int),
                 ("dgamma_part", vp), ("dbeta_part", vp), ("ld_part", C.c_long), ("dfilm", vp),
                 ("ld_dfilm", C.c_long), ("resid", vp), ("ld_resid", C.c_long), ("in_stats", vp),
                 ("ld_in_stats", C.c_long)]
@@ -62,7 +63,7 @@ class LayerNormArgs(C.Structure):
                 ("x", vp), ("ldx", C.c_long), ("gamma", vp), ("beta", vp), ("y", vp), ("ldy", C.c_long),
                 ("stats", vp), ("dy", vp), ("lddy", C.c_long), ("dx", vp), ("lddx", C.c_long),
                 ("accumulate_dx", C.c_int), ("dgamma_part", vp), ("dbeta_part", vp), ("ld_part", C.c_long),
-                ("parts", C.c_int), ("pad_", C.c_int), ("resid", vp), ("ld_resid", C.c_long)]
+                ("parts", C.c_int), ("dtype", C.c_int), ("resid", vp), ("ld_resid", C.c_long)]
 
 
 class AttnArgs(C.Structure):
@@ -72,14 +73,14 @@ class AttnArgs(C.Structure):
                 ("o", vp), ("ldo", C.c_long), ("lse", vp),
                 ("d_o", vp), ("lddo", C.c_long), ("dq", vp), ("lddq", C.c_long),
                 ("dk", vp), ("lddk", C.c_long), ("dv", vp), ("lddv", C.c_long), ("fp8_qk", C.c_int),
-                ("pad_", C.c_int)]
+                ("dtype", C.c_int)]
 
 
 class EwArgs(C.Structure):
     _fields_ = [("op", C.c_int), ("rows", C.c_int), ("cols", C.c_int),
                 ("x", vp), ("ldx", C.c_long), ("x2", vp), ("ldx2", C.c_long), ("y", vp), ("ldy", C.c_long),
                 ("accumulate", C.c_int), ("resample", C.c_int), ("batch", C.c_int), ("h", C.c_int),
-                ("w", C.c_int), ("pad_", C.c_int)]
+                ("w", C.c_int), ("dtype", C.c_int)]
 
 
 class SmallConvArgs(C.Structure):
@@ -143,6 +144,8 @@ _PROTOS = {
     "encdiff_small_conv_fwd": [C.POINTER(SmallConvArgs), vp],
     "encdiff_small_conv_bwd": [C.POINTER(SmallConvArgs), vp],
     "encdiff_timestep_embedding": [vp, C.c_int, C.c_int, C.c_float, vp, vp],
+    "encdiff_timestep_embedding_f32": [vp, C.c_int, C.c_int, C.c_float, vp, vp],
+    "encdiff_nchw_rows_f32": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_long, C.c_int, vp],
     "encdiff_q_sample": [vp, vp, vp, vp, vp, C.c_int, C.c_int, vp, vp],
     "encdiff_l1_loss": [vp, vp, vp, vp, C.c_int, C.c_int, C.c_float, vp, vp, vp, vp, vp],
     "encdiff_ddim_step": [vp, vp, vp, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, vp, vp, vp],

@@ -948,6 +948,7 @@ int dispatch_dh(const EncdiffAttnArgs& a, bool bwd, hipStream_t s) {
 
 int attn_dispatch(const EncdiffAttnArgs* a, bool bwd, void* stream) {
   if (!a || !a->q || !a->k || !a->v || !a->o) return ENCDIFF_ERR_ARG;
+  if (a->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_UNSUPPORTED;  // fp32: forward entry only
   if (bwd && (!a->d_o || !a->dq || !a->dk || !a->dv || !a->lse)) return ENCDIFF_ERR_ARG;
   if (a->batch <= 0 || a->heads <= 0 || a->sq <= 0 || a->sk <= 0 || a->dh % 8) return ENCDIFF_ERR_SHAPE;
   if (a->batch * a->heads % mfma_hpb(*a)) return ENCDIFF_ERR_SHAPE;
@@ -961,5 +962,9 @@ int attn_dispatch(const EncdiffAttnArgs* a, bool bwd, void* stream) {
 
 }  // namespace
 
-extern "C" int encdiff_attention_fwd(const EncdiffAttnArgs* a, void* stream) { return attn_dispatch(a, false, stream); }
+extern "C" int encdiff_attention_fwd(const EncdiffAttnArgs* a, void* stream) {
+  if (a && a->dtype == ENCDIFF_DT_F32) return ed_attention_fwd_f32(a, (hipStream_t)stream);
+  if (a && a->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_ARG;
+  return attn_dispatch(a, false, stream);
+}
 extern "C" int encdiff_attention_bwd(const EncdiffAttnArgs* a, void* stream) { return attn_dispatch(a, true, stream); }

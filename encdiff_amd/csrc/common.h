@@ -75,3 +75,10 @@ ED_DEV float wave_sum(float v) {
     hipError_t _e = hipGetLastError();                      \
     if (_e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)_e; \
   } while (0)
+
+// fp32 (ENCDIFF_DT_F32) forms of the entry points, fp32.hip
+int ed_gemm_f32(const EncdiffGemmArgs* p, hipStream_t s);
+int ed_groupnorm_fwd_f32(const EncdiffGroupNormArgs* a, hipStream_t s);
+int ed_layernorm_fwd_f32(const EncdiffLayerNormArgs* a, hipStream_t s);
+int ed_attention_fwd_f32(const EncdiffAttnArgs* a, hipStream_t s);
+int ed_elementwise_f32(const EncdiffEwArgs* a, hipStream_t s);

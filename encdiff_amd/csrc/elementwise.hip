@@ -627,6 +627,8 @@ int grid_for(long n, int per_thread = 1) {
 
 extern "C" int encdiff_elementwise(const EncdiffEwArgs* a, void* stream) {
   if (!a || !a->x || !a->y) return ENCDIFF_ERR_ARG;
+  if (a->dtype == ENCDIFF_DT_F32) return ed_elementwise_f32(a, (hipStream_t)stream);
+  if (a->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_ARG;
   if (a->cols % 8 || (long)a->rows * (a->cols / 8) >= (1L << 31)) return ENCDIFF_ERR_SHAPE;
   hipLaunchKernelGGL(ew_kernel, dim3(grid_for((long)a->rows * a->cols, 8)), dim3(256), 0, (hipStream_t)stream, *a);
   ED_CHECK_LAUNCH();

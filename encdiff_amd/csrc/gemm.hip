@@ -209,9 +209,14 @@ template <int N>
 ED_DEV void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-template <int LPS>
+template <int LPS, int MAXA = 2>
 ED_DEV void vm_wait_stages(int ahead) {
-  if (ahead >= 2) vm_wait<2 * LPS>();
+  // ahead = stages still allowed in flight behind the one about to be read (<= ring depth - 2)
+  if (MAXA >= 6 && ahead >= 6) vm_wait<6 * LPS>();
+  else if (MAXA >= 5 && ahead == 5) vm_wait<5 * LPS>();
+  else if (MAXA >= 4 && ahead == 4) vm_wait<4 * LPS>();
+  else if (MAXA >= 3 && ahead == 3) vm_wait<3 * LPS>();
+  else if (ahead >= 2) vm_wait<2 * LPS>();
   else if (ahead == 1) vm_wait<LPS>();
   else vm_wait<0>();
 }
@@ -562,7 +567,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   // barrier (tile it visible to all waves; every wave is done with tile it-1, whose slot is
   // refilled next), issue tile it+NSTAGE-1, multiply tile it.
   constexpr int D = G::NSTAGE;
-  static_assert(D - 2 <= 2, "vm_wait_stages covers up to two stages ahead");
+  static_assert(D - 2 <= 6 && (D - 2) * G::LPS <= 63, "vm_wait_stages covers up to six stages ahead");
   if (nkt > 0) {
     // halo mode: the window's DMAs are issued first, so the wait for ring tile 0 covers them
     if constexpr (G::HALO) stage_halo();
@@ -571,7 +576,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       if (st < nkt) stage(ring + st * G::STAGE, kt_begin + st);
     int rd = 0, wr = D - 1;  // ring slots of the tile read now / the tile issued next
     for (int it = 0; it < nkt; ++it) {
-      vm_wait_stages<G::LPS>(min(D - 2, nkt - 1 - it));
+      vm_wait_stages<G::LPS, D - 2>(min(D - 2, nkt - 1 - it));
       asm volatile("s_barrier" ::: "memory");  // (asm: the compiler may not move LDS-DMA issue across it)
       if (it + D - 1 < nkt) stage(ring + wr * G::STAGE, kt_begin + it + D - 1);
       compute(ring + rd * G::STAGE, kt_begin + it);
@@ -1165,6 +1170,8 @@ hipError_t launch_modes(const EncdiffGemmArgs& p, const GemmAux& aux, int tile, 
     case 6: return launch_t<64, 128, AM, BMD, 3>(p, aux, s);
     case 7: return launch_t<64, 64, AM, BMD, 2, 128>(p, aux, s);
     case 8: return launch_t<64, 128, AM, BMD, 2, 128>(p, aux, s);
+    case 9: return launch_t<64, 64, AM, BMD, 6>(p, aux, s);
+    case 10: return launch_t<64, 64, AM, BMD, 8>(p, aux, s);
     default: return launch_t<64, 64, AM, BMD>(p, aux, s);
   }
 }
@@ -1254,7 +1261,7 @@ struct GemmPlan {
 };
 
 int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
-  if (!pa) return ENCDIFF_ERR_ARG;
+  if (!pa || pa->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_ARG;  // fp32: encdiff_gemm only
   EncdiffGemmArgs p = *pa;
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return ENCDIFF_ERR_SHAPE;
   if (p.split_k < 1) p.split_k = 1;
@@ -1422,6 +1429,17 @@ hipError_t launch_pair_tiles(const GemmPlan& g1, const GemmPlan& g2, const Encdi
   if (g1.tile == 5) {  // weight gradient with a 4-deep ring (64 KB of LDS): every k-tile of a short split in flight
     return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 2, 64, 64, 4>(g1, g2, pf, nf, s);
   }
+  if (g1.tile == 9 || g1.tile == 10) {  // 6- / 8-deep rings (96 / 128 KB): one workgroup per CU, all loads in flight
+    const bool d6 = g1.tile == 9;
+    switch (g2.tile) {
+      case 9: return d6 ? launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 6, 64, 64, 6>(g1, g2, pf, nf, s)
+                        : launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 6, 64, 64, 8>(g1, g2, pf, nf, s);
+      case 10: return d6 ? launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 8, 64, 64, 6>(g1, g2, pf, nf, s)
+                         : launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 8, 64, 64, 8>(g1, g2, pf, nf, s);
+      default: return d6 ? launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 2, 64, 64, 6>(g1, g2, pf, nf, s)
+                         : launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 2, 64, 64, 8>(g1, g2, pf, nf, s);
+    }
+  }
   if (g1.tile == 7) {  // weight gradient with 128-deep k stages (64 KB of LDS): dgrad tile 7 or 64x64
     if (g2.tile == 7) return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 2, 128, 128>(g1, g2, pf, nf, s);
     return launch_pair_t<AM1, BMD1, 64, 64, AM2, BMD2, 2, 64, 128>(g1, g2, pf, nf, s);
@@ -1446,6 +1464,8 @@ hipError_t launch_finalize(const EncdiffGemmArgs& u, hipStream_t s) {
 }  // namespace
 
 extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
+  if (pa && pa->dtype == ENCDIFF_DT_F32) return ed_gemm_f32(pa, (hipStream_t)stream);
+  if (pa && pa->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_ARG;
   GemmPlan g;
   const int rc = prepare(pa, g);
   if (rc != ENCDIFF_OK) return rc;
@@ -1474,7 +1494,8 @@ extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffG
   // both split-K problems need disjoint slabs
   if (g1.ws_path && g2.ws_path && g1.p.workspace == g2.p.workspace) return ENCDIFF_ERR_ARG;
   const bool defer1 = defer && g1.ws_path;
-  if ((!lin && !conv) || (g1.tile != 4 && g1.tile != 5 && g1.tile != 7)) {  // pairs the fused kernel does not cover
+  if ((!lin && !conv) || (g1.tile != 4 && g1.tile != 5 && g1.tile != 7 && g1.tile != 9 && g1.tile != 10)) {
+    // pairs the fused kernel does not cover
     if (have_prev && (e = launch_finalize(gp.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
     GemmPlan w = g1;
     w.ws_path = g1.ws_path && !defer1;

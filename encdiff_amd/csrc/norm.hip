@@ -662,7 +662,8 @@ int gn_check(const EncdiffGroupNormArgs* a) {
 }  // namespace
 
 extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream) {
-  if (!a || !a->x || !a->y || !a->stats || !a->gamma || !a->beta) return ENCDIFF_ERR_ARG;
+  if (a && a->dtype == ENCDIFF_DT_F32) return ed_groupnorm_fwd_f32(a, (hipStream_t)stream);
+  if (!a || a->dtype != ENCDIFF_DT_BF16 || !a->x || !a->y || !a->stats || !a->gamma || !a->beta) return ENCDIFF_ERR_ARG;
   const int cs = gn_check(a);
   if (cs < 0) return cs;
   // producer statistics feed the two statistics kernels where their layout fits; other
@@ -695,6 +696,7 @@ extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream
 }
 
 extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream) {
+  if (a && a->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_UNSUPPORTED;  // fp32: forward only
   if (!a || !a->x || !a->dy || !a->dx || !a->stats || !a->dgamma_part || !a->dbeta_part) return ENCDIFF_ERR_ARG;
   if (a->film && !a->dfilm) return ENCDIFF_ERR_ARG;
   const int cs = gn_check(a);
@@ -731,5 +733,12 @@ static int ln_dispatch(const EncdiffLayerNormArgs* a, bool bwd, void* stream) {
   }
 }
 
-extern "C" int encdiff_layernorm_fwd(const EncdiffLayerNormArgs* a, void* stream) { return ln_dispatch(a, false, stream); }
-extern "C" int encdiff_layernorm_bwd(const EncdiffLayerNormArgs* a, void* stream) { return ln_dispatch(a, true, stream); }
+extern "C" int encdiff_layernorm_fwd(const EncdiffLayerNormArgs* a, void* stream) {
+  if (a && a->dtype == ENCDIFF_DT_F32) return ed_layernorm_fwd_f32(a, (hipStream_t)stream);
+  if (a && a->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_ARG;
+  return ln_dispatch(a, false, stream);
+}
+extern "C" int encdiff_layernorm_bwd(const EncdiffLayerNormArgs* a, void* stream) {
+  if (a && a->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_UNSUPPORTED;  // fp32: forward only
+  return ln_dispatch(a, true, stream);
+}

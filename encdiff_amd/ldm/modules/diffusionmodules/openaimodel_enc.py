@@ -189,6 +189,15 @@ class UNetModel(nn.Module):
         c = context[0] if isinstance(context, (list, tuple)) else context
         c = c.reshape(x.shape[0], -1).float()
         ex = self.executor()
+        if getattr(self, "hip_precision", "bf16") == "fp32":
+            # the reference's precision (SURVEY §8(b) convention 5): fp32 activations end to end,
+            # forward only (parity checks, reference-precision sampling)
+            if torch.is_grad_enabled():
+                raise RuntimeError("hip_precision='fp32' is a forward-only path (use torch.no_grad())")
+            if getattr(self, "_f32", None) is None or self._f32.ex is not ex:
+                from encdiff_amd.unet_f32 import UNetF32
+                self._f32 = UNetF32(ex)
+            return self._f32.forward(x, timesteps, c)
         ex.infer = not torch.is_grad_enabled()  # inference-only fusions (no saved activations)
         if torch.is_grad_enabled():
             self._arena.attach_grads()

@@ -793,3 +793,76 @@ def encoder_warp_bwd(u, params, unit_stride, units, context_dim, dout, du, grads
     check(lib.encdiff_encoder_warp_bwd(_p(u), u.stride(0), u.shape[0], units, _p(params), unit_stride, context_dim,
                                        _p(dout), dout.stride(0), _p(du), du.stride(0), _p(grads), _p(part), _s()),
           "encdiff_encoder_warp_bwd")
+
+
+# ------------------------------------------------------------------ fp32 (ENCDIFF_DT_F32) forward
+# The reference-precision forms of the same entry points (include/encdiff_hip.h "dtype"): fp32
+# activations end to end, for the fp32 parity path (unet_f32.py).
+def _f32(t):
+    assert t.dtype == F32, "fp32 operand expected"
+    return t
+
+
+def gemm_f32(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, conv: Optional[L.ConvGeom] = None, bias=None,
+             resid=None, accumulate=False, alpha=1.0):
+    args = L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=L.OPB_ROWK,
+                      c_mode=L.OUT_F32_ACCUM if accumulate else L.OUT_F32, a=_p(_f32(a)), lda=lda, b=_p(_f32(b)),
+                      ldb=ldb, c=_p(_f32(c)), ldc=ldc, conv=conv if conv is not None else L.ConvGeom(), alpha=alpha,
+                      split_k=1, bias=_p(bias), resid=_p(resid), ld_resid=_ld(resid) if resid is not None else 0,
+                      dtype=L.DT_F32)
+    check(lib.encdiff_gemm(C.byref(args), _s()), "encdiff_gemm(fp32)")
+
+
+def linear_f32(x, w, y, bias=None, resid=None):
+    """y[M][N] = x[M][K] w[N][K]^T (+bias)(+resid), fp32 rows."""
+    M, K = x.shape
+    N = w.shape[0]
+    gemm_f32(M, N, K, x, _ld(x), w, _ld(w), y, _ld(y), bias=bias, resid=resid)
+
+
+def conv3x3_f32(x, g: Geom, cin, w, y, bias=None, resid=None, resample=0):
+    """3x3 conv (pad 1) of fp32 NHWC rows; w [cout][9*cin] (tap-major, channel inner); resample
+    NONE or UP2 (nearest x2 read through the im2col gather, g = the output geometry)."""
+    gemm_f32(g.pixels, w.shape[0], 9 * cin, x, 0, w, _ld(w), y, _ld(y), a_mode=L.OPA_IM2COL,
+             conv=L.ConvGeom(batch=g.batch, h=g.h, w=g.w, cin=cin, resample=resample, ld_src=_ld(x)),
+             bias=bias, resid=resid)
+
+
+def groupnorm_f32(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_film=0, groups=32):
+    a = L.GroupNormArgs(batch=g.batch, hw=g.h * g.w, c=x.shape[1], groups=groups, eps=eps, silu=int(silu),
+                        x=_p(_f32(x)), ldx=_ld(x), gamma=_p(gamma), beta=_p(beta), film=_p(film), ld_film=ld_film,
+                        y=_p(_f32(y)), ldy=_ld(y), stats=_p(stats), dtype=L.DT_F32)
+    check(lib.encdiff_groupnorm_fwd(C.byref(a), _s()), "encdiff_groupnorm_fwd(fp32)")
+
+
+def layernorm_f32(x, gamma, beta, y, eps=1e-5):
+    rows, c = x.shape
+    a = L.LayerNormArgs(rows=rows, c=c, eps=eps, x=_p(_f32(x)), ldx=_ld(x), gamma=_p(gamma), beta=_p(beta),
+                        y=_p(_f32(y)), ldy=_ld(y), dtype=L.DT_F32)
+    check(lib.encdiff_layernorm_fwd(C.byref(a), _s()), "encdiff_layernorm_fwd(fp32)")
+
+
+def attention_f32(q, k, v, o, batch, heads, sq, sk, dh, lse=None):
+    a = L.AttnArgs(batch=batch, heads=heads, sq=sq, sk=sk, dh=dh, scale=dh ** -0.5,
+                   q=_p(_f32(q)), ldq=_ld(q), k=_p(_f32(k)), ldk=_ld(k), v=_p(_f32(v)), ldv=_ld(v),
+                   o=_p(_f32(o)), ldo=_ld(o), lse=_p(lse), dtype=L.DT_F32)
+    check(lib.encdiff_attention_fwd(C.byref(a), _s()), "encdiff_attention_fwd(fp32)")
+
+
+def ew_f32(op, x, y, x2=None, rows=None, cols=None, accumulate=False, resample=0, g: Optional[Geom] = None):
+    rows = rows if rows is not None else y.shape[0]
+    cols = cols if cols is not None else y.shape[1]
+    a = L.EwArgs(op=op, rows=rows, cols=cols, x=_p(_f32(x)), ldx=_ld(x), x2=_p(x2),
+                 ldx2=_ld(x2) if x2 is not None else 0, y=_p(_f32(y)), ldy=_ld(y), accumulate=int(accumulate),
+                 resample=resample, batch=g.batch if g else 0, h=g.h if g else 0, w=g.w if g else 0, dtype=L.DT_F32)
+    check(lib.encdiff_elementwise(C.byref(a), _s()), "encdiff_elementwise(fp32)")
+
+
+def timestep_embedding_f32(t, dim, out, max_period=10000.0):
+    check(lib.encdiff_timestep_embedding_f32(_p(t), t.shape[0], dim, max_period, _p(_f32(out)), _s()),
+          "encdiff_timestep_embedding_f32")
+
+
+def nchw_rows_f32(x, batch, c, hw, cpad, y, ld, to_rows=True):
+    check(lib.encdiff_nchw_rows_f32(_p(_f32(x)), batch, c, hw, cpad, _p(_f32(y)), ld, 0 if to_rows else 1, _s()),
+          "encdiff_nchw_rows_f32")

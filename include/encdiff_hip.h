@@ -21,6 +21,15 @@
  *  - Layout: activations are [rows][channels] bf16 (NHWC for images, token-major
  *    for transformer tokens) with a row stride `ld`; statistics / master weights /
  *    gradients are fp32.
+ *  - dtype: the GEMM, GroupNorm, LayerNorm, attention and elementwise args carry a `dtype`
+ *    field.  ENCDIFF_DT_BF16 (0, the default) is the product path above.  ENCDIFF_DT_F32
+ *    runs the same entry point on fp32 activations (every bf16 operand / output named in
+ *    the struct becomes fp32; forward only): the reference's precision (main_val.py:525),
+ *    so a denoiser forward can be held to the fp32 tolerance.  Supported there: GEMM
+ *    OPA_ROWK / OPA_IM2COL (resample NONE / UP2) x OPB_ROWK into OUT_F32 / OUT_F32_ACCUM
+ *    (alpha, bias, fp32 resid; no split-K / epilogue statistics); GroupNorm without
+ *    in_stats; LayerNorm; attention dh in {8, 16, 32, 64} (no fp8); elementwise COPY, SILU,
+ *    GEGLU, ADD, RESAMPLE.  Other combinations return ENCDIFF_ERR_UNSUPPORTED.
  */
 #ifndef ENCDIFF_HIP_H
 #define ENCDIFF_HIP_H
@@ -34,6 +43,8 @@ extern "C" {
 #define ENCDIFF_ERR_SHAPE (-2)
 #define ENCDIFF_ERR_UNSUPPORTED (-3)
 #define ENCDIFF_ERR_LAUNCH (-1000)
+
+enum { ENCDIFF_DT_BF16 = 0, ENCDIFF_DT_F32 = 1 };
 
 /* ---------------------------------------------------------------- GEMM / conv
  * C[M][N] = alpha * sum_k A[m][k] * B[k][n]  (+ bias[n]) (+ resid[m][n])
@@ -110,8 +121,10 @@ typedef struct EncdiffGemmArgs {
   float* bias_grad;          /* OPA_ROWM only: += sum_k A[m][k] into bias_grad[m]  */
   int tile;                  /* 0 = auto, else 1:128x128 2:128x64 3:64x128 4:64x64, 5:64x64 with a
                                 4-deep LDS ring, 6:64x128 with a 3-deep ring, 7:64x64 and
-                                8:64x128 with 128-deep k stages (others: 64) */
-  int pad2_;
+                                8:64x128 with 128-deep k stages (others: 64), 9 / 10: 64x64 with a
+                                6- / 8-deep ring (96 / 128 KB of LDS: a short split's k-tiles all
+                                in flight at once), 16-23: halo tiles (implicit im2col only) */
+  int dtype;                 /* ENCDIFF_DT_BF16 (a, b, resid and BF16 outputs bf16) or ENCDIFF_DT_F32 */
   float* workspace;          /* split_k > 1 with a BF16/F32/F32_ACCUM c_mode: fp32 scratch of split_k*M*N
                                 (+ split_k*M when bias_grad is set: per-split bias-gradient slabs);
                                 each split writes its own [M][N] slab, a finalize pass sums the
@@ -176,7 +189,7 @@ typedef struct EncdiffGroupNormArgs {
   const void* dy; long lddy;
   void* dx; long lddx;       /* bf16                                                */
   int accumulate_dx;         /* dx += result                                        */
-  int pad_;
+  int dtype;                 /* ENCDIFF_DT_F32: x, y fp32 (forward)                 */
   float* dgamma_part;        /* fp32 [batch][ld_part] per-image partial sums (reduced later) */
   float* dbeta_part;
   long ld_part;
@@ -207,7 +220,7 @@ typedef struct EncdiffLayerNormArgs {
   float* dbeta_part;
   long ld_part;
   int parts;                 /* number of partial rows (grid size of the backward) */
-  int pad_;
+  int dtype;                 /* ENCDIFF_DT_F32: x, y fp32 (forward)                 */
   const void* resid; long ld_resid; /* backward: optional bf16 residual-branch gradient:
                                         dx = resid + LN_bwd (out of place; may alias dx) */
 } EncdiffLayerNormArgs;
@@ -234,8 +247,9 @@ typedef struct EncdiffAttnArgs {
   void* dq; long lddq;
   void* dk; long lddk;
   void* dv; long lddv;
-  int fp8_qk, pad_;          /* 1: scores Q K^T on fp8 (OCP e4m3) MFMA, fwd and bwd recompute;
+  int fp8_qk;                /* 1: scores Q K^T on fp8 (OCP e4m3) MFMA, fwd and bwd recompute;
                                 softmax, P V and the gradient products stay bf16 / fp32 */
+  int dtype;                 /* ENCDIFF_DT_F32: q, k, v, o fp32 (forward)             */
 } EncdiffAttnArgs;
 
 int encdiff_attention_fwd(const EncdiffAttnArgs* args, void* stream);
@@ -263,7 +277,7 @@ typedef struct EncdiffEwArgs {
   int accumulate;            /* y += result                                        */
   int resample;              /* ENCDIFF_RESAMPLE_* for RESAMPLE ops                */
   int batch, h, w;           /* output spatial dims for RESAMPLE ops               */
-  int pad_;
+  int dtype;                 /* ENCDIFF_DT_F32: x, x2, y fp32                       */
 } EncdiffEwArgs;
 
 int encdiff_elementwise(const EncdiffEwArgs* args, void* stream);
@@ -299,6 +313,16 @@ int encdiff_small_conv_bwd(const EncdiffSmallConvArgs* args, void* stream);
  */
 int encdiff_timestep_embedding(const long long* t, int batch, int dim, float max_period,
                                void* out_bf16, void* stream);
+
+/* The same embedding in fp32 [batch][dim] (the ENCDIFF_DT_F32 forward). */
+int encdiff_timestep_embedding_f32(const long long* t, int batch, int dim, float max_period, float* out,
+                                   void* stream);
+
+/* fp32 layout change of the denoiser's input / output (the ENCDIFF_DT_F32 forward):
+ * dir 0: x NCHW [batch][c][hw] -> y rows [batch*hw][ld], channels c..cpad-1 zero;
+ * dir 1: x rows [batch*hw][ld] -> y NCHW (first c channels). */
+int encdiff_nchw_rows_f32(const float* x, int batch, int c, int hw, int cpad, float* y, long ld, int dir,
+                          void* stream);
 
 /* q_sample (ddpm_enc.py:292-295): x_t = sqrt_ac[t] x0 + sqrt_1mac[t] eps.
  * x0, eps, x_t fp32 NCHW [batch][3*hw]. */

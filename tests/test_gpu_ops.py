@@ -156,11 +156,12 @@ def test_split_k_in_kernel_combine(O, tile, split):
     assert int(O._counters().abs().sum()) == 0
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 def test_gemm_tiles(O, tile):
     """Every tile shape / LDS ring depth (tiles 5, 6: 4- and 3-deep rings; 7, 8: 128-deep k
-    stages) on a ragged problem with a k-tile count that is not a multiple of the ring depth,
-    split-K 1 and 3, and on a 3x3 conv forward + input gradient."""
+    stages; 9, 10: 6- and 8-deep rings) on a ragged problem with a k-tile count that is not a
+    multiple of the ring depth, split-K 1 and 3, on a 3x3 conv forward + input gradient, and (deep
+    rings) a linear layer's paired weight / input gradient."""
     torch.manual_seed(3)
     M, N, K = 328, 200, 1000
     x, w = bf(M, K), bf(N, K, scale=K ** -0.5)
@@ -192,6 +193,22 @@ def test_gemm_tiles(O, tile):
     assert rel(nhwc(y, g), ref) < 1e-2, tile
     ref.backward(nhwc(dy, g))
     assert rel(nhwc(dx, g), xin.grad) < 1e-2, tile
+    if tile in (5, 9, 10):  # paired linear backward, both halves on the deep ring
+        L = O.L
+        Mt, Ct, Ci = 2048, 64, 96
+        dyl, xl, wl = bf(Mt, Ct), bf(Mt, Ci), bf(Ct, Ci)
+        for split in (1, 4, 16):
+            dw = torch.full((Ct, Ci), 0.25, device=dev)
+            dxl = torch.empty(Mt, Ci, device=dev, dtype=torch.bfloat16)
+            O.gemm_pair(lambda off: O.gemm_args(Ct, Ci, Mt, dyl, Ct, xl, Ci, dw, Ci, a_mode=L.OPA_ROWM,
+                                                b_mode=L.OPB_ROWN, c_mode=L.OUT_F32_ACCUM, split_k=split, tile=tile,
+                                                ws_offset=off),
+                        lambda off: O.gemm_args(Mt, Ci, Ct, dyl, Ct, wl, Ci, dxl, Ci, b_mode=L.OPB_ROWN, split_k=1,
+                                                tile=tile, ws_offset=off))
+            O.flush()
+            torch.cuda.synchronize()
+            assert rel(dw, dyl.float().t() @ xl.float() + 0.25) < 1e-5, (tile, split)
+            assert rel(dxl, dyl.float() @ wl.float()) < 1e-2, (tile, split)
 
 
 HALO_TWIN = {16: 4, 17: 2, 18: 1, 22: 3}  # halo tile -> the ring tile of the same BM x BN

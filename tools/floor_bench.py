@@ -36,5 +36,31 @@ def main():
         print(f"gemm {M:5d}x{N:4d}x{K:5d} split {split}: {us:6.2f} us")
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+
+
+def boundary():
+    """Per-node cost of a trivial kernel after producers of different sizes (graph replay): the
+    dependent-boundary price inside a step (MI355X_MICROARCH.md price list 'boundary')."""
+    from encdiff_amd import ops
+    from gn_bench import timed
+    L = ops.L
+    bf = torch.bfloat16
+    dev = "cuda"
+    x = torch.randn(64, 64, device=dev).to(bf)
+    y = torch.empty_like(x)
+    ew = lambda: ops.ew(L.EW_COPY, x, y)  # noqa: E731
+    print(f"ew alone                  {timed(ew):6.2f} us")
+    for mb in (1, 4, 16):
+        n = mb * 1024 * 1024 // 2
+        a = torch.randn(n // 64, 64, device=dev).to(bf)
+        b = torch.empty_like(a)
+        big = lambda: ops.ew(L.EW_COPY, a, b)  # noqa: E731
+        t_big = timed(big)
+        t_pair = timed(lambda: (big(), ew()))
+        print(f"copy {mb:2d} MB {t_big:6.2f} us; + trivial kernel after it: +{t_pair - t_big:5.2f} us")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "boundary":
+    boundary()

@@ -142,7 +142,8 @@ def main():
         # LDS for the larger tile, so the deep-ring / deep-k tiles (5-8) cost the weight-gradient
         # blocks occupancy in the step (this standalone timing cannot see it): not candidates
         dgrad = a.b_mode in (L.OPB_ROWN, L.OPB_CONV_DGRAD) and not wgrad
-        cands = (1, 2, 3, 4, 5, 7) if wgrad else ((1, 2, 3, 4, 5) if dgrad else (1, 2, 3, 4, 5, 6, 7, 8))
+        cands = (1, 2, 3, 4, 5, 7, 9, 10) if wgrad else ((1, 2, 3, 4, 5, 9, 10) if dgrad else
+                                                      (1, 2, 3, 4, 5, 6, 7, 8, 9, 10))
         if a.a_mode == L.OPA_IM2COL and a.b_mode in (L.OPB_ROWK, L.OPB_CONV_DGRAD):
             # halo tiles (window staged once; split-K 1); paired input gradients: 16, 17, 18, 22
             halo = (16, 17, 18, 22) if dgrad else tuple(ops.HALO_TILES)
@@ -216,12 +217,13 @@ def main():
             seen_p.add((wk, dk))
             w_split = table[wk][1]
             conv = d.a_mode == L.OPA_IM2COL
-            dc = {(table[dk][0], table[dk][1])} | {(t, s) for t in (1, 2, 3, 4, 5) for s in (1, 2, 4, 8) if d.K // s >= 64}
+            dc = {(table[dk][0], table[dk][1])} | {(t, s) for t in (1, 2, 3, 4, 5, 9, 10) for s in (1, 2, 4, 8)
+                                                   if d.K // s >= 64}
             if conv:
                 dc |= {(t, 1) for t in (16, 17, 18, 22)
                        if ops.halo_fits(t, d.conv.batch, d.conv.h, d.conv.w, d.conv.cin, d.conv.resample)}
             best = None
-            for wt in sorted({4, 5, 7, table[wk][0]}):  # tiles 1-3: unpaired (back to back)
+            for wt in sorted({4, 5, 7, 9, 10, table[wk][0]}):  # tiles 1-3: unpaired (back to back)
                 wa = copy_args(w, wt, w_split, 0)
                 for dt, ds_ in sorted(dc):
                     if ds_ > 1 and ds_ * d.M * (d.N + 1) + ops.ws_floats(wa) > ops.WS_FLOATS:
