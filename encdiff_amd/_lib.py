@@ -147,6 +147,7 @@ _PROTOS = {
     "encdiff_timestep_embedding_f32": [vp, C.c_int, C.c_int, C.c_float, vp, vp],
     "encdiff_nchw_rows_f32": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_long, C.c_int, vp],
     "encdiff_q_sample": [vp, vp, vp, vp, vp, C.c_int, C.c_int, vp, vp],
+    "encdiff_q_sample_scaled": [vp, vp, vp, vp, vp, vp, C.c_int, C.c_int, vp, vp],
     "encdiff_l1_loss": [vp, vp, vp, vp, C.c_int, C.c_int, C.c_float, vp, vp, vp, vp, vp],
     "encdiff_ddim_step": [vp, vp, vp, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, vp, vp, vp],
     "encdiff_ddim_step_indexed": [vp, vp, vp, C.c_int, vp, vp, C.c_int, vp, vp, vp],
@@ -158,6 +159,9 @@ _PROTOS = {
     "encdiff_encoder_warp_bwd": [vp, C.c_long, C.c_int, C.c_int, vp, C.c_long, C.c_int, vp, C.c_long, vp, C.c_long,
                                  vp, vp, vp],
     "encdiff_encoder_warp_partials_floats": [C.c_int, C.c_int, C.c_long],
+    "encdiff_encoder_head_fwd": [vp, C.c_long, C.c_int, C.c_int, vp, vp, C.c_int, vp, C.c_long, vp],
+    "encdiff_encoder_head_bwd": [vp, C.c_long, C.c_int, C.c_int, vp, C.c_int, vp, C.c_long, vp, C.c_long, vp, vp,
+                                 vp],
     "encdiff_gather_images_u8": [vp, C.c_longlong, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, C.c_int,
                                  vp, vp],
     "encdiff_batchnorm_partials_floats": [C.c_int, C.c_int],

@@ -111,6 +111,7 @@ class Encoder4TrunkExecutor:
             self.res.append(dict(prefix=f"encoder.{ri}.convs.", conv3=c3, bn=bnm, conv1=c1,
                                  post_bn=(f"encoder.{bi}", mods[bi]) if bi is not None else None))
         self.flat = mods[lin]
+        self.lin_name = f"encoder.{lin}"
         pk = PackTable(arena)
         a = arena
         c0 = self.convs[0]
@@ -218,6 +219,7 @@ class Encoder4TrunkExecutor:
                 b[f"{k}{j}"] = t(n4, d, F32 if k in ("t", "r") else BF16)
         b["dw0"] = t(d, 16 * 8, F32)
         b["flat"] = torch.empty(B, 16 * d, device=self.dev, dtype=F32)
+        b["u"] = torch.empty(B, self.flat.weight.shape[0], device=self.dev, dtype=F32)
         self._bufs[B] = b
         return b
 
@@ -265,9 +267,11 @@ class Encoder4TrunkExecutor:
         L.check(L.lib.encdiff_batchnorm_apply(C.byref(a), ops._s()), "encdiff_batchnorm_apply")
 
     # ------------------------------------------------------------ forward
-    def forward(self, img: torch.Tensor, train: bool = True) -> torch.Tensor:
-        """img fp32 NCHW (B, 3, 64, 64) -> trunk output fp32 (B, d*16) in NCHW-flatten order.
-        train=False: BatchNorm with the running statistics (eval mode; no backward)."""
+    def forward(self, img: torch.Tensor, train: bool = True, head: bool = False) -> torch.Tensor:
+        """img fp32 NCHW (B, 3, 64, 64) -> trunk output fp32 (B, d*16) in NCHW-flatten order, or
+        with head=True the codes u = Linear(View(trunk)) (B, latent_unit) (encdiff_encoder_head_fwd on
+        the NHWC rows: no flatten copy).  train=False: BatchNorm with the running statistics (eval
+        mode; no backward)."""
         assert img.is_cuda and img.dtype == F32 and img.shape[1:] == (self.cin_img, self.img, self.img), \
             f"HIP Encoder4 trunk: fp32 (B, {self.cin_img}, {self.img}, {self.img}) device input"
         B = img.shape[0]
@@ -302,19 +306,37 @@ class Encoder4TrunkExecutor:
                 bn(B, key, mod, b[f"r{j}"], b[f"R{j + 1}"][:, 3 * d:], True)
         if train and self.enc.training:
             self._count_batch()  # num_batches_tracked += 1 of every trunk BatchNorm2d (one launch)
+        if head:
+            r1, u = b["r1"], b["u"]
+            L.check(L.lib.encdiff_encoder_head_fwd(r1.data_ptr(), r1.stride(0), B, d,
+                                                   self.P(self.lin_name + ".weight").data_ptr(),
+                                                   self.P(self.lin_name + ".bias").data_ptr(), u.shape[1],
+                                                   u.data_ptr(), u.stride(0), ops._s()), "encdiff_encoder_head_fwd")
+            return u
         flat = b["flat"]
         flat.view(B, d, 4, 4).copy_(b["r1"].view(B, 4, 4, d).permute(0, 3, 1, 2))
         return flat
 
     # ------------------------------------------------------------ backward
-    def backward(self, d_flat: torch.Tensor):
-        """d_flat fp32 (B, d*16), NCHW-flatten order -> weight / BN gradients (+=) in the arena."""
+    def backward(self, d_flat: torch.Tensor, head: bool = False):
+        """d_flat fp32 (B, d*16), NCHW-flatten order -> weight / BN gradients (+=) in the arena.
+        head=True: d_flat is d u (B, latent_unit) of forward(head=True); the head's backward
+        (encdiff_encoder_head_bwd) writes the trunk output gradient and the Linear's gradients."""
         B = d_flat.shape[0]
         b = self._bufs[B]
         d = self.d
         g4 = Geom(B, 4, 4)
         dh = b["dr1"]
-        dh.view(B, 4, 4, d).copy_(d_flat.view(B, d, 4, 4).permute(0, 2, 3, 1))
+        if head:
+            du, r1 = d_flat.contiguous(), b["r1"]
+            L.check(L.lib.encdiff_encoder_head_bwd(r1.data_ptr(), r1.stride(0), B, d,
+                                                   self.P(self.lin_name + ".weight").data_ptr(), du.shape[1],
+                                                   du.data_ptr(), du.stride(0), dh.data_ptr(), dh.stride(0),
+                                                   self.G(self.lin_name + ".weight").data_ptr(),
+                                                   self.G(self.lin_name + ".bias").data_ptr(), ops._s()),
+                    "encdiff_encoder_head_bwd")
+        else:
+            dh.view(B, 4, 4, d).copy_(d_flat.view(B, d, 4, 4).permute(0, 2, 3, 1))
         for j in (1, 0):
             r = self.res[j]
             p = r["prefix"]
@@ -354,16 +376,17 @@ class Encoder4TrunkExecutor:
 
 
 class TrunkFn(torch.autograd.Function):
-    """Encoder4 trunk on HIP: image -> (B, d*16) fp32.  The parameters' gradients go straight
-    to the arena (their .grad views); `anchor` (a trunk parameter) only makes the output
-    require grad so the backward runs; the image gets no gradient."""
+    """Encoder4 trunk + head on HIP: image -> codes u (B, latent_unit) fp32 (the trunk, View and
+    Linear of Encoder4.encoder).  The parameters' gradients go straight to the arena (their .grad
+    views); `anchor` (a trunk parameter) only makes the output require grad so the backward
+    runs; the image gets no gradient."""
 
     @staticmethod
     def forward(ctx, img, anchor, ex):
         ctx.ex = ex
-        return ex.forward(img)
+        return ex.forward(img, head=True)
 
     @staticmethod
-    def backward(ctx, d_flat):
-        ctx.ex.backward(d_flat.contiguous())
+    def backward(ctx, du):
+        ctx.ex.backward(du, head=True)
         return None, None, None

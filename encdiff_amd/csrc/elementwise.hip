@@ -361,12 +361,13 @@ __global__ void temb_kernel(const long long* t, int batch, int dim, float max_pe
 }
 
 __global__ void qsample_kernel(const float* x0, const float* eps, const long long* t, const float* sa,
-                               const float* s1a, int batch, int per, float* xt) {
+                               const float* s1a, int batch, int per, float* xt, const float* x0_scale) {
   const long n = (long)batch * per;
+  const float sc = x0_scale ? *x0_scale : 1.f;  // get_first_stage_encoding's scale_factor, folded in
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int b = (int)(i / per);
     const long long tt = t[b];
-    xt[i] = sa[tt] * x0[i] + s1a[tt] * eps[i];
+    xt[i] = sa[tt] * (sc * x0[i]) + s1a[tt] * eps[i];
   }
 }
 
@@ -701,7 +702,17 @@ extern "C" int encdiff_q_sample(const float* x0, const float* eps, const long lo
                                 const float* s1a, int batch, int per, float* xt, void* stream) {
   if (!x0 || !eps || !t || !sa || !s1a || !xt) return ENCDIFF_ERR_ARG;
   hipLaunchKernelGGL(qsample_kernel, dim3(grid_for((long)batch * per)), dim3(256), 0, (hipStream_t)stream, x0, eps,
-                     t, sa, s1a, batch, per, xt);
+                     t, sa, s1a, batch, per, xt, (const float*)nullptr);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_q_sample_scaled(const float* x0, const float* x0_scale, const float* eps, const long long* t,
+                                       const float* sa, const float* s1a, int batch, int per, float* xt,
+                                       void* stream) {
+  if (!x0 || !x0_scale || !eps || !t || !sa || !s1a || !xt) return ENCDIFF_ERR_ARG;
+  hipLaunchKernelGGL(qsample_kernel, dim3(grid_for((long)batch * per)), dim3(256), 0, (hipStream_t)stream, x0, eps,
+                     t, sa, s1a, batch, per, xt, x0_scale);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }

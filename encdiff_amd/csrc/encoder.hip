@@ -252,3 +252,125 @@ extern "C" int encdiff_encoder_warp_bwd(const float* u, long ldu, int batch, int
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
+
+// ------------------------------------------------------------------ trunk head: View + Linear
+// Encoder4.encoder[-2:] (openaimodel_enc.py:1012-1013): View((-1, d*16)) of the NCHW trunk
+// output then Linear(d*16, latent_unit), on the trunk's NHWC fp32 rows directly: input element
+// (image b, channel c, pixel p) sits at r[(b*16 + p)*ldr + c] and is column k = c*16 + p of the
+// reference weight W[units][d*16].  fp32 throughout (the reference's precision).
+namespace {
+
+constexpr int HPIX = 16;  // the 4x4 grid the trunk ends on
+
+// forward: grid (image, unit quad); wave w of a workgroup owns unit j = 4 * blockIdx.y + w, lane l
+// sums columns k = l, l + 64, ... with 8 loads in flight (W rows read coalesced; the image's 8 KB
+// of rows stay in L1/L2), then one wave sum.
+__global__ __launch_bounds__(256) void head_fwd_kernel(const float* r, long ldr, int d, const float* W,
+                                                       const float* bias, int units, float* u, long ldu) {
+  const int b = blockIdx.x, K = d * HPIX, lane = threadIdx.x & 63;
+  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (j >= units) return;
+  const float* x = r + (long)b * HPIX * ldr;
+  const float* w = W + (long)j * K;
+  float a = 0.f;
+#pragma unroll 8
+  for (int k = lane; k < K; k += 64) {
+    const int c = k / HPIX, p = k - c * HPIX;
+    a += x[(long)p * ldr + c] * w[k];
+  }
+  a = wave_sum(a);
+  if (lane == 0) u[(long)b * ldu + j] = a + bias[j];
+}
+
+// backward, one launch: blocks [0, batch) write dr (bf16 NHWC, the trunk's output gradient) of one
+// image each (thread per column k, the image's du in LDS); the remaining blocks own 64 weight
+// columns each, 4 batch quarters per column (256 threads): dW[j][k] += sum_b du[b][j] x[b][k], the
+// quarters added in order through LDS (deterministic, no atomics); the first of them adds db.
+template <int UM>
+__global__ __launch_bounds__(256) void head_bwd_kernel(const float* r, long ldr, int d, const float* W, int units,
+                                                       int batch, const float* du, long lddu, bf16_t* dr, long lddr,
+                                                       float* dW, float* db) {
+  extern __shared__ float sdu[];  // [batch][UM] (dW blocks; then [4][UM][64] partials) or [UM]
+  const int K = d * HPIX;
+  // loads are never predicated (a runtime-conditional load is branched around and waited for one
+  // at a time): du is zero-padded to UM units in LDS, W rows beyond `units` clamp to row 0
+  if ((int)blockIdx.x < batch) {
+    const int b = blockIdx.x;
+    for (int j = threadIdx.x; j < UM; j += 256) sdu[j] = j < units ? du[(long)b * lddu + j] : 0.f;
+    __syncthreads();
+    for (int k = threadIdx.x; k < K; k += 256) {
+      const int c = k / HPIX, p = k - c * HPIX;
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < UM; ++j) a += sdu[j] * W[(long)(j < units ? j : 0) * K + k];
+      dr[((long)b * HPIX + p) * lddr + c] = f2bf(a);
+    }
+    return;
+  }
+  for (int e = threadIdx.x; e < batch * UM; e += 256) {
+    const int b = e / UM, j = e - b * UM;
+    sdu[e] = j < units ? du[(long)b * lddu + j] : 0.f;
+  }
+  __syncthreads();
+  const int blk = blockIdx.x - batch;
+  const int kl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int k = blk * 64 + kl;
+  const int qb = (batch + 3) / 4, b0 = q * qb, b1 = min(batch, b0 + qb);
+  float acc[UM];  // UM >= units, compile-time indices only (registers)
+#pragma unroll
+  for (int j = 0; j < UM; ++j) acc[j] = 0.f;
+  if (k < K) {
+    const int c = k / HPIX, p = k - c * HPIX;
+#pragma unroll 8
+    for (int b = b0; b < b1; ++b) {
+      const float xv = r[((long)b * HPIX + p) * ldr + c];
+#pragma unroll
+      for (int j = 0; j < UM; ++j) acc[j] += sdu[b * UM + j] * xv;
+    }
+  }
+  __syncthreads();  // sdu is reused for the partials
+  float* part = sdu;  // [4][UM][64]
+#pragma unroll
+  for (int j = 0; j < UM; ++j) part[(q * UM + j) * 64 + kl] = acc[j];
+  __syncthreads();
+  if (q == 0 && k < K) {
+#pragma unroll
+    for (int j = 0; j < UM; ++j)
+      if (j < units)
+        dW[(long)j * K + k] += ((part[j * 64 + kl] + part[(UM + j) * 64 + kl]) + part[(2 * UM + j) * 64 + kl]) +
+                               part[(3 * UM + j) * 64 + kl];
+  }
+  if (blk == 0 && threadIdx.x < units) {
+    float a = 0.f;
+    for (int b = 0; b < batch; ++b) a += du[(long)b * lddu + threadIdx.x];
+    db[threadIdx.x] += a;
+  }
+}
+
+}  // namespace
+
+extern "C" int encdiff_encoder_head_fwd(const float* r, long ldr, int batch, int d, const float* W, const float* bias,
+                                        int units, float* u, long ldu, void* stream) {
+  if (!r || !W || !bias || !u || batch <= 0 || d <= 0 || units <= 0 || ldr < d || ldu < units) return ENCDIFF_ERR_ARG;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(batch, (units + 3) / 4), dim3(256), 0, (hipStream_t)stream, r, ldr, d, W, bias,
+                     units, u, ldu);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_encoder_head_bwd(const float* r, long ldr, int batch, int d, const float* W, int units,
+                                        const float* du, long lddu, void* dr, long lddr, float* dW, float* db,
+                                        void* stream) {
+  if (!r || !W || !du || !dr || !dW || !db || batch <= 0 || d <= 0 || units <= 0 || units > 64 || lddr < d)
+    return ENCDIFF_ERR_ARG;
+  const int um = units <= 20 ? 20 : (units <= 40 ? 40 : 64);
+  size_t lds = (size_t)batch * um * sizeof(float);
+  if (lds < (size_t)4 * um * 64 * sizeof(float)) lds = (size_t)4 * um * 64 * sizeof(float);
+  if (lds > 64 * 1024) return ENCDIFF_ERR_SHAPE;
+  const int kb = (d * HPIX + 63) / 64;
+  auto kern = units <= 20 ? head_bwd_kernel<20> : (units <= 40 ? head_bwd_kernel<40> : head_bwd_kernel<64>);
+  hipLaunchKernelGGL(kern, dim3(batch + kb), dim3(256), lds, (hipStream_t)stream, r, ldr, d, W, units, batch, du, lddu,
+                     (bf16_t*)dr, lddr, dW, db);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}

@@ -346,9 +346,8 @@ class Encoder4(nn.Module):
         if (ex.arena.master._version, ex.arena.gen) != self._trunk_version:  # parameters modified in place
             self.repack_hip()
         if not self.training:
-            return self.encoder[-1](ex.forward(x.float(), train=False))
-        flat = TrunkFn.apply(x, self.encoder[0].weight, ex)
-        return self.encoder[-1](flat)
+            return ex.forward(x.float(), train=False, head=True).clone()
+        return TrunkFn.apply(x, self.encoder[0].weight, ex)
 
     def warp(self, u):
         if self._warp_bind is not None:

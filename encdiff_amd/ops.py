@@ -704,8 +704,13 @@ def timestep_embedding(t, dim, out, max_period=10000.0):
           "encdiff_timestep_embedding")
 
 
-def q_sample(x0, eps, t, sqrt_ac, sqrt_1mac, xt):
+def q_sample(x0, eps, t, sqrt_ac, sqrt_1mac, xt, x0_scale=None):
+    """x_t = sqrt_ac[t] x0 + sqrt_1mac[t] eps; x0_scale (device scalar): x0 := x0_scale * x0."""
     b = x0.shape[0]
+    if x0_scale is not None:
+        check(lib.encdiff_q_sample_scaled(_p(x0), _p(x0_scale), _p(eps), _p(t), _p(sqrt_ac), _p(sqrt_1mac), b,
+                                          x0.numel() // b, _p(xt), _s()), "encdiff_q_sample_scaled")
+        return
     check(lib.encdiff_q_sample(_p(x0), _p(eps), _p(t), _p(sqrt_ac), _p(sqrt_1mac), b, x0.numel() // b, _p(xt),
                                _s()), "encdiff_q_sample")
 

@@ -70,6 +70,13 @@ class HipTrainer:
         self.data = data
         self.img = torch.empty(batch_size, 3, self.res, self.res, device=self.dev)
         self.loss_buf = torch.zeros(4, device=self.dev)
+        # direct executor path (see _fwd_bwd): the EncDiff objective only
+        self._direct = (ldm.parameterization == "eps" and ldm.loss_type == "l1" and not ldm.learn_logvar and
+                        float(ldm.original_elbo_weight) == 0.0 and float(ldm.l_simple_weight) == 1.0 and
+                        os.environ.get("ENCDIFF_TRAIN_DIRECT", "1") != "0")
+        z_shape = (batch_size, ldm.channels, ldm.image_size, ldm.image_size)
+        self._xt = torch.empty(z_shape, device=self.dev)
+        self._seed = torch.empty(z_shape, device=self.dev)
         self.graph = graph
         self._feed = None  # test hook: batch, t and noise from static buffers (enable_feed)
         self._g_fb = None
@@ -99,21 +106,50 @@ class HipTrainer:
             self.data.draw(self.img, advance=advance)
 
     def _fwd_bwd(self):
-        """Everything up to the UNet backward.  At world size 1 Encoder4's backward runs
-        inside it (plain loss.backward()); with DP the autograd graph is cut at the concept
-        tokens so the UNet gradient bucket can be all-reduced while Encoder4's backward runs
-        (`_cond_bwd`)."""
+        """Everything up to the UNet backward.  The loss and the UNet run on the executor
+        directly (LatentDiffusion.p_losses restated without autograd: q_sample with the
+        scale_factor folded in, UNet forward, the fused L1 loss + gradient seed, UNet backward);
+        only the as-is Encoder4 keeps torch autograd, seeded with d(context).  At world size 1
+        Encoder4's backward runs inside this; with DP it is deferred (`_cond_bwd`) so the UNet
+        gradient buckets can be all-reduced meanwhile.  Objectives outside the EncDiff one (eps,
+        L1, fixed logvar, no ELBO term) take the reference-API p_losses + loss.backward() path."""
         ldm = self.ldm
         self.arena.grad.zero_()
         self._draw_batch()
         with torch.no_grad():
-            z = ldm.get_first_stage_encoding(ldm.encode_first_stage(self.img)).detach()
+            z = ldm.encode_first_stage(self.img)  # frozen VQ (HIP); scale_factor applied in q_sample
         c = ldm.get_learned_conditioning(self.img)
         if self._feed is not None:
             t, noise = self._feed["t"], self._feed["noise"]
         else:
             t = torch.randint(0, ldm.num_timesteps, (self.B,), device=self.dev)
             noise = torch.randn_like(z)
+        if not self._direct:
+            return self._fwd_bwd_api(z, c, t, noise)
+        ex = self.unet.executor()
+        ex.infer = False
+        self.arena.attach_grads()
+        sf = ldm.scale_factor
+        if not isinstance(sf, torch.Tensor):
+            sf = self._sf_dev = torch.full((1,), float(sf), device=self.dev)
+        from . import ops
+        ops.q_sample(z, noise, t, ldm.sqrt_alphas_cumprod, ldm.sqrt_one_minus_alphas_cumprod, self._xt, x0_scale=sf)
+        eps = ex.forward(self._xt, t, c.detach().reshape(self.B, -1).float())
+        ops.l1_loss(eps, noise, t, ldm.lvlb_weights, self.loss_buf[:2], grad=self._seed)
+        if self.world == 1:
+            dc = ex.backward(self._seed)
+            c.backward(dc.view_as(c))
+            return
+        if not self._split_checked:
+            self._plan_split(ex)
+        # split: d(context) is the executor's buffer, complete after backward_rest()
+        dc = ex.backward(self._seed, split=self._split_lo is not None)
+        self._c, self._dc = c, dc.view_as(c)
+
+    def _fwd_bwd_api(self, z, c, t, noise):
+        """The reference-API form (LatentDiffusion.p_losses + autograd) for other objectives."""
+        ldm = self.ldm
+        z = ldm.get_first_stage_encoding(z)
         if self.world == 1:
             loss, ld = ldm.p_losses(z, c, t, noise)
             loss.backward()
@@ -126,7 +162,6 @@ class HipTrainer:
             ex.split_requested = self._split_lo is not None
             loss.backward()
             ex.split_requested = False
-            # split: d(context) is the executor's buffer, complete after backward_rest()
             self._c, self._dc = c, (ex.d_ctx if self._split_lo is not None else c_det.grad)
         self.loss_buf[0].copy_(ld["train/loss_simple"])
         self.loss_buf[1].copy_(ld["train/loss_vlb"])

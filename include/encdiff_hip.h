@@ -329,6 +329,12 @@ int encdiff_nchw_rows_f32(const float* x, int batch, int c, int hw, int cpad, fl
 int encdiff_q_sample(const float* x0, const float* eps, const long long* t, const float* sqrt_ac,
                      const float* sqrt_1mac, int batch, int per_sample, float* x_t, void* stream);
 
+/* The same with x0 = scale[0] * z: get_first_stage_encoding's scale_factor (ddpm_enc.py:775-783,
+ * a device scalar) applied on the fly, so the scaled latent is never materialised. */
+int encdiff_q_sample_scaled(const float* z, const float* scale, const float* eps, const long long* t,
+                            const float* sqrt_ac, const float* sqrt_1mac, int batch, int per_sample, float* x_t,
+                            void* stream);
+
 /* p_losses L1 (ddpm_enc.py:1194-1213): loss_simple[b] = mean|eps - pred|,
  * out[0] = mean_b loss_simple (= loss with logvar 0), out[1] = mean_b lvlb[t_b] loss_simple[b];
  * grad_pred = sign(pred - eps) / (batch * per_sample) * l_simple_weight.
@@ -423,6 +429,17 @@ int encdiff_encoder_warp_fwd(const float* u, long ldu, int batch, int units, con
 int encdiff_encoder_warp_bwd(const float* u, long ldu, int batch, int units, const float* params,
                              long unit_stride, int context_dim, const float* dout, long lddo, float* du,
                              long lddu, float* grads, float* partials, void* stream);
+/* Encoder4's trunk head (openaimodel_enc.py:1012-1013): View((-1, d*16)) of the NCHW 4x4 trunk
+ * output + Linear(d*16, units), read straight from the trunk's NHWC fp32 rows r [batch*16][ldr]
+ * (element (b, c, p) at r[(b*16 + p)*ldr + c], column k = c*16 + p of W [units][d*16], the
+ * reference layout).  fp32.  fwd: u [batch][ldu] = x W^T + bias.  bwd (one launch): dr (bf16
+ * NHWC rows, the trunk's output gradient) = du W, dW += du^T x, db += sum_b du (batch order,
+ * deterministic).  Replaces the flatten copy, the Linear GEMMs and their gradient adds. */
+int encdiff_encoder_head_fwd(const float* r, long ldr, int batch, int d, const float* W, const float* bias,
+                             int units, float* u, long ldu, void* stream);
+int encdiff_encoder_head_bwd(const float* r, long ldr, int batch, int d, const float* W, int units,
+                             const float* du, long lddu, void* dr, long lddr, float* dW, float* db,
+                             void* stream);
 /* fp32 scratch the backward needs for its per-batch-chunk weight-gradient partials. */
 int encdiff_encoder_warp_partials_floats(int batch, int units, long unit_stride);
 

@@ -64,3 +64,26 @@ def boundary():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "boundary":
     boundary()
+
+
+def graph_size():
+    """Per-node cost of trivial kernels vs the number of nodes in one captured graph, and with
+    several distinct kernels interleaved (the step's graph holds ~840 nodes)."""
+    from encdiff_amd import ops
+    from gn_bench import timed
+    L = ops.L
+    bf = torch.bfloat16
+    dev = "cuda"
+    x = torch.randn(64, 64, device=dev).to(bf)
+    y = torch.empty_like(x)
+    t = torch.zeros(128, dtype=torch.long, device=dev)
+    te = torch.empty(128, 64, device=dev, dtype=bf)
+    z = torch.zeros(4096, device=dev)
+    for reps in (50, 200, 800):
+        print(f"{reps:4d} ew nodes: {timed(lambda: ops.ew(L.EW_COPY, x, y), reps=reps):6.2f} us/node; "
+              f"ew+temb+torch add: {timed(lambda: (ops.ew(L.EW_COPY, x, y), ops.timestep_embedding(t, 64, te), z.add_(1)), reps=reps) / 3:6.2f} us/node",
+              flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "graph":
+    graph_size()
