@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--ddim-batch", type=int, default=8)
     ap.add_argument("--skip-ddim", action="store_true")
     ap.add_argument("--skip-cpu", action="store_true")
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="DP: all-reduce pieces of at most this many MB (default ENCDIFF_DP_BUCKET_MB or coarse buckets)")
     ap.add_argument("--config", default="shapes3d", choices=["shapes3d", "celeba128"],
                     help="shapes3d: configs[1] (the bench line); celeba128: configs[4], builder-defined")
     return ap.parse_args()
@@ -296,7 +298,7 @@ def main():
     ldm, cfg = build_ldm(args.config)
     metric, workload = WORKLOADS[args.config]
     pool = {"shapes3d": 480000, "celeba128": 202599}[args.config]  # dataset sizes (CelebA: 202,599 images)
-    tr = HipTrainer(ldm, args.batch, graph=not args.no_graph, pool_size=pool)
+    tr = HipTrainer(ldm, args.batch, graph=not args.no_graph, pool_size=pool, bucket_mb=args.bucket_mb or 0.0)
     tr.init_scale_factor()
     tr.capture(warmup=3)
     for _ in range(args.warmup):
@@ -306,6 +308,13 @@ def main():
     torch.cuda._sleep(1000)
     dt = time_steps(tr, args.steps)
     torch.cuda._sleep(1000)
+    dp_info = None
+    if world > 1:  # exchange timing on extra steps (the timed ones carry no extra events)
+        tr.dp_timing = True
+        for _ in range(min(10, args.steps)):
+            tr.step()
+        tr.dp_timing = False
+        dp_info = tr.dp_stats()
     if world > 1:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -317,6 +326,8 @@ def main():
     roof = kernel_roofline(tr)  # every rank (its recording step runs the DP exchange)
     if rank == 0:
         extra["roofline"] = roof
+        if dp_info is not None:
+            extra["dp"] = dp_info
         f_step = 3 * F_UNET_FWD_PER_IMG * args.batch  # configs[1]'s UNet; other configs: see the GEMM roofline
         if args.config == "shapes3d":
             extra["step_roofline"] = {"bound": "mfma", "unit": "TFLOP/s",

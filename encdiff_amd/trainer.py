@@ -53,7 +53,12 @@ class HipTrainer:
             self.sched = opt[1][0]["scheduler"]
         else:
             self.opt, self.sched = opt, None
+        self.bucket_mb = bucket_mb if bucket_mb else None  # None: ENCDIFF_DP_BUCKET_MB (0 = coarse buckets)
         self.buckets = GradBuckets.from_arena(arena)
+        if self.bucket_mb is not None:
+            self.buckets = GradBuckets(arena.grad, self.buckets.bounds, max_mb=self.bucket_mb)
+        self.dp_timing = False  # HIP events around the exchange (dp_stats)
+        self._dp_ev = []
         self._comm = torch.cuda.Stream() if self.world > 1 else None
         self.unet = ldm.model.diffusion_model
         # DP: split the UNet backward after the output blocks so their gradient bucket is
@@ -181,7 +186,7 @@ class HipTrainer:
         self._split_lo = lo
         rec = self.buckets.record
         self.buckets = GradBuckets(a.grad, [0, lo, a.ema_numel, a.numel], self.buckets.group,
-                                   self.buckets.grad_dtype)
+                                   self.buckets.grad_dtype, max_mb=self.buckets.max_mb)
         self.buckets.record = rec
 
     def _unet_rest(self):
@@ -200,6 +205,8 @@ class HipTrainer:
         (remaining UNet) with the cond stage backward, then bucket 2.  The current stream
         waits for all of them."""
         cur = torch.cuda.current_stream()
+        self.buckets.timing = self.dp_timing
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if self.dp_timing else None
         if unet_rest is not None:
             self._comm.wait_stream(cur)
             with torch.cuda.stream(self._comm):
@@ -209,19 +216,39 @@ class HipTrainer:
             with torch.cuda.stream(self._comm):
                 w_unet = self.buckets.start(0)
             cond_bwd()
+            if ev:
+                ev[0].record()  # the backward is complete
             w_cond = self.buckets.start(2)
             self.buckets.finish(1, w_out)
             self.buckets.finish(0, w_unet)
             self.buckets.finish(2, w_cond)
-            return
-        self._comm.wait_stream(cur)
-        with torch.cuda.stream(self._comm):
-            w0 = self.buckets.start(0)
-        cond_bwd()
-        w1 = self.buckets.start(1) if len(self.buckets) > 1 else None
-        self.buckets.finish(0, w0)
-        if len(self.buckets) > 1:
-            self.buckets.finish(1, w1)
+        else:
+            self._comm.wait_stream(cur)
+            with torch.cuda.stream(self._comm):
+                w0 = self.buckets.start(0)
+            cond_bwd()
+            if ev:
+                ev[0].record()
+            w1 = self.buckets.start(1) if len(self.buckets) > 1 else None
+            self.buckets.finish(0, w0)
+            if len(self.buckets) > 1:
+                self.buckets.finish(1, w1)
+        if ev:
+            ev[1].record()  # every bucket is reduced: the optimizer may start
+            self._dp_ev.append(ev)
+
+    def dp_stats(self):
+        """Exchange timing of the steps run with dp_timing on: the exposed wait from the end of
+        the backward to the optimizer's start (ms per step), and each coarse bucket's all-reduce
+        time (its pieces issued together, measured on the stream that issued them)."""
+        if not self._dp_ev:
+            return None
+        torch.cuda.synchronize()
+        exp = [a.elapsed_time(b) for a, b in self._dp_ev]
+        self._dp_ev = []
+        return {"exposed_ms": round(sum(exp) / len(exp), 4), "exposed_ms_max": round(max(exp), 4),
+                "bucket_mb": self.buckets.max_mb, "buckets": self.buckets.stats(),
+                "split_backward": self._split_lo is not None}
 
     # ---------------------------------------------------------------- setup
     def init_scale_factor(self):

@@ -53,6 +53,18 @@ def _worker(rank, world, port, outdir):
         b.finish(0, w0)
         b.finish(1, w1)
         res["bucket_err"] = float((ar.grad - full).abs().max())
+        # 1a. the bucket-size knob: each coarse bucket cut into pieces of <= max_mb, same mean
+        ar.grad.copy_(torch.randn(1000, generator=torch.Generator().manual_seed(dp.rank_seed(7, rank))))
+        full = ar.grad.clone()
+        dist.all_reduce(full)
+        full /= world
+        bp = dp.GradBuckets.from_arena(ar)
+        bp = dp.GradBuckets(ar.grad, bp.bounds, max_mb=256 * 4 / 2 ** 20)  # 256 fp32 per piece
+        assert [len(p) for p in bp.pieces] == [3, 2] and bp.pieces[0][0] == (0, 224)
+        assert all(hi - lo <= 256 for pc in bp.pieces for lo, hi in pc)
+        assert [pc[0][0] for pc in bp.pieces] == [0, 640] and [pc[-1][1] for pc in bp.pieces] == [640, 1000]
+        bp.allreduce_all()
+        res["piece_err"] = float((ar.grad - full).abs().max())
         # 1b. the same in the bf16 wire format: mean within bf16 rounding, equal on all ranks
         ar.grad.copy_(torch.randn(1000, generator=torch.Generator().manual_seed(dp.rank_seed(99, rank))))
         full = ar.grad.clone()
@@ -120,6 +132,7 @@ def test_gloo_world2():
     for r in res:
         assert r["bf16_rel"] < 1e-2
         assert r["bucket_err"] < 1e-6
+        assert r["piece_err"] < 1e-6
         assert r["dp_grad_err"] < 1e-6
         assert r["opt_rank_diff"] == 0.0
         assert r["scale_factor"] == 0.5

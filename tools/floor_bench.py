@@ -87,3 +87,34 @@ def graph_size():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "graph":
     graph_size()
+
+
+def after_real():
+    """Marginal graph-replay cost of a trivial kernel placed after real step kernels (a conv GEMM,
+    a GroupNorm), vs alone: does the dependent boundary grow behind real producers?"""
+    from encdiff_amd import ops
+    from encdiff_amd.ops import Geom
+    from gn_bench import timed
+    L = ops.L
+    bf = torch.bfloat16
+    dev = "cuda"
+    x = torch.randn(64, 64, device=dev).to(bf)
+    y = torch.empty_like(x)
+    ew = lambda: ops.ew(L.EW_COPY, x, y)  # noqa: E731
+    g = Geom(128, 16, 16)
+    a = torch.randn(g.pixels, 64, device=dev).to(bf)
+    w = (torch.randn(64, 576, device=dev) * 0.05).to(bf)
+    o = torch.empty(g.pixels, 64, device=dev, dtype=bf)
+    conv = lambda: ops.conv3x3_fwd(a, g, 64, w, o)  # noqa: E731
+    gam, bet = torch.ones(64, device=dev), torch.zeros(64, device=dev)
+    st = torch.empty(128, 64, device=dev)
+    gn = lambda: ops.groupnorm_fwd(o, g, gam, bet, a, st, 1e-5, True)  # noqa: E731
+    t_ew, t_conv, t_gn = timed(ew), timed(conv), timed(gn)
+    print(f"ew {t_ew:6.2f}  conv {t_conv:6.2f}  gn {t_gn:6.2f} us")
+    print(f"conv+ew {timed(lambda: (conv(), ew())):6.2f} (sum {t_conv + t_ew:6.2f})")
+    print(f"conv+gn {timed(lambda: (conv(), gn())):6.2f} (sum {t_conv + t_gn:6.2f})")
+    print(f"conv+gn+ew {timed(lambda: (conv(), gn(), ew())):6.2f}")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "real":
+    after_real()
