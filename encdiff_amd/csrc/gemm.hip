@@ -1104,6 +1104,358 @@ __global__ __launch_bounds__(256) void gemm_finalize2_kernel(const EncdiffGemmAr
   else gemm_finalize(p2, blockIdx.x - g1, gridDim.x - g1);
 }
 
+// ---------------------------------------------------------------------------
+// 3x3 conv weight gradient, tile id 32 (WG3): dW[co][tap*cin + ci] += sum_p dY[p][co] x[p+tap][ci]
+// (openaimodel_enc.py ResBlock / Upsample convs, autograd's weight gradient).
+//
+// The GEMM form (M = cout, N = 9 cin, K = pixels) stages every k-tile of dY once per 64 output
+// columns and the im2col of x once per tap, and fills the chip only through deep split-K whose
+// fp32 slabs are most of its HBM traffic.  Here a workgroup owns an output part of 32 couts x
+// 16 cins x all 9 taps and a chunk of whole images; its 4 waves run independently over a
+// quarter of the chunk each (no barrier in the main loop) and their partials are summed in LDS
+// at the end, so a chunk writes ONE slab for 4x the pixels.  Per 32-pixel stage a wave stages
+// dY (32 pixels x 32 couts, 2 KiB) and a zero-bordered halo of x (the stage's rows +-1, 16
+// channels, 32 B per pixel slot) by LDS-DMA into its own ring; the B operand of tap (ty, tx)
+// is the halo read at a constant offset (the ds_read immediate), so 9 taps cost 9 reads of one
+// staged image instead of 9 staged im2col tiles.  18 MFMAs (2 cout tiles x 9 taps) per stage.
+// k order within a stage: k = 8 g4 + 4 t + tq is pixel (img, y, x0 + tq) of the lane quad
+// (g4, t) below, chosen so that the two 16-lane groups of each 32-lane half read halo rows
+// (or images) whose slot distance is 4 mod 8: the transposed reads are bank-conflict free.
+template <int W>
+struct Wg3 {
+  static constexpr int NI = W == 16 ? 1 : 2;                   // images per 32-pixel stage
+  static constexpr int R = W == 4 ? 4 : 2;                     // image rows per stage
+  static constexpr int WP = W == 16 ? 20 : (W == 8 ? 12 : 6);  // halo row pitch in pixel slots
+  static constexpr int HR = R + 2;                             // halo rows per image
+  static constexpr int NSLOT = NI * HR * WP;                   // halo pixel slots (32 B each)
+  static constexpr int HCH = (2 * NSLOT + 63) / 64;            // halo LDS-DMA instructions (1 KiB)
+  static constexpr int DYB = 32 * 64;                          // 32 k-rows x 32 couts (bf16)
+  static constexpr int STAGE = DYB + HCH * 1024;               // bytes per ring stage
+  static constexpr int LPS = 2 + HCH;                          // LDS-DMA instructions per stage
+  static constexpr int T1 = W == 4 ? WP * 32 : 128;            // halo byte step of the lane's 2nd quad
+  // lane quad (g4, t) of a stage -> (image, row, first column), stage-relative
+  static ED_DEV void quad(int g4, int t, int& img, int& y, int& x0) {
+    if constexpr (W == 16) { img = 0; y = g4 & 1; x0 = 8 * (g4 >> 1) + 4 * t; }
+    else if constexpr (W == 8) { img = g4 >> 1; y = g4 & 1; x0 = 4 * t; }
+    else { img = g4 & 1; y = 2 * (g4 >> 1) + t; x0 = 0; }
+  }
+};
+
+// ds_read_b64_tr_b16 with an immediate byte offset (the tap / stage displacement)
+template <int OFF>
+ED_DEV v4s tr16_off(uint32_t a) {
+  v4s r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+template <int N>
+ED_DEV void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+ED_DEV v8bf cat8(v4s lo, v4s hi) {
+  return __builtin_bit_cast(v8bf, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+// LDS byte address of a shared-memory pointer
+ED_DEV uint32_t lds_addr(const void* p) {
+  typedef __attribute__((address_space(3))) const char lds_char;
+  return (uint32_t)(uintptr_t)(lds_char*)p;
+}
+// bijective XCD remap: blocks b and b + 8 run on one XCD; consecutive logical ids share it
+ED_DEV int xcd_remap(int b, int n) {
+  const int q = n >> 3, r = n & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+template <int W, int NS>
+struct Wg3Stage {
+  // one 32-pixel stage in ring slot J: 2 cout tiles x 9 taps of MFMAs, reads software-pipelined
+  // PD taps ahead with counted lgkmcnt waits (asm reads: hipcc does not track them)
+  template <int J>
+  static ED_DEV void compute(uint32_t a0, uint32_t a1, uint32_t bb, v4f (&acc)[2][9], bool bg, float (&bs)[2]) {
+    using G = Wg3<W>;
+    constexpr int SB = J * G::STAGE;
+    constexpr int PD = 4;
+    v8bf af0 = cat8(tr16_off<SB>(a0), tr16_off<SB + 256>(a0));
+    v8bf af1 = cat8(tr16_off<SB>(a1), tr16_off<SB + 256>(a1));
+    v8bf bf[9];
+#define WG3_B(T) bf[T] = cat8(tr16_off<SB + G::DYB + ((T) / 3 * G::WP + (T) % 3) * 32>(bb), \
+                              tr16_off<SB + G::DYB + ((T) / 3 * G::WP + (T) % 3) * 32 + G::T1>(bb))
+    WG3_B(0); WG3_B(1); WG3_B(2); WG3_B(3);
+#define WG3_T(T, NEXT, WAITN)                                                          \
+    if constexpr ((NEXT) < 9) { WG3_B(NEXT); }                                         \
+    lgkm_wait<WAITN>();                                                                \
+    acc[0][T] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af0, bf[T], acc[0][T], 0, 0, 0); \
+    acc[1][T] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af1, bf[T], acc[1][T], 0, 0, 0);
+    WG3_T(0, 4, 8) WG3_T(1, 5, 8) WG3_T(2, 6, 8) WG3_T(3, 7, 8) WG3_T(4, 8, 8)
+    WG3_T(5, 9, 6) WG3_T(6, 9, 4) WG3_T(7, 9, 2) WG3_T(8, 9, 0)
+#undef WG3_T
+#undef WG3_B
+    static_assert(PD == 4, "the wait counts above assume 4 taps in flight");
+    if (bg) {  // bias gradient: this lane's 8 pixels of its cout in each tile
+      const v8s s0 = __builtin_bit_cast(v8s, af0), s1 = __builtin_bit_cast(v8s, af1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        bs[0] += bf2f((bf16_t)s0[e]);
+        bs[1] += bf2f((bf16_t)s1[e]);
+      }
+    }
+  }
+};
+
+// (the body is a __device__ function, as gemm_tile: a kernel template whose own body calls a lambda
+// holding device builtins loses its host launch stub.  TAG: one body specialization per kernel --
+// hipcc's host pass rejects a second kernel instantiation calling the same one)
+template <int W, bool UP, int NS, int WPG, int TAG = 0>
+__device__ __forceinline__ void wgrad3x3_body(const EncdiffGemmArgs& p, const int nblk, char* wsm) {
+  using G = Wg3<W>;
+  constexpr int H = W;
+  constexpr uint32_t OOB = 0x80000000u;
+  typedef __attribute__((address_space(3))) void lds_void;
+  const int cin = p.conv.cin, cout = p.M;
+  const int ncit = cin >> 4, nparts = (cout >> 5) * ncit;
+  const int bid = xcd_remap(blockIdx.x, nblk);  // a chunk's parts (sharing dY / x rows) on one XCD
+  const int z = bid / nparts, part = bid - z * nparts;
+  const int cot = part / ncit, cit = part - cot * ncit;
+  const int co0 = cot * 32, ci0 = cit * 16;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int l16 = lane & 15, g4 = lane >> 4, tq = l16 >> 2, tp = l16 & 3;
+  const int ipz = p.conv.batch / p.split_k;               // images of this chunk
+  const int nst = (ipz / G::NI) * (H / G::R) / WPG;      // 32-pixel stages of this wave
+  const int st0 = wave * nst;                             // its first stage (chunk order)
+  const int zb = z * ipz;
+  char* ring = wsm + wave * (NS * G::STAGE);
+  const uint32_t ring_a = lds_addr(ring);
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.a, 0, 0x7FFFFFF0, 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, 0, 0x7FFFFFF0, 0x00020000);
+  const uint32_t lda2 = (uint32_t)p.lda * 2u, ldx2 = (uint32_t)p.conv.ld_src * 2u;
+
+  // staging invariants: dY chunk i (row r = k order, 16-B slot with the odd-8-row half swap)
+  uint32_t dy_off[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = lane + 64 * i, r = c >> 2, gs = (c & 3) ^ (((r >> 3) & 1) << 1);
+    int img, y, x0;
+    G::quad(r >> 3, (r >> 2) & 1, img, y, x0);
+    dy_off[i] = (uint32_t)((img * H + y) * W + x0 + (r & 3)) * lda2 + (uint32_t)(co0 + gs * 8) * 2u;
+  }
+  // halo chunk i: pixel slot s = c / 2, channel half c % 2
+  int h_img[G::HCH], h_hy[G::HCH], h_xs[G::HCH];
+  uint32_t h_ch[G::HCH];
+#pragma unroll
+  for (int i = 0; i < G::HCH; ++i) {
+    const int c = lane + 64 * i, s = c >> 1;
+    h_img[i] = s / (G::HR * G::WP);
+    const int rem = s - h_img[i] * (G::HR * G::WP);
+    h_hy[i] = rem / G::WP;
+    const int hx = rem - h_hy[i] * G::WP;
+    h_xs[i] = (s < G::NSLOT && hx >= 1 && hx <= W) ? hx - 1 : -1;  // -1: zero border / pad slot
+    h_ch[i] = (uint32_t)(ci0 + (c & 1) * 8) * 2u;
+  }
+  auto stage = [&](int slot, int sw) {
+    const int st = st0 + sw;
+    const int b0 = zb + (st / (H / G::R)) * G::NI, y0 = (st % (H / G::R)) * G::R;
+    char* sd = ring + slot * G::STAGE;
+    const uint32_t pix0 = (uint32_t)(b0 * H + y0) * W;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)(sd + i * 1024), 16, dy_off[i] + pix0 * lda2, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < G::HCH; ++i) {
+      const int ys = y0 + h_hy[i] - 1, xs = h_xs[i];
+      const bool ok = xs >= 0 && (unsigned)ys < (unsigned)H;
+      const uint32_t b = (uint32_t)(b0 + h_img[i]);
+      const uint32_t sp = UP ? (b * (H / 2) + (uint32_t)(ys >> 1)) * (W / 2) + (uint32_t)(xs >> 1)
+                             : (b * H + (uint32_t)ys) * W + (uint32_t)xs;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_void*)(sd + G::DYB + i * 1024), 16, ok ? sp * ldx2 + h_ch[i] : OOB,
+                                               0, 0, 0);
+    }
+  };
+  // fragment read bases (ring slot 0; the slot offset is the reads' immediate)
+  const uint32_t a0 = ring_a + (uint32_t)((g4 * 8 + tq) * 64 + ((0 ^ (g4 & 1)) * 32) + tp * 8);
+  const uint32_t a1 = ring_a + (uint32_t)((g4 * 8 + tq) * 64 + ((1 ^ (g4 & 1)) * 32) + tp * 8);
+  uint32_t bb;
+  {
+    int img, y, x0;
+    G::quad(g4, 0, img, y, x0);
+    bb = ring_a + (uint32_t)(((img * G::HR + y) * G::WP + x0 + tq) * 32 + tp * 8);
+  }
+  v4f acc[2][9];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[m][t] = (v4f){0.f, 0.f, 0.f, 0.f};
+  const bool bg = p.bias_grad != nullptr && cit == 0;
+  float bs[2] = {0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nst) stage(s, s);
+  for (int s0 = 0; s0 < nst; s0 += NS) {
+#define WG3_IT(J)                                                                              \
+    if (s0 + (J) < nst) {                                                                      \
+      const int s = s0 + (J);                                                                  \
+      if (s + NS - 1 < nst) { vm_wait<G::LPS * (NS - 2)>(); }                                  \
+      else { vm_wait_stages<G::LPS, NS - 2>(nst - 1 - s); }                                    \
+      if (s + NS - 1 < nst) stage(((J) + NS - 1) % NS, s + NS - 1);                           \
+      Wg3Stage<W, NS>::template compute<J>(a0, a1, bb, acc, bg, bs);                           \
+    }
+    WG3_IT(0)
+    WG3_IT(1)
+    if constexpr (NS > 2) { WG3_IT(2) }
+    if constexpr (NS > 3) { WG3_IT(3) }
+    if constexpr (NS > 4) { WG3_IT(4) }
+    if constexpr (NS > 5) { WG3_IT(5) }
+    if constexpr (NS > 6) { WG3_IT(6) }
+    static_assert(NS <= 7, "ring slots are unrolled up to 7");
+#undef WG3_IT
+  }
+
+  // ---- epilogue, one cout tile (16 couts) at a time so the LDS image stays <= the ring: every
+  // wave parks its partial [16 co][9 tap][16 ci] in LDS, then all threads sum the WPG partials in
+  // wave order (fixed: reproducible) over float4 runs of 4 cins and store them 16 B per lane --
+  // into this chunk's slab write-through (sc1: measured 1 us faster than write-back slabs, whose
+  // dirty lines the end of the kernel flushes), or into C itself without split-K ----
+  constexpr int HALF = 16 * 9 * 16;
+  float* red = (float*)wsm;             // [WPG][HALF]
+  float* bred = red + WPG * HALF;       // [WPG][32] bias partials
+  const bool slab = p.split_k > 1;
+  const long MN = (long)p.M * p.N;
+  float* out = (float*)p.c + (slab ? (long)z * MN : 0);
+  const long ldo = slab ? p.N : p.ldc;
+  const auto rso = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, 0x7FFFFFF0, 0x00020000);
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    __syncthreads();  // ring (m = 0) / the previous half's image (m = 1) no longer read
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[wave * HALF + ((4 * g4 + q) * 9 + t) * 16 + l16] = acc[m][t][q];
+    if (m == 0 && bg) {
+#pragma unroll
+      for (int mm = 0; mm < 2; ++mm) {
+        float v = bs[mm];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (lane < 16) bred[wave * 32 + mm * 16 + lane] = v;
+      }
+    }
+    __syncthreads();
+    for (int f = threadIdx.x; f < HALF / 4; f += WPG * 64) {
+      float4 v = *(const float4*)(red + 4 * f);
+#pragma unroll
+      for (int w = 1; w < WPG; ++w) {
+        const float4 u = *(const float4*)(red + w * HALF + 4 * f);
+        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+      }
+      const int c4 = f & 3, ct = f >> 2, t = ct % 9, co = co0 + m * 16 + ct / 9;
+      const long off = (long)co * ldo + t * cin + ci0 + 4 * c4;
+      if (slab) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rso, (int)(off * 4), 0, 16);
+      } else {
+        float4* o = (float4*)(out + off);
+        v.x *= p.alpha; v.y *= p.alpha; v.z *= p.alpha; v.w *= p.alpha;
+        if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) {
+          const float4 c = *o;
+          v.x += c.x; v.y += c.y; v.z += c.z; v.w += c.w;
+        }
+        *o = v;
+      }
+    }
+  }
+  if (bg && threadIdx.x < 32) {
+    float v = bred[threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < WPG; ++w) v += bred[w * 32 + threadIdx.x];
+    const int co = co0 + threadIdx.x;
+    if (slab) p.workspace[(long)p.split_k * MN + (long)z * p.M + co] = v;
+    else p.bias_grad[co] += v;
+  }
+}
+
+// The WG3 grid: blocks [0, nblk) the weight gradient, then (BM2 > 0) the layer's input-gradient
+// GEMM tiles in the same grid (as gemm2_kernel pairs two GEMM tiles: each alone leaves most of the
+// chip idle), then a deferred finalize of an earlier weight gradient riding along.
+template <int W, bool UP, int NS, int WPG, int BM2 = 0, int BN2 = 0, int AM2 = 0, int BMD2 = 0, int NS2 = 0>
+__global__ __launch_bounds__(WPG * 64) void wgrad3x3_kernel(const EncdiffGemmArgs p, int nblk, const EncdiffGemmArgs pf,
+                                                            int nf, const EncdiffGemmArgs p2, const GemmAux aux2, int gx2,
+                                                            int gy2) {
+  extern __shared__ __attribute__((aligned(16))) char wsm[];
+  int i = blockIdx.x;
+  if (i < nblk) {
+    wgrad3x3_body<W, UP, NS, WPG, BM2 * 1000 + BN2 * 10 + AM2>(p, nblk, wsm);
+    return;
+  }
+  i -= nblk;
+  if constexpr (BM2 > 0) {
+    const int n2 = gx2 * gy2 * p2.split_k;
+    if (i < n2) {
+      const int bx = i % gx2, t = i / gx2;
+      gemm_tile<BM2, BN2, AM2, BMD2, NS2, BK>(p2, aux2, bx, t % gy2, t / gy2, (bf16_t*)wsm);
+      return;
+    }
+    i -= n2;
+  }
+  // finalize blocks are 256 threads: waves beyond 4 end (s_barrier waits for the surviving waves only)
+  if (threadIdx.x >= 256) return;
+  gemm_finalize(pf, i, nf);
+}
+
+// tile 32: 4 waves per workgroup, paired with the layer's input gradient in one grid where the pair
+// path allows; 34: 4 waves, never paired; 33: 8 waves (two per SIMD on one workgroup per CU), never
+// paired; 3-deep stage rings alone, 2-deep paired
+template <int W, int NS, int WPG>
+constexpr size_t wg3_lds() {
+  constexpr size_t ring = WPG * NS * Wg3<W>::STAGE, red = (WPG * 16 * 9 * 16 + WPG * 32) * 4;
+  return ring > red ? ring : red;
+}
+__host__ __device__ constexpr int wg3_waves(int tile) { return tile == 33 ? 8 : 4; }
+constexpr int WG3_PAIR_NS = 2;  // paired launch: 2-deep rings keep the shared LDS size small
+
+// eligibility of a prepared weight-gradient plan for the WG3 kernel
+int wg3_check(const EncdiffGemmArgs& p) {
+  const EncdiffConvGeom& g = p.conv;
+  if (p.a_mode != ENCDIFF_OPA_ROWM || p.b_mode != ENCDIFF_OPB_IM2COL) return ENCDIFF_ERR_UNSUPPORTED;
+  if (g.resample != ENCDIFF_RESAMPLE_NONE && g.resample != ENCDIFF_RESAMPLE_UP2) return ENCDIFF_ERR_UNSUPPORTED;
+  if (g.h != g.w || (g.w != 4 && g.w != 8 && g.w != 16)) return ENCDIFF_ERR_UNSUPPORTED;
+  if (p.M % 32 || g.cin % 16 || p.N != 9 * g.cin || (long)p.K != (long)g.batch * g.h * g.w) return ENCDIFF_ERR_SHAPE;
+  if (p.c_mode != ENCDIFF_OUT_F32 && p.c_mode != ENCDIFF_OUT_F32_ACCUM) return ENCDIFF_ERR_UNSUPPORTED;
+  const int ni = g.w == 16 ? 1 : 2, rows = g.w == 4 ? 4 : 2;
+  if (p.split_k < 1 || g.batch % p.split_k || (g.batch / p.split_k) % ni) return ENCDIFF_ERR_SHAPE;
+  const int nst = (g.batch / p.split_k / ni) * (g.h / rows);  // 32-pixel stages per chunk
+  if (nst % wg3_waves(p.tile)) return ENCDIFF_ERR_SHAPE;
+  if (p.lda % 8 || g.ld_src % 8 || ((uintptr_t)p.a & 15) || ((uintptr_t)p.b & 15)) return ENCDIFF_ERR_SHAPE;
+  // float4 epilogue stores: slabs or C itself 16-byte aligned
+  if (p.split_k > 1 ? ((uintptr_t)p.workspace & 15) != 0 : (p.ldc % 4 || ((uintptr_t)p.c & 15))) return ENCDIFF_ERR_SHAPE;
+  return ENCDIFF_OK;
+}
+
+template <int W, bool UP, int NS, int WPG>
+hipError_t wg3_launch_t(const EncdiffGemmArgs& p, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
+  constexpr size_t lds = wg3_lds<W, NS, WPG>();
+  static const hipError_t attr_ok = hipFuncSetAttribute((const void*)wgrad3x3_kernel<W, UP, NS, WPG>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr_ok != hipSuccess) return attr_ok;
+  const int nblk = (p.M / 32) * (p.conv.cin / 16) * p.split_k;
+  hipLaunchKernelGGL((wgrad3x3_kernel<W, UP, NS, WPG>), dim3((unsigned)(nblk + nf)), dim3(WPG * 64), lds, s, p, nblk, pf,
+                     nf, p, GemmAux{}, 0, 0);
+  return hipGetLastError();
+}
+
+template <int WPG>
+hipError_t wg3_launch_w(const EncdiffGemmArgs& p, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
+  const bool up = p.conv.resample == ENCDIFF_RESAMPLE_UP2;
+  switch (p.conv.w) {
+    case 4: return up ? wg3_launch_t<4, true, 3, WPG>(p, pf, nf, s) : wg3_launch_t<4, false, 3, WPG>(p, pf, nf, s);
+    case 8: return up ? wg3_launch_t<8, true, 3, WPG>(p, pf, nf, s) : wg3_launch_t<8, false, 3, WPG>(p, pf, nf, s);
+    default: return up ? wg3_launch_t<16, true, 3, WPG>(p, pf, nf, s) : wg3_launch_t<16, false, 3, WPG>(p, pf, nf, s);
+  }
+}
+
+hipError_t wg3_launch(const EncdiffGemmArgs& p, int tile, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
+  return tile == 33 ? wg3_launch_w<8>(p, pf, nf, s) : wg3_launch_w<4>(p, pf, nf, s);
+}
+
 template <int BM, int BN, int AM, int BMD, int NS = 2, int KB = BK>
 hipError_t launch_t(const EncdiffGemmArgs& p, const GemmAux& aux, hipStream_t s) {
   using G = Gemm<BM, BN, AM, BMD, NS, KB>;
@@ -1314,7 +1666,10 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
   }
   g.tile = p.tile ? p.tile : pick_tile(p);
   g.aux.halo = HaloGeom{};
-  if (g.tile >= 16) {
+  if (g.tile >= 32 && g.tile <= 34) {  // 3x3 conv weight gradient kernel (WG3)
+    const int rc = wg3_check(p);
+    if (rc != ENCDIFF_OK) return rc;
+  } else if (g.tile >= 16) {
     const int rc = prepare_halo(p, g.tile, g.aux.halo);
     if (rc != ENCDIFF_OK) return rc;
   }
@@ -1356,7 +1711,8 @@ int fin_blocks(const EncdiffGemmArgs& u) {
 int launch_one(const GemmPlan& g, hipStream_t s) {
   const int am = g.p.a_mode, bm = g.p.b_mode;
   hipError_t e;
-  if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_ROWK, B_ROWK>(g.p, g.aux, g.tile, s);
+  if (g.tile >= 32 && g.tile <= 34) e = wg3_launch(g.p, g.tile, g.user, 0, s);
+  else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_ROWK, B_ROWK>(g.p, g.aux, g.tile, s);
   else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_IM2COL, B_ROWK>(g.p, g.aux, g.tile, s);
   else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWK, B_ROWN>(g.p, g.aux, g.tile, s);
   else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_CONV_DGRAD)
@@ -1456,6 +1812,55 @@ hipError_t launch_pair_tiles(const GemmPlan& g1, const GemmPlan& g2, const Encdi
   }
 }
 
+template <int W, bool UP, int BM2, int BN2, int AM2, int BMD2, int NS2>
+hipError_t wg3pair_launch_t(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
+  static const hipError_t attr_ok =
+      hipFuncSetAttribute((const void*)wgrad3x3_kernel<W, UP, WG3_PAIR_NS, 4, BM2, BN2, AM2, BMD2, NS2>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, HALO_LDS_MAX);
+  if (attr_ok != hipSuccess) return attr_ok;
+  size_t lds = wg3_lds<W, WG3_PAIR_NS, 4>();
+  if constexpr (AM2 == A_HALO) {
+    const size_t h = halo_lds_bytes(g2.aux.halo, BM2, BN2);
+    if (h > lds) lds = h;
+  } else {
+    constexpr size_t l2 = Gemm<BM2, BN2, AM2, BMD2, NS2, BK>::LDS_BYTES;
+    if (l2 > lds) lds = l2;
+  }
+  const int n1 = (g1.p.M / 32) * (g1.p.conv.cin / 16) * g1.p.split_k;
+  const int gx2 = AM2 == A_HALO ? g2.p.M / BM2 : (g2.p.M + BM2 - 1) / BM2, gy2 = (g2.p.N + BN2 - 1) / BN2;
+  const long nb = (long)n1 + (long)gx2 * gy2 * g2.p.split_k + nf;
+  hipLaunchKernelGGL((wgrad3x3_kernel<W, UP, WG3_PAIR_NS, 4, BM2, BN2, AM2, BMD2, NS2>), dim3((unsigned)nb), dim3(256), lds, s,
+                     g1.p, n1, pf, nf, g2.p, g2.aux, gx2, gy2);
+  return hipGetLastError();
+}
+
+template <int W, bool UP>
+hipError_t wg3pair_launch_w(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
+  switch (g2.tile) {
+    case 4: return wg3pair_launch_t<W, UP, 64, 64, A_IM2COL, B_CONVD, 2>(g1, g2, pf, nf, s);
+    case 2: return wg3pair_launch_t<W, UP, 128, 64, A_IM2COL, B_CONVD, 2>(g1, g2, pf, nf, s);
+    case 16: return wg3pair_launch_t<W, UP, 64, 64, A_HALO, B_CONVD, HALO_NS>(g1, g2, pf, nf, s);
+    case 17: return wg3pair_launch_t<W, UP, 128, 64, A_HALO, B_CONVD, HALO_NS>(g1, g2, pf, nf, s);
+    case 22: return wg3pair_launch_t<W, UP, 64, 128, A_HALO, B_CONVD, HALO_NS>(g1, g2, pf, nf, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// the input-gradient tiles the paired WG3 launch covers
+bool wg3pair_ok(const GemmPlan& g1, const GemmPlan& g2) {
+  return g1.tile == 32 && g2.p.a_mode == ENCDIFF_OPA_IM2COL && g2.p.b_mode == ENCDIFF_OPB_CONV_DGRAD &&
+         (g2.tile == 4 || g2.tile == 2 || g2.tile == 16 || g2.tile == 17 || g2.tile == 22);
+}
+
+hipError_t wg3pair_launch(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
+  const bool up = g1.p.conv.resample == ENCDIFF_RESAMPLE_UP2;
+  switch (g1.p.conv.w) {
+    case 4: return up ? wg3pair_launch_w<4, true>(g1, g2, pf, nf, s) : wg3pair_launch_w<4, false>(g1, g2, pf, nf, s);
+    case 8: return up ? wg3pair_launch_w<8, true>(g1, g2, pf, nf, s) : wg3pair_launch_w<8, false>(g1, g2, pf, nf, s);
+    default: return up ? wg3pair_launch_w<16, true>(g1, g2, pf, nf, s) : wg3pair_launch_w<16, false>(g1, g2, pf, nf, s);
+  }
+}
+
 hipError_t launch_finalize(const EncdiffGemmArgs& u, hipStream_t s) {
   hipLaunchKernelGGL(gemm_finalize_kernel, dim3((unsigned)fin_blocks(u)), dim3(256), 0, s, u);
   return hipGetLastError();
@@ -1494,6 +1899,23 @@ extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffG
   // both split-K problems need disjoint slabs
   if (g1.ws_path && g2.ws_path && g1.p.workspace == g2.p.workspace) return ENCDIFF_ERR_ARG;
   const bool defer1 = defer && g1.ws_path;
+  if (g1.tile >= 32 && g1.tile <= 34) {
+    const EncdiffGemmArgs& pf = have_prev ? gp.user : g1.user;
+    const int nf = have_prev ? fin_blocks(gp.user) : 0;
+    if (wg3pair_ok(g1, g2)) {  // WG3 + input gradient + previous finalize in one grid
+      e = wg3pair_launch(g1, g2, pf, nf, s);
+      if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+      const bool f1 = g1.ws_path && !defer1, f2 = g2.ws_path && !g2.fold;
+      if (f1 && (e = launch_finalize(g1.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+      if (f2 && (e = launch_finalize(g2.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+      return ENCDIFF_OK;
+    }
+    // WG3 weight gradient (+ the previous finalize riding along), then the input gradient
+    e = wg3_launch(g1.p, g1.tile, pf, nf, s);
+    if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+    if (g1.ws_path && !defer1 && (e = launch_finalize(g1.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+    return launch_one(g2, s);
+  }
   if ((!lin && !conv) || (g1.tile != 4 && g1.tile != 5 && g1.tile != 7 && g1.tile != 9 && g1.tile != 10)) {
     // pairs the fused kernel does not cover
     if (have_prev && (e = launch_finalize(gp.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;

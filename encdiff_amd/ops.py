@@ -188,12 +188,52 @@ def plan(M, N, K, a_mode, b_mode, c_mode, resample=0):
     return tile, split
 
 
+WG3 = int(os.environ.get("ENCDIFF_WG3", "1"))  # 3x3 conv weight gradients on the WG3 kernel (tiles 32 / 33)
+WG3_TILE = int(os.environ.get("ENCDIFF_WG3_TILE", "32"))  # 32: 3-deep stage ring, 33: 7-deep
+WG3_SPLIT = 0  # experiments: force the WG3 split
+
+
+def wg3_split(batch, h, w, cout, cin, resample, lda, ld_src, c_mode, tile=None):
+    """Pixel chunks (split) of a 3x3 conv weight gradient on gemm.hip's WG3 kernel, or None when
+    the problem is not eligible (mirror of gemm.hip wg3_check).  A workgroup owns 32 couts x 16
+    cins x 9 taps of one chunk of whole images; its 4 (tile 32) or 8 (tile 33) waves split the
+    chunk's 32-pixel stages: the largest power-of-two split whose waves still run >= 32 / waves
+    stages and whose grid stays within 2 (4-wave) or 1 (8-wave) workgroups per CU, so the fp32
+    partial slabs stay few."""
+    tile = tile or WG3_TILE
+    waves = 8 if tile == 33 else 4
+    if (resample not in (L.RESAMPLE_NONE, L.RESAMPLE_UP2) or h != w or h not in (4, 8, 16) or cout % 32 or cin % 16
+            or lda % 8 or ld_src % 8 or c_mode not in (L.OUT_F32, L.OUT_F32_ACCUM)):
+        return None
+    ni = 1 if h == 16 else 2
+    rows = 4 if h == 4 else 2
+
+    def stages(p):  # 32-pixel stages per chunk
+        return (batch // p // ni) * (h // rows) if batch % (p * ni) == 0 else 0
+    if stages(1) % waves:
+        return None
+    nparts = (cout // 32) * (cin // 16)
+    best, p = None, 1
+    while stages(p) and stages(p) % waves == 0:
+        if stages(p) // waves >= 32 // waves and nparts * p <= 256 * (2 if waves == 4 else 1):
+            best = p
+        p *= 2
+    return best or 1
+
+
 def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK, c_mode=L.OUT_BF16,
               conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=None, bias=None,
               resid=None, ld_resid=0, bias_grad=None, tile=0, ws_offset=0, aux=None, ld_aux=0,
               gn_stats=None, ln=None):
     """EncdiffGemmArgs with the measured (tile, split) plan; split-K slabs start `ws_offset`
     floats into this stream's workspace."""
+    if (WG3 and tile == 0 and split_k is None and a_mode == L.OPA_ROWM and b_mode == L.OPB_IM2COL and
+            conv is not None and N == 9 * conv.cin and K == conv.batch * conv.h * conv.w):
+        sp = wg3_split(conv.batch, conv.h, conv.w, M, conv.cin, conv.resample, lda, conv.ld_src, c_mode)
+        if sp is not None and WG3_SPLIT:
+            sp = WG3_SPLIT
+        if sp is not None and (sp == 1 or sp * M * (N + 1) <= WS_HALF // 2):
+            tile, split_k = WG3_TILE, sp
     if split_k is None or tile == 0:
         t, sp = plan(M, N, K, a_mode, b_mode, c_mode, conv.resample if conv is not None else 0)
         tile = tile or FORCE_TILE or t

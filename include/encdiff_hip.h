@@ -123,7 +123,13 @@ typedef struct EncdiffGemmArgs {
                                 4-deep LDS ring, 6:64x128 with a 3-deep ring, 7:64x64 and
                                 8:64x128 with 128-deep k stages (others: 64), 9 / 10: 64x64 with a
                                 6- / 8-deep ring (96 / 128 KB of LDS: a short split's k-tiles all
-                                in flight at once), 16-23: halo tiles (implicit im2col only) */
+                                in flight at once), 16-23: halo tiles (implicit im2col only), 32-34:
+                                3x3 conv weight gradient kernel WG3 (OPA_ROWM x OPB_IM2COL, resample
+                                NONE / UP2, h == w in {4, 8, 16}, M % 32 == 0, cin % 16 == 0; split_k =
+                                chunks of whole images, each chunk one fp32 slab): workgroups of 32 couts
+                                x 16 cins x 9 taps whose waves split the chunk's pixels; 32 shares one
+                                grid with the layer's input gradient in encdiff_gemm_pair_ex, 34 never
+                                pairs, 33 uses 8-wave workgroups */
   int dtype;                 /* ENCDIFF_DT_BF16 (a, b, resid and BF16 outputs bf16) or ENCDIFF_DT_F32 */
   float* workspace;          /* split_k > 1 with a BF16/F32/F32_ACCUM c_mode: fp32 scratch of split_k*M*N
                                 (+ split_k*M when bias_grad is set: per-split bias-gradient slabs);

@@ -359,6 +359,61 @@ def test_conv3x3(O, B, H, cin, cout, mode):
     assert rel(db2, db) < 1e-5
 
 
+@pytest.mark.parametrize("B,H,cin,cout,mode", [(128, 16, 64, 64, 0), (16, 16, 192, 64, 0), (32, 16, 128, 128, 2),
+                                                (128, 8, 128, 128, 0), (64, 8, 384, 128, 0), (128, 4, 256, 256, 0),
+                                                (16, 4, 512, 256, 2), (8, 8, 64, 32, 0)])
+@pytest.mark.parametrize("tile", [32, 33, 34])
+def test_conv3x3_wgrad_wg3(O, B, H, cin, cout, mode, tile):
+    """The 3x3 weight-gradient kernel (gemm.hip WG3, tile 32) vs a torch fp32 reference and vs the
+    split-K GEMM form: dW (channels-last, accumulated onto a nonzero dW) and the bias gradient;
+    then two paired backward launches in a row (the first's finalize deferred into the second)."""
+    from encdiff_amd.ops import Geom
+    from encdiff_amd import _lib as L
+    torch.manual_seed(11)
+    g = Geom(B, H, H)
+    gs = Geom(B, H // 2, H // 2) if mode == 2 else g
+    x, dy = bf(gs.pixels, cin), bf(g.pixels, cout)
+    sp = O.wg3_split(B, H, H, cout, cin, mode, cout, cin, L.OUT_F32_ACCUM, tile=tile)
+    assert sp is not None, "shape expected to be WG3-eligible"
+    xin = nhwc(x, gs)
+    if mode == 2:
+        xin = F.interpolate(xin, scale_factor=2, mode="nearest")
+    w0 = torch.zeros(cout, cin, 3, 3, device=dev, requires_grad=True)
+    F.conv2d(xin, w0, padding=1).backward(nhwc(dy, g))
+    ref = w0.grad.permute(0, 2, 3, 1).reshape(cout, 9 * cin)
+    init = torch.randn(cout, 9 * cin, device=dev)
+    got = {}
+    for wg3 in (1, 0):
+        O.WG3, O.WG3_TILE = wg3, tile
+        try:
+            a = O.conv3x3_wgrad_cl_args(dy, x, g, cin, init.clone(), None, mode)
+            assert (a.tile in (32, 33, 34)) == bool(wg3) and (not wg3 or a.split_k == sp)
+            dw, db = init.clone(), torch.full((cout,), 0.5, device=dev)
+            O.conv3x3_wgrad_cl(dy, x, g, cin, dw, db, resample=mode)
+            torch.cuda.synchronize()
+        finally:
+            O.WG3, O.WG3_TILE = 1, 32
+        got[wg3] = (dw, db)
+    dw, db = got[1]
+    assert rel(dw - init, ref) < 2e-3, rel(dw - init, ref)
+    assert rel(db - 0.5, nhwc(dy, g).sum((0, 2, 3))) < 2e-3
+    assert rel(dw, got[0][0]) < 1e-5 and rel(db, got[0][1]) < 1e-5
+    # two paired backward launches: WG3 weight gradients, the first finalize rides in the second
+    wf = bf(cout, 9 * cin, scale=(9 * cin) ** -0.5)
+    dws = [init.clone(), init.clone()]
+    dxs = [torch.empty(g.pixels, cin, device=dev, dtype=torch.bfloat16) for _ in range(2)]
+    O.WG3_TILE = tile
+    try:
+        for i in range(2):
+            O.conv3x3_bwd_cl(dy, g, wf, x, cin, dws[i], dxs[i], resample=mode)
+        O.flush()
+    finally:
+        O.WG3_TILE = 32
+    torch.cuda.synchronize()
+    for i in range(2):
+        assert torch.equal(dws[i], got[1][0]) or rel(dws[i], got[1][0]) < 1e-6
+
+
 @pytest.mark.parametrize("C,H,film,silu,eps", [(64, 16, True, True, 1e-5), (192, 16, False, True, 1e-5),
                                                 (384, 8, True, True, 1e-5), (256, 4, False, False, 1e-6),
                                                 (512, 2, True, True, 1e-5), (64, 64, True, True, 1e-5),
