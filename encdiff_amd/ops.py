@@ -210,7 +210,7 @@ def wg3_split(batch, h, w, cout, cin, resample, lda, ld_src, c_mode, tile=None):
 
     def stages(p):  # 32-pixel stages per chunk
         return (batch // p // ni) * (h // rows) if batch % (p * ni) == 0 else 0
-    if stages(1) % waves:
+    if not stages(1) or stages(1) % waves:
         return None
     nparts = (cout // 32) * (cin // 16)
     best, p = None, 1

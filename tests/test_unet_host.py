@@ -107,3 +107,23 @@ def test_dp_split_layout(params):
     for gname, bname in sorted(gn, key=lambda p: not UNetExecutor._early_final(p[0])):
         bad.add(gname, bname)
     assert bad.split_col(UNetExecutor._early_final) is None
+
+
+def test_wg3_split_matches_kernel_rule():
+    """ops.wg3_split (host plan of the 3x3 weight-gradient kernel WG3) only returns splits that
+    gemm.hip wg3_check accepts: whole-image chunks (images per chunk a multiple of the images per
+    32-pixel stage) whose stage count divides over the workgroup's waves; odd batches fall back."""
+    from encdiff_amd import ops, _lib as L
+    for B in (1, 2, 3, 4, 6, 8, 16, 32, 64, 128, 512):
+        for h in (4, 8, 16, 32):
+            for tile in (32, 33, 34):
+                sp = ops.wg3_split(B, h, h, 64, 64, 0, 64, 64, L.OUT_F32_ACCUM, tile=tile)
+                if h == 32:
+                    assert sp is None
+                if sp is None:
+                    continue
+                ni, rows = (1 if h == 16 else 2), (4 if h == 4 else 2)
+                assert B % sp == 0 and (B // sp) % ni == 0
+                assert ((B // sp // ni) * (h // rows)) % (8 if tile == 33 else 4) == 0
+    assert ops.wg3_split(128, 16, 16, 64, 64, 0, 64, 64, L.OUT_BF16) is None  # fp32 outputs only
+    assert ops.wg3_split(128, 16, 16, 48, 64, 0, 64, 64, L.OUT_F32_ACCUM) is None  # cout % 32
