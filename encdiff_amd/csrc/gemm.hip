@@ -1413,6 +1413,249 @@ constexpr size_t wg3_lds() {
 __host__ __device__ constexpr int wg3_waves(int tile) { return tile == 33 ? 8 : 4; }
 constexpr int WG3_PAIR_NS = 2;  // paired launch: 2-deep rings keep the shared LDS size small
 
+// ---------------------------------------------------------------------------
+// Linear weight gradient, tile id 36 (WGL): dW[m][n] += sum_t dY[t][m] x[t][n] over T tokens
+// (every nn.Linear / 1x1 conv of the UNet: attention.py proj_in/out, to_q/k/v/out, ff; the
+// ResBlock skip).  Small output, long K: as WG3, a workgroup owns a 64 x 64 output part and a
+// chunk of tokens, its 4 waves run independently over a quarter of the chunk each (32-token
+// stages: dY and x rows, 4 KiB each, staged by LDS-DMA into the wave's own ring; 4 x 4 MFMA tiles
+// per stage) and their partials are summed in LDS: one slab per chunk.  Rows are 128 B (64
+// bf16); the 32-B column groups a transposed read touches are XOR-swizzled by row bits 1 and 3
+// so both 16-lane groups of a 32-lane half hit distinct banks.
+struct Wgl {
+  static constexpr int ROWB = 128;               // 64 columns x bf16
+  static constexpr int OPB = 32 * ROWB;          // one operand of a 32-token stage (4 KiB)
+  static constexpr int STAGE = 2 * OPB;          // dY rows then x rows
+  static constexpr int LPS = 8;                  // LDS-DMA instructions per stage
+  // 16-B slot of global chunk gc (0..7) in row r
+  static ED_DEV int slot(int r, int gc) { return ((((gc >> 1) ^ ((r >> 1) & 1) ^ (((r >> 3) & 1) << 1))) << 1) | (gc & 1); }
+};
+
+template <int NS>
+struct WglStage {
+  template <int J>
+  static ED_DEV void compute(const uint32_t (&ab)[4], const uint32_t (&bb)[4], v4f (&acc)[4][4], bool bg, float (&bs)[4]) {
+    constexpr int SB = J * Wgl::STAGE;
+    v8bf af[4], bf[4];
+#define WGL_RD(F, BASE, I, OFF) F[I] = cat8(tr16_off<SB + (OFF)>(BASE[I]), tr16_off<SB + (OFF) + 4 * Wgl::ROWB>(BASE[I]))
+    WGL_RD(af, ab, 0, 0); WGL_RD(af, ab, 1, 0); WGL_RD(af, ab, 2, 0); WGL_RD(af, ab, 3, 0);
+    WGL_RD(bf, bb, 0, Wgl::OPB); WGL_RD(bf, bb, 1, Wgl::OPB);
+    WGL_RD(bf, bb, 2, Wgl::OPB); WGL_RD(bf, bb, 3, Wgl::OPB);
+    lgkm_wait<4>();  // A and B tiles 0, 1 landed (tiles 2, 3 = the 4 youngest reads)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[0], acc[i][0], 0, 0, 0);
+      acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[1], acc[i][1], 0, 0, 0);
+    }
+    lgkm_wait<0>();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[i][2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[2], acc[i][2], 0, 0, 0);
+      acc[i][3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[3], acc[i][3], 0, 0, 0);
+    }
+#undef WGL_RD
+    if (bg) {  // bias gradient: this lane's 8 tokens of its output column in each m tile
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const v8s sv = __builtin_bit_cast(v8s, af[i]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bs[i] += bf2f((bf16_t)sv[e]);
+      }
+    }
+  }
+};
+
+template <int NS, int TAG = 0>
+__device__ __forceinline__ void wgradlin_body(const EncdiffGemmArgs& p, const int nblk, char* wsm) {
+  typedef __attribute__((address_space(3))) void lds_void;
+  const int ntn = p.N >> 6, nparts = (p.M >> 6) * ntn;
+  const int bid = xcd_remap(blockIdx.x, nblk);  // a chunk's parts (sharing dY / x rows) on one XCD
+  const int z = bid / nparts, part = bid - z * nparts;
+  const int mt = part / ntn, nt = part - mt * ntn;
+  const int m0 = mt * 64, n0 = nt * 64;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int l16 = lane & 15, g4 = lane >> 4, tq = l16 >> 2, tp = l16 & 3;
+  const int tpz = p.K / p.split_k;        // tokens of this chunk
+  const int nst = tpz / (32 * 4);         // 32-token stages of this wave
+  const int t0 = z * tpz + wave * nst * 32;
+  char* ring = wsm + wave * (NS * Wgl::STAGE);
+  const uint32_t ring_a = lds_addr(ring);
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.a, 0, 0x7FFFFFF0, 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.b, 0, 0x7FFFFFF0, 0x00020000);
+  const uint32_t lda2 = (uint32_t)p.lda * 2u, ldb2 = (uint32_t)p.ldb * 2u;
+  // staging: LDS chunk c = lane + 64 i of an operand -> row r = c / 8, slot c % 8 holds global chunk gc
+  uint32_t a_off[4], b_off[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = lane + 64 * i, r = c >> 3, sl = c & 7;
+    int gc = 0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g)
+      if (Wgl::slot(r, g) == sl) gc = g;
+    a_off[i] = (uint32_t)r * lda2 + (uint32_t)(m0 + gc * 8) * 2u;
+    b_off[i] = (uint32_t)r * ldb2 + (uint32_t)(n0 + gc * 8) * 2u;
+  }
+  auto stage = [&](int slot, int sw) {
+    char* sd = ring + slot * Wgl::STAGE;
+    const uint32_t row0 = (uint32_t)(t0 + sw * 32);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)(sd + i * 1024), 16, a_off[i] + row0 * lda2, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_void*)(sd + Wgl::OPB + i * 1024), 16, b_off[i] + row0 * ldb2, 0,
+                                               0, 0);
+  };
+  // fragment bases (ring slot 0, first 4 rows of the lane's k group): column tile i at row r
+  uint32_t ab[4], bb[4];
+  {
+    const int r = g4 * 8 + tq;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int gc = 2 * i + (tp >> 1);  // 16-B chunk of columns 16 i + 4 tp .. + 3
+      const uint32_t o = (uint32_t)(r * Wgl::ROWB + Wgl::slot(r, gc) * 16 + (tp & 1) * 8);
+      ab[i] = ring_a + o;
+      bb[i] = ring_a + o;
+    }
+  }
+  // (rows r and r + 4 differ in bit 2 only: same swizzle, the second read is 4 rows on)
+  v4f acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+  const bool bg = p.bias_grad != nullptr && nt == 0;
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nst) stage(s, s);
+  for (int s0 = 0; s0 < nst; s0 += NS) {
+#define WGL_IT(J)                                                                              \
+    if (s0 + (J) < nst) {                                                                      \
+      const int s = s0 + (J);                                                                  \
+      if (s + NS - 1 < nst) { vm_wait<Wgl::LPS * (NS - 2)>(); }                                \
+      else { vm_wait_stages<Wgl::LPS, NS - 2>(nst - 1 - s); }                                  \
+      if (s + NS - 1 < nst) stage(((J) + NS - 1) % NS, s + NS - 1);                           \
+      WglStage<NS>::template compute<J>(ab, bb, acc, bg, bs);                                  \
+    }
+    WGL_IT(0)
+    WGL_IT(1)
+    if constexpr (NS > 2) { WGL_IT(2) }
+    if constexpr (NS > 3) { WGL_IT(3) }
+    static_assert(NS <= 4, "ring slots are unrolled up to 4");
+#undef WGL_IT
+  }
+  // ---- epilogue (as WG3's): 32 output rows at a time through LDS, partials summed in wave order
+  constexpr int HALF = 32 * 64;
+  float* red = (float*)wsm;        // [4][HALF]
+  float* bred = red + 4 * HALF;    // [4][64]
+  const bool slab = p.split_k > 1;
+  const long MN = (long)p.M * p.N;
+  float* out = (float*)p.c + (slab ? (long)z * MN : 0);
+  const long ldo = slab ? p.N : p.ldc;
+  const auto rso = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, 0x7FFFFFF0, 0x00020000);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[wave * HALF + (i * 16 + 4 * g4 + q) * 64 + j * 16 + l16] = acc[2 * h + i][j][q];
+    if (h == 0 && bg) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = bs[i];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (lane < 16) bred[wave * 64 + i * 16 + lane] = v;
+      }
+    }
+    __syncthreads();
+    for (int f = threadIdx.x; f < HALF / 4; f += 256) {
+      float4 v = *(const float4*)(red + 4 * f);
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        const float4 u = *(const float4*)(red + w * HALF + 4 * f);
+        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+      }
+      const int row = m0 + h * 32 + (f >> 4), col = n0 + 4 * (f & 15);
+      const long off = (long)row * ldo + col;
+      if (slab) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rso, (int)(off * 4), 0, 16);
+      } else {
+        float4* o = (float4*)(out + off);
+        v.x *= p.alpha; v.y *= p.alpha; v.z *= p.alpha; v.w *= p.alpha;
+        if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) {
+          const float4 c = *o;
+          v.x += c.x; v.y += c.y; v.z += c.z; v.w += c.w;
+        }
+        *o = v;
+      }
+    }
+  }
+  if (bg && threadIdx.x < 64) {
+    float v = bred[threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) v += bred[w * 64 + threadIdx.x];
+    const int m = m0 + threadIdx.x;
+    if (slab) p.workspace[(long)p.split_k * MN + (long)z * p.M + m] = v;
+    else p.bias_grad[m] += v;
+  }
+}
+
+// The WGL grid: [0, nblk) the weight gradient, then (BM2 > 0) the layer's input-gradient GEMM tiles,
+// then a deferred finalize riding along
+template <int NS, int BM2 = 0, int BN2 = 0, int AM2 = 0, int BMD2 = 0, int NS2 = 0, int KB2 = BK>
+__global__ __launch_bounds__(256) void wgradlin_kernel(const EncdiffGemmArgs p, int nblk, const EncdiffGemmArgs pf, int nf,
+                                                       const EncdiffGemmArgs p2, const GemmAux aux2, int gx2, int gy2) {
+  extern __shared__ __attribute__((aligned(16))) char wsm[];
+  int i = blockIdx.x;
+  if (i < nblk) {
+    wgradlin_body<NS, BM2 * 100000 + BN2 * 100 + NS2 * 10 + (KB2 == BK ? 0 : 1)>(p, nblk, wsm);
+    return;
+  }
+  i -= nblk;
+  if constexpr (BM2 > 0) {
+    const int n2 = gx2 * gy2 * p2.split_k;
+    if (i < n2) {
+      const int bx = i % gx2, t = i / gx2;
+      gemm_tile<BM2, BN2, AM2, BMD2, NS2, KB2>(p2, aux2, bx, t % gy2, t / gy2, (bf16_t*)wsm);
+      return;
+    }
+    i -= n2;
+  }
+  gemm_finalize(pf, i, nf);
+}
+
+constexpr int WGL_NS = 3, WGL_PAIR_NS = 2;
+template <int NS>
+constexpr size_t wgl_lds() {
+  constexpr size_t ring = 4 * NS * Wgl::STAGE, red = (4 * 32 * 64 + 4 * 64) * 4;
+  return ring > red ? ring : red;
+}
+
+int wgl_check(const EncdiffGemmArgs& p) {
+  if (p.a_mode != ENCDIFF_OPA_ROWM || p.b_mode != ENCDIFF_OPB_ROWN) return ENCDIFF_ERR_UNSUPPORTED;
+  if (p.c_mode != ENCDIFF_OUT_F32 && p.c_mode != ENCDIFF_OUT_F32_ACCUM) return ENCDIFF_ERR_UNSUPPORTED;
+  if (p.M % 64 || p.N % 64 || p.split_k < 1 || p.K % (p.split_k * 128)) return ENCDIFF_ERR_SHAPE;
+  if (p.lda % 8 || p.ldb % 8 || ((uintptr_t)p.a & 15) || ((uintptr_t)p.b & 15)) return ENCDIFF_ERR_SHAPE;
+  if (p.split_k > 1 ? ((uintptr_t)p.workspace & 15) != 0 : (p.ldc % 4 || ((uintptr_t)p.c & 15))) return ENCDIFF_ERR_SHAPE;
+  return ENCDIFF_OK;
+}
+
+hipError_t wgl_launch(const EncdiffGemmArgs& p, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
+  constexpr size_t lds = wgl_lds<WGL_NS>();
+  static const hipError_t attr_ok =
+      hipFuncSetAttribute((const void*)wgradlin_kernel<WGL_NS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr_ok != hipSuccess) return attr_ok;
+  const int nblk = (p.M / 64) * (p.N / 64) * p.split_k;
+  hipLaunchKernelGGL((wgradlin_kernel<WGL_NS>), dim3((unsigned)(nblk + nf)), dim3(256), lds, s, p, nblk, pf, nf, p,
+                     GemmAux{}, 0, 0);
+  return hipGetLastError();
+}
+
 // eligibility of a prepared weight-gradient plan for the WG3 kernel
 int wg3_check(const EncdiffGemmArgs& p) {
   const EncdiffConvGeom& g = p.conv;
@@ -1670,6 +1913,9 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
   if (g.tile >= 32 && g.tile <= 34) {  // 3x3 conv weight gradient kernel (WG3)
     const int rc = wg3_check(p);
     if (rc != ENCDIFF_OK) return rc;
+  } else if (g.tile == 36) {  // linear weight gradient kernel (WGL)
+    const int rc = wgl_check(p);
+    if (rc != ENCDIFF_OK) return rc;
   } else if (g.tile >= 16) {
     const int rc = prepare_halo(p, g.tile, g.aux.halo);
     if (rc != ENCDIFF_OK) return rc;
@@ -1713,6 +1959,7 @@ int launch_one(const GemmPlan& g, hipStream_t s) {
   const int am = g.p.a_mode, bm = g.p.b_mode;
   hipError_t e;
   if (g.tile >= 32 && g.tile <= 34) e = wg3_launch(g.p, g.tile, g.user, 0, s);
+  else if (g.tile == 36) e = wgl_launch(g.p, g.user, 0, s);
   else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_ROWK, B_ROWK>(g.p, g.aux, g.tile, s);
   else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_IM2COL, B_ROWK>(g.p, g.aux, g.tile, s);
   else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWK, B_ROWN>(g.p, g.aux, g.tile, s);
@@ -1862,6 +2109,38 @@ hipError_t wg3pair_launch(const GemmPlan& g1, const GemmPlan& g2, const EncdiffG
   }
 }
 
+template <int BM2, int BN2, int NS2, int KB2>
+hipError_t wglpair_launch_t(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
+  using G2 = Gemm<BM2, BN2, A_ROWK, B_ROWN, NS2, KB2>;
+  constexpr size_t l1 = wgl_lds<WGL_PAIR_NS>(), lds = l1 > G2::LDS_BYTES ? l1 : G2::LDS_BYTES;
+  static const hipError_t attr_ok =
+      hipFuncSetAttribute((const void*)wgradlin_kernel<WGL_PAIR_NS, BM2, BN2, A_ROWK, B_ROWN, NS2, KB2>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr_ok != hipSuccess) return attr_ok;
+  const int n1 = (g1.p.M / 64) * (g1.p.N / 64) * g1.p.split_k;
+  const int gx2 = (g2.p.M + BM2 - 1) / BM2, gy2 = (g2.p.N + BN2 - 1) / BN2;
+  const long nb = (long)n1 + (long)gx2 * gy2 * g2.p.split_k + nf;
+  hipLaunchKernelGGL((wgradlin_kernel<WGL_PAIR_NS, BM2, BN2, A_ROWK, B_ROWN, NS2, KB2>), dim3((unsigned)nb), dim3(256), lds,
+                     s, g1.p, n1, pf, nf, g2.p, g2.aux, gx2, gy2);
+  return hipGetLastError();
+}
+
+bool wglpair_ok(const GemmPlan& g1, const GemmPlan& g2) {
+  return g1.tile == 36 && g2.p.a_mode == ENCDIFF_OPA_ROWK && g2.p.b_mode == ENCDIFF_OPB_ROWN && !g2.fold &&
+         (g2.tile >= 1 && g2.tile <= 5 || g2.tile == 7);
+}
+
+hipError_t wglpair_launch(const GemmPlan& g1, const GemmPlan& g2, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
+  switch (g2.tile) {
+    case 1: return wglpair_launch_t<128, 128, 2, BK>(g1, g2, pf, nf, s);
+    case 2: return wglpair_launch_t<128, 64, 2, BK>(g1, g2, pf, nf, s);
+    case 3: return wglpair_launch_t<64, 128, 2, BK>(g1, g2, pf, nf, s);
+    case 5: return wglpair_launch_t<64, 64, 4, BK>(g1, g2, pf, nf, s);
+    case 7: return wglpair_launch_t<64, 64, 2, 128>(g1, g2, pf, nf, s);
+    default: return wglpair_launch_t<64, 64, 2, BK>(g1, g2, pf, nf, s);
+  }
+}
+
 hipError_t launch_finalize(const EncdiffGemmArgs& u, hipStream_t s) {
   hipLaunchKernelGGL(gemm_finalize_kernel, dim3((unsigned)fin_blocks(u)), dim3(256), 0, s, u);
   return hipGetLastError();
@@ -1900,6 +2179,17 @@ extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffG
   // both split-K problems need disjoint slabs
   if (g1.ws_path && g2.ws_path && g1.p.workspace == g2.p.workspace) return ENCDIFF_ERR_ARG;
   const bool defer1 = defer && g1.ws_path;
+  if (g1.tile == 36) {  // WGL weight gradient (+ input gradient, + previous finalize)
+    const EncdiffGemmArgs& pf = have_prev ? gp.user : g1.user;
+    const int nf = have_prev ? fin_blocks(gp.user) : 0;
+    const bool paired = wglpair_ok(g1, g2);
+    e = paired ? wglpair_launch(g1, g2, pf, nf, s) : wgl_launch(g1.p, pf, nf, s);
+    if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+    if (g1.ws_path && !defer1 && (e = launch_finalize(g1.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+    if (!paired) return launch_one(g2, s);
+    if (g2.ws_path && (e = launch_finalize(g2.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+    return ENCDIFF_OK;
+  }
   if (g1.tile >= 32 && g1.tile <= 34) {
     const EncdiffGemmArgs& pf = have_prev ? gp.user : g1.user;
     const int nf = have_prev ? fin_blocks(gp.user) : 0;

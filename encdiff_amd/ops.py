@@ -221,6 +221,26 @@ def wg3_split(batch, h, w, cout, cin, resample, lda, ld_src, c_mode, tile=None):
     return best or 1
 
 
+# linear weight gradients on the WGL kernel (tile 36): 0 off, 1 square c x c layers only, 2 every eligible one
+WGL = int(os.environ.get("ENCDIFF_WGL", "1"))
+
+
+def wgl_split(M, N, K, lda, ldb, c_mode):
+    """Token chunks (split) of a linear weight gradient dW[M][N] += dY^T x on gemm.hip's WGL kernel
+    (tile 36), or None when not eligible (mirror of gemm.hip wgl_check): workgroups own 64 x 64
+    output parts, their 4 waves a quarter of a chunk each in 32-token stages; the largest
+    power-of-two split whose waves still run >= 2 stages and whose grid stays <= 256 workgroups."""
+    if M % 64 or N % 64 or lda % 8 or ldb % 8 or c_mode not in (L.OUT_F32, L.OUT_F32_ACCUM) or K % 256:
+        return None
+    parts = (M // 64) * (N // 64)
+    best, p = None, 1
+    while K % (p * 128) == 0:
+        if K // (p * 128) >= 2 and parts * p <= 256:
+            best = p
+        p *= 2
+    return best
+
+
 def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK, c_mode=L.OUT_BF16,
               conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=None, bias=None,
               resid=None, ld_resid=0, bias_grad=None, tile=0, ws_offset=0, aux=None, ld_aux=0,
@@ -234,6 +254,10 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
             sp = WG3_SPLIT
         if sp is not None and (sp == 1 or sp * M * (N + 1) <= WS_HALF // 2):
             tile, split_k = WG3_TILE, sp
+    if WGL and tile == 0 and split_k is None and a_mode == L.OPA_ROWM and b_mode == L.OPB_ROWN and (WGL == 2 or M == N):
+        sp = wgl_split(M, N, K, lda, ldb, c_mode)
+        if sp is not None and (sp == 1 or sp * M * (N + 1) <= WS_HALF // 2):
+            tile, split_k = 36, sp
     if split_k is None or tile == 0:
         t, sp = plan(M, N, K, a_mode, b_mode, c_mode, conv.resample if conv is not None else 0)
         tile = tile or FORCE_TILE or t

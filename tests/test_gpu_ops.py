@@ -414,6 +414,51 @@ def test_conv3x3_wgrad_wg3(O, B, H, cin, cout, mode, tile):
         assert torch.equal(dws[i], got[1][0]) or rel(dws[i], got[1][0]) < 1e-6
 
 
+@pytest.mark.parametrize("T,cout,cin", [(32768, 64, 64), (8192, 128, 128), (2048, 256, 256), (32768, 512, 64),
+                                         (8192, 1024, 128), (2048, 2048, 256), (256, 64, 128), (2048, 192, 64)])
+def test_linear_wgrad_wgl(O, T, cout, cin):
+    """The linear weight-gradient kernel (gemm.hip WGL, tile 36) vs a torch fp32 reference and vs
+    the split-K GEMM form (dW accumulated onto a nonzero dW, bias gradient), then two paired
+    backward launches in a row (input gradient in the same grid, the first finalize deferred)."""
+    torch.manual_seed(12)
+    dy, x = bf(T, cout), bf(T, cin)
+    sp = O.wgl_split(cout, cin, T, cout, cin, O.L.OUT_F32_ACCUM)
+    assert sp is not None
+    ref = dy.float().t() @ x.float()
+    init = torch.randn(cout, cin, device=dev)
+    got = {}
+    for wgl in (1, 0):
+        O.WGL = 2 * wgl
+        try:
+            a = O.linear_wgrad_args(dy, x, init.clone())
+            assert (a.tile == 36) == bool(wgl) and (not wgl or a.split_k == sp)
+            dw, db = init.clone(), torch.full((cout,), 0.5, device=dev)
+            O.linear_wgrad(dy, x, dw, db)
+            O.flush()
+            torch.cuda.synchronize()
+        finally:
+            O.WGL = 1
+        got[wgl] = (dw, db)
+    dw, db = got[1]
+    assert rel(dw - init, ref) < 2e-3, rel(dw - init, ref)
+    assert rel(db - 0.5, dy.float().sum(0)) < 2e-3
+    assert rel(dw, got[0][0]) < 1e-5 and rel(db, got[0][1]) < 1e-5
+    w = bf(cout, cin, scale=cout ** -0.5)
+    dws = [init.clone(), init.clone()]
+    dxs = [torch.empty(T, cin, device=dev, dtype=torch.bfloat16) for _ in range(2)]
+    O.WGL = 2  # (the step's default pairs only square layers on WGL)
+    try:
+        for i in range(2):
+            O.linear_bwd(dy, w, x, dxs[i], dws[i])
+        O.flush()
+        torch.cuda.synchronize()
+    finally:
+        O.WGL = 1
+    for i in range(2):
+        assert torch.equal(dws[i], got[1][0]) or rel(dws[i], got[1][0]) < 1e-6
+        assert rel(dxs[i], dy.float() @ w.float()) < 1e-2
+
+
 @pytest.mark.parametrize("C,H,film,silu,eps", [(64, 16, True, True, 1e-5), (192, 16, False, True, 1e-5),
                                                 (384, 8, True, True, 1e-5), (256, 4, False, False, 1e-6),
                                                 (512, 2, True, True, 1e-5), (64, 64, True, True, 1e-5),
