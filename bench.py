@@ -201,7 +201,7 @@ def kernel_roofline(tr, reps=10):
         e1.record(s)
         s.synchronize()
     t_set = e0.elapsed_time(e1) / 1e3 / reps
-    out = {"kernel": f"GEMM family (gemm_kernel / paired gemm2_kernel + split-K finalizes): {len(probs)} "
+    out = {"kernel": f"GEMM family (gemm_kernel / paired gemm2_kernel / WG3 + WGL weight-gradient grids + split-K finalizes): {len(probs)} "
                      f"conv/linear GEMM problems of the step (UNet, VQ encoder, Encoder4; fwd+dgrad+wgrad) "
                      f"in {len(calls)} calls",
            "bound": "mfma", "achieved": flops / t_set / 1e12, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",

@@ -252,6 +252,8 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
         sp = wg3_split(conv.batch, conv.h, conv.w, M, conv.cin, conv.resample, lda, conv.ld_src, c_mode)
         if sp is not None and WG3_SPLIT:
             sp = WG3_SPLIT
+        elif sp is not None and conv.batch == 128:  # measured pair split (tools/wg3_tune.py), training batch
+            sp = _tile_table().get(f"wg3,{conv.h},{conv.cin},{M},{conv.resample}", sp)
         if sp is not None and (sp == 1 or sp * M * (N + 1) <= WS_HALF // 2):
             tile, split_k = WG3_TILE, sp
     if WGL and tile == 0 and split_k is None and a_mode == L.OPA_ROWM and b_mode == L.OPB_ROWN and (WGL == 2 or M == N):

@@ -75,7 +75,8 @@ def _window(rows, counter):
     assert len(marks) >= 2, "markers missing"
     win = rows[marks[-2] + 1:marks[-1]]
     cal = [r for r in win if "ew_kernel" in r[1] and r[2] == counter]
-    fam = ("gemm_kernel", "gemm2_kernel", "gemm_finalize")  # single, paired, split-K finalize kernels
+    # single, paired, split-K finalize kernels, and the weight-gradient kernels (WG3 3x3 conv, WGL linear)
+    fam = ("gemm_kernel", "gemm2_kernel", "gemm_finalize", "wgrad3x3_kernel", "wgradlin_kernel")
     gem = [r for r in win if any(k in r[1] for k in fam) and r[2] == counter]
     launches = len({r[0] for r in win if any(k in r[1] for k in fam)})
     return sum(r[3] for r in cal), sum(r[3] for r in gem), launches
