@@ -61,15 +61,18 @@ class CrossAttention(nn.Module):
             raise NotImplementedError("attention masks are not used by EncDiff (attention.py:185-188 unused)")
         if not x.is_cuda:
             raise RuntimeError("CrossAttention runs on the MI355X HIP path only (no CPU fallback)")
-        import torch.nn.functional as F
         import encdiff_amd.torch_ops  # noqa: F401  (registers torch.ops.encdiff.*)
         c = x if context is None else context
         bf = torch.bfloat16
-        q = F.linear(x.to(bf), self.to_q.weight.to(bf))
-        k = F.linear(c.to(bf), self.to_k.weight.to(bf))
-        v = F.linear(c.to(bf), self.to_v.weight.to(bf))
+        # q / k / v projections on the library's GEMM engine (encdiff::linear, autograd through
+        # encdiff::linear_bwd), then the MFMA attention
+        q = torch.ops.encdiff.linear(x.to(bf), self.to_q.weight.to(bf))
+        k = torch.ops.encdiff.linear(c.to(bf), self.to_k.weight.to(bf))
+        v = torch.ops.encdiff.linear(c.to(bf), self.to_v.weight.to(bf))
         o, _ = torch.ops.encdiff.attention_fwd(q.contiguous(), k.contiguous(), v.contiguous(), self.heads, False)
-        return self.to_out(o.to(x.dtype))
+        lin, drop = self.to_out[0], self.to_out[1]
+        y = torch.ops.encdiff.linear(o, lin.weight.to(bf)).to(x.dtype)
+        return drop(y + lin.bias if lin.bias is not None else y)
 
 
 class BasicTransformerBlock(nn.Module):

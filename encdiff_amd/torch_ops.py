@@ -130,3 +130,52 @@ def _attn_backward(ctx, d_o, d_lse):
 
 
 attention_fwd.register_autograd(_attn_backward, setup_context=_attn_setup)
+
+
+@custom_op("encdiff::linear", mutates_args=())
+def linear(x: Tensor, w: Tensor) -> Tensor:
+    """y = x w^T on the GEMM engine (encdiff_gemm): x (..., K) bf16, w (N, K) bf16 -> (..., N) bf16.
+    The standalone CrossAttention's q / k / v projections (attention.py:159-167)."""
+    _dev(x, w)
+    K = x.shape[-1]
+    x2 = x.reshape(-1, K).contiguous()
+    y = torch.empty(x2.shape[0], w.shape[0], device=x.device, dtype=torch.bfloat16)
+    ops.linear_fwd(x2, w.contiguous(), y)
+    return y.view(*x.shape[:-1], w.shape[0])
+
+
+@linear.register_fake
+def _(x, w):
+    return x.new_empty(*x.shape[:-1], w.shape[0], dtype=torch.bfloat16)
+
+
+@custom_op("encdiff::linear_bwd", mutates_args=())
+def linear_bwd(dy: Tensor, x: Tensor, w: Tensor) -> Tuple[Tensor, Tensor]:
+    """-> (dx = dy w (bf16), dw = dy^T x (fp32)): the input and weight gradient GEMMs."""
+    _dev(dy, x, w)
+    N, K = w.shape
+    dy2, x2 = dy.reshape(-1, N).contiguous(), x.reshape(-1, K).contiguous()
+    dx = torch.empty_like(x2)
+    dw = torch.zeros(N, K, device=w.device, dtype=torch.float32)
+    ops.linear_bwd(dy2, w.contiguous(), x2, dx, dw)
+    ops.flush()
+    return dx.view(x.shape), dw
+
+
+@linear_bwd.register_fake
+def _(dy, x, w):
+    return torch.empty_like(x), w.new_empty(w.shape, dtype=torch.float32)
+
+
+def _linear_setup(ctx, inputs, output):
+    x, w = inputs
+    ctx.save_for_backward(x, w)
+
+
+def _linear_backward(ctx, dy):
+    x, w = ctx.saved_tensors
+    dx, dw = linear_bwd(dy.to(torch.bfloat16).contiguous(), x, w)
+    return dx, dw.to(w.dtype)
+
+
+linear.register_autograd(_linear_backward, setup_context=_linear_setup)

@@ -1111,3 +1111,36 @@ def test_attention_fwd_streamed_kv(O, B, heads, sq, dh):
     ref = (s.softmax(-1) @ split(v)).reshape(B, heads, sq, dh).permute(0, 2, 1, 3).reshape(B * sq, C)
     assert rel(o, ref) < 1e-2
     assert rel(lse, torch.logsumexp(s, -1)) < 1e-4
+
+
+@pytest.mark.parametrize("dq,dc,heads,dh,sq,sk", [(64, 320, 8, 8, 256, 20), (128, 128, 4, 32, 64, 64)])
+def test_cross_attention_module(O, dq, dc, heads, dh, sq, sk):
+    """The standalone CrossAttention module (attention.py:152-193): q / k / v / out on encdiff::linear (GEMM
+    engine), MFMA attention, to_out -- forward and the gradients of x, context and the projection
+    weights vs a torch fp32 reference on the same bf16-rounded operands."""
+    from encdiff_amd.ldm.modules.attention import CrossAttention
+    torch.manual_seed(21)
+    m = CrossAttention(dq, context_dim=dc, heads=heads, dim_head=dh).cuda()
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(p.to(torch.bfloat16).float())
+    x = (torch.randn(2, sq, dq, device=dev)).to(torch.bfloat16).float().requires_grad_(True)
+    c = (torch.randn(2, sk, dc, device=dev)).to(torch.bfloat16).float().requires_grad_(True)
+    out = m(x, c)
+    g = torch.randn_like(out)
+    out.backward(g)
+    got = [out.detach(), x.grad, c.grad, m.to_q.weight.grad, m.to_k.weight.grad, m.to_v.weight.grad]
+    xr, cr = x.detach().clone().requires_grad_(True), c.detach().clone().requires_grad_(True)
+    wq, wk, wv = (t.weight.detach().clone().requires_grad_(True) for t in (m.to_q, m.to_k, m.to_v))
+
+    def split(t):
+        return t.view(t.shape[0], t.shape[1], heads, dh).permute(0, 2, 1, 3)
+    q, k, v = split(xr @ wq.t()), split(cr @ wk.t()), split(cr @ wv.t())
+    a = torch.softmax(q @ k.transpose(-1, -2) * dh ** -0.5, -1) @ v
+    ref = m.to_out(a.permute(0, 2, 1, 3).reshape(2, sq, heads * dh).to(torch.bfloat16).float())
+    ref.backward(g)
+    want = [ref.detach(), xr.grad, cr.grad, wq.grad, wk.grad, wv.grad]
+    for name, a_, b_ in zip(("out", "dx", "dcontext", "dWq", "dWk", "dWv"), got, want):
+        r = rel(a_, b_)
+        print(name, r)
+        assert r < 3e-2, (name, r)
