@@ -129,7 +129,10 @@ typedef struct EncdiffGemmArgs {
                                 chunks of whole images, each chunk one fp32 slab): workgroups of 32 couts
                                 x 16 cins x 9 taps whose waves split the chunk's pixels; 32 shares one
                                 grid with the layer's input gradient in encdiff_gemm_pair_ex, 34 never
-                                pairs, 33 uses 8-wave workgroups */
+                                pairs, 33 uses 8-wave workgroups; 36: linear weight gradient kernel WGL
+                                (OPA_ROWM x OPB_ROWN, M % 64 == 0, N % 64 == 0, K % (split_k*128) == 0;
+                                64 x 64 output parts, waves split each chunk's tokens), paired with the
+                                input gradient in encdiff_gemm_pair_ex */
   int dtype;                 /* ENCDIFF_DT_BF16 (a, b, resid and BF16 outputs bf16) or ENCDIFF_DT_F32 */
   float* workspace;          /* split_k > 1 with a BF16/F32/F32_ACCUM c_mode: fp32 scratch of split_k*M*N
                                 (+ split_k*M when bias_grad is set: per-split bias-gradient slabs);
