@@ -1,11 +1,13 @@
 """BASELINE.json configs[4] end to end: the builder-defined CelebA 128x128 LatentDiffusion
 (encdiff_amd.configs.CELEBA128: VQ-f4 latent (B, 3, 32, 32), model_channels 128, 40 concept
-tokens, Encoder4 with a fifth stride-2 stage, fp8 (e4m3) scores in the S = 1024 self-attention)
-trained by the same graph-captured HipTrainer as the benchmark, vs the CPU oracle configured
-alike (its fp8 scores emulated with torch.float8_e4m3fn).  No reference config exists for
+tokens, Encoder4 with a fifth stride-2 stage; bf16 attention, or with ENCDIFF_ATTN_FP8=1 fp8 (e4m3)
+scores in the S = 1024 self-attention) trained by the same graph-captured HipTrainer as the
+benchmark, vs the CPU oracle configured alike (fp8 scores emulated with torch.float8_e4m3fn).  No reference config exists for
 this one, so the oracle -- pinned to the reference on Shapes3D -- is
 the checker ("parity unpinned" by the reference itself); tolerances as in test_gpu_trainer.py
 (oracle/step_check.py TOL), every single UNet parameter gradient included."""
+import os
+
 import pytest
 import torch
 
@@ -20,7 +22,10 @@ def test_celeba128_step_matches_oracle():
     from oracle.step_check import GraphStepCheck, failures, summary
     chk = GraphStepCheck(B=B, config="celeba128", seed=77, warmup=1)
     st = [t for t in chk.ldm.model.diffusion_model._spec.sts if t.fp8]
-    assert st and all(t.h == 32 for t in st), "fp8 scores on the 32x32 (S = 1024) level only"
+    if os.environ.get("ENCDIFF_ATTN_FP8", "0") == "1":  # the optional fp8-score variant
+        assert st and all(t.h == 32 for t in st), "fp8 scores on the 32x32 (S = 1024) level only"
+    else:
+        assert not st, "configs[4] attention runs on bf16 MFMA by default"
     assert chk.tr.res == 128
     r = chk.check(grad_names=[], cond_names=[])
     print(summary(r))
