@@ -2225,12 +2225,14 @@ extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffG
   if (f1 && f2) {
     const int n1 = fin_blocks(g1.user), n2 = fin_blocks(g2.user);
     hipLaunchKernelGGL(gemm_finalize2_kernel, dim3((unsigned)(n1 + n2)), dim3(256), 0, s, g1.user, g2.user, n1);
+    e = hipGetLastError();
   } else if (f1) {
-    launch_finalize(g1.user, s);
+    e = launch_finalize(g1.user, s);
   } else if (f2) {
-    launch_finalize(g2.user, s);
+    e = launch_finalize(g2.user, s);
+  } else {
+    e = hipGetLastError();
   }
-  e = hipGetLastError();
   return e != hipSuccess ? ENCDIFF_ERR_LAUNCH - (int)e : ENCDIFF_OK;
 }
 
