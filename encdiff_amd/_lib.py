@@ -55,7 +55,7 @@ class GroupNormArgs(C.Structure):
                 ("accumulate_dx", C.c_int), ("dtype", C.c_int),
                 ("dgamma_part", vp), ("dbeta_part", vp), ("ld_part", C.c_long), ("dfilm", vp),
                 ("ld_dfilm", C.c_long), ("resid", vp), ("ld_resid", C.c_long), ("in_stats", vp),
-                ("ld_in_stats", C.c_long)]
+                ("ld_in_stats", C.c_long), ("x_from", vp)]
 
 
 class LayerNormArgs(C.Structure):
@@ -134,6 +134,7 @@ _PROTOS = {
     "encdiff_gemm_pair": [C.POINTER(GemmArgs), C.POINTER(GemmArgs), vp],
     "encdiff_gemm_pair_ex": [C.POINTER(GemmArgs), C.POINTER(GemmArgs), C.POINTER(GemmArgs), C.c_int, vp],
     "encdiff_gemm_finalize": [C.POINTER(GemmArgs), vp],
+    "encdiff_gemm_ex": [C.POINTER(GemmArgs), C.c_int, C.POINTER(C.c_int), vp],
     "encdiff_groupnorm_fwd": [C.POINTER(GroupNormArgs), vp],
     "encdiff_groupnorm_bwd": [C.POINTER(GroupNormArgs), vp],
     "encdiff_layernorm_fwd": [C.POINTER(LayerNormArgs), vp],

@@ -2157,6 +2157,20 @@ extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
   return launch_one(g, (hipStream_t)stream);
 }
 
+extern "C" int encdiff_gemm_ex(const EncdiffGemmArgs* pa, int defer_finalize, int* planned, void* stream) {
+  if (planned) *planned = 0;
+  if (!defer_finalize || (pa && pa->dtype == ENCDIFF_DT_F32)) return encdiff_gemm(pa, stream);
+  GemmPlan g;
+  const int rc = prepare(pa, g);
+  if (rc != ENCDIFF_OK) return rc;
+  if (!g.ws_path || g.fold) return launch_one(g, (hipStream_t)stream);
+  GemmPlan t = g;
+  t.ws_path = false;  // tile kernel only: the slabs wait for the consumer
+  const int r = launch_one(t, (hipStream_t)stream);
+  if (r == ENCDIFF_OK && planned) *planned = 1;
+  return r;
+}
+
 extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad,
                                     const EncdiffGemmArgs* prev_wgrad, int defer, void* stream) {
   GemmPlan g1, g2, gp;

@@ -133,24 +133,111 @@ ED_DEV uint4 gn_row(const GnSlice& L, const uint4* tile, const bf16_t* g, long l
   return L.tiled ? tile[px * L.nvc + L.tv] : *(const uint4*)(g + (long)px * ld);
 }
 
+// x as the deferred split-K finalize of its producer GEMM (EncdiffGroupNormArgs.x_from): fp32
+// slabs [split][M][C] behind ws, C = alpha * sum_z slab[z] (+ bias)(+ resid) -- gemm.hip's
+// gemm_finalize, same summation order (one ordered sum up to 8 slabs, else four z-groups added
+// ((0 + 1) + 2) + 3), same rounding -- so x is bitwise what the finalize pass would have written.
+struct GnSlabs {
+  const float* ws;  // NULL: x is read from memory
+  long total;       // M * C
+  int split;
+  float alpha;
+  const float* bias;
+  const bf16_t* resid;
+  long ld_resid;
+};
+
+// Slabs are loaded 8 at a time, every load of a batch issued before the first add (a chain of
+// dependent loads per slab made the small-batch launches latency-bound: 32 slabs at B = 8).
+ED_DEV void gn_slab_batch(const float* w, long stride, int z0, int split, float (&v)[8][8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (z0 + j < split) {
+      load8f(w + (long)(z0 + j) * stride, v[j]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[j][i] = 0.f;
+    }
+  }
+}
+
+ED_DEV uint4 gn_slab_row(const GnSlabs& sl, long row, int c, int cb) {
+  const float* w = sl.ws + row * c + cb;
+  float a[8], v[8][8];
+  if (sl.split <= 8) {
+    gn_slab_batch(w, sl.total, 0, sl.split, v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (j < sl.split) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] += v[j][i];
+      }
+    }
+  } else {  // z-group k sums slabs k, k + 4, ... in order
+    float g[4][8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[k][i] = 0.f;
+    for (int z0 = 0; z0 < sl.split; z0 += 8) {
+      gn_slab_batch(w, sl.total, z0, sl.split, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (z0 + j < sl.split) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) g[j & 3][i] += v[j][i];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = ((g[0][i] + g[1][i]) + g[2][i]) + g[3][i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = sl.alpha * a[i];
+  if (sl.bias) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] += sl.bias[cb + i];
+  }
+  if (sl.resid) {
+    float r[8];
+    unpack8(*(const uint4*)(sl.resid + row * sl.ld_resid + cb), r);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] += r[i];
+  }
+  return pack8(a);
+}
+
 // phase 0: stream the slice from HBM (4 loads in flight per thread), fill the tile, and
-// accumulate the per-channel sum and sum of squares in the same pass.
-ED_DEV void gn_stream_in(const GnSlice& L, uint4* tile, const bf16_t* X, long ld, int HW, float* s, float* ss) {
-#pragma unroll 4
-  for (int px = L.tp; px < HW; px += L.np) {
-    const uint4 u = *(const uint4*)(X + (long)px * ld);
+// accumulate the per-channel sum and sum of squares in the same pass.  With slabs, x is
+// combined from them first and written back (the producer's output).
+ED_DEV void gn_stream_in(const GnSlice& L, uint4* tile, const bf16_t* X, long ld, int HW, float* s, float* ss,
+                         const GnSlabs& sl, int C) {
+  auto acc = [&](const uint4& u, int px) {
     if (L.tiled) tile[px * L.nvc + L.tv] = u;
     float v[8];
     unpack8(u, v);
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s[i] += v[i]; ss[i] += v[i] * v[i]; }
+  };
+  if (sl.ws) {  // (rolled: a row already has up to 8 slab loads in flight)
+    for (int px = L.tp; px < HW; px += L.np) {
+      const uint4 u = gn_slab_row(sl, (long)L.b * HW + px, C, L.cb);
+      *(uint4*)(const_cast<bf16_t*>(X) + (long)px * ld) = u;
+      acc(u, px);
+    }
+    return;
   }
+#pragma unroll 4
+  for (int px = L.tp; px < HW; px += L.np) acc(*(const uint4*)(X + (long)px * ld), px);
 }
 
 // One reduction round: sum and sum of squares together (var = E[x^2] - mean^2 in fp32 over
 // bf16 inputs of O(1) magnitude; the second read of the slice and a second reduction with
 // its barriers were the longest part of this latency-bound kernel).
-__global__ __launch_bounds__(GN_THREADS) void gn_fwd_kernel(const EncdiffGroupNormArgs p, int cs, int tile_cap) {
+__global__ __launch_bounds__(GN_THREADS) void gn_fwd_kernel(const EncdiffGroupNormArgs p, int cs, int tile_cap,
+                                                            const GnSlabs sl) {
   extern __shared__ uint4 tile[];  // tile_cap vectors (0: untiled, re-read from L2/HBM)
   __shared__ float red[4096], chs[1024], gsh[2 * 64];
   const GnSlice L(p, cs, tile_cap);
@@ -160,7 +247,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_fwd_kernel(const EncdiffGroupNo
   float s[2][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) s[0][i] = s[1][i] = 0.f;
-  if (L.active) gn_stream_in(L, tile, X, p.ldx, HW, s[0], s[1]);
+  if (L.active) gn_stream_in(L, tile, X, p.ldx, HW, s[0], s[1], sl, p.c);
   // per-channel affine / FiLM constants (independent of the statistics)
   float ga[8], be[8], sc[8], sf[8];
   load8f(p.gamma + L.cb, ga);
@@ -662,10 +749,22 @@ int gn_check(const EncdiffGroupNormArgs* a) {
 }  // namespace
 
 extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream) {
-  if (a && a->dtype == ENCDIFF_DT_F32) return ed_groupnorm_fwd_f32(a, (hipStream_t)stream);
+  if (a && a->dtype == ENCDIFF_DT_F32) return a->x_from ? ENCDIFF_ERR_UNSUPPORTED : ed_groupnorm_fwd_f32(a, (hipStream_t)stream);
   if (!a || a->dtype != ENCDIFF_DT_BF16 || !a->x || !a->y || !a->stats || !a->gamma || !a->beta) return ENCDIFF_ERR_ARG;
   const int cs = gn_check(a);
   if (cs < 0) return cs;
+  GnSlabs sl{};
+  if (a->x_from) {  // x = the deferred split-K finalize of its producer (self-reducing kernel only)
+    const EncdiffGemmArgs& g = *a->x_from;
+    const bool tp = g.a_mode == ENCDIFF_OPA_IM2COL && g.conv.resample == ENCDIFF_RESAMPLE_K4S2_TP;
+    if (a->in_stats || g.dtype != ENCDIFF_DT_BF16 || g.c_mode != ENCDIFF_OUT_BF16 || g.split_k < 2 || !g.workspace ||
+        g.split_counters || g.bias_grad || tp || g.c != a->x || g.ldc != a->ldx || g.N != a->c ||
+        (long)g.M != (long)a->batch * a->hw || ((uintptr_t)g.workspace & 15) ||
+        (g.bias && ((uintptr_t)g.bias & 15)) ||
+        (g.resid && (g.ld_resid % 8 || ((uintptr_t)g.resid & 15))))
+      return ENCDIFF_ERR_ARG;
+    sl = GnSlabs{g.workspace, (long)g.M * g.N, g.split_k, g.alpha, g.bias, (const bf16_t*)g.resid, g.ld_resid};
+  }
   // producer statistics feed the two statistics kernels where their layout fits; other
   // shapes (e.g. a 384-channel concat at 32x32) take the self-reducing kernel below
   const bool st_ok = a->in_stats && a->hw % 64 == 0 && a->ld_in_stats >= a->c;
@@ -690,7 +789,7 @@ extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
   (void)attr;
   hipLaunchKernelGGL(gn_fwd_kernel, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), (size_t)cap * 16,
-                     (hipStream_t)stream, *a, cs, cap);
+                     (hipStream_t)stream, *a, cs, cap, sl);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }

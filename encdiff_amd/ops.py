@@ -469,14 +469,30 @@ def linear_bwd_geglu(dy, w, a, f, df, dw, db=None, d_a=None):
 
 # ------------------------------------------------------------------ 3x3 convolutions
 def conv3x3_fwd(x, g: Geom, cin, wf, out, bias=None, resid=None, resample=L.RESAMPLE_NONE, gn_stats=None,
-                out_f32=False):
+                out_f32=False, defer=False):
     """out[pixels][cout] = conv3x3(resample(x)) with packed weights wf [cout][9*cin]
-    (gn_stats: as linear_fwd; out_f32: fp32 output)."""
+    (gn_stats: as linear_fwd; out_f32: fp32 output).  defer: when the plan leaves split-K slabs
+    for a finalize pass, skip it and return the GemmArgs -- the caller hands them to
+    groupnorm_fwd(x_from=...) (which writes `out`) or to finalize(); else None (out written)."""
     cout = wf.shape[0]
-    gemm(g.pixels, cout, 9 * cin, x, _ld(x), wf, _ld(wf), out, _ld(out), a_mode=L.OPA_IM2COL,
-         c_mode=L.OUT_F32 if out_f32 else L.OUT_BF16, conv=_conv_geom(g, cin, resample, x), bias=bias, resid=resid,
-         ld_resid=_ld(resid) if resid is not None else 0, gn_stats=gn_stats,
-         split_k=1 if gn_stats is not None else None)
+    args = gemm_args(g.pixels, cout, 9 * cin, x, _ld(x), wf, _ld(wf), out, _ld(out), a_mode=L.OPA_IM2COL,
+                     c_mode=L.OUT_F32 if out_f32 else L.OUT_BF16, conv=_conv_geom(g, cin, resample, x), bias=bias,
+                     resid=resid, ld_resid=_ld(resid) if resid is not None else 0, gn_stats=gn_stats,
+                     split_k=1 if gn_stats is not None else None)
+    if ws_floats(args):
+        flush()
+    if not defer:
+        check(lib.encdiff_gemm(C.byref(args), _s()), "encdiff_gemm")
+        return None
+    planned = C.c_int(0)
+    check(lib.encdiff_gemm_ex(C.byref(args), 1, C.byref(planned), _s()), "encdiff_gemm_ex")
+    return args if planned.value else None
+
+
+def finalize(args):
+    """Run the split-K finalize a deferred conv3x3_fwd left (no-op for None)."""
+    if args is not None:
+        check(lib.encdiff_gemm_finalize(C.byref(args), _s()), "encdiff_gemm_finalize")
 
 
 def conv3x3_dgrad(dy, g: Geom, wf, dx, resid=None):
@@ -566,13 +582,17 @@ def conv4x4s2_bwd_cl(dy, g_out: Geom, wf, x, cin, dw_cl, dx, db=None):
 
 
 # ------------------------------------------------------------------ normalisation
-def groupnorm_fwd(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_film=0, groups=32, in_stats=None):
-    """in_stats: the segment sums x's producer GEMM wrote (gn_stats), else a reduction pass."""
+def groupnorm_fwd(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_film=0, groups=32, in_stats=None,
+                  x_from=None):
+    """in_stats: the segment sums x's producer GEMM wrote (gn_stats), else a reduction pass.
+    x_from: the GemmArgs a deferred conv3x3_fwd returned for x -- its slabs are combined here
+    (x written, bitwise the finalize's result), one launch instead of two."""
     c = x.shape[1]
     a = L.GroupNormArgs(batch=g.batch, hw=g.h * g.w, c=c, groups=groups, eps=eps, silu=int(silu),
                         x=_p(x), ldx=_ld(x), gamma=_p(gamma), beta=_p(beta), film=_p(film), ld_film=ld_film,
                         y=_p(y), ldy=_ld(y), stats=_p(stats), in_stats=_p(in_stats),
-                        ld_in_stats=_ld(in_stats) if in_stats is not None else 0)
+                        ld_in_stats=_ld(in_stats) if in_stats is not None else 0,
+                        x_from=None if x_from is None else C.addressof(x_from))
     check(lib.encdiff_groupnorm_fwd(C.byref(a), _s()), "encdiff_groupnorm_fwd")
 
 

@@ -38,6 +38,10 @@ ST_GN_EPS = 1e-6   # Normalize (attention.py:76-77)
 # GroupNorm forward statistics from the producing GEMM's epilogue at >= 8x8 (0: reduce in the
 # GroupNorm kernel, for A/B runs)
 GN_FROM_PRODUCER = os.environ.get("ENCDIFF_GN_FROM_PRODUCER", "1") != "0"
+# a split-K ResBlock conv's finalize folded into the GroupNorm forward that reads its output
+# (conv1 -> GN2 in the block, conv2 -> the next block's GN1): one launch instead of two
+# (0: separate finalize launches, for A/B runs)
+GN_FIN = os.environ.get("ENCDIFF_GN_FIN", "1") != "0"
 LN_EPS = 1e-5      # nn.LayerNorm default (attention.py:206-208)
 # the row-local SpatialTransformer tail (attn1.to_out .. proj_out) as one kernel
 # (encdiff_st_tail_fwd) in no-grad forwards (0: the separate launches, for A/B runs)
@@ -454,6 +458,7 @@ class UNetExecutor:
         B = x.shape[0]
         self.bind(B)
         sp, mc = self.spec, self.mc
+        self._pend = None  # GemmArgs of a ResBlock output whose split-K finalize is deferred
         self._x = x.contiguous()
         self._t_in = t.contiguous()
         # timestep embedding + time MLP (openaimodel_enc.py:726-727)
@@ -494,13 +499,26 @@ class UNetExecutor:
                 h = self._layer_fwd(layer, h)
         self._h_last = h
         ops.groupnorm_fwd(h, g0, self.P("out.0.weight"), self.P("out.0.bias"), self.a_out, self.st_out, GN_EPS, True,
-                          in_stats=self._gst(h))
+                          in_stats=self._gst(h), x_from=self._take_pend(h))
         ops.small_conv_out_fwd(self.a_out, g0, self.P("out.2.weight"), self.P("out.2.bias"), self.eps)
         return self.eps
+
+    def _take_pend(self, x):
+        """The deferred finalize of x's producer when the GroupNorm about to read x can combine
+        its slabs (x is exactly that GEMM's output); any other pending finalize runs now."""
+        p, self._pend = self._pend, None
+        if p is None:
+            return None
+        if p.c == x.data_ptr() and p.N == x.shape[1] and p.ldc == x.stride(0) and self._gst(x) is None:
+            return p
+        ops.finalize(p)
+        return None
 
     def _layer_fwd(self, layer, x):
         if isinstance(layer, ResSpec):
             return self._res_fwd(layer, x)
+        ops.finalize(self._pend)  # the transformer reads x directly
+        self._pend = None
         return self._st_fwd(layer, x)
 
     def _res_fwd(self, r: ResSpec, x):
@@ -510,14 +528,15 @@ class UNetExecutor:
         S["x"] = x
         gi, go = Geom(B, r.hin, r.hin), Geom(B, r.hout, r.hout)
         ops.groupnorm_fwd(x, gi, self.P(r.prefix + "in_layers.0.weight"), self.P(r.prefix + "in_layers.0.bias"),
-                          S["a1"], S["st1"], GN_EPS, True, in_stats=self._gst(x))
+                          S["a1"], S["st1"], GN_EPS, True, in_stats=self._gst(x), x_from=self._take_pend(x))
         a1, rs = self._conv1_input(r, S, go)
-        ops.conv3x3_fwd(a1, go, r.cin, self.W(r.prefix + "in_layers.2.weight"), S["h1"],
-                        bias=self.P(r.prefix + "in_layers.2.bias"), resample=rs, gn_stats=self._gst(S["h1"]))
+        f1 = ops.conv3x3_fwd(a1, go, r.cin, self.W(r.prefix + "in_layers.2.weight"), S["h1"],
+                             bias=self.P(r.prefix + "in_layers.2.bias"), resample=rs, gn_stats=self._gst(S["h1"]),
+                             defer=GN_FIN and self._gst(S["h1"]) is None)
         film = self.E[:, r.film_off:]
         ops.groupnorm_fwd(S["h1"], go, self.P(r.prefix + "out_layers.0.weight"), self.P(r.prefix + "out_layers.0.bias"),
                           S["a2"], S["st2"], GN_EPS, True, film=film, ld_film=self.E.shape[1],
-                          in_stats=self._gst(S["h1"]))
+                          in_stats=self._gst(S["h1"]), x_from=f1)
         # skip path into the output buffer, then conv2 adds onto it
         out = S["out"]
         if r.cin != r.cout:
@@ -529,8 +548,11 @@ class UNetExecutor:
             resid = S["xr"]
         else:
             resid = x
-        ops.conv3x3_fwd(S["a2"], go, r.cout, self.W(r.prefix + "out_layers.3.weight"), out,
-                        bias=self.P(r.prefix + "out_layers.3.bias"), resid=resid, gn_stats=self._gst(out))
+        # (deferred: the next ResBlock's GN1 or the output GroupNorm combines the slabs, any
+        # other reader finalizes first -- _take_pend / _layer_fwd)
+        self._pend = ops.conv3x3_fwd(S["a2"], go, r.cout, self.W(r.prefix + "out_layers.3.weight"), out,
+                                     bias=self.P(r.prefix + "out_layers.3.bias"), resid=resid, gn_stats=self._gst(out),
+                                     defer=GN_FIN and self._gst(out) is None)
         return out
 
     @staticmethod

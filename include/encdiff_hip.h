@@ -178,6 +178,14 @@ int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dg
 /* The split-K finalize of a GEMM launched with a deferred finalize (no-op without slabs). */
 int encdiff_gemm_finalize(const EncdiffGemmArgs* args, void* stream);
 
+/* encdiff_gemm with an optional deferred finalize.  defer_finalize != 0 and the plan keeps
+ * split-K slabs without combining them in the kernel: only the tile kernel is launched and
+ * *planned (if non-NULL) is set to 1; the caller then hands `args` to the consumer that
+ * combines the slabs (EncdiffGroupNormArgs.x_from) or to encdiff_gemm_finalize before anything
+ * else touches the workspace or C.  Otherwise identical to encdiff_gemm (*planned = 0).
+ * Replaces the same nn.Conv2d / nn.Linear forward as encdiff_gemm. */
+int encdiff_gemm_ex(const EncdiffGemmArgs* args, int defer_finalize, int* planned, void* stream);
+
 /* ---------------------------------------------------------------- GroupNorm
  * y = act( GN(x) * (1 + scale[b,c]) + shift[b,c] )
  * Replaces GroupNorm32 + SiLU (+ FiLM) of ResBlock in/out_layers and UNet.out
@@ -207,6 +215,12 @@ typedef struct EncdiffGroupNormArgs {
   const float* in_stats; long ld_in_stats;  /* forward, optional: per-64-row-segment channel sums
                                 of x written by its producer GEMM (EncdiffGemmArgs.gn_stats; hw
                                 a multiple of 64): the statistics come from them, x is read once */
+  const EncdiffGemmArgs* x_from;  /* forward, optional (bf16, no in_stats): x is the output of this
+                                GEMM, launched by encdiff_gemm_ex with its split-K finalize deferred
+                                (bf16 C == x, ldc == ldx, N == c, M == batch*hw): the kernel sums
+                                the slabs in the finalize's order, applies alpha / bias / resid,
+                                WRITES x (bitwise the finalize's result) and normalises it -- one
+                                launch instead of finalize + GroupNorm */
 } EncdiffGroupNormArgs;
 
 int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* args, void* stream);

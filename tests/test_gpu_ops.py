@@ -1062,6 +1062,85 @@ def test_groupnorm_from_producer_stats(O, H, C, silu, film):
     assert rel(nhwc(outs[1][0], g), ref) < 1e-2
 
 
+@pytest.mark.parametrize("B,H,cin,cout,split,resid,film", [
+    (128, 2, 256, 256, 8, "sep", False), (8, 4, 256, 256, 16, None, True), (16, 8, 128, 128, 2, "inplace", True),
+    (8, 16, 64, 64, 4, None, False), (8, 2, 256, 256, 32, "inplace", False)])
+def test_groupnorm_from_deferred_finalize(O, B, H, cin, cout, split, resid, film):
+    """encdiff_gemm_ex with the finalize deferred + GroupNorm forward combining the slabs
+    (x_from) vs encdiff_gemm (tile kernel + finalize pass) + GroupNorm: the conv output x, the
+    normalised output and the saved statistics bitwise equal (<= 8 slabs in one ordered sum,
+    deeper splits in four z-groups, bias, separate and in-place residual)."""
+    import ctypes as C
+    from encdiff_amd import _lib as L
+    from encdiff_amd.ops import Geom, _conv_geom
+    torch.manual_seed(31)
+    g = Geom(B, H, H)
+    a = bf(g.pixels, cin)
+    w = bf(cout, 9 * cin, scale=(9 * cin) ** -0.5)
+    bias = torch.randn(cout, device=dev) * 0.1
+    r = bf(g.pixels, cout)
+    gam = torch.randn(cout, device=dev)
+    bet = torch.randn(cout, device=dev)
+    fl = torch.randn(B, 2 * cout, device=dev) * 0.2 if film else None
+    fold = O.SPLIT_FOLD
+    O.SPLIT_FOLD = 0  # slabs for a finalize pass, not the in-kernel combine
+    outs = []
+    try:
+        for defer in (False, True):
+            x = r.clone() if resid == "inplace" else torch.empty(g.pixels, cout, device=dev, dtype=torch.bfloat16)
+            rs = x if resid == "inplace" else (r if resid == "sep" else None)
+            args = O.gemm_args(g.pixels, cout, 9 * cin, a, cin, w, 9 * cin, x, cout, a_mode=L.OPA_IM2COL,
+                               conv=_conv_geom(g, cin, L.RESAMPLE_NONE, a), bias=bias, resid=rs,
+                               ld_resid=cout if rs is not None else 0, split_k=split, tile=4)
+            assert args.split_k == split and not args.split_counters
+            planned = C.c_int(-1)
+            O.check(O.lib.encdiff_gemm_ex(C.byref(args), int(defer), C.byref(planned), O._s()), "gemm_ex")
+            assert planned.value == int(defer)
+            y = torch.empty(g.pixels, cout, device=dev, dtype=torch.bfloat16)
+            st = torch.empty(B * 32 * 2, device=dev)
+            O.groupnorm_fwd(x, g, gam, bet, y, st, 1e-5, True, film=fl, ld_film=2 * cout if film else 0,
+                            x_from=args if defer else None)
+            torch.cuda.synchronize()
+            outs.append((x, y, st))
+    finally:
+        O.SPLIT_FOLD = fold
+    for u, v in zip(outs[0], outs[1]):
+        assert torch.equal(u, v)
+    xr = F.conv2d(nhwc(a, g), w.float().reshape(cout, 3, 3, cin).permute(0, 3, 1, 2), bias, padding=1)
+    if resid:
+        xr = xr + nhwc(r, g)
+    assert rel(nhwc(outs[1][0], g), xr) < 1e-2
+
+
+def test_groupnorm_x_from_rejects_mismatch(O):
+    """x_from whose output is not exactly x (here: a different buffer) is refused, not guessed."""
+    import ctypes as C
+    from encdiff_amd import _lib as L
+    from encdiff_amd.ops import Geom, _conv_geom
+    g = Geom(8, 4, 4)
+    a = bf(g.pixels, 64)
+    w = bf(64, 9 * 64)
+    x = torch.empty(g.pixels, 64, device=dev, dtype=torch.bfloat16)
+    other = torch.empty_like(x)
+    fold = O.SPLIT_FOLD
+    O.SPLIT_FOLD = 0
+    try:
+        args = O.gemm_args(g.pixels, 64, 9 * 64, a, 64, w, 9 * 64, x, 64, a_mode=L.OPA_IM2COL,
+                           conv=_conv_geom(g, 64, L.RESAMPLE_NONE, a), split_k=4)
+    finally:
+        O.SPLIT_FOLD = fold
+    planned = C.c_int(0)
+    O.check(O.lib.encdiff_gemm_ex(C.byref(args), 1, C.byref(planned), O._s()), "gemm_ex")
+    assert planned.value == 1
+    y = torch.empty_like(x)
+    st = torch.empty(8 * 64, device=dev)
+    with pytest.raises(RuntimeError):
+        O.groupnorm_fwd(other, g, torch.ones(64, device=dev), torch.zeros(64, device=dev), y, st, 1e-5, True,
+                        x_from=args)
+    O.finalize(args)
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("M,C,resid", [(4096, 64, True), (1024, 128, False), (8192, 128, True)])
 def test_linear_layernorm_fused(O, M, C, resid):
     """LayerNorm in the producing GEMM's epilogue (attention.py norm1/2/3 after proj_in /

@@ -132,6 +132,52 @@ def test_unet_split_backward_bitwise(unet):
     assert torch.equal(part, g0[lo:])
 
 
+@pytest.mark.parametrize("B,train", [(8, False), (64, True)])
+def test_unet_gn_fin_bitwise(unet, B, train):
+    """Split-K ResBlock convs hand their slabs to the GroupNorm that reads their output
+    (EncdiffGroupNormArgs.x_from) instead of a finalize launch: eps (and at a training batch the
+    gradients and d(context)) bitwise equal to the separate finalize + GroupNorm launches, and
+    the fused path actually runs."""
+    from encdiff_amd import ops, unet as U
+    torch.manual_seed(29)
+    x = torch.randn(B, 3, 16, 16, device="cuda")
+    t = torch.randint(0, 1000, (B,), device="cuda")
+    c = torch.randn(B, 320, device="cuda")
+    g = torch.randn(B, 3, 16, 16, device="cuda")
+    fused = []
+    orig = ops.groupnorm_fwd
+
+    def counted(*a, **k):
+        fused.append(k.get("x_from") is not None)
+        return orig(*a, **k)
+    ops.groupnorm_fwd = counted
+
+    def run(on):
+        U.GN_FIN = on
+        fused.clear()
+        ex = unet.executor()
+        if not train:
+            with torch.no_grad():
+                return (unet(x, t, [c]).clone(),), sum(fused)
+        unet._arena.zero_grad()
+        cc = c.clone().requires_grad_(True)
+        eps = unet(x, t, context=[cc])
+        n = sum(fused)
+        eps.backward(g)
+        torch.cuda.synchronize()
+        return (eps.detach().clone(), unet._arena.grad.clone(), cc.grad.clone()), n
+    try:
+        a, n_on = run(True)
+        b, n_off = run(False)
+    finally:
+        U.GN_FIN = True
+        ops.groupnorm_fwd = orig
+    print(f"B={B}: {n_on} GroupNorm forwards combined their producer's slabs")
+    assert n_on > 0 and n_off == 0
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+
+
 def test_st_tail_fused_inference(unet, golden_dir):
     """No-grad forwards run each SpatialTransformer's row-local head (proj_in, norm1, q/k/v) and tail (attn1.to_out .. proj_out,
     attention.py:211-215, 250-261) as ONE kernel (encdiff_st_tail_fwd).  It must match the
