@@ -135,6 +135,8 @@ _PROTOS = {
     "encdiff_gemm_pair_ex": [C.POINTER(GemmArgs), C.POINTER(GemmArgs), C.POINTER(GemmArgs), C.c_int, vp],
     "encdiff_gemm_finalize": [C.POINTER(GemmArgs), vp],
     "encdiff_gemm_ex": [C.POINTER(GemmArgs), C.c_int, C.POINTER(C.c_int), vp],
+    "encdiff_gemm_pair_dx": [C.POINTER(GemmArgs), C.POINTER(GemmArgs), C.POINTER(GemmArgs), C.c_int, C.c_int,
+                             C.POINTER(C.c_int), vp],
     "encdiff_groupnorm_fwd": [C.POINTER(GroupNormArgs), vp],
     "encdiff_groupnorm_bwd": [C.POINTER(GroupNormArgs), vp],
     "encdiff_layernorm_fwd": [C.POINTER(LayerNormArgs), vp],

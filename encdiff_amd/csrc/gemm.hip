@@ -2171,8 +2171,11 @@ extern "C" int encdiff_gemm_ex(const EncdiffGemmArgs* pa, int defer_finalize, in
   return r;
 }
 
-extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad,
-                                    const EncdiffGemmArgs* prev_wgrad, int defer, void* stream) {
+// encdiff_gemm_pair_ex / encdiff_gemm_pair_dx: defer_d skips the input gradient's finalize
+// (*dd = 1 when it had one to skip)
+static int gemm_pair_impl(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad,
+                          const EncdiffGemmArgs* prev_wgrad, int defer, bool defer_d, int* dd, void* stream) {
+  *dd = 0;
   GemmPlan g1, g2, gp;
   int rc = prepare(wgrad, g1);
   if (rc != ENCDIFF_OK) return rc;
@@ -2193,6 +2196,17 @@ extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffG
   // both split-K problems need disjoint slabs
   if (g1.ws_path && g2.ws_path && g1.p.workspace == g2.p.workspace) return ENCDIFF_ERR_ARG;
   const bool defer1 = defer && g1.ws_path;
+  const bool dslabs = g2.ws_path && !g2.fold;  // the input gradient has a finalize pass
+  auto run_g2 = [&]() -> int {  // input gradient alone, its finalize unless deferred
+    if (defer_d && dslabs) {
+      GemmPlan t = g2;
+      t.ws_path = false;
+      const int r = launch_one(t, s);
+      if (r == ENCDIFF_OK) *dd = 1;
+      return r;
+    }
+    return launch_one(g2, s);
+  };
   if (g1.tile == 36) {  // WGL weight gradient (+ input gradient, + previous finalize)
     const EncdiffGemmArgs& pf = have_prev ? gp.user : g1.user;
     const int nf = have_prev ? fin_blocks(gp.user) : 0;
@@ -2200,7 +2214,11 @@ extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffG
     e = paired ? wglpair_launch(g1, g2, pf, nf, s) : wgl_launch(g1.p, pf, nf, s);
     if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
     if (g1.ws_path && !defer1 && (e = launch_finalize(g1.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
-    if (!paired) return launch_one(g2, s);
+    if (!paired) return run_g2();
+    if (defer_d && dslabs) {
+      *dd = 1;
+      return ENCDIFF_OK;
+    }
     if (g2.ws_path && (e = launch_finalize(g2.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
     return ENCDIFF_OK;
   }
@@ -2210,16 +2228,17 @@ extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffG
     if (wg3pair_ok(g1, g2)) {  // WG3 + input gradient + previous finalize in one grid
       e = wg3pair_launch(g1, g2, pf, nf, s);
       if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
-      const bool f1 = g1.ws_path && !defer1, f2 = g2.ws_path && !g2.fold;
+      const bool f1 = g1.ws_path && !defer1, f2 = dslabs && !defer_d;
       if (f1 && (e = launch_finalize(g1.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
       if (f2 && (e = launch_finalize(g2.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
+      if (dslabs && defer_d) *dd = 1;
       return ENCDIFF_OK;
     }
     // WG3 weight gradient (+ the previous finalize riding along), then the input gradient
     e = wg3_launch(g1.p, g1.tile, pf, nf, s);
     if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
     if (g1.ws_path && !defer1 && (e = launch_finalize(g1.user, s)) != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
-    return launch_one(g2, s);
+    return run_g2();
   }
   if ((!lin && !conv) || (g1.tile != 4 && g1.tile != 5 && g1.tile != 7 && g1.tile != 9 && g1.tile != 10)) {
     // pairs the fused kernel does not cover
@@ -2227,7 +2246,7 @@ extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffG
     GemmPlan w = g1;
     w.ws_path = g1.ws_path && !defer1;
     rc = launch_one(w, s);
-    return rc != ENCDIFF_OK ? rc : launch_one(g2, s);
+    return rc != ENCDIFF_OK ? rc : run_g2();
   }
   const EncdiffGemmArgs pf = have_prev ? gp.user : g1.user;
   const int nf = have_prev ? fin_blocks(gp.user) : 0;
@@ -2235,7 +2254,8 @@ extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffG
           : launch_pair_tiles<A_ROWM, B_IM2COL, A_IM2COL, B_CONVD>(g1, g2, pf, nf, s);
   if (e != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)e;
   const bool f1 = g1.ws_path && !defer1;
-  const bool f2 = g2.ws_path && !g2.fold;
+  const bool f2 = dslabs && !defer_d;
+  if (dslabs && defer_d) *dd = 1;
   if (f1 && f2) {
     const int n1 = fin_blocks(g1.user), n2 = fin_blocks(g2.user);
     hipLaunchKernelGGL(gemm_finalize2_kernel, dim3((unsigned)(n1 + n2)), dim3(256), 0, s, g1.user, g2.user, n1);
@@ -2248,6 +2268,21 @@ extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffG
     e = hipGetLastError();
   }
   return e != hipSuccess ? ENCDIFF_ERR_LAUNCH - (int)e : ENCDIFF_OK;
+}
+
+extern "C" int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad,
+                                    const EncdiffGemmArgs* prev_wgrad, int defer, void* stream) {
+  int dd;
+  return gemm_pair_impl(wgrad, dgrad, prev_wgrad, defer, false, &dd, stream);
+}
+
+extern "C" int encdiff_gemm_pair_dx(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad,
+                                    const EncdiffGemmArgs* prev_wgrad, int defer, int defer_dgrad, int* dgrad_deferred,
+                                    void* stream) {
+  int dd = 0;
+  const int rc = gemm_pair_impl(wgrad, dgrad, prev_wgrad, defer, defer_dgrad != 0, &dd, stream);
+  if (dgrad_deferred) *dgrad_deferred = rc == ENCDIFF_OK ? dd : 0;
+  return rc;
 }
 
 extern "C" int encdiff_gemm_pair(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad, void* stream) {

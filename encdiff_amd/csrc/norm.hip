@@ -466,7 +466,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const EncdiffGroup
   }
 }
 
-__global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNormArgs p, int cs) {
+__global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNormArgs p, int cs, const GnSlabs sl) {
   __shared__ uint4 tx[GN_TILE], td[GN_TILE];
   __shared__ float red[4 * 2048], chs[4 * 512], gsh[2 * 64];
   const GnSlice L(p, cs);
@@ -508,7 +508,12 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
       bx[u] = bd[u] = (uint4){0u, 0u, 0u, 0u};
       if (px < HW) {
         bx[u] = *(const uint4*)(X + (long)px * p.ldx);
-        bd[u] = *(const uint4*)(DY + (long)px * p.lddy);
+        if (sl.ws) {  // dy combined from its producer's slabs and written back
+          bd[u] = gn_slab_row(sl, off + px, p.c, L.cb);
+          *(uint4*)(const_cast<bf16_t*>(DY) + (long)px * p.lddy) = bd[u];
+        } else {
+          bd[u] = *(const uint4*)(DY + (long)px * p.lddy);
+        }
       }
     }
 #pragma unroll
@@ -739,6 +744,18 @@ int gn_slice(int C, int HW, int cpg, int batch) {
   return C;
 }
 
+// slabs of a GEMM whose deferred finalize output is the tensor t (ld) a GroupNorm reads
+int gn_slabs_of(const EncdiffGemmArgs& g, const void* t, long ld, const EncdiffGroupNormArgs* a, GnSlabs& sl) {
+  const bool tp = g.a_mode == ENCDIFF_OPA_IM2COL && g.conv.resample == ENCDIFF_RESAMPLE_K4S2_TP;
+  if (g.dtype != ENCDIFF_DT_BF16 || g.c_mode != ENCDIFF_OUT_BF16 || g.split_k < 2 || !g.workspace ||
+      g.split_counters || g.bias_grad || tp || g.c != t || g.ldc != ld || g.N != a->c ||
+      (long)g.M != (long)a->batch * a->hw || ((uintptr_t)g.workspace & 15) || (g.bias && ((uintptr_t)g.bias & 15)) ||
+      (g.resid && (g.ld_resid % 8 || ((uintptr_t)g.resid & 15))))
+    return ENCDIFF_ERR_ARG;
+  sl = GnSlabs{g.workspace, (long)g.M * g.N, g.split_k, g.alpha, g.bias, (const bf16_t*)g.resid, g.ld_resid};
+  return ENCDIFF_OK;
+}
+
 int gn_check(const EncdiffGroupNormArgs* a) {
   if (a->c % 8 || a->groups <= 0 || a->c % a->groups) return ENCDIFF_ERR_SHAPE;
   const int cs = gn_slice(a->c, a->hw, a->c / a->groups, a->batch);
@@ -755,15 +772,9 @@ extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream
   if (cs < 0) return cs;
   GnSlabs sl{};
   if (a->x_from) {  // x = the deferred split-K finalize of its producer (self-reducing kernel only)
-    const EncdiffGemmArgs& g = *a->x_from;
-    const bool tp = g.a_mode == ENCDIFF_OPA_IM2COL && g.conv.resample == ENCDIFF_RESAMPLE_K4S2_TP;
-    if (a->in_stats || g.dtype != ENCDIFF_DT_BF16 || g.c_mode != ENCDIFF_OUT_BF16 || g.split_k < 2 || !g.workspace ||
-        g.split_counters || g.bias_grad || tp || g.c != a->x || g.ldc != a->ldx || g.N != a->c ||
-        (long)g.M != (long)a->batch * a->hw || ((uintptr_t)g.workspace & 15) ||
-        (g.bias && ((uintptr_t)g.bias & 15)) ||
-        (g.resid && (g.ld_resid % 8 || ((uintptr_t)g.resid & 15))))
-      return ENCDIFF_ERR_ARG;
-    sl = GnSlabs{g.workspace, (long)g.M * g.N, g.split_k, g.alpha, g.bias, (const bf16_t*)g.resid, g.ld_resid};
+    if (a->in_stats) return ENCDIFF_ERR_ARG;
+    const int rc = gn_slabs_of(*a->x_from, a->x, a->ldx, a, sl);
+    if (rc != ENCDIFF_OK) return rc;
   }
   // producer statistics feed the two statistics kernels where their layout fits; other
   // shapes (e.g. a 384-channel concat at 32x32) take the self-reducing kernel below
@@ -800,7 +811,13 @@ extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream
   if (a->film && !a->dfilm) return ENCDIFF_ERR_ARG;
   const int cs = gn_check(a);
   if (cs < 0) return cs;
-  hipLaunchKernelGGL(gn_bwd_kernel, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream, *a, cs);
+  GnSlabs sl{};
+  if (a->x_from) {  // dy = the deferred split-K finalize of its producer
+    const int rc = gn_slabs_of(*a->x_from, a->dy, a->lddy, a, sl);
+    if (rc != ENCDIFF_OK) return rc;
+  }
+  hipLaunchKernelGGL(gn_bwd_kernel, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream, *a, cs,
+                     sl);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }

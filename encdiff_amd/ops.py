@@ -319,13 +319,15 @@ def gemm(M, N, K, a, lda, b, ldb, c, ldc, **kw):
 PAIR = True  # fuse a layer's weight- and input-gradient GEMMs into one launch (encdiff_gemm_pair_ex)
 
 
-def gemm_pair(wgrad_fn, dgrad_fn):
+def gemm_pair(wgrad_fn, dgrad_fn, defer_dx=False):
     """Launch a layer's weight-gradient and input-gradient GEMMs together (`wgrad_fn(off)`,
     `dgrad_fn(off)` build their GemmArgs with split-K slabs at workspace offset `off`).
     Consecutive pairs alternate between the two workspace halves: the weight gradient's
     finalize is deferred into the NEXT pair's launch (its slabs stay intact in the other
     half), so a backward of N layers needs no finalize launches for weight gradients but the
-    last (`flush`)."""
+    last (`flush`).  defer_dx: the input gradient's finalize is skipped too when it has one;
+    its GemmArgs are returned for the consumer (groupnorm_bwd(dy_from=...)) or finalize(),
+    which must run before the next pair (else None: dx written)."""
     key = torch.cuda.current_stream().cuda_stream
     if not PAIR:
         flush()
@@ -333,24 +335,26 @@ def gemm_pair(wgrad_fn, dgrad_fn):
         d = dgrad_fn(ws_floats(w))
         check(lib.encdiff_gemm(C.byref(w), _s()), "encdiff_gemm")
         check(lib.encdiff_gemm(C.byref(d), _s()), "encdiff_gemm")
-        return
+        return None
     w = wgrad_fn(0)
     nw = ws_floats(w)
     if nw + ws_floats(dgrad_fn(0)) > WS_HALF:  # does not fit a half: plain pair, whole workspace
         flush()
         d = dgrad_fn(nw)
         check(lib.encdiff_gemm_pair(C.byref(w), C.byref(d), _s()), "encdiff_gemm_pair")
-        return
+        return None
     h = 1 - _HALF.get(key, 1)
     if h:
         w = wgrad_fn(h * WS_HALF)
     d = dgrad_fn(h * WS_HALF + nw)
     prev = _PENDING.pop(key, None)
-    check(lib.encdiff_gemm_pair_ex(C.byref(w), C.byref(d), C.byref(prev) if prev is not None else None, 1, _s()),
-          "encdiff_gemm_pair_ex")
+    dd = C.c_int(0)
+    check(lib.encdiff_gemm_pair_dx(C.byref(w), C.byref(d), C.byref(prev) if prev is not None else None, 1,
+                                   int(defer_dx), C.byref(dd), _s()), "encdiff_gemm_pair_dx")
     if nw:
         _PENDING[key] = w
     _HALF[key] = h
+    return d if dd.value else None
 
 
 # ------------------------------------------------------------------ linear layers
@@ -536,11 +540,12 @@ def conv3x3_dgrad_args(dy, g: Geom, wf, dx, resid=None, ws_offset=0):
                      resid=resid, ld_resid=_ld(resid) if resid is not None else 0, ws_offset=ws_offset)
 
 
-def conv3x3_bwd_cl(dy, g: Geom, wf, x, cin, dw_cl, dx, db=None, resample=L.RESAMPLE_NONE, resid=None):
+def conv3x3_bwd_cl(dy, g: Geom, wf, x, cin, dw_cl, dx, db=None, resample=L.RESAMPLE_NONE, resid=None,
+                   defer_dx=False):
     """Backward of one 3x3 conv: dw_cl += dy^T im2col(resample(x)) (+ db) and
-    dx = conv3x3^T(dy) (+ resid) at the conv resolution, one launch."""
-    gemm_pair(lambda off: conv3x3_wgrad_cl_args(dy, x, g, cin, dw_cl, db, resample, off),
-              lambda off: conv3x3_dgrad_args(dy, g, wf, dx, resid, off))
+    dx = conv3x3^T(dy) (+ resid) at the conv resolution, one launch (defer_dx: as gemm_pair)."""
+    return gemm_pair(lambda off: conv3x3_wgrad_cl_args(dy, x, g, cin, dw_cl, db, resample, off),
+                     lambda off: conv3x3_dgrad_args(dy, g, wf, dx, resid, off), defer_dx=defer_dx)
 
 
 # ------------------------------------------------------------------ 4x4 stride-2 convolutions
@@ -597,15 +602,18 @@ def groupnorm_fwd(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_fi
 
 
 def groupnorm_bwd(x, g: Geom, gamma, beta, stats, eps, silu, dy, dx, dgamma_part, dbeta_part, film=None,
-                  ld_film=0, dfilm=None, ld_dfilm=0, accumulate=False, groups=32, ld_part=None, resid=None):
-    """dx (+)= GN_bwd(dy) (+ resid: the block's skip-branch gradient, added in the same pass)."""
+                  ld_film=0, dfilm=None, ld_dfilm=0, accumulate=False, groups=32, ld_part=None, resid=None,
+                  dy_from=None):
+    """dx (+)= GN_bwd(dy) (+ resid: the block's skip-branch gradient, added in the same pass).
+    dy_from: the GemmArgs of dy's producer whose finalize gemm_pair deferred (dy written here)."""
     c = x.shape[1]
     a = L.GroupNormArgs(batch=g.batch, hw=g.h * g.w, c=c, groups=groups, eps=eps, silu=int(silu),
                         x=_p(x), ldx=_ld(x), gamma=_p(gamma), beta=_p(beta), film=_p(film), ld_film=ld_film,
                         stats=_p(stats), dy=_p(dy), lddy=_ld(dy), dx=_p(dx), lddx=_ld(dx),
                         accumulate_dx=int(accumulate), dgamma_part=_p(dgamma_part), dbeta_part=_p(dbeta_part),
                         ld_part=c if ld_part is None else ld_part, dfilm=_p(dfilm), ld_dfilm=ld_dfilm,
-                        resid=_p(resid), ld_resid=_ld(resid) if resid is not None else 0)
+                        resid=_p(resid), ld_resid=_ld(resid) if resid is not None else 0,
+                        x_from=None if dy_from is None else C.addressof(dy_from))
     check(lib.encdiff_groupnorm_bwd(C.byref(a), _s()), "encdiff_groupnorm_bwd")
 
 

@@ -38,9 +38,9 @@ ST_GN_EPS = 1e-6   # Normalize (attention.py:76-77)
 # GroupNorm forward statistics from the producing GEMM's epilogue at >= 8x8 (0: reduce in the
 # GroupNorm kernel, for A/B runs)
 GN_FROM_PRODUCER = os.environ.get("ENCDIFF_GN_FROM_PRODUCER", "1") != "0"
-# a split-K ResBlock conv's finalize folded into the GroupNorm forward that reads its output
-# (conv1 -> GN2 in the block, conv2 -> the next block's GN1): one launch instead of two
-# (0: separate finalize launches, for A/B runs)
+# a split-K ResBlock conv's finalize folded into the GroupNorm that reads its output: forward
+# conv1 -> GN2 in the block, conv2 -> the next block's GN1; backward the conv input gradients
+# -> GN2 / GN1 backward.  One launch instead of two (0: separate finalize launches, A/B runs)
 GN_FIN = os.environ.get("ENCDIFF_GN_FIN", "1") != "0"
 LN_EPS = 1e-5      # nn.LayerNorm default (attention.py:206-208)
 # the row-local SpatialTransformer tail (attn1.to_out .. proj_out) as one kernel
@@ -801,14 +801,16 @@ class UNetExecutor:
         self.ln.reduce(0, lcol)
         return self.d_ctx
 
-    def conv_bwd(self, dy, g, cin, name, x, dx, db, resample=0):
-        """Backward of a 3x3 conv (weight `name`): weight and input gradient in one launch."""
+    def conv_bwd(self, dy, g, cin, name, x, dx, db, resample=0, defer_dx=False):
+        """Backward of a 3x3 conv (weight `name`): weight and input gradient in one launch.
+        defer_dx: returns the input gradient's GemmArgs when its split-K finalize was left to
+        the GroupNorm backward that reads dx (groupnorm_bwd(dy_from=...)), else None."""
         if name in self.arena.cl:
-            ops.conv3x3_bwd_cl(dy, g, self.W(name), x, cin, self.arena.raw(self.arena.grad, name), dx, db,
-                               resample=resample)
-        else:
-            ops.conv3x3_dgrad(dy, g, self.W(name), dx)
-            self.conv_wgrad(dy, x, g, cin, name, db, resample=resample)
+            return ops.conv3x3_bwd_cl(dy, g, self.W(name), x, cin, self.arena.raw(self.arena.grad, name), dx, db,
+                                      resample=resample, defer_dx=defer_dx)
+        ops.conv3x3_dgrad(dy, g, self.W(name), dx)
+        self.conv_wgrad(dy, x, g, cin, name, db, resample=resample)
+        return None
 
     def _layer_bwd(self, layer, dout, dx, acc):
         if isinstance(layer, ResSpec):
@@ -823,14 +825,15 @@ class UNetExecutor:
         gi, go = Geom(B, r.hin, r.hin), Geom(B, r.hout, r.hout)
         pre = r.prefix
         # conv2: input + weight gradient in one launch
-        self.conv_bwd(dout, go, r.cout, pre + "out_layers.3.weight", S["a2"], S["d_a2"],
-                      self.G(pre + "out_layers.3.bias"))
+        # (the input gradients' split-K finalizes ride in the GroupNorm backwards that read them)
+        f2 = self.conv_bwd(dout, go, r.cout, pre + "out_layers.3.weight", S["a2"], S["d_a2"],
+                           self.G(pre + "out_layers.3.bias"), defer_dx=GN_FIN)
         # GN2 + FiLM + SiLU
         dg, db = self.gn.parts(pre + "out_layers.0.weight", r.cout)
         ops.groupnorm_bwd(S["h1"], go, self.P(pre + "out_layers.0.weight"), self.P(pre + "out_layers.0.bias"),
                           S["st2"], GN_EPS, True, S["d_a2"], S["d_h1"], dg, db, film=self.E[:, r.film_off:],
                           ld_film=self.E.shape[1], dfilm=self.dE[:, r.film_off:], ld_dfilm=self.dE.shape[1],
-                          ld_part=self.gn.ld)
+                          ld_part=self.gn.ld, dy_from=f2)
         # conv1 (on the resampled GN1 output)
         if r.updown == L.RESAMPLE_DOWN2:
             a1, rs = S["a1r"], L.RESAMPLE_NONE
@@ -838,15 +841,15 @@ class UNetExecutor:
             a1, rs = S["a1"], r.updown
         dg, db = self.gn.parts(pre + "in_layers.0.weight", r.cin)
         d_a1 = S["d_a1"]
-        self.conv_bwd(S["d_h1"], go, r.cin, pre + "in_layers.2.weight", a1, S["d_a1r"] if r.updown else d_a1,
-                      self.G(pre + "in_layers.2.bias"), resample=rs)
+        f1 = self.conv_bwd(S["d_h1"], go, r.cin, pre + "in_layers.2.weight", a1, S["d_a1r"] if r.updown else d_a1,
+                           self.G(pre + "in_layers.2.bias"), resample=rs, defer_dx=GN_FIN and not r.updown)
         if r.updown:
             ops.resample_bwd(S["d_a1r"], d_a1, gi, r.updown)
         identity = r.cin == r.cout and not r.updown
         # identity skip: its gradient (dout) rides in the GN1 backward pass
         ops.groupnorm_bwd(x, gi, self.P(pre + "in_layers.0.weight"), self.P(pre + "in_layers.0.bias"), S["st1"],
                           GN_EPS, True, d_a1, dx, dg, db, accumulate=acc, ld_part=self.gn.ld,
-                          resid=dout if identity else None)
+                          resid=dout if identity else None, dy_from=f1)
         # skip path
         if r.cin != r.cout:
             ops.linear_bwd(dout, self.W(pre + "skip_connection.weight"), x, dx,

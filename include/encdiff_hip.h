@@ -175,6 +175,15 @@ int encdiff_gemm_pair(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad
 int encdiff_gemm_pair_ex(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad,
                          const EncdiffGemmArgs* prev_wgrad, int defer, void* stream);
 
+/* encdiff_gemm_pair_ex that may also defer the INPUT gradient's finalize: defer_dgrad != 0 and
+ * `dgrad` leaves split-K slabs for a finalize pass -> that pass is not launched and
+ * *dgrad_deferred = 1; the caller hands `dgrad` to its consumer (EncdiffGroupNormArgs.x_from of
+ * a GroupNorm backward) or to encdiff_gemm_finalize before the workspace half is reused.
+ * Otherwise *dgrad_deferred = 0 and the result is encdiff_gemm_pair_ex's. */
+int encdiff_gemm_pair_dx(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dgrad,
+                         const EncdiffGemmArgs* prev_wgrad, int defer, int defer_dgrad, int* dgrad_deferred,
+                         void* stream);
+
 /* The split-K finalize of a GEMM launched with a deferred finalize (no-op without slabs). */
 int encdiff_gemm_finalize(const EncdiffGemmArgs* args, void* stream);
 
@@ -220,7 +229,10 @@ typedef struct EncdiffGroupNormArgs {
                                 (bf16 C == x, ldc == ldx, N == c, M == batch*hw): the kernel sums
                                 the slabs in the finalize's order, applies alpha / bias / resid,
                                 WRITES x (bitwise the finalize's result) and normalises it -- one
-                                launch instead of finalize + GroupNorm */
+                                launch instead of finalize + GroupNorm.  Backward: the same for dy
+                                (C == dy, ldc == lddy; e.g. the input gradient of the conv that read
+                                this GroupNorm's output, its finalize deferred by
+                                encdiff_gemm_pair_dx) */
 } EncdiffGroupNormArgs;
 
 int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* args, void* stream);

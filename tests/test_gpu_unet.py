@@ -135,26 +135,33 @@ def test_unet_split_backward_bitwise(unet):
 @pytest.mark.parametrize("B,train", [(8, False), (64, True)])
 def test_unet_gn_fin_bitwise(unet, B, train):
     """Split-K ResBlock convs hand their slabs to the GroupNorm that reads their output
-    (EncdiffGroupNormArgs.x_from) instead of a finalize launch: eps (and at a training batch the
-    gradients and d(context)) bitwise equal to the separate finalize + GroupNorm launches, and
-    the fused path actually runs."""
+    (EncdiffGroupNormArgs.x_from; in the backward the conv input gradients to the GroupNorm
+    backward) instead of a finalize launch: eps (and at a training batch the gradients and
+    d(context)) bitwise equal to the separate finalize + GroupNorm launches, and the fused
+    paths actually run."""
     from encdiff_amd import ops, unet as U
     torch.manual_seed(29)
     x = torch.randn(B, 3, 16, 16, device="cuda")
     t = torch.randint(0, 1000, (B,), device="cuda")
     c = torch.randn(B, 320, device="cuda")
     g = torch.randn(B, 3, 16, 16, device="cuda")
-    fused = []
-    orig = ops.groupnorm_fwd
+    fused, fused_b = [], []
+    orig, orig_b = ops.groupnorm_fwd, ops.groupnorm_bwd
 
     def counted(*a, **k):
         fused.append(k.get("x_from") is not None)
         return orig(*a, **k)
+
+    def counted_b(*a, **k):
+        fused_b.append(k.get("dy_from") is not None)
+        return orig_b(*a, **k)
     ops.groupnorm_fwd = counted
+    ops.groupnorm_bwd = counted_b
 
     def run(on):
         U.GN_FIN = on
         fused.clear()
+        fused_b.clear()
         ex = unet.executor()
         if not train:
             with torch.no_grad():
@@ -165,15 +172,17 @@ def test_unet_gn_fin_bitwise(unet, B, train):
         n = sum(fused)
         eps.backward(g)
         torch.cuda.synchronize()
-        return (eps.detach().clone(), unet._arena.grad.clone(), cc.grad.clone()), n
+        return (eps.detach().clone(), unet._arena.grad.clone(), cc.grad.clone()), n + 1000 * sum(fused_b)
     try:
         a, n_on = run(True)
         b, n_off = run(False)
     finally:
         U.GN_FIN = True
-        ops.groupnorm_fwd = orig
-    print(f"B={B}: {n_on} GroupNorm forwards combined their producer's slabs")
-    assert n_on > 0 and n_off == 0
+        ops.groupnorm_fwd, ops.groupnorm_bwd = orig, orig_b
+    print(f"B={B}: {n_on % 1000} GroupNorm forwards / {n_on // 1000} backwards combined their producer's slabs")
+    assert n_on % 1000 > 0 and n_off == 0
+    if train:
+        assert n_on // 1000 > 0
     for u, v in zip(a, b):
         assert torch.equal(u, v)
 
