@@ -63,7 +63,8 @@ class LayerNormArgs(C.Structure):
                 ("x", vp), ("ldx", C.c_long), ("gamma", vp), ("beta", vp), ("y", vp), ("ldy", C.c_long),
                 ("stats", vp), ("dy", vp), ("lddy", C.c_long), ("dx", vp), ("lddx", C.c_long),
                 ("accumulate_dx", C.c_int), ("dgamma_part", vp), ("dbeta_part", vp), ("ld_part", C.c_long),
-                ("parts", C.c_int), ("dtype", C.c_int), ("resid", vp), ("ld_resid", C.c_long)]
+                ("parts", C.c_int), ("dtype", C.c_int), ("resid", vp), ("ld_resid", C.c_long),
+                ("dy_from", vp)]
 
 
 class AttnArgs(C.Structure):

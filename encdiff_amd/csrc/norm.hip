@@ -653,7 +653,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const EncdiffLayerNormArgs 
 }
 
 template <int C>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const EncdiffLayerNormArgs p) {
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const EncdiffLayerNormArgs p, const GnSlabs sl) {
   constexpr int LPR = C / 8;
   constexpr int RPB = 256 / LPR;
   __shared__ float red[2][RPB][C];
@@ -675,7 +675,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const EncdiffLayerNormArgs 
       rp_on[u] = false;
       if (row >= p.rows) continue;
       unpack8(*(const uint4*)((const bf16_t*)p.x + (long)row * p.ldx + lr * 8), v[u]);
-      unpack8(*(const uint4*)((const bf16_t*)p.dy + (long)row * p.lddy + lr * 8), d[u]);
+      if (sl.ws) {  // dy combined from its producer's slabs and written back
+        const uint4 du = gn_slab_row(sl, row, C, lr * 8);
+        *(uint4*)((bf16_t*)p.dy + (long)row * p.lddy + lr * 8) = du;
+        unpack8(du, d[u]);
+      } else {
+        unpack8(*(const uint4*)((const bf16_t*)p.dy + (long)row * p.lddy + lr * 8), d[u]);
+      }
       mean[u] = p.stats[2 * row];
       rstd[u] = p.stats[2 * row + 1];
       // residual-branch gradient: dx itself (in place) or a separate tensor (out of place, so a
@@ -826,7 +832,17 @@ template <int C>
 static int ln_launch(const EncdiffLayerNormArgs& a, bool bwd, hipStream_t s) {
   constexpr int RPB = 256 / (C / 8);
   if (bwd) {
-    hipLaunchKernelGGL(ln_bwd_kernel<C>, dim3(a.parts), dim3(256), 0, s, a);
+    GnSlabs sl{};
+    if (a.dy_from) {  // dy = the deferred split-K finalize of its producer (same checks as GroupNorm's)
+      const EncdiffGemmArgs& g = *a.dy_from;
+      if (g.dtype != ENCDIFF_DT_BF16 || g.c_mode != ENCDIFF_OUT_BF16 || g.split_k < 2 || !g.workspace ||
+          g.split_counters || g.bias_grad || g.a_mode == ENCDIFF_OPA_IM2COL || g.c != a.dy || g.ldc != a.lddy ||
+          g.N != C || g.M != a.rows || ((uintptr_t)g.workspace & 15) || (g.bias && ((uintptr_t)g.bias & 15)) ||
+          (g.resid && (g.ld_resid % 8 || ((uintptr_t)g.resid & 15))))
+        return ENCDIFF_ERR_ARG;
+      sl = GnSlabs{g.workspace, (long)g.M * g.N, g.split_k, g.alpha, g.bias, (const bf16_t*)g.resid, g.ld_resid};
+    }
+    hipLaunchKernelGGL(ln_bwd_kernel<C>, dim3(a.parts), dim3(256), 0, s, a, sl);
   } else {
     int grid = (a.rows + RPB - 1) / RPB;
     if (grid > 4096) grid = 4096;

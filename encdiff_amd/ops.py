@@ -432,9 +432,11 @@ def linear_wgrad(dy, x, dw, db=None):
     check(lib.encdiff_gemm(C.byref(args), _s()), "encdiff_gemm")
 
 
-def linear_bwd(dy, w, x, dx, dw, db=None, resid=None):
-    """Backward of one linear layer: dw += dy^T x (+ db), dx = dy w (+ resid), one launch."""
-    gemm_pair(lambda off: linear_wgrad_args(dy, x, dw, db, off), lambda off: linear_dgrad_args(dy, w, dx, resid, off))
+def linear_bwd(dy, w, x, dx, dw, db=None, resid=None, defer_dx=False):
+    """Backward of one linear layer: dw += dy^T x (+ db), dx = dy w (+ resid), one launch
+    (defer_dx: as gemm_pair)."""
+    return gemm_pair(lambda off: linear_wgrad_args(dy, x, dw, db, off),
+                     lambda off: linear_dgrad_args(dy, w, dx, resid, off), defer_dx=defer_dx)
 
 
 # GEGLU feed-forward (attention.py GEGLU / FeedForward): the activation runs in the GEMM
@@ -631,15 +633,18 @@ def layernorm_fwd(x, gamma, beta, y, stats, eps=1e-5):
     check(lib.encdiff_layernorm_fwd(C.byref(a), _s()), "encdiff_layernorm_fwd")
 
 
-def layernorm_bwd(x, gamma, stats, dy, dx, dgamma_part, dbeta_part, accumulate=False, ld_part=None, resid=None):
-    """dx = LN_bwd(dy) (+ dx if accumulate) (+ resid: the residual-branch gradient, out of place)."""
+def layernorm_bwd(x, gamma, stats, dy, dx, dgamma_part, dbeta_part, accumulate=False, ld_part=None, resid=None,
+                  dy_from=None):
+    """dx = LN_bwd(dy) (+ dx if accumulate) (+ resid: the residual-branch gradient, out of place).
+    dy_from: as groupnorm_bwd."""
     rows, c = x.shape
     parts = layernorm_parts(rows, c)
     ld_part = c if ld_part is None else ld_part
     a = L.LayerNormArgs(rows=rows, c=c, eps=0.0, x=_p(x), ldx=_ld(x), gamma=_p(gamma), stats=_p(stats),
                         dy=_p(dy), lddy=_ld(dy), dx=_p(dx), lddx=_ld(dx), accumulate_dx=int(accumulate),
                         dgamma_part=_p(dgamma_part), dbeta_part=_p(dbeta_part), ld_part=ld_part, parts=parts,
-                        resid=_p(resid), ld_resid=_ld(resid) if resid is not None else 0)
+                        resid=_p(resid), ld_resid=_ld(resid) if resid is not None else 0,
+                        dy_from=None if dy_from is None else C.addressof(dy_from))
     check(lib.encdiff_layernorm_bwd(C.byref(a), _s()), "encdiff_layernorm_bwd")
 
 

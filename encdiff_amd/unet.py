@@ -40,7 +40,8 @@ ST_GN_EPS = 1e-6   # Normalize (attention.py:76-77)
 GN_FROM_PRODUCER = os.environ.get("ENCDIFF_GN_FROM_PRODUCER", "1") != "0"
 # a split-K ResBlock conv's finalize folded into the GroupNorm that reads its output: forward
 # conv1 -> GN2 in the block, conv2 -> the next block's GN1; backward the conv input gradients
-# -> GN2 / GN1 backward.  One launch instead of two (0: separate finalize launches, A/B runs)
+# -> GN2 / GN1 backward, transformer linears -> the LayerNorm / GroupNorm backward reading their
+# input gradient.  One launch instead of two (0: separate finalize launches, A/B runs)
 GN_FIN = os.environ.get("ENCDIFF_GN_FIN", "1") != "0"
 LN_EPS = 1e-5      # nn.LayerNorm default (attention.py:206-208)
 # the row-local SpatialTransformer tail (attn1.to_out .. proj_out) as one kernel
@@ -874,12 +875,12 @@ class UNetExecutor:
         # FF
         ops.linear_bwd_geglu(d_t3, self.W(tb + "ff.net.2.weight"), S["a"], S["f"], S["d_f"],
                              self.G(tb + "ff.net.2.weight"), self.G(tb + "ff.net.2.bias"), d_a=d_a)
-        ops.linear_bwd(S["d_f"], self.W(tb + "ff.net.0.proj.weight"), S["n3"], d_n,
-                       self.G(tb + "ff.net.0.proj.weight"), self.G(tb + "ff.net.0.proj.bias"))
+        fin = ops.linear_bwd(S["d_f"], self.W(tb + "ff.net.0.proj.weight"), S["n3"], d_n,
+                             self.G(tb + "ff.net.0.proj.weight"), self.G(tb + "ff.net.0.proj.bias"), defer_dx=GN_FIN)
         dg, db = self.ln.parts(tb + "norm3.weight", c)
         d_t2 = S["d_t2"]  # d(t2) = d(t3) (residual) + norm3 backward
         ops.layernorm_bwd(S["t2"], self.P(tb + "norm3.weight"), S["s3"], d_n, d_t2, dg, db, ld_part=self.ln.ld,
-                          resid=d_t3)
+                          resid=d_t3, dy_from=fin)
         # cross-attention
         ops.linear_bwd(d_t2, self.W(tb + "attn2.to_out.0.weight"), S["o2"], d_o,
                        self.G(tb + "attn2.to_out.0.weight"), self.G(tb + "attn2.to_out.0.bias"))
@@ -889,26 +890,28 @@ class UNetExecutor:
         dv2 = self.dKV[:, s.kv_off + c:s.kv_off + 2 * c]
         ops.attention_bwd(S["q2"], k2, v2, S["o2"], S["lse2"], d_o, S["d_q2"], dk2, dv2, B, s.heads, ntok, self.lu,
                           s.dh)
-        ops.linear_bwd(S["d_q2"], self.W(tb + "attn2.to_q.weight"), S["n2"], d_n, self.G(tb + "attn2.to_q.weight"))
+        fin = ops.linear_bwd(S["d_q2"], self.W(tb + "attn2.to_q.weight"), S["n2"], d_n,
+                             self.G(tb + "attn2.to_q.weight"), defer_dx=GN_FIN)
         dg, db = self.ln.parts(tb + "norm2.weight", c)
         d_t1 = S["d_t1"]
         ops.layernorm_bwd(S["t1"], self.P(tb + "norm2.weight"), S["s2"], d_n, d_t1, dg, db, ld_part=self.ln.ld,
-                          resid=d_t2)
+                          resid=d_t2, dy_from=fin)
         # self-attention
         ops.linear_bwd(d_t1, self.W(tb + "attn1.to_out.0.weight"), S["o1"], d_o,
                        self.G(tb + "attn1.to_out.0.weight"), self.G(tb + "attn1.to_out.0.bias"))
         qkv, dqkv = S["qkv"], S["d_qkv"]
         ops.attention_bwd(qkv[:, :c], qkv[:, c:2 * c], qkv[:, 2 * c:], S["o1"], S["lse1"], d_o, dqkv[:, :c],
                           dqkv[:, c:2 * c], dqkv[:, 2 * c:], B, s.heads, ntok, ntok, s.dh, fp8=s.fp8)
-        ops.linear_bwd(dqkv, self.W(s.prefix + "qkv"), S["n1"], d_n, self.qkv_grad[s.prefix])
+        fin = ops.linear_bwd(dqkv, self.W(s.prefix + "qkv"), S["n1"], d_n, self.qkv_grad[s.prefix], defer_dx=GN_FIN)
         dg, db = self.ln.parts(tb + "norm1.weight", c)
         d_t0 = S["d_t0"]
         ops.layernorm_bwd(S["t0"], self.P(tb + "norm1.weight"), S["s1"], d_n, d_t0, dg, db, ld_part=self.ln.ld,
-                          resid=d_t1)
+                          resid=d_t1, dy_from=fin)
         # proj_in
-        ops.linear_bwd(d_t0, self.W(s.prefix + "proj_in.weight"), S["gn"], X["d_g"],
-                       self.G(s.prefix + "proj_in.weight").view(c, c), self.G(s.prefix + "proj_in.bias"))
+        fin = ops.linear_bwd(d_t0, self.W(s.prefix + "proj_in.weight"), S["gn"], X["d_g"],
+                             self.G(s.prefix + "proj_in.weight").view(c, c), self.G(s.prefix + "proj_in.bias"),
+                             defer_dx=GN_FIN)
         dg, db = self.gn.parts(s.prefix + "norm.weight", c)
-        # + the residual x_in branch (dout), in the same pass
+        # + the residual x_in branch (dout), in the same pass (and proj_in's input-gradient finalize)
         ops.groupnorm_bwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["stg"], ST_GN_EPS,
-                          False, X["d_g"], dx, dg, db, accumulate=acc, ld_part=self.gn.ld, resid=dout)
+                          False, X["d_g"], dx, dg, db, accumulate=acc, ld_part=self.gn.ld, resid=dout, dy_from=fin)

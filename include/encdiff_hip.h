@@ -258,6 +258,11 @@ typedef struct EncdiffLayerNormArgs {
   int dtype;                 /* ENCDIFF_DT_F32: x, y fp32 (forward)                 */
   const void* resid; long ld_resid; /* backward: optional bf16 residual-branch gradient:
                                         dx = resid + LN_bwd (out of place; may alias dx) */
+  const EncdiffGemmArgs* dy_from;   /* backward, optional: dy is the output of this GEMM whose
+                                        split-K finalize was deferred (encdiff_gemm_pair_dx; bf16
+                                        C == dy, ldc == lddy, N == c, M == rows): its slabs are
+                                        combined here as the finalize would, dy written, as
+                                        EncdiffGroupNormArgs.x_from */
 } EncdiffLayerNormArgs;
 
 int encdiff_layernorm_fwd(const EncdiffLayerNormArgs* args, void* stream);

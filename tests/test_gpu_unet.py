@@ -146,7 +146,7 @@ def test_unet_gn_fin_bitwise(unet, B, train):
     c = torch.randn(B, 320, device="cuda")
     g = torch.randn(B, 3, 16, 16, device="cuda")
     fused, fused_b = [], []
-    orig, orig_b = ops.groupnorm_fwd, ops.groupnorm_bwd
+    orig, orig_b, orig_l = ops.groupnorm_fwd, ops.groupnorm_bwd, ops.layernorm_bwd
 
     def counted(*a, **k):
         fused.append(k.get("x_from") is not None)
@@ -155,8 +155,12 @@ def test_unet_gn_fin_bitwise(unet, B, train):
     def counted_b(*a, **k):
         fused_b.append(k.get("dy_from") is not None)
         return orig_b(*a, **k)
+    def counted_l(*a, **k):
+        fused_b.append(k.get("dy_from") is not None)
+        return orig_l(*a, **k)
     ops.groupnorm_fwd = counted
     ops.groupnorm_bwd = counted_b
+    ops.layernorm_bwd = counted_l
 
     def run(on):
         U.GN_FIN = on
@@ -178,8 +182,9 @@ def test_unet_gn_fin_bitwise(unet, B, train):
         b, n_off = run(False)
     finally:
         U.GN_FIN = True
-        ops.groupnorm_fwd, ops.groupnorm_bwd = orig, orig_b
-    print(f"B={B}: {n_on % 1000} GroupNorm forwards / {n_on // 1000} backwards combined their producer's slabs")
+        ops.groupnorm_fwd, ops.groupnorm_bwd, ops.layernorm_bwd = orig, orig_b, orig_l
+    print(f"B={B}: {n_on % 1000} GroupNorm forwards / {n_on // 1000} Group/LayerNorm backwards combined their "
+          f"producer's slabs")
     assert n_on % 1000 > 0 and n_off == 0
     if train:
         assert n_on // 1000 > 0
