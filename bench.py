@@ -106,22 +106,26 @@ def _copy_args(argp):
 
 def record_gemms(tr):
     """Every GEMM-family launch of one eager training step, in order: single GEMMs
-    (encdiff_gemm), paired weight/input-gradient GEMMs with a deferred finalize riding along
-    (encdiff_gemm_pair_ex, encdiff_gemm_pair) and explicit finalizes (encdiff_gemm_finalize).
+    (encdiff_gemm, encdiff_gemm_ex), paired weight/input-gradient GEMMs with a deferred finalize
+    riding along (encdiff_gemm_pair_ex, encdiff_gemm_pair_dx, encdiff_gemm_pair) and explicit
+    finalizes (encdiff_gemm_finalize).  A finalize the step left to the GroupNorm / LayerNorm
+    reading the output (gemm_ex / pair_dx deferrals) is recorded as part of its GEMM: the replay
+    launches it, so the family keeps its full split-K cost.
     Returns [(kind, args...)]; `gemm_problems` lists the GEMM problems inside."""
     from encdiff_amd import _lib as L
     calls = []
-    names = ("encdiff_gemm", "encdiff_gemm_pair", "encdiff_gemm_pair_ex", "encdiff_gemm_finalize")
+    names = ("encdiff_gemm", "encdiff_gemm_ex", "encdiff_gemm_pair", "encdiff_gemm_pair_ex", "encdiff_gemm_pair_dx",
+             "encdiff_gemm_finalize")
     orig = {n: getattr(L.lib, n) for n in names}
 
     def rec(name):
         def f(*a):
             stream = a[-1]
-            if name == "encdiff_gemm":
+            if name in ("encdiff_gemm", "encdiff_gemm_ex"):
                 calls.append(("gemm", _copy_args(a[0])))
             elif name == "encdiff_gemm_pair":
                 calls.append(("pair_ex", _copy_args(a[0]), _copy_args(a[1]), None, 0))
-            elif name == "encdiff_gemm_pair_ex":
+            elif name in ("encdiff_gemm_pair_ex", "encdiff_gemm_pair_dx"):
                 calls.append(("pair_ex", _copy_args(a[0]), _copy_args(a[1]), _copy_args(a[2]), a[3]))
             else:
                 calls.append(("finalize", _copy_args(a[0])))
