@@ -73,7 +73,7 @@ WORKLOADS = {
                  "configs[1]: Shapes3D VQ-f4 16x16 latent LatentDiffusion training step (shapes3d-vq-4-16-encdiff)"),
     "celeba128": ("training imgs/sec (node) CelebA 128x128 LDM (builder-defined configs[4])",
                   "configs[4]: CelebA-shaped 128x128 VQ-f4 32x32 latent, model_channels 128, 40 concept tokens, "
-                  "5-stage Encoder4, fp8 scores at the S=1024 self-attention"),
+                  "5-stage Encoder4, bf16 MFMA attention (ENCDIFF_ATTN_FP8=1: e4m3 scores at the S=1024 level)"),
 }
 
 

@@ -62,20 +62,26 @@ class ResBlock(TimestepBlock):
 
 
 class _UNetFn(torch.autograd.Function):
-    """eps = UNet(x_t, t, context); backward returns d(context) only (x_t needs no
-    gradient in the EncDiff objective); weight grads go to the arena."""
+    """eps = UNet(x_t, t, context); backward returns d(context), and d(x_t) only when x_t
+    requires grad (the EncDiff objective does not ask for it); weight grads go to the arena."""
 
     @staticmethod
     def forward(ctx, x, t, c, ex: UNetExecutor):
         ctx.ex = ex
+        ctx.want_dx = bool(ctx.needs_input_grad[0])
         return ex.forward(x, t, c).clone()
 
     @staticmethod
     def backward(ctx, g):
         # ex.split_requested (data-parallel trainer): only the output blocks run here; the
         # d(context) buffer is filled by ex.backward_rest(), which the trainer calls itself
-        dc = ctx.ex.backward(g.float(), split=ctx.ex.split_requested)
-        return None, None, dc.clone(), None
+        ex = ctx.ex
+        ex.want_dx = ctx.want_dx and not ex.split_requested
+        try:
+            dc = ex.backward(g.float(), split=ex.split_requested)
+        finally:
+            want, ex.want_dx = ex.want_dx, False
+        return (ex.d_x.clone() if want else None), None, dc.clone(), None
 
 
 _SUPPORTED = dict(dims=2, num_classes=None, use_fp16=False, num_head_channels=-1, transformer_depth=1,

@@ -278,6 +278,7 @@ class UNetExecutor:
         self.B = None
         self._sets: Dict[int, dict] = {}
         self.split_requested = False  # data-parallel trainer: backward(split=True) via autograd
+        self.want_dx = False  # backward also writes d x_t (self.d_x): set by _UNetFn when x requires grad
         self.infer = False  # no backward follows the next forward (UNetModel.forward under no_grad)
         self._base_names = set(self.__dict__) | {"_base_names"}
         self.pack.repack()
@@ -783,6 +784,17 @@ class UNetExecutor:
                  bias_grad=self.G("input_blocks.0.0.bias"))
         cin0 = self._x.shape[1]
         ops.grad_fold(self.dw_in, self.mc, cin0, 8, 9, self.G("input_blocks.0.0.weight"))
+        if self.want_dx:
+            # d x_t (only when the caller asked for it: the EncDiff objective needs none): the
+            # input conv's input gradient over the channel-padded rows, fp32, back to NCHW
+            if getattr(self, "d_x", None) is None or self.d_x.shape != self._x.shape:
+                self.dx8 = torch.empty(g0.pixels, 8, device=self.dev, dtype=F32)
+                self.d_x = torch.empty_like(self._x, dtype=F32)
+            ops.gemm(g0.pixels, 8, 9 * self.mc, dy0, dy0.stride(0), self.W("input_conv"), 72, self.dx8, 8,
+                     a_mode=L.OPA_IM2COL, b_mode=L.OPB_CONV_DGRAD, c_mode=L.OUT_F32,
+                     conv=L.ConvGeom(batch=B, h=self.H, w=self.H, cin=self.mc, resample=0, ld_src=dy0.stride(0)),
+                     conv_cout=self.mc)
+            ops.nchw_rows_f32(self.dx8, B, cin0, self.H * self.H, 8, self.d_x, 8, to_rows=False)
         # batched emb_layers backward -> time MLP
         ops.ew(L.EW_F32_TO_BF16, self.dE, self.dE16)
         ops.linear_bwd(self.dE16, self.W("emb_all"), self.emb_s, self.d_emb_s, self.emb_w_grad, self.emb_bias_grad)

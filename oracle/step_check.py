@@ -48,13 +48,16 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-def recipe_ldm(config="shapes3d"):
+def recipe_ldm(config="shapes3d", unet_params=None):
     """LatentDiffusion from the reference-shaped config with recipe weights in the UNet,
-    Encoder4 and the VQ first stage, on cuda."""
+    Encoder4 and the VQ first stage, on cuda.  ``unet_params`` overrides UNetModel kwargs
+    (e.g. ``attn_fp8_min_tokens``) for this instance only."""
     import encdiff_amd  # noqa: F401
     from encdiff_amd.configs import model_config
     from encdiff_amd.ldm.util import instantiate_from_config
     cfg = model_config(config)
+    if unet_params:
+        cfg["params"]["unet_config"]["params"].update(unet_params)
     torch.manual_seed(0)
     ldm = instantiate_from_config(cfg)
     with torch.no_grad():
@@ -74,11 +77,11 @@ class GraphStepCheck:
     ``check()`` runs one replay + one oracle step and returns the error dict; the oracle
     then adopts the device parameters so that the next check starts from identical state."""
 
-    def __init__(self, B=128, config="shapes3d", lr=1e-4, seed=2024, warmup=2, threads=16):
+    def __init__(self, B=128, config="shapes3d", lr=1e-4, seed=2024, warmup=2, threads=16, unet_params=None):
         from encdiff_amd.trainer import HipTrainer
         torch.set_num_threads(max(1, min(threads, torch.get_num_threads())))
         self.B, self.config = B, config
-        ldm, cfg = recipe_ldm(config)
+        ldm, cfg = recipe_ldm(config, unet_params)
         ucfg = cfg["params"]["unet_config"]["params"]
         self.lu = ucfg["latent_unit"]
         self.res = 64 if config == "shapes3d" else 128

@@ -288,6 +288,7 @@ def main():
     e['lr_n'] = ns
     e['lr_f'] = np.array([sched(int(n)) for n in ns], dtype=np.float64)
     np.savez_compressed(os.path.join(OUT, 'ema_adamw_lr.npz'), **e)
+    unet_bf16(cfg)
     print('fixtures written to', OUT)
 
 
@@ -324,5 +325,39 @@ def ddim_only(cfg):
     ddim_long(ldm, cond)
 
 
+def unet_bf16(cfg):
+    """--only-bf16: the REFERENCE UNet on unet_b4.npz's inputs under torch.autocast(bf16) (CPU),
+    forward and backward (the checkpoint recompute inside the backward autocast too), written as
+    unet_b4_bf16.npz: eps, dx, dctx and the same 16 weight gradients.  This is the error the
+    reference itself makes when it computes in bf16 -- the yardstick for the bf16 product
+    backward's tolerance (tests/test_gpu_unet.py)."""
+    from ldm.modules.diffusionmodules.openaimodel_enc import UNetModel
+    up = cfg['model']['params']['unet_config']['params']
+    unet = UNetModel(**up)
+    set_recipe(unet, '')
+    unet.eval()
+    fx = np.load(os.path.join(OUT, 'unet_b4.npz'))
+    x = torch.tensor(fx['x']).requires_grad_(True)
+    ctx = torch.tensor(fx['ctx']).requires_grad_(True)
+    with torch.autocast('cpu', dtype=torch.bfloat16):
+        out = unet(x, torch.tensor(fx['t']), context=[ctx])
+    # a second autocast region: the first one's cache of bf16 weight casts (made under the
+    # checkpoint's no_grad forward) would cut the recompute off from the fp32 parameters
+    with torch.autocast('cpu', dtype=torch.bfloat16):
+        out.float().backward(torch.tensor(fx['gout']))
+    pd = dict(unet.named_parameters())
+    res = dict(eps=out.detach().float().numpy(), dx=x.grad.numpy(), dctx=ctx.grad.numpy())
+    for k in fx.files:
+        if k.startswith('grad.'):
+            res[k] = pd[k[5:]].grad.float().numpy()
+    np.savez_compressed(os.path.join(OUT, 'unet_b4_bf16.npz'), **res)
+    print('unet_b4_bf16 written')
+
+
 if __name__ == '__main__':
-    main()
+    if '--only-bf16' in sys.argv:
+        install_shims()
+        torch.set_num_threads(8)
+        unet_bf16(load_yaml_cfg())
+    else:
+        main()
