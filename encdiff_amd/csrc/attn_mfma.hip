@@ -967,4 +967,7 @@ extern "C" int encdiff_attention_fwd(const EncdiffAttnArgs* a, void* stream) {
   if (a && a->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_ARG;
   return attn_dispatch(a, false, stream);
 }
-extern "C" int encdiff_attention_bwd(const EncdiffAttnArgs* a, void* stream) { return attn_dispatch(a, true, stream); }
+extern "C" int encdiff_attention_bwd(const EncdiffAttnArgs* a, void* stream) {
+  if (a && a->dtype == ENCDIFF_DT_F32) return ed_attention_bwd_f32(a, (hipStream_t)stream);
+  return attn_dispatch(a, true, stream);
+}

@@ -82,3 +82,6 @@ int ed_groupnorm_fwd_f32(const EncdiffGroupNormArgs* a, hipStream_t s);
 int ed_layernorm_fwd_f32(const EncdiffLayerNormArgs* a, hipStream_t s);
 int ed_attention_fwd_f32(const EncdiffAttnArgs* a, hipStream_t s);
 int ed_elementwise_f32(const EncdiffEwArgs* a, hipStream_t s);
+int ed_groupnorm_bwd_f32(const EncdiffGroupNormArgs* a, hipStream_t s);
+int ed_layernorm_bwd_f32(const EncdiffLayerNormArgs* a, hipStream_t s);
+int ed_attention_bwd_f32(const EncdiffAttnArgs* a, hipStream_t s);

@@ -203,6 +203,24 @@ ED_DEV v4s ds_read_tr16(const bf16_t* p) {
   return r;
 }
 
+// ds_read_b128 as inline asm, for tiles whose fragment waits are counted by hand (compute()):
+// a compiler-issued read would be waited for by the compiler, which does not count the asm reads.
+ED_DEV v8bf ds_read_b128(const bf16_t* p) {
+  typedef __attribute__((address_space(3))) const char lds_char;
+  const uint32_t a = (uint32_t)(uintptr_t)(lds_char*)p;
+  v4u32 r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(a));
+  return __builtin_bit_cast(v8bf, r);
+}
+
+// Fragment reads software-pipelined across k-substeps (compute()): measured in the step with both
+// builds on one box (round 4, tools/bench_ab.sh): 9.516-9.524 ms/step pipelined vs 9.503-9.522
+// without -- no gain (five resident workgroups per CU already hide the LDS latency) for 4-12 more
+// VGPRs, so it is off; -DED_FRAG_PIPE=1 builds it.
+#ifndef ED_FRAG_PIPE
+#define ED_FRAG_PIPE 0
+#endif
+
 // Wait until at most N of this thread's vector-memory loads are outstanding (LDS-DMA stages
 // still in flight behind the one about to be read).
 template <int N>
@@ -489,6 +507,9 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   auto frag_kinner = [&](const bf16_t* s, int row, int kk, int mask) -> v8bf {
     return *(const v8bf*)(s + row * BK + swz(row, kk * 4 + g4, mask) * 8);
   };
+  auto frag_kinner_asm = [&](const bf16_t* s, int row, int kk, int mask) -> v8bf {
+    return ds_read_b128(s + row * BK + swz(row, kk * 4 + g4, mask) * 8);
+  };
   auto frag_kouter = [&](auto tile, const bf16_t* s, int colbase, int kk) -> v8bf {
     // rows k = kk*32 + g4*8 + tq (+4): 4 bf16 at column colbase + 4*tp, swizzled chunk
     using T = decltype(tile);
@@ -535,8 +556,50 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       for (int r = rg * (BK / RG); r < (rg + 1) * (BK / RG); ++r)
         bsum += bf2f(sa[r * TA::LD + TA::sw(r, col >> 3) * 8 + (col & 7)]);
     }
+    constexpr int KK = BK / 32;
+    if constexpr (ED_FRAG_PIPE && (!AKI || !BKI) && !G::HALO && KK > 1) {
+      // Tiles with a transposed (k-outer) operand read every fragment by inline asm, so the
+      // waits are ours: the fragments of k-substep kk+1 are issued BEFORE the MFMAs of kk, which
+      // wait only for kk's reads (counted lgkmcnt: LDS returns in order) -- the LDS latency of
+      // the next substep hides behind this one's MFMAs instead of draining to zero each time.
+      constexpr int RA = AKI ? 1 : 2, RB = BKI ? 1 : 2;
+      constexpr int NR = TM * RA + TN * RB;          // LDS read instructions per substep
+      constexpr int NW = NR > 15 ? 15 : NR;           // lgkmcnt is 4 bits: over-wait when larger
+      v8bf af[2][TM], bfr[2][TN];
+      auto load = [&](int kk, v8bf* a, v8bf* b) {
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
+        for (int i = 0; i < TM; ++i) {
+          if constexpr (AKI) a[i] = frag_kinner_asm(sa, wr + 16 * i + l16, kk, TA::SWM);
+          else a[i] = frag_kouter(TA{}, sa, wr + 16 * i, kk);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (BKI) b[j] = frag_kinner_asm(sb, wc + 16 * j + l16, kk, TB::SWM);
+          else b[j] = frag_kouter(TB{}, sb, wc + 16 * j, kk);
+        }
+      };
+      load(0, af[0], bfr[0]);
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const int cur = kk & 1;
+        if (kk + 1 < KK) {
+          load(kk + 1, af[cur ^ 1], bfr[cur ^ 1]);
+          asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NW) : "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][i], bfr[cur][j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      return;
+    }
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
       v8bf af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {

@@ -812,7 +812,8 @@ extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream
 }
 
 extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream) {
-  if (a && a->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_UNSUPPORTED;  // fp32: forward only
+  if (a && a->dtype == ENCDIFF_DT_F32) return ed_groupnorm_bwd_f32(a, (hipStream_t)stream);
+  if (a && a->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_UNSUPPORTED;
   if (!a || !a->x || !a->dy || !a->dx || !a->stats || !a->dgamma_part || !a->dbeta_part) return ENCDIFF_ERR_ARG;
   if (a->film && !a->dfilm) return ENCDIFF_ERR_ARG;
   const int cs = gn_check(a);
@@ -871,6 +872,7 @@ extern "C" int encdiff_layernorm_fwd(const EncdiffLayerNormArgs* a, void* stream
   return ln_dispatch(a, false, stream);
 }
 extern "C" int encdiff_layernorm_bwd(const EncdiffLayerNormArgs* a, void* stream) {
-  if (a && a->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_UNSUPPORTED;  // fp32: forward only
+  if (a && a->dtype == ENCDIFF_DT_F32) return ed_layernorm_bwd_f32(a, (hipStream_t)stream);
+  if (a && a->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_UNSUPPORTED;
   return ln_dispatch(a, true, stream);
 }

@@ -84,6 +84,22 @@ class _UNetFn(torch.autograd.Function):
         return (ex.d_x.clone() if want else None), None, dc.clone(), None
 
 
+class _UNetF32Fn(torch.autograd.Function):
+    """eps = UNet(x_t, t, context) on the fp32 path (unet_f32.UNetF32): the forward saves its
+    activations, the backward returns d x_t and d context and adds every UNet weight gradient
+    to the arena (the parameters' .grad views)."""
+
+    @staticmethod
+    def forward(ctx, x, t, c, f32):
+        ctx.f32 = f32
+        return f32.forward(x, t, c, save=True)
+
+    @staticmethod
+    def backward(ctx, g):
+        dx, dc = ctx.f32.backward(g.float())
+        return dx, None, dc, None
+
+
 _SUPPORTED = dict(dims=2, num_classes=None, use_fp16=False, num_head_channels=-1, transformer_depth=1,
                   use_spatial_transformer=True, use_scale_shift_norm=True, resblock_updown=True, n_embed=None,
                   legacy=True)
@@ -196,14 +212,15 @@ class UNetModel(nn.Module):
         c = c.reshape(x.shape[0], -1).float()
         ex = self.executor()
         if getattr(self, "hip_precision", "bf16") == "fp32":
-            # the reference's precision (SURVEY §8(b) convention 5): fp32 activations end to end,
-            # forward only (parity checks, reference-precision sampling)
-            if torch.is_grad_enabled():
-                raise RuntimeError("hip_precision='fp32' is a forward-only path (use torch.no_grad())")
+            # the reference's precision (SURVEY §8(b) convention 5): fp32 activations end to end
+            # (parity checks, reference-precision sampling and gradients)
             if getattr(self, "_f32", None) is None or self._f32.ex is not ex:
                 from encdiff_amd.unet_f32 import UNetF32
                 self._f32 = UNetF32(ex)
-            return self._f32.forward(x, timesteps, c)
+            if not torch.is_grad_enabled():
+                return self._f32.forward(x, timesteps, c)
+            self._arena.attach_grads()
+            return _UNetF32Fn.apply(x.float(), timesteps.long(), c, self._f32)
         ex.infer = not torch.is_grad_enabled()  # inference-only fusions (no saved activations)
         if torch.is_grad_enabled():
             self._arena.attach_grads()

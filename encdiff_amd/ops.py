@@ -907,14 +907,75 @@ def _f32(t):
     return t
 
 
-def gemm_f32(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, conv: Optional[L.ConvGeom] = None, bias=None,
-             resid=None, accumulate=False, alpha=1.0):
-    args = L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=L.OPB_ROWK,
+def gemm_f32(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK,
+             conv: Optional[L.ConvGeom] = None, bias=None, resid=None, accumulate=False, alpha=1.0, conv_cout=0,
+             bias_grad=None):
+    args = L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=b_mode,
                       c_mode=L.OUT_F32_ACCUM if accumulate else L.OUT_F32, a=_p(_f32(a)), lda=lda, b=_p(_f32(b)),
                       ldb=ldb, c=_p(_f32(c)), ldc=ldc, conv=conv if conv is not None else L.ConvGeom(), alpha=alpha,
                       split_k=1, bias=_p(bias), resid=_p(resid), ld_resid=_ld(resid) if resid is not None else 0,
-                      dtype=L.DT_F32)
+                      conv_cout=conv_cout, bias_grad=_p(bias_grad), dtype=L.DT_F32)
     check(lib.encdiff_gemm(C.byref(args), _s()), "encdiff_gemm(fp32)")
+
+
+# ---- fp32 backward (the reference-precision gradient path, unet_f32.py)
+def linear_dgrad_f32(dy, w, dx, accumulate=False):
+    """dx[M][K] (+)= dy[M][N] w[N][K] (the input gradient of y = x w^T)."""
+    M, N = dy.shape
+    gemm_f32(M, w.shape[1], N, dy, _ld(dy), w, _ld(w), dx, _ld(dx), b_mode=L.OPB_ROWN, accumulate=accumulate)
+
+
+def linear_wgrad_f32(dy, x, dw, db=None):
+    """dw[N][K] += dy^T x, db[N] += column sums of dy (accumulated into arena gradients)."""
+    M, N = dy.shape
+    gemm_f32(N, x.shape[1], M, dy, _ld(dy), x, _ld(x), dw, _ld(dw), a_mode=L.OPA_ROWM, b_mode=L.OPB_ROWN,
+             accumulate=True, bias_grad=db)
+
+
+def conv3x3_dgrad_f32(dy, g: Geom, w, dx, accumulate=False):
+    """dx[pixels][cin] (+)= conv3x3^T(dy) at the conv resolution; w [cout][9*cin] tap-major."""
+    cout, cin = w.shape[0], w.shape[1] // 9
+    gemm_f32(g.pixels, cin, 9 * cout, dy, 0, w, _ld(w), dx, _ld(dx), a_mode=L.OPA_IM2COL,
+             b_mode=L.OPB_CONV_DGRAD, conv=L.ConvGeom(batch=g.batch, h=g.h, w=g.w, cin=cout, resample=0,
+                                                      ld_src=_ld(dy)), conv_cout=cout, accumulate=accumulate)
+
+
+def conv3x3_wgrad_f32(dy, x, g: Geom, cin, dw, db=None, resample=0):
+    """dw[cout][9*cin] += dy^T im2col(resample(x)) (channels-last taps), db += column sums of dy."""
+    cout = dy.shape[1]
+    gemm_f32(cout, 9 * cin, g.pixels, dy, _ld(dy), x, _ld(x), dw, _ld(dw), a_mode=L.OPA_ROWM, b_mode=L.OPB_IM2COL,
+             conv=L.ConvGeom(batch=g.batch, h=g.h, w=g.w, cin=cin, resample=resample, ld_src=_ld(x)),
+             accumulate=True, bias_grad=db)
+
+
+def groupnorm_bwd_f32(x, g: Geom, gamma, beta, stats, silu, dy, dx, dgamma_part, dbeta_part, ld_part, film=None,
+                      ld_film=0, dfilm=None, ld_dfilm=0, accumulate=False, resid=None, groups=32):
+    c = x.shape[1]
+    a = L.GroupNormArgs(batch=g.batch, hw=g.h * g.w, c=c, groups=groups, silu=int(silu), x=_p(_f32(x)), ldx=_ld(x),
+                        gamma=_p(gamma), beta=_p(beta), film=_p(film), ld_film=ld_film, stats=_p(stats),
+                        dy=_p(_f32(dy)), lddy=_ld(dy), dx=_p(_f32(dx)), lddx=_ld(dx), accumulate_dx=int(accumulate),
+                        dgamma_part=_p(dgamma_part), dbeta_part=_p(dbeta_part), ld_part=ld_part, dfilm=_p(dfilm),
+                        ld_dfilm=ld_dfilm, resid=_p(resid), ld_resid=_ld(resid) if resid is not None else 0,
+                        dtype=L.DT_F32)
+    check(lib.encdiff_groupnorm_bwd(C.byref(a), _s()), "encdiff_groupnorm_bwd(fp32)")
+
+
+def layernorm_bwd_f32(x, gamma, stats, dy, dx, dgamma_part, dbeta_part, parts, ld_part, accumulate=False,
+                      resid=None):
+    rows, c = x.shape
+    a = L.LayerNormArgs(rows=rows, c=c, x=_p(_f32(x)), ldx=_ld(x), gamma=_p(gamma), stats=_p(stats),
+                        dy=_p(_f32(dy)), lddy=_ld(dy), dx=_p(_f32(dx)), lddx=_ld(dx), accumulate_dx=int(accumulate),
+                        dgamma_part=_p(dgamma_part), dbeta_part=_p(dbeta_part), ld_part=ld_part, parts=parts,
+                        resid=_p(resid), ld_resid=_ld(resid) if resid is not None else 0, dtype=L.DT_F32)
+    check(lib.encdiff_layernorm_bwd(C.byref(a), _s()), "encdiff_layernorm_bwd(fp32)")
+
+
+def attention_bwd_f32(q, k, v, o, lse, d_o, dq, dk, dv, batch, heads, sq, sk, dh):
+    a = L.AttnArgs(batch=batch, heads=heads, sq=sq, sk=sk, dh=dh, scale=dh ** -0.5,
+                   q=_p(_f32(q)), ldq=_ld(q), k=_p(_f32(k)), ldk=_ld(k), v=_p(_f32(v)), ldv=_ld(v),
+                   o=_p(_f32(o)), ldo=_ld(o), lse=_p(lse), d_o=_p(_f32(d_o)), lddo=_ld(d_o), dq=_p(_f32(dq)),
+                   lddq=_ld(dq), dk=_p(_f32(dk)), lddk=_ld(dk), dv=_p(_f32(dv)), lddv=_ld(dv), dtype=L.DT_F32)
+    check(lib.encdiff_attention_bwd(C.byref(a), _s()), "encdiff_attention_bwd(fp32)")
 
 
 def linear_f32(x, w, y, bias=None, resid=None):
@@ -939,10 +1000,10 @@ def groupnorm_f32(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_fi
     check(lib.encdiff_groupnorm_fwd(C.byref(a), _s()), "encdiff_groupnorm_fwd(fp32)")
 
 
-def layernorm_f32(x, gamma, beta, y, eps=1e-5):
+def layernorm_f32(x, gamma, beta, y, eps=1e-5, stats=None):
     rows, c = x.shape
     a = L.LayerNormArgs(rows=rows, c=c, eps=eps, x=_p(_f32(x)), ldx=_ld(x), gamma=_p(gamma), beta=_p(beta),
-                        y=_p(_f32(y)), ldy=_ld(y), dtype=L.DT_F32)
+                        y=_p(_f32(y)), ldy=_ld(y), stats=_p(stats), dtype=L.DT_F32)
     check(lib.encdiff_layernorm_fwd(C.byref(a), _s()), "encdiff_layernorm_fwd(fp32)")
 
 

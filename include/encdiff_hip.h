@@ -24,12 +24,15 @@
  *  - dtype: the GEMM, GroupNorm, LayerNorm, attention and elementwise args carry a `dtype`
  *    field.  ENCDIFF_DT_BF16 (0, the default) is the product path above.  ENCDIFF_DT_F32
  *    runs the same entry point on fp32 activations (every bf16 operand / output named in
- *    the struct becomes fp32; forward only): the reference's precision (main_val.py:525),
- *    so a denoiser forward can be held to the fp32 tolerance.  Supported there: GEMM
- *    OPA_ROWK / OPA_IM2COL (resample NONE / UP2) x OPB_ROWK into OUT_F32 / OUT_F32_ACCUM
- *    (alpha, bias, fp32 resid; no split-K / epilogue statistics); GroupNorm without
- *    in_stats; LayerNorm; attention dh in {8, 16, 32, 64} (no fp8); elementwise COPY, SILU,
- *    GEGLU, ADD, RESAMPLE.  Other combinations return ENCDIFF_ERR_UNSUPPORTED.
+ *    the struct becomes fp32), forward AND backward: the reference's precision
+ *    (main_val.py:525), so the denoiser's output and gradients can be held to the fp32
+ *    tolerance.  Supported there: GEMM OPA_ROWK x OPB_ROWK / OPB_ROWN, OPA_IM2COL (resample
+ *    NONE / UP2) x OPB_ROWK / OPB_CONV_DGRAD, OPA_ROWM x OPB_ROWN / OPB_IM2COL (+ bias_grad)
+ *    into OUT_F32 / OUT_F32_ACCUM (alpha, bias, fp32 resid; no split-K / epilogue
+ *    statistics); GroupNorm fwd / bwd (FiLM, SiLU, resid, accumulate) without in_stats /
+ *    x_from; LayerNorm fwd / bwd (c <= 512, no dy_from); attention fwd / bwd dh in
+ *    {8, 16, 32, 64} (no fp8); elementwise COPY, SILU, SILU_BWD, GEGLU, GEGLU_BWD, ADD,
+ *    RESAMPLE, RESAMPLE_BWD.  Other combinations return ENCDIFF_ERR_UNSUPPORTED.
  */
 #ifndef ENCDIFF_HIP_H
 #define ENCDIFF_HIP_H
@@ -215,7 +218,7 @@ typedef struct EncdiffGroupNormArgs {
   const void* dy; long lddy;
   void* dx; long lddx;       /* bf16                                                */
   int accumulate_dx;         /* dx += result                                        */
-  int dtype;                 /* ENCDIFF_DT_F32: x, y fp32 (forward)                 */
+  int dtype;                 /* ENCDIFF_DT_F32: every activation / gradient fp32    */
   float* dgamma_part;        /* fp32 [batch][ld_part] per-image partial sums (reduced later) */
   float* dbeta_part;
   long ld_part;
@@ -255,7 +258,7 @@ typedef struct EncdiffLayerNormArgs {
   float* dbeta_part;
   long ld_part;
   int parts;                 /* number of partial rows (grid size of the backward) */
-  int dtype;                 /* ENCDIFF_DT_F32: x, y fp32 (forward)                 */
+  int dtype;                 /* ENCDIFF_DT_F32: every activation / gradient fp32    */
   const void* resid; long ld_resid; /* backward: optional bf16 residual-branch gradient:
                                         dx = resid + LN_bwd (out of place; may alias dx) */
   const EncdiffGemmArgs* dy_from;   /* backward, optional: dy is the output of this GEMM whose
@@ -289,7 +292,7 @@ typedef struct EncdiffAttnArgs {
   void* dv; long lddv;
   int fp8_qk;                /* 1: scores Q K^T on fp8 (OCP e4m3) MFMA, fwd and bwd recompute;
                                 softmax, P V and the gradient products stay bf16 / fp32 */
-  int dtype;                 /* ENCDIFF_DT_F32: q, k, v, o fp32 (forward)             */
+  int dtype;                 /* ENCDIFF_DT_F32: q, k, v, o, d_o, dq, dk, dv fp32      */
 } EncdiffAttnArgs;
 
 int encdiff_attention_fwd(const EncdiffAttnArgs* args, void* stream);

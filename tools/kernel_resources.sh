@@ -1,10 +1,10 @@
 #!/bin/bash
-# Print VGPR/SGPR/spill/LDS/scratch usage of every kernel in a .hip source (device-only compile).
-# usage: bash tools/kernel_resources.sh encdiff_amd/csrc/norm.hip [filter]
+# Print VGPR/SGPR/spill/LDS/scratch usage of every kernel in a .hip source (device-only compile,
+# the library's flags).  usage: bash tools/kernel_resources.sh encdiff_amd/csrc/norm.hip [filter] [extra flags...]
 set -e
-SRC=$1; FILT=${2:-.}
+SRC=$1; FILT=${2:-.}; shift 2 || true
 OUT=$(mktemp /tmp/kres.XXXXXX.co)
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=fast --cuda-device-only --no-gpu-bundle-output -c "$SRC" -o "$OUT"
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=fast -mllvm -amdgpu-mfma-vgpr-form=1 -Iinclude "$@" --cuda-device-only --no-gpu-bundle-output -c "$SRC" -o "$OUT"
 /opt/rocm/lib/llvm/bin/llvm-readelf --notes "$OUT" | awk '
   /\.name:/ {name=$2}
   /\.vgpr_count:/ {v=$2} /\.sgpr_count:/ {s=$2}
