@@ -231,13 +231,37 @@ def ddim_rate(ldm, B, S, eta=0.0):
     shape = (ldm.channels, ldm.image_size, ldm.image_size)
     x_T = torch.randn(B, *shape, device="cuda")
     with torch.no_grad():
-        sampler.sample(S, B, shape, cond, eta=eta, verbose=False, x_T=x_T)  # capture + warm-up
+        for _ in range(2):  # the first call replays the one-step graph, the second captures the loop
+            sampler.sample(S, B, shape, cond, eta=eta, verbose=False, x_T=x_T)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         sampler.sample(S, B, shape, cond, eta=eta, verbose=False, x_T=x_T)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
     return S / dt
+
+
+def log_images_time(ldm, N=8, S=200, eta=1.0):
+    """The reference's logging workload (ddpm_enc.py:1473-1596 defaults: N=8, ddim_steps=200,
+    ddim_eta=1.) with sample_swap (:1522-1535: every concept unit swapped, latent_unit x N rows)
+    as a COLD call -- wall time including the two DDIM graph captures (160-row swap batch and the
+    8-row sample batch), the EMA scopes and the VQ decodes -- then the same call warm."""
+    g = torch.Generator(device="cuda").manual_seed(7)
+    batch = {"image": torch.rand(N, 64 * ldm.image_size // 16, 64 * ldm.image_size // 16, 3, device="cuda",
+                                 generator=g) * 2 - 1}
+    out = {}
+    for k in ("cold_s", "warm_s"):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            log = ldm.log_images(batch, N=N, ddim_steps=S, ddim_eta=eta, sample_swap=True)
+        torch.cuda.synchronize()
+        out[k] = round(time.perf_counter() - t0, 4)
+    lu = ldm.model.diffusion_model.latent_unit
+    assert log["samples_swapping"].shape[0] == lu * N and log["samples"].shape[0] == N
+    out.update(N=N, S=S, eta=eta, sample_swap_rows=lu * N, ddim_steps_total=S * 2,
+               note="cold = first call incl. graph capture; DDIM steps of both loops (swap + samples)")
+    return out
 
 
 def cpu_baseline(warmup=3, steps=50, ddim_steps=50, probe_steps=4):
@@ -345,6 +369,8 @@ def main():
                                            "batch": args.ddim_batch, "S": args.ddim_steps, "eta": 0.0}
             extra["ddim_steps_per_sec_b128"] = {"value": ddim_rate(ldm, 128, args.ddim_steps, eta=1.0),
                                                 "batch": 128, "S": args.ddim_steps, "eta": 1.0}
+            if args.config == "shapes3d":
+                extra["ddim_log_images_s"] = log_images_time(ldm)
         if not args.skip_cpu and world == 1 and args.config == "shapes3d":  # CPU baseline: N=1, configs[1]
             extra["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -125,6 +125,16 @@ class StHeadArgs(C.Structure):
                 ("n1", vp), ("ld_n1", C.c_long), ("s1", vp), ("qkv", vp), ("ld_qkv", C.c_long)]
 
 
+class ZeroJob(C.Structure):
+    _fields_ = [("ptr", vp), ("rows", C.c_longlong), ("row_bytes", C.c_longlong), ("ld_bytes", C.c_longlong)]
+
+
+class StepPrologueArgs(C.Structure):
+    _fields_ = [("jobs", vp), ("njobs", C.c_int), ("batch", C.c_int), ("timesteps", C.c_int), ("pad_", C.c_int),
+                ("seed", C.c_ulonglong), ("rng_counter", vp), ("data_step", vp), ("t", vp), ("noise", vp),
+                ("n_noise", C.c_longlong), ("done", vp), ("pad2_", C.c_int)]
+
+
 class PackJob(C.Structure):
     _fields_ = [("src_off", C.c_longlong), ("dst_off", C.c_longlong), ("rows", C.c_int), ("cols", C.c_int),
                 ("kind", C.c_int), ("cin", C.c_int)]
@@ -176,6 +186,7 @@ _PROTOS = {
     "encdiff_nchw_to_rows_split3": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_long, vp],
     "encdiff_st_tail_fwd": [C.POINTER(StTailArgs), vp],
     "encdiff_st_head_fwd": [C.POINTER(StHeadArgs), vp],
+    "encdiff_step_prologue": [C.POINTER(StepPrologueArgs), vp],
     "encdiff_version": [],
 }
 

@@ -486,6 +486,68 @@ __global__ __launch_bounds__(256) void gather_u8_kernel(const uint8_t* __restric
 
 __global__ void counter_inc_kernel(long long* counter) { *counter += 1; }
 
+// ------------------------------------------------ step prologue (RNG + zeroing + counters)
+// Philox4x32-10 (Salmon et al., SC'11): 4 x 32-bit counter, 2 x 32-bit key, 10 rounds.
+ED_DEV uint4 philox10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t h0 = __umulhi(0xD2511F53u, c.x), l0 = 0xD2511F53u * c.x;
+    const uint32_t h1 = __umulhi(0xCD9E8D57u, c.z), l1 = 0xCD9E8D57u * c.z;
+    c = make_uint4(h1 ^ c.y ^ k0, l1, h0 ^ c.w ^ k1, l0);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+ED_DEV float u01(uint32_t x) { return ((float)x + 1.0f) * 2.3283064365386963e-10f; }  // (0, 1]
+
+__global__ __launch_bounds__(256) void step_prologue_kernel(const EncdiffStepPrologueArgs a) {
+  const long long ctr = *a.rng_counter;
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+  const uint32_t c_lo = (uint32_t)ctr, c_hi = (uint32_t)((unsigned long long)ctr >> 32);
+  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x, gs = (long long)gridDim.x * blockDim.x;
+  if (a.noise) {
+    for (long long q = gid; q * 4 < a.n_noise; q += gs) {
+      const uint4 r = philox10(make_uint4((uint32_t)q, c_lo, c_hi, 0u), k0, k1);
+      const float m0 = sqrtf(-2.f * logf(u01(r.x))), m1 = sqrtf(-2.f * logf(u01(r.z)));
+      float s0, c0, s1, c1;
+      sincospif(2.f * u01(r.y), &s0, &c0);
+      sincospif(2.f * u01(r.w), &s1, &c1);
+      const float v[4] = {m0 * c0, m0 * s0, m1 * c1, m1 * s1};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (q * 4 + j < a.n_noise) a.noise[q * 4 + j] = v[j];
+    }
+  }
+  if (a.t) {
+    for (long long b = gid; b < a.batch; b += gs) {
+      const uint4 r = philox10(make_uint4((uint32_t)b, c_lo, c_hi, 1u), k0, k1);
+      a.t[b] = (long long)(((unsigned long long)r.x * (unsigned)a.timesteps) >> 32);
+    }
+  }
+  for (int j = 0; j < a.njobs; ++j) {
+    const EncdiffZeroJob z = a.jobs[j];
+    const long long per = z.row_bytes >> 4, n = z.rows * per;
+    for (long long i = gid; i < n; i += gs) {
+      const long long r = i / per, cc = i - r * per;
+      *(uint4*)((char*)z.ptr + r * z.ld_bytes + cc * 16) = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  // the last workgroup advances the counters (every workgroup read *rng_counter before its ticket)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const int tk = atomicAdd(a.done, 1);
+    if (tk == (int)gridDim.x - 1) {
+      *a.rng_counter = ctr + 1;
+      if (a.data_step) *a.data_step += 1;
+      *a.done = 0;
+      __threadfence();
+    }
+  }
+}
+
+
 // ------------------------------------------------ optimizer
 __global__ __launch_bounds__(256) void adamw_ema_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
@@ -763,6 +825,16 @@ extern "C" int encdiff_gather_images_u8(const void* pool, long long n_images, in
     hipLaunchKernelGGL(counter_inc_kernel, dim3(1), dim3(1), 0, s, step);
     ED_CHECK_LAUNCH();
   }
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_step_prologue(const EncdiffStepPrologueArgs* a, void* stream) {
+  if (!a || !a->rng_counter || !a->done || a->njobs < 0 || (a->njobs && !a->jobs)) return ENCDIFF_ERR_ARG;
+  if (a->t && (a->batch <= 0 || a->timesteps <= 0)) return ENCDIFF_ERR_ARG;
+  if (a->noise && a->n_noise <= 0) return ENCDIFF_ERR_ARG;
+  // workgroups: the zeroing (a 155 MB gradient arena) dominates -- 2048 x 256 threads x 16 B
+  hipLaunchKernelGGL(step_prologue_kernel, dim3(a->njobs ? 2048 : 64), dim3(256), 0, (hipStream_t)stream, *a);
+  ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
 

@@ -666,6 +666,11 @@ def attention_bwd(q, k, v, o, lse, d_o, dq, dk, dv, batch, heads, sq, sk, dh, fp
 
 
 ST_TAIL_STATS_ADD = os.environ.get("ENCDIFF_ST_TAIL_STATS_ADD", "1") != "0"
+# producer-statistics slots the tails add into: seen (ADD_REGIONS, ptr -> view) and those a training
+# step's prologue zeroes (PREZEROED) while PROLOGUE_STEP is set (trainer.HipTrainer)
+ADD_REGIONS: dict = {}
+PREZEROED: set = set()
+PROLOGUE_STEP = False
 
 
 def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps, save=None,
@@ -693,8 +698,13 @@ def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps
     if gn_stats is not None:  # the next GroupNorm's producer statistics of out
         a.gn_stats, a.ld_gn_stats = _p(gn_stats), _ld(gn_stats)
         if c == 128 and rows // 64 < 256 and ST_TAIL_STATS_ADD:
-            # two 32-row tiles per 64-row segment add into the zeroed slots (twice the workgroups)
-            gn_stats[:, :c].zero_()  # only this tensor's columns (the view may span a concat's other producer)
+            # two 32-row tiles per 64-row segment add into the zeroed slots (twice the workgroups);
+            # only this tensor's columns (the view may span a concat's other producer).  Inside a
+            # training step whose prologue zeroes the registered slots (StepPrologue) no fill runs.
+            view = gn_stats[:, :c]
+            if not (PROLOGUE_STEP and view.data_ptr() in PREZEROED):
+                view.zero_()
+                ADD_REGIONS[view.data_ptr()] = view
             a.gn_stats_add = 1
     rc = lib.encdiff_st_tail_fwd(C.byref(a), _s())
     if rc in (-2, -3):
@@ -860,6 +870,54 @@ def grad_fold(dw, co, cin, cpad, taps, gw, db=None, gb=None):
 def reduce_partials(part, ld, rows, cols, col_index, grad):
     check(lib.encdiff_reduce_partials(_p(part), ld, rows, cols, _p(col_index), _p(grad), _s()),
           "encdiff_reduce_partials")
+
+
+class StepPrologue:
+    """ONE launch in front of a training step (encdiff_step_prologue): zero the registered byte
+    regions (the gradient arena, producer-statistics slots that the step's kernels add into),
+    draw t ~ U{0..T-1} and noise ~ N(0, 1) with Philox4x32-10 from a device counter, advance that
+    counter and (optionally) the image pool's epoch step.  Replaces torch.randint / randn_like
+    (ddpm_enc.py:1041, :1184), the arena grad.zero_() and the pool's counter increment.  The job
+    table lives in device memory; call `set_jobs` whenever the regions change (not during capture)."""
+
+    def __init__(self, dev, seed: int):
+        self.dev = torch.device(dev)
+        self.seed = int(seed) & ((1 << 64) - 1)
+        self.counter = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.done = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.jobs_dev = None
+        self.njobs = 0
+        self._keep = []
+
+    def set_jobs(self, regions):
+        """regions: 2-D (or 1-D) tensor views to zero; row bytes and strides multiples of 16 B."""
+        jobs = []
+        self._keep = list(regions)
+        for r in regions:
+            r2 = r.view(1, -1) if r.dim() == 1 else r
+            assert r2.dim() == 2 and r2.stride(1) == 1, "zero job: 2-D rows with unit column stride"
+            es = r2.element_size()
+            rb, ld = r2.shape[1] * es, r2.stride(0) * es
+            assert rb % 16 == 0 and ld % 16 == 0 and r2.data_ptr() % 16 == 0, "zero job: 16-byte multiples"
+            jobs.append(L.ZeroJob(ptr=r2.data_ptr(), rows=r2.shape[0], row_bytes=rb, ld_bytes=ld))
+        n = len(jobs)
+        raw = bytearray(C.sizeof(L.ZeroJob) * max(n, 1))
+        for i, j in enumerate(jobs):
+            C.memmove((C.c_char * C.sizeof(L.ZeroJob)).from_buffer(raw, i * C.sizeof(L.ZeroJob)), C.byref(j),
+                       C.sizeof(L.ZeroJob))
+        self.jobs_dev = torch.frombuffer(raw, dtype=torch.uint8).to(self.dev)
+        self.njobs = n
+
+    def __call__(self, t=None, noise=None, timesteps=1000, data_step=None):
+        a = L.StepPrologueArgs(jobs=_p(self.jobs_dev), njobs=self.njobs, batch=t.numel() if t is not None else 0,
+                               timesteps=timesteps, seed=self.seed, rng_counter=_p(self.counter),
+                               data_step=_p(data_step), t=_p(t), noise=_p(noise),
+                               n_noise=noise.numel() if noise is not None else 0, done=_p(self.done))
+        if t is not None:
+            assert t.dtype == torch.int64 and t.is_contiguous()
+        if noise is not None:
+            assert noise.dtype == F32 and noise.is_contiguous()
+        check(lib.encdiff_step_prologue(C.byref(a), _s()), "encdiff_step_prologue")
 
 
 def gather_images_u8(pool_u8, perm, step, batch, out, advance=True):

@@ -89,6 +89,23 @@ class HipTrainer:
         self._g_opt = None
         self._c = self._dc = None
         torch.manual_seed(rank_seed(seed, self.rank))
+        from . import ops
+        self._t = torch.empty(batch_size, dtype=torch.long, device=self.dev)
+        self._noise = torch.empty(z_shape, device=self.dev)
+        self._pro = ops.StepPrologue(self.dev, seed=rank_seed(seed, self.rank))
+        self._pro.set_jobs([self.arena.grad])
+        self._pro_final = False  # statistics slots registered after the first step
+
+    def _prologue_regions(self):
+        """After the first step: the prologue also zeroes every producer-statistics slot the
+        step's kernels added into (seen by ops.st_tail_fwd), so no fill runs inside the step."""
+        from . import ops
+        if self._pro_final:
+            return
+        regions = list(ops.ADD_REGIONS.values())
+        self._pro.set_jobs([self.arena.grad] + regions)
+        ops.PREZEROED.update(r.data_ptr() for r in regions)
+        self._pro_final = True
 
     # ---------------------------------------------------------------- test hook
     def enable_feed(self):
@@ -119,16 +136,21 @@ class HipTrainer:
         gradient buckets can be all-reduced meanwhile.  Objectives outside the EncDiff one (eps,
         L1, fixed logvar, no ELBO term) take the reference-API p_losses + loss.backward() path."""
         ldm = self.ldm
-        self.arena.grad.zero_()
-        self._draw_batch()
+        from . import ops
+        # the batch gather reads the pool's epoch step; the prologue (ONE launch) then zeroes the
+        # gradient arena and the statistics slots the step adds into, draws t and the noise
+        # (Philox) and advances the epoch step and its own counter
+        self._draw_batch(advance=False)
+        if self._feed is not None:
+            t, noise = self._feed["t"], self._feed["noise"]
+            self._pro(timesteps=ldm.num_timesteps, data_step=self.data.step)
+        else:
+            t, noise = self._t, self._noise
+            self._pro(t, noise, timesteps=ldm.num_timesteps, data_step=self.data.step)
+        ops.PROLOGUE_STEP = self._pro_final
         with torch.no_grad():
             z = ldm.encode_first_stage(self.img)  # frozen VQ (HIP); scale_factor applied in q_sample
         c = ldm.get_learned_conditioning(self.img)
-        if self._feed is not None:
-            t, noise = self._feed["t"], self._feed["noise"]
-        else:
-            t = torch.randint(0, ldm.num_timesteps, (self.B,), device=self.dev)
-            noise = torch.randn_like(z)
         if not self._direct:
             return self._fwd_bwd_api(z, c, t, noise)
         ex = self.unet.executor()
@@ -272,34 +294,44 @@ class HipTrainer:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         self._g_fb = torch.cuda.CUDAGraph()
+        from . import ops
+        self._prologue_regions()
         with torch.cuda.stream(s):
-            with torch.cuda.graph(self._g_fb, stream=s):
-                self._fwd_bwd()
-                if self.world == 1:
-                    self.opt.launch()
-            if self.world > 1:
-                pool = self._g_fb.pool()
-                if self._split_lo is not None:
-                    self._g_rest = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(self._g_rest, stream=s, pool=pool):
-                        self._unet_rest()
-                self._g_cond = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self._g_cond, stream=s, pool=pool):
-                    self._cond_bwd()
-                self._g_opt = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self._g_opt, stream=s, pool=pool):
-                    self.opt.launch()
+            try:
+                with torch.cuda.graph(self._g_fb, stream=s):
+                    self._fwd_bwd()
+                    if self.world == 1:
+                        self.opt.launch()
+                if self.world > 1:
+                    pool = self._g_fb.pool()
+                    if self._split_lo is not None:
+                        self._g_rest = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(self._g_rest, stream=s, pool=pool):
+                            self._unet_rest()
+                    self._g_cond = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self._g_cond, stream=s, pool=pool):
+                        self._cond_bwd()
+                    self._g_opt = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self._g_opt, stream=s, pool=pool):
+                        self.opt.launch()
+            finally:
+                ops.PROLOGUE_STEP = False
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
 
     # ---------------------------------------------------------------- steps
     def step_eager(self):
+        from . import ops
         self.opt.stage_hyper()
-        self._fwd_bwd()
-        if self.world > 1:
-            self._exchange(self._cond_bwd, self._unet_rest if self._split_lo is not None else None)
+        try:
+            self._fwd_bwd()
+            if self.world > 1:
+                self._exchange(self._cond_bwd, self._unet_rest if self._split_lo is not None else None)
+        finally:
+            ops.PROLOGUE_STEP = False
         self.opt.launch()
         self._post()
+        self._prologue_regions()
 
     def step(self):
         if self._g_fb is None:

@@ -599,6 +599,41 @@ typedef struct EncdiffStHeadArgs {
 
 int encdiff_st_head_fwd(const EncdiffStHeadArgs* args, void* stream);
 
+/* ---------------------------------------------------------------- step prologue
+ * The per-step device work in front of the training step, as ONE launch:
+ *   - zero jobs: 2-D byte regions set to 0 (the gradient arena, producer-statistics slots that
+ *     the step's kernels add into); ptr and row_bytes / ld_bytes multiples of 16;
+ *   - t[b] ~ U{0 .. timesteps-1} (LatentDiffusion.forward, ddpm_enc.py:1041) and noise[i] ~ N(0, 1)
+ *     (p_losses, ddpm_enc.py:1184 torch.randn_like(x_start)), Philox4x32-10 keyed by `seed`
+ *     with the device counter *rng_counter (stream offsets: noise element i uses block i / 4 of
+ *     stream 0, t[b] block b of stream 1), then Box-Muller on uniforms in (0, 1];
+ *   - *rng_counter += 1 and, when given, *data_step += 1 (the image pool's epoch step read by
+ *     encdiff_gather_images_u8 earlier in the step) by the last workgroup to finish (ticket
+ *     `done`, zero on entry, left zero), so a captured step advances both by itself.
+ * t or noise may be NULL (a test feeding its own). */
+typedef struct EncdiffZeroJob {
+  void* ptr;
+  long long rows, row_bytes, ld_bytes;
+} EncdiffZeroJob;
+
+typedef struct EncdiffStepPrologueArgs {
+  const EncdiffZeroJob* jobs;  /* device array */
+  int njobs;
+  int batch;
+  int timesteps;
+  int pad_;
+  unsigned long long seed;
+  long long* rng_counter;      /* device */
+  long long* data_step;        /* device, optional */
+  long long* t;                /* device int64 [batch], optional */
+  float* noise;                /* device fp32 [n_noise], optional */
+  long long n_noise;
+  int* done;                   /* device ticket */
+  int pad2_;
+} EncdiffStepPrologueArgs;
+
+int encdiff_step_prologue(const EncdiffStepPrologueArgs* args, void* stream);
+
 /* Library/device information (for tests): returns the number of exported kernels. */
 int encdiff_version(void);
 

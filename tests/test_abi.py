@@ -32,7 +32,8 @@ STRUCTS = {
     "EncdiffConvGeom": "ConvGeom", "EncdiffGemmArgs": "GemmArgs", "EncdiffGroupNormArgs": "GroupNormArgs",
     "EncdiffLayerNormArgs": "LayerNormArgs", "EncdiffAttnArgs": "AttnArgs", "EncdiffEwArgs": "EwArgs",
     "EncdiffSmallConvArgs": "SmallConvArgs", "EncdiffPackJob": "PackJob", "EncdiffBatchNormArgs": "BatchNormArgs",
-    "EncdiffStTailArgs": "StTailArgs", "EncdiffStHeadArgs": "StHeadArgs",
+    "EncdiffStTailArgs": "StTailArgs", "EncdiffStHeadArgs": "StHeadArgs", "EncdiffZeroJob": "ZeroJob",
+    "EncdiffStepPrologueArgs": "StepPrologueArgs",
 }
 
 

@@ -124,11 +124,13 @@ def test_ddim_matches_reference(ldm, golden_dir, graph, eta):
     assert len(inter["x_inter"]) >= 2
 
 
-def test_ddim_sampler_reuse(ldm, golden_dir):
+def test_ddim_sampler_reuse(ldm, golden_dir, monkeypatch):
     """One sampler, several sample() calls (the captured loop must not keep reading a
     previous call's schedule tables): eta 0 -> 1 -> 0 and a new x_T / conditioning, each equal to a
     fresh eager run; a second call with the same inputs is bitwise identical."""
+    from encdiff_amd.ldm.models.diffusion import ddim as D
     from encdiff_amd.ldm.models.diffusion.ddim import DDIMSampler
+    monkeypatch.setattr(D, "LOOP_GRAPH_AFTER", 0)  # every call on the whole-loop graph
     fx = np.load(os.path.join(golden_dir, "ddim.npz"))
     cond = torch.tensor(fx["cond"]).cuda()
     xT = torch.tensor(fx["xT"]).cuda()
@@ -346,13 +348,16 @@ def test_log_images_swap_matches_oracle(ldm):
                              plot_diffusion_rows=False)
     assert log["samples_swapping"].shape == (20 * N, 3, 64, 64)
     assert torch.isfinite(log["samples_swapping"]).all() and torch.isfinite(log["samples"]).all()
-    # the second log_images call reuses the model's sampler and its captured loop graphs
+    # later log_images calls reuse the model's sampler: the second captures the whole-loop graphs
+    # (D.LOOP_GRAPH_AFTER), every call after it replays them without capturing anything
     sampler = ldm.ddim_sampler()
-    n_graphs = len(sampler._graphs)
     with torch.no_grad():
-        ldm.log_images({"image": img.permute(0, 2, 3, 1)}, N=N, ddim_steps=S, ddim_eta=0.0, sample_swap=True,
-                       plot_diffusion_rows=False)
+        for _ in range(2):
+            n_graphs = len(sampler._graphs)
+            ldm.log_images({"image": img.permute(0, 2, 3, 1)}, N=N, ddim_steps=S, ddim_eta=0.0, sample_swap=True,
+                           plot_diffusion_rows=False)
     assert ldm.ddim_sampler() is sampler and len(sampler._graphs) == n_graphs
+    assert any(k[0] == "loop" for k in sampler._graphs) and any(k[0] == "step" for k in sampler._graphs)
 
 
 @pytest.mark.parametrize("path", ["loop", "step"])
@@ -366,6 +371,8 @@ def test_ddim_s200_matches_reference(ldm, golden_dir, eta, path, monkeypatch):
     fx = np.load(os.path.join(golden_dir, "ddim_s200.npz"))
     if path == "step":
         monkeypatch.setattr(D, "GRAPH_MAX_STEPS", 64)
+    else:
+        monkeypatch.setattr(D, "LOOP_GRAPH_AFTER", 0)  # the first call captures the whole loop
     cond = torch.tensor(fx["cond"]).cuda()
     s = D.DDIMSampler(ldm, use_graph=True)
     with torch.no_grad():
@@ -415,11 +422,13 @@ def test_ddim_b128_matches_oracle(ldm):
     ldm.train()
 
 
-def test_captured_graphs_follow_ema_scope(ldm):
+def test_captured_graphs_follow_ema_scope(ldm, monkeypatch):
     """a DDIM loop graph captured OUTSIDE ema_scope() must sample with the EMA
     weights when replayed INSIDE it (the replay refreshes stale bf16 packs), and the training
     graph replayed after the scope must run on the restored training weights."""
+    from encdiff_amd.ldm.models.diffusion import ddim as D
     from encdiff_amd.ldm.models.diffusion.ddim import DDIMSampler
+    monkeypatch.setattr(D, "LOOP_GRAPH_AFTER", 0)  # the loop graph is captured by the first call
     ldm.setup_hip_training()
     x = torch.randn(2, 3, 16, 16, device="cuda")
     c = torch.randn(2, 320, device="cuda") * 0.5

@@ -784,6 +784,54 @@ def test_gather_images_u8(O):
     assert int(pool.step) == pool.steps_per_epoch + 2
 
 
+def test_step_prologue(O):
+    """encdiff_step_prologue (one launch in front of a training step): zero jobs clear exactly their
+    regions (strided 2-D views included), t ~ U{0..T-1} and noise ~ N(0, 1) (ddpm_enc.py:1041,
+    :1184) with the right moments, the Philox stream is a function of (seed, counter) only
+    (same counter -> same draw; counter and data step advance by one per launch, also under graph
+    replay), and the ticket is left at zero."""
+    from encdiff_amd import ops as P
+    pro = P.StepPrologue(dev, seed=1234)
+    big = torch.randn(3, 1000, device=dev)
+    side = torch.randn(16, 192, device=dev)
+    keep = side.clone()
+    pro.set_jobs([big, side[:, 64:128]])
+    t = torch.empty(4096, dtype=torch.long, device=dev)
+    noise = torch.empty(128, 3, 16, 16, device=dev)
+    step = torch.zeros(1, dtype=torch.long, device=dev)
+    pro(t, noise, timesteps=1000, data_step=step)
+    torch.cuda.synchronize()
+    assert int(big.abs().sum()) == 0
+    assert side[:, 64:128].abs().sum().item() == 0
+    assert torch.equal(side[:, :64], keep[:, :64]) and torch.equal(side[:, 128:], keep[:, 128:])
+    assert int(t.min()) >= 0 and int(t.max()) <= 999 and len(torch.unique(t)) > 900
+    assert abs(t.float().mean().item() - 499.5) < 15
+    n = noise.flatten().double()
+    assert abs(n.mean().item()) < 0.02 and abs(n.std().item() - 1) < 0.02
+    assert abs(((n.abs() < 1).double().mean()).item() - 0.6827) < 0.01
+    assert int(pro.counter) == 1 and int(step) == 1 and int(pro.done) == 0
+    t1, n1 = t.clone(), noise.clone()
+    pro(t, noise, timesteps=1000, data_step=step)
+    assert not torch.equal(t, t1) and not torch.equal(noise, n1)
+    pro.counter.fill_(0)
+    pro(t, noise, timesteps=1000)
+    assert torch.equal(t, t1) and torch.equal(noise, n1)
+    # graph replay advances the counter by itself
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            pro(t, noise, timesteps=1000, data_step=step)
+    torch.cuda.current_stream().wait_stream(s)
+    c0, s0 = int(pro.counter), int(step)
+    g.replay()
+    a = noise.clone()
+    g.replay()
+    torch.cuda.synchronize()
+    assert int(pro.counter) == c0 + 2 and int(step) == s0 + 2 and not torch.equal(a, noise)
+
+
 @pytest.mark.parametrize("B", [128, 50])
 def test_encoder_warp(O, B):
     """Encoder4.warp on HIP (fp32) vs the as-is torch modules (fp32) on the same params:
