@@ -243,14 +243,15 @@ def ddim_rate(ldm, B, S, eta=0.0):
 
 def log_images_time(ldm, N=8, S=200, eta=1.0):
     """The reference's logging workload (ddpm_enc.py:1473-1596 defaults: N=8, ddim_steps=200,
-    ddim_eta=1.) with sample_swap (:1522-1535: every concept unit swapped, latent_unit x N rows)
-    as a COLD call -- wall time including the two DDIM graph captures (160-row swap batch and the
-    8-row sample batch), the EMA scopes and the VQ decodes -- then the same call warm."""
+    ddim_eta=1.) with sample_swap (:1522-1535: every concept unit swapped, latent_unit x N rows):
+    wall time of the COLD first call (one-step DDIM graphs captured and replayed for the 160-row
+    swap batch and the 8-row sample batch, EMA scopes, VQ decodes), of the second call (captures
+    the whole-loop graphs, ddim.LOOP_GRAPH_AFTER) and of a warm third call."""
     g = torch.Generator(device="cuda").manual_seed(7)
     batch = {"image": torch.rand(N, 64 * ldm.image_size // 16, 64 * ldm.image_size // 16, 3, device="cuda",
                                  generator=g) * 2 - 1}
     out = {}
-    for k in ("cold_s", "warm_s"):
+    for k in ("cold_s", "second_s", "warm_s"):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         with torch.no_grad():
@@ -260,7 +261,8 @@ def log_images_time(ldm, N=8, S=200, eta=1.0):
     lu = ldm.model.diffusion_model.latent_unit
     assert log["samples_swapping"].shape[0] == lu * N and log["samples"].shape[0] == N
     out.update(N=N, S=S, eta=eta, sample_swap_rows=lu * N, ddim_steps_total=S * 2,
-               note="cold = first call incl. graph capture; DDIM steps of both loops (swap + samples)")
+               note="cold = first call (one-step graphs); second = whole-loop graph capture; warm = replay; "
+                    "DDIM steps of both loops (swap + samples)")
     return out
 
 

@@ -43,7 +43,9 @@ class GemmArgs(C.Structure):
                 ("tile", C.c_int), ("dtype", C.c_int), ("workspace", vp),
                 ("aux", vp), ("ld_aux", C.c_long), ("gn_stats", vp), ("ld_gn_stats", C.c_long),
                 ("ln_gamma", vp), ("ln_beta", vp), ("ln_y", vp), ("ld_ln_y", C.c_long), ("ln_stats", vp),
-                ("ln_eps", C.c_float), ("pad3_", C.c_int), ("split_counters", vp)]
+                ("ln_eps", C.c_float), ("pad3_", C.c_int), ("split_counters", vp),
+                ("agn_gamma", vp), ("agn_beta", vp), ("agn_film", vp), ("ld_agn_film", C.c_long),
+                ("agn_eps", C.c_float), ("agn_silu", C.c_int)]
 
 
 class GroupNormArgs(C.Structure):

@@ -180,12 +180,33 @@ ED_DEV float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 __host__ __device__ constexpr int fwd_tiles_per_task(int dh) { return dh == 8 ? 4 : 2; }
 
+template <bool B>
+struct BoundTag {
+  static constexpr bool value = B;
+};
+// Bound path of the forward: the log2-domain softmax offset of a query row is the Cauchy-Schwarz
+// bound scale * log2e * |q| * max_k |k| (>= every score of the row), used only while it is <= this:
+// the row's largest p is then >= 2^-2*FWD_BOUND_MAX (a normal fp32 / bf16 value), so the shifted
+// exponentials are exact up to rounding and no running max, rescale or alpha exp is needed
+constexpr float FWD_BOUND_MAX = 40.f;
+ED_DEV float bf16_sq4(s4 v) {
+  float a = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float f = __uint_as_float((unsigned)(unsigned short)v[i] << 16);
+    a = __builtin_fmaf(f, f, a);
+  }
+  return a;
+}
+
 // Forward.  A wave task is a PAIR (dh 8: four) of 16-query tiles of one head: the K and V^T fragments
 // read from LDS serve both, and the two online-softmax chains are independent.  Keys are
 // consumed 32 at a time (two MFMA tiles) per softmax update; the running max is kept in the
 // log2 domain (scale * log2 e) and p = exp2(s * scale * log2e - m) is one FMA + a raw
 // v_exp_f32 (arguments <= 0, underflow to 0 is the correct limit).  MASK: key count not a
-// multiple of 32 (keys past SK get -inf).
+// multiple of 32 (keys past SK get -inf).  With every key of the head resident, a task whose
+// rows have a small score bound (FWD_BOUND_MAX) uses that bound as a fixed offset instead of the
+// running max (no max tree, no rescale of the accumulators): the same softmax up to rounding.
 template <int DH, bool MASK, bool F8, int SC = 0>
 __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, int hpb, int kch) {
   constexpr int DP = DH < 16 ? 16 : DH;
@@ -203,6 +224,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
   const int KR = kch < SKP ? kch : SKP;  // key rows resident in LDS at a time
   bf16_t* Ks = sm;                        // [hpb][KR][DP]
   bf16_t* Vs = sm + hpb * KR * DP;        // [hpb][KR][DP], read transposed (ds_read_b64_tr_b16)
+  float* kn = (float*)(sm + 2 * hpb * KR * DP);  // [hpb] max_k |k|^2 (resident K only)
   constexpr int NT = fwd_tiles_per_task(DH);  // 16-query tiles per wave task (independent chains)
   const int qtiles = (SQ + 15) >> 4, npairs = (qtiles + NT - 1) / NT;
   const float sl2 = p.scale * LOG2E;
@@ -242,8 +264,33 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
       for (int dt = 0; dt < KC; ++dt) o[u][dt] = (v4f){0.f, 0.f, 0.f, 0.f};
     }
   };
+  // bound path for the task's tiles (wave-uniform): m[u] = the rows' score bounds
+  auto pick_bound = [&]() -> bool {
+    if constexpr (F8 || DH > 32) {  // (dh 64 / 128: the second consume variant costs ~70 VGPRs)
+      return false;
+    } else {
+      const float k2 = kn[hl];
+      float mb[NT];
+      bool ok = true;
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        float n2 = 0.f;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) n2 += bf16_sq4(qf[u][kc]);
+        n2 = sum_x32(sum_x16(n2));
+        // small relative + absolute slack over the fp32 rounding of the MFMA dot products
+        mb[u] = __builtin_sqrtf(n2 * k2) * sl2 * 1.001f + 1e-6f;
+        ok = ok && mb[u] <= FWD_BOUND_MAX;
+      }
+      if (!__all(ok)) return false;
+#pragma unroll
+      for (int u = 0; u < NT; ++u) m[u] = mb[u];
+      return true;
+    }
+  };
   // keys [kbase, kbase + klen) of the task's head, staged at local rows 0 .. klen-1
-  auto consume = [&](int kbase, int klen) {
+  auto consume = [&](auto bnd, int kbase, int klen) {
+    constexpr bool BOUND = decltype(bnd)::value;
     const bf16_t* kb = Ks + hl * KR * DP;
     const bf16_t* vb = Vs + hl * KR * DP;
 #pragma unroll 2
@@ -278,24 +325,36 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
           for (int i = 0; i < 4; ++i)
             sv[4 * t + i] = (!MASK || kbase + k0 + t * 16 + 4 * g + i < SK) ? sc[i] : -INFINITY;
         }
-        // max over raw scores (the scale is positive), the log2-domain max = that * sl2
-        float tmax = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
-                           fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])));
-        tmax = max_x32(max_x16(tmax));
-        const float mn = fmaxf(m[u], tmax * sl2);
-        const float alpha = ex2(m[u] - mn);
-        m[u] = mn;
+        float mn = m[u], alpha = 1.f;
+        if constexpr (!BOUND) {
+          // max over raw scores (the scale is positive), the log2-domain max = that * sl2
+          float tmax = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), fmaxf(sv[2], sv[3])),
+                             fmaxf(fmaxf(sv[4], sv[5]), fmaxf(sv[6], sv[7])));
+          tmax = max_x32(max_x16(tmax));
+          mn = fmaxf(m[u], tmax * sl2);
+          alpha = ex2(m[u] - mn);
+          m[u] = mn;
+        }
         float pv[8];
+        {  // the exp arguments as packed pairs (v_pk_fma_f32: half the issue slots of 8 v_fma_f32)
+          const v2f s2 = {sl2, sl2}, nm = {-mn, -mn};
 #pragma unroll
-        for (int i = 0; i < 8; ++i) pv[i] = ex2(__builtin_fmaf(sv[i], sl2, -mn));
+          for (int i = 0; i < 8; i += 2) {
+            const v2f a = __builtin_elementwise_fma((v2f){sv[i], sv[i + 1]}, s2, nm);
+            pv[i] = ex2(a[0]);
+            pv[i + 1] = ex2(a[1]);
+          }
+        }
         if constexpr (!ONES) {
           float ls = 0.f;
 #pragma unroll
           for (int i = 0; i < 8; ++i) ls += pv[i];
-          l[u] = l[u] * alpha + ls;
+          l[u] = BOUND ? l[u] + ls : l[u] * alpha + ls;
         }
+        if constexpr (!BOUND) {
 #pragma unroll
-        for (int dt = 0; dt < KC; ++dt) o[u][dt] *= alpha;
+          for (int dt = 0; dt < KC; ++dt) o[u][dt] *= alpha;
+        }
         pf[u][0] = pack4(pv[0], pv[1], pv[2], pv[3]);
         pf[u][1] = pack4(pv[4], pv[5], pv[6], pv[7]);
       }
@@ -340,12 +399,29 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
   if (KR == SKP) {  // every head's K / V resident: waves loop over their tasks
     // the first task's Q loads are issued with the K / V staging loads (one round trip)
     if (wave < hpb * npairs) init(wave);
+    if (tid < hpb) kn[tid] = 0.f;
     stage_kv_u<DH, DP, 2, ONES>((const bf16_t*)p.k, p.ldk, (const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, Ks, Vs,
                                 SKP * DP, 0);
     __syncthreads();
+    if constexpr (!F8 && DH <= 32) {  // max_k |k|^2 per head (LDS max over non-negative floats as ints)
+      for (int r = tid; r < hpb * SKP; r += 256) {
+        const int hr = r / SKP;
+        const bf16_t* kr = Ks + hr * SKP * DP + (r - hr * SKP) * DP;
+        float n2 = 0.f;
+#pragma unroll
+        for (int c = 0; c < DH; c += 4) n2 += bf16_sq4(*(const s4*)(kr + c));
+        atomicMax((int*)&kn[hr], __float_as_int(n2));
+      }
+      __syncthreads();
+    }
     for (int task = wave; task < hpb * npairs; task += 4) {
       if (task != wave) init(task);
-      consume(0, SKP);
+      if constexpr (F8 || DH > 32) {
+        consume(BoundTag<false>{}, 0, SKP);
+      } else {
+        if (pick_bound()) consume(BoundTag<true>{}, 0, SKP);
+        else consume(BoundTag<false>{}, 0, SKP);
+      }
       finish();
     }
     return;
@@ -362,7 +438,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
     stage_heads<DH, DP>((const bf16_t*)p.k, p.ldk, SK, klen, H, bh0, 1, Ks, KR * DP, c0);
     stage_heads<DH, DP, ONES>((const bf16_t*)p.v, p.ldv, SK, klen, H, bh0, 1, Vs, KR * DP, c0);
     __syncthreads();
-    if (active) consume(c0, klen);
+    if (active) consume(BoundTag<false>{}, c0, klen);
   }
   if (active) finish();
 }
@@ -477,6 +553,12 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
     const s4 v = ld4(t + row * RP + kc * 16 + 4 * (DH < 16 ? (g & 1) : g));
     return (DH < 16 && g >= 2) ? (s4){0, 0, 0, 0} : v;
   };
+  // the same fragment WITHOUT zeroing the k = 8..15 half (dh = 8: lanes g >= 2 hold a duplicate of
+  // the row's k = 0..7, finite values): for the operand of an MFMA whose other operand was built by
+  // rowf -- its zero half cancels them -- so the per-query-tile loops issue no selects
+  auto rowf_raw = [&](const bf16_t* t, int row, int kc) -> s4 {
+    return ld4(t + row * RP + kc * 16 + 4 * (DH < 16 ? (g & 1) : g));
+  };
   if (dsl > 1) {
     // Key chunks of dsl keys (one head, host-checked: hpb 1, <= 16 query tiles): phase A on the
     // chunk's key tiles leaves the chunk's dS^T in LDS, phase B adds the chunk's share of dQ^T
@@ -514,22 +596,30 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
 #pragma unroll
           for (int dt = 0; dt < KC; ++dt) { dk[u][dt] = (v4f){0.f, 0.f, 0.f, 0.f}; dv[u][dt] = dk[u][dt]; }
         auto qstep = [&](const int qt, const int u) {
-          v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+          // dP starts from -D (the row constant in the accumulator): dS = P * dP needs no subtraction
+          const float4 dv4 = *(const float4*)(Dv + qt * 16 + 4 * g);
+          v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {-dv4.x, -dv4.y, -dv4.z, -dv4.w};
           if constexpr (F8) {
 #pragma unroll
             for (int kc = 0; kc < KC8; ++kc) s = mma8(frag8<DH>(Qs, RP, qt * 16 + l16, kc, g), kf8[kc], s);
           }
 #pragma unroll
           for (int kc = 0; kc < KC; ++kc) {
-            if constexpr (!F8) s = mma(rowf(Qs, qt * 16 + l16, kc), kf[kc], s);
-            dp = mma(rowf(Gs, qt * 16 + l16, kc), vf[kc], dp);
+            if constexpr (!F8) s = mma(rowf_raw(Qs, qt * 16 + l16, kc), kf[kc], s);
+            dp = mma(rowf_raw(Gs, qt * 16 + l16, kc), vf[kc], dp);
           }
           float pv[4], ds[4];
+          {  // exp arguments as packed pairs (v_pk_fma_f32)
+            const int q0 = qt * 16 + 4 * g;
+            const v2f sl = {sl2, sl2};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int q = qt * 16 + 4 * g + i;
-            pv[i] = (!MASK || (kv && q < SQ)) ? ex2(__builtin_fmaf(s[i], sl2, -lse[q])) : 0.f;
-            ds[i] = pv[i] * (dp[i] - Dv[q]);
+            for (int i = 0; i < 4; i += 2) {
+              const v2f e = __builtin_elementwise_fma((v2f){s[i], s[i + 1]}, sl, (v2f){-lse[q0 + i], -lse[q0 + i + 1]});
+              pv[i] = (!MASK || (kv && q0 + i < SQ)) ? ex2(e[0]) : 0.f;
+              pv[i + 1] = (!MASK || (kv && q0 + i + 1 < SQ)) ? ex2(e[1]) : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ds[i] = pv[i] * dp[i];
           }
           const s4 pf = pack4(pv[0], pv[1], pv[2], pv[3]);
           const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);
@@ -632,22 +722,30 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
     // the two query tiles of a step are independent chains (LDS read -> MFMA -> exp -> MFMA);
     // without a partial last step they are straight-line code the compiler interleaves
     auto qstep = [&](const int qt, const int u) {
-        v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+        // dP starts from -D (the row constant in the accumulator): dS = P * dP needs no subtraction
+        const float4 dv4 = *(const float4*)(Dv + qt * 16 + 4 * g);
+        v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {-dv4.x, -dv4.y, -dv4.z, -dv4.w};
         if constexpr (F8) {
 #pragma unroll
           for (int kc = 0; kc < KC8; ++kc) s = mma8(frag8<DH>(Qs, RP, qt * 16 + l16, kc, g), kf8[kc], s);
         }
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
-          if constexpr (!F8) s = mma(rowf(Qs, qt * 16 + l16, kc), kf[kc], s);
-          dp = mma(rowf(Gs, qt * 16 + l16, kc), vf[kc], dp);
+          if constexpr (!F8) s = mma(rowf_raw(Qs, qt * 16 + l16, kc), kf[kc], s);
+          dp = mma(rowf_raw(Gs, qt * 16 + l16, kc), vf[kc], dp);
         }
         float pv[4], ds[4];
+        {  // exp arguments as packed pairs (v_pk_fma_f32)
+          const int q0 = qt * 16 + 4 * g;
+          const v2f sl = {sl2, sl2};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int q = qt * 16 + 4 * g + i;
-          pv[i] = (!MASK || (kv && q < SQ)) ? ex2(__builtin_fmaf(s[i], sl2, -lse[q])) : 0.f;
-          ds[i] = pv[i] * (dp[i] - Dv[q]);
+          for (int i = 0; i < 4; i += 2) {
+            const v2f e = __builtin_elementwise_fma((v2f){s[i], s[i + 1]}, sl, (v2f){-lse[q0 + i], -lse[q0 + i + 1]});
+            pv[i] = (!MASK || (kv && q0 + i < SQ)) ? ex2(e[0]) : 0.f;
+            pv[i + 1] = (!MASK || (kv && q0 + i + 1 < SQ)) ? ex2(e[1]) : 0.f;
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ds[i] = pv[i] * dp[i];
         }
         const s4 pf = pack4(pv[0], pv[1], pv[2], pv[3]);
         const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);
@@ -779,22 +877,22 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
         for (int kc = 0; kc < KC8; ++kc) qf8[kc] = frag8<DH>(Qs, RP, q, kc, g);
       }
       auto kstep = [&](const int kt, const int u) {
-        v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+        v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {-Dq, -Dq, -Dq, -Dq};  // dP^T - D from the accumulator
         if constexpr (F8) {
 #pragma unroll
           for (int kc = 0; kc < KC8; ++kc) st = mma8(frag8<DH>(Ks, RP, kt * 16 + l16, kc, g), qf8[kc], st);
         }
 #pragma unroll
         for (int kc = 0; kc < KC; ++kc) {
-          if constexpr (!F8) st = mma(rowf(Ks, kt * 16 + l16, kc), qf[kc], st);
-          dpt = mma(rowf(Vs, kt * 16 + l16, kc), gf[kc], dpt);
+          if constexpr (!F8) st = mma(rowf_raw(Ks, kt * 16 + l16, kc), qf[kc], st);
+          dpt = mma(rowf_raw(Vs, kt * 16 + l16, kc), gf[kc], dpt);
         }
         float ds[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int key = kt * 16 + 4 * g + i;
           const float pr = (!MASK || (qv && key < SK)) ? ex2(__builtin_fmaf(st[i], sl2, -lq)) : 0.f;
-          ds[i] = pr * (dpt[i] - Dq);
+          ds[i] = pr * dpt[i];
         }
         const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);
 #pragma unroll
@@ -837,7 +935,7 @@ int launch_mfma_fwd(const EncdiffAttnArgs& a, hipStream_t s) {
   constexpr int DP = DH < 16 ? 16 : DH;
   int hpb = mfma_hpb(a);
   const int SKP = (a.sk + 31) & ~31;
-  size_t lds = (size_t)hpb * 2 * SKP * DP * sizeof(bf16_t);
+  size_t lds = (size_t)hpb * 2 * SKP * DP * sizeof(bf16_t) + 16 * sizeof(float);  // + the key norms
   int kch = SKP, nqb = 1;
   if (lds > 160 * 1024) {
     // K / V of a head exceed LDS (the VQ AttnBlock at 32x32 = 1024 tokens, dh 128): one head per

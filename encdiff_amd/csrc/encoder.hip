@@ -286,6 +286,8 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* r, long ldr,
 // image each (thread per column k, the image's du in LDS); the remaining blocks own 64 weight
 // columns each, 4 batch quarters per column (256 threads): dW[j][k] += sum_b du[b][j] x[b][k], the
 // quarters added in order through LDS (deterministic, no atomics); the first of them adds db.
+constexpr int HEAD_CB = 256;  // images of du staged in LDS at a time by the dW blocks
+
 template <int UM>
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float* r, long ldr, int d, const float* W, int units,
                                                        int batch, const float* du, long lddu, bf16_t* dr, long lddr,
@@ -307,11 +309,6 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* r, long ldr,
     }
     return;
   }
-  for (int e = threadIdx.x; e < batch * UM; e += 256) {
-    const int b = e / UM, j = e - b * UM;
-    sdu[e] = j < units ? du[(long)b * lddu + j] : 0.f;
-  }
-  __syncthreads();
   const int blk = blockIdx.x - batch;
   const int kl = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int k = blk * 64 + kl;
@@ -319,13 +316,25 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* r, long ldr,
   float acc[UM];  // UM >= units, compile-time indices only (registers)
 #pragma unroll
   for (int j = 0; j < UM; ++j) acc[j] = 0.f;
-  if (k < K) {
-    const int c = k / HPIX, p = k - c * HPIX;
+  // du staged HEAD_CB images at a time (any batch fits the LDS); each quarter still adds its images
+  // in increasing order, so the chunking does not change a bit of the result
+  for (int c0 = 0; c0 < batch; c0 += HEAD_CB) {
+    const int c1 = min(batch, c0 + HEAD_CB);
+    __syncthreads();  // the previous chunk is consumed
+    for (int e = threadIdx.x; e < (c1 - c0) * UM; e += 256) {
+      const int b = e / UM, j = e - b * UM;
+      sdu[e] = j < units ? du[(long)(c0 + b) * lddu + j] : 0.f;
+    }
+    __syncthreads();
+    if (k < K) {
+      const int c = k / HPIX, p = k - c * HPIX;
+      const int bs = max(b0, c0), be = min(b1, c1);
 #pragma unroll 8
-    for (int b = b0; b < b1; ++b) {
-      const float xv = r[((long)b * HPIX + p) * ldr + c];
+      for (int b = bs; b < be; ++b) {
+        const float xv = r[((long)b * HPIX + p) * ldr + c];
 #pragma unroll
-      for (int j = 0; j < UM; ++j) acc[j] += sdu[b * UM + j] * xv;
+        for (int j = 0; j < UM; ++j) acc[j] += sdu[(b - c0) * UM + j] * xv;
+      }
     }
   }
   __syncthreads();  // sdu is reused for the partials
@@ -364,9 +373,8 @@ extern "C" int encdiff_encoder_head_bwd(const float* r, long ldr, int batch, int
   if (!r || !W || !du || !dr || !dW || !db || batch <= 0 || d <= 0 || units <= 0 || units > 64 || lddr < d)
     return ENCDIFF_ERR_ARG;
   const int um = units <= 20 ? 20 : (units <= 40 ? 40 : 64);
-  size_t lds = (size_t)batch * um * sizeof(float);
-  if (lds < (size_t)4 * um * 64 * sizeof(float)) lds = (size_t)4 * um * 64 * sizeof(float);
-  if (lds > 64 * 1024) return ENCDIFF_ERR_SHAPE;
+  size_t lds = (size_t)(batch < HEAD_CB ? batch : HEAD_CB) * um * sizeof(float);
+  if (lds < (size_t)4 * um * 64 * sizeof(float)) lds = (size_t)4 * um * 64 * sizeof(float);  // <= 64 KB
   const int kb = (d * HPIX + 63) / 64;
   auto kern = units <= 20 ? head_bwd_kernel<20> : (units <= 40 ? head_bwd_kernel<40> : head_bwd_kernel<64>);
   hipLaunchKernelGGL(kern, dim3(batch + kb), dim3(256), lds, (hipStream_t)stream, r, ldr, d, W, units, batch, du, lddu,

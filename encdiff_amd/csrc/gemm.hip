@@ -24,8 +24,9 @@ enum { A_ROWK = ENCDIFF_OPA_ROWK, A_IM2COL = ENCDIFF_OPA_IM2COL, A_ROWM = ENCDIF
 enum { B_ROWK = ENCDIFF_OPB_ROWK, B_ROWN = ENCDIFF_OPB_ROWN, B_CONVD = ENCDIFF_OPB_CONV_DGRAD,
        B_IM2COL = ENCDIFF_OPB_IM2COL };
 
-// internal A mode (tiles >= 16): implicit im2col read from a per-workgroup halo image in LDS
-enum { A_HALO = 16 };
+// internal A modes: implicit im2col read from a per-workgroup halo image in LDS (tiles >= 16);
+// implicit im2col with GroupNorm(+FiLM)(+SiLU) applied to each staged A tile (EncdiffGemmArgs.agn_*)
+enum { A_HALO = 16, A_IM2COL_GN = 17 };
 
 template <int AM> struct AKInner { static constexpr bool v = AM != A_ROWM; };
 template <int BMd> struct BKInner { static constexpr bool v = BMd == B_ROWK; };
@@ -178,6 +179,8 @@ struct Gemm {
   static constexpr int TM = BM / 32;  // 16x16 MFMA tiles per wave along M
   static constexpr int TN = BN / 32;
   static constexpr bool HALO = AM == A_HALO;
+  static constexpr bool AGN = AM == A_IM2COL_GN;  // GroupNorm applied to the staged A tiles
+  static constexpr bool IM2 = AM == A_IM2COL || AGN;
   static constexpr int ASTAGE = HALO ? 0 : TA::ELEMS;  // halo mode: the ring holds B only
   static constexpr int STAGE = ASTAGE + TB::ELEMS;     // elements per LDS stage
   // LDS ring depth.  Measured on the step's GEMMs: 3-4 stages for every GEMM (one or two
@@ -320,7 +323,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   const uint32_t ldsrc2 = (uint32_t)p.conv.ld_src * 2u;
   // a k-tile of an im2col / flipped-weight operand lies inside one tap: tap and channel base are
   // uniform per k-tile
-  const bool a_tapk = AM == A_IM2COL && (p.conv.cin % BK) == 0;
+  const bool a_tapk = G::IM2 && (p.conv.cin % BK) == 0;
   const bool b_tapk = BMD == B_CONVD && (p.conv_cout % BK) == 0;
   // weight-gradient im2col operand (k = output pixel): with w | BK and hw | BK or BK | hw, pixel
   // k0 + r splits into a uniform part of k0 and a per-lane part of r (no per-k-tile division)
@@ -328,6 +331,8 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   if constexpr (BMD == B_IM2COL) b_pix = (BK % aux.w.d) == 0 && ((aux.hw.d % BK) == 0 || (BK % aux.hw.d) == 0);
   uint32_t a_off[APT > 0 ? APT : 1];  // invariant byte offset (OOB: masked row)
   int a_k[APT > 0 ? APT : 1], a_y[APT > 0 ? APT : 1], a_x[APT > 0 ? APT : 1];
+  int a_bl[APT > 0 ? APT : 1];  // AGN: the chunk row's image, relative to the tile's first image
+  uint32_t agn_b0 = 0;          // AGN: the tile's first image
   uint32_t b_off[BPT], b_n2[BPT];
   int b_k[BPT], b_ys[BPT];
   uint32_t b_base[BPT], b_xsh[BPT];
@@ -344,11 +349,12 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       const int m = m0 + gs * 8;
       a_k[i] = row;
       a_off[i] = m < p.M ? ((uint32_t)row * (uint32_t)p.lda + (uint32_t)m) * 2u : OOB;
-    } else if constexpr (AM == A_IM2COL) {  // this row = output pixel (fixed): source window origin
+    } else if constexpr (G::IM2) {  // this row = output pixel (fixed): source window origin
       const uint32_t mm0 = (uint32_t)(m0 + row);
       const bool min = mm0 < (uint32_t)p.M;
       const uint32_t mm = min ? mm0 - mbase : 0u;
       const uint32_t bb = fdiv(mm, aux.hw);
+      if constexpr (G::AGN) a_bl[i] = (int)(bb - fdiv((uint32_t)m0, aux.hw));
       const uint32_t r = mm - bb * aux.hw.d;
       const int y = (int)fdiv(r, aux.w), x = (int)(r - (uint32_t)y * aux.w.d);
       a_k[i] = gs * 8;
@@ -399,7 +405,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     // uniform per-k-tile values
     uint32_t a_ch = 0u, b_cv = 0u, b_pb = 0u;
     int a_ty = 0, a_tx = 0, b_yo = 0;
-    if constexpr (AM == A_IM2COL) {
+    if constexpr (G::IM2) {
       if (a_tapk) {
         const uint32_t tap = fdiv((uint32_t)k0, aux.cin);
         a_ch = (uint32_t)k0 - tap * (uint32_t)p.conv.cin;
@@ -624,6 +630,134 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     }
   };
 
+  // AGN (EncdiffGemmArgs.agn_*): GroupNorm32(+FiLM)(+SiLU) of the im2col source, folded into the
+  // staging.  Prologue: the statistics of every image the tile's rows read, from x itself (per
+  // channel sum / sum of squares over the image's pixels -- thread = (8-channel vector, pixel
+  // lane), lanes added in order -- then per group), turned into per-(image, channel) affine
+  // coefficients z = x * mul + add (mul = rstd gamma (1 + scale), add = (beta - mean rstd gamma)
+  // (1 + scale) + shift) in LDS behind the ring.  Per k-tile: every thread rewrites its own staged
+  // A chunks in place (after its LDS-DMA landed, before the barrier that publishes the tile);
+  // zero-padding chunks stay zero.
+  float2* agn_coef = (float2*)((char*)smem + G::LDS_BYTES);
+  if constexpr (G::AGN) {
+    const int cin = p.conv.cin, nv = cin >> 3, cpg = cin >> 5;
+    const int shw = md.hs * md.ws;  // source image pixels (UP2: the half-resolution image)
+    const uint32_t last = min((uint32_t)(m0 + BM), (uint32_t)p.M) - 1u;
+    agn_b0 = fdiv((uint32_t)m0, aux.hw);
+    const int nimg = (int)fdiv(last, aux.hw) - (int)agn_b0 + 1;
+    const int tv = tid % nv, tp = tid / nv, np = 256 / nv;  // host: cin <= 1024
+    // pixel lanes per image: every image of the tile in ONE pass of loads (small levels hold many
+    // images per 64-row tile; a loop over images serialised a global round trip per image)
+    const int lpi = np / nimg > 0 ? np / nimg : 1, ipass = np / lpi;
+    float* red = (float*)smem;        // [2][np][cin] per-lane partials (the ring is not staged yet)
+    float* gst = red + 2 * np * cin;  // [nimg][32][2]
+    float2* chs = agn_coef;           // [nimg][cin] (sum, sum of squares), then the coefficients
+    const long lds = p.conv.ld_src;
+    for (int j0 = 0; j0 < nimg; j0 += ipass) {
+      const int j = j0 + tp / lpi, li = tp - (tp / lpi) * lpi;
+      float sa[8], sq[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sa[i] = sq[i] = 0.f;
+      if (tp < ipass * lpi && j < nimg) {
+        const bf16_t* xb = A + (size_t)(agn_b0 + j) * shw * lds + tv * 8;
+        for (int px0 = li; px0 < shw; px0 += 8 * lpi) {
+          uint4 u[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int px = px0 + r * lpi;
+            u[r] = px < shw ? *(const uint4*)(xb + (size_t)px * lds) : make_uint4(0u, 0u, 0u, 0u);
+          }
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            float v[8];
+            unpack8(u[r], v);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { sa[i] += v[i]; sq[i] += v[i] * v[i]; }
+          }
+        }
+      }
+      if (tp < np) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          red[tp * cin + tv * 8 + i] = sa[i];
+          red[(np + tp) * cin + tv * 8 + i] = sq[i];
+        }
+      }
+      __syncthreads();
+      for (int e = tid; e < ipass * cin; e += 256) {  // (image, channel): its lanes added in order
+        const int jj = e / cin, c = e - jj * cin;
+        if (j0 + jj < nimg) {
+          float a = 0.f, q = 0.f;
+          for (int r = jj * lpi; r < (jj + 1) * lpi; ++r) { a += red[r * cin + c]; q += red[(np + r) * cin + c]; }
+          chs[(j0 + jj) * cin + c] = make_float2(a, q);
+        }
+      }
+      __syncthreads();
+    }
+    for (int e = tid; e < nimg * 32; e += 256) {  // (image, group) statistics
+      const int j = e >> 5, g = e & 31;
+      float a = 0.f, q = 0.f;
+      for (int c = g * cpg; c < (g + 1) * cpg; ++c) { const float2 v = chs[j * cin + c]; a += v.x; q += v.y; }
+      const float inv = 1.f / ((float)shw * (float)cpg);
+      const float mean = a * inv, var = fmaxf(q * inv - mean * mean, 0.f);
+      gst[2 * e] = mean;
+      gst[2 * e + 1] = rsqrtf(var + p.agn_eps);
+    }
+    __syncthreads();
+    for (int e = tid; e < nimg * cin; e += 256) {  // coefficients, in place of the channel sums
+      const int j = e / cin, c = e - j * cin, g = c / cpg, b = (int)agn_b0 + j;
+      float mul = gst[2 * (j * 32 + g) + 1] * p.agn_gamma[c];
+      float add = p.agn_beta[c] - gst[2 * (j * 32 + g)] * mul;
+      if (p.agn_film) {
+        const float sc = 1.f + p.agn_film[(long)b * p.ld_agn_film + c];
+        mul *= sc;
+        add = add * sc + p.agn_film[(long)b * p.ld_agn_film + cin + c];
+      }
+      agn_coef[e] = make_float2(mul, add);
+    }
+    __syncthreads();  // the ring is staged next
+  }
+  auto agn_transform = [&](bf16_t* sa, int kt) {
+    const int k0 = kt * BK;
+    uint32_t ch0 = 0u;
+    int ty0 = 0, tx0 = 0;
+    if (a_tapk) {
+      const uint32_t tap = fdiv((uint32_t)k0, aux.cin);
+      ch0 = (uint32_t)k0 - tap * (uint32_t)p.conv.cin;
+      tap_yx(md, tap, ty0, tx0);
+    }
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int k = k0 + a_k[i];
+      if (k >= p.K) continue;
+      uint32_t ch;
+      int ty, tx;
+      if (a_tapk) {
+        ch = ch0 + (uint32_t)a_k[i];
+        ty = ty0;
+        tx = tx0;
+      } else {
+        const uint32_t tap = fdiv((uint32_t)k, aux.cin);
+        ch = (uint32_t)k - tap * (uint32_t)p.conv.cin;
+        tap_yx(md, tap, ty, tx);
+      }
+      const int ys = a_y[i] + ty, xs = a_x[i] + tx;
+      if ((unsigned)ys >= (unsigned)md.lh || (unsigned)xs >= (unsigned)md.lw) continue;  // zero padding / masked row
+      bf16_t* q = sa + (tid + 256 * i) * 8;  // this thread's LDS-DMA chunk (lane-linear)
+      float v[8];
+      unpack8(*(const uint4*)q, v);
+      const float2* cf = agn_coef + a_bl[i] * p.conv.cin + ch;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float2 m = cf[e];
+        const float z = v[e] * m.x + m.y;
+        v[e] = p.agn_silu ? silu_f(z) : z;
+      }
+      *(uint4*)q = pack8(v);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the rewrites land before the barrier publishes them
+  };
+
   // NSTAGE-deep LDS ring: tiles it+1 .. it+NSTAGE-2 stay in flight while tile it is
   // multiplied, so the K loop is bound by MFMA / bandwidth rather than by one load latency
   // per k-tile.  Per iteration: wait for tile it (vmcnt = loads issued after it), one
@@ -640,6 +774,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     int rd = 0, wr = D - 1;  // ring slots of the tile read now / the tile issued next
     for (int it = 0; it < nkt; ++it) {
       vm_wait_stages<G::LPS, D - 2>(min(D - 2, nkt - 1 - it));
+      if constexpr (G::AGN) agn_transform(ring + rd * G::STAGE, kt_begin + it);
       asm volatile("s_barrier" ::: "memory");  // (asm: the compiler may not move LDS-DMA issue across it)
       if (it + D - 1 < nkt) stage(ring + wr * G::STAGE, kt_begin + it + D - 1);
       compute(ring + rd * G::STAGE, kt_begin + it);
@@ -1058,6 +1193,8 @@ __device__ __forceinline__ void fin_store(const EncdiffGemmArgs& p, const bf16_t
 }
 
 __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const int bid, const int nblk) {
+  // no FMA contraction: norm.hip's gn_slab_row restates this combine and must round identically
+#pragma clang fp contract(off)
   __shared__ float4 part[FIN_ZG][64];
   const long total = (long)p.M * p.N;
   const bf16_t* R = (const bf16_t*)p.resid;
@@ -1460,8 +1597,8 @@ __global__ __launch_bounds__(WPG * 64) void wgrad3x3_kernel(const EncdiffGemmArg
     }
     i -= n2;
   }
-  // finalize blocks are 256 threads: waves beyond 4 end (s_barrier waits for the surviving waves only)
-  if (threadIdx.x >= 256) return;
+  // finalize blocks (4-wave grids only: wg3_launch launches a tile-33 grid's finalize on its own)
+  if (WPG != 4) return;
   gemm_finalize(pf, i, nf);
 }
 
@@ -1760,7 +1897,17 @@ hipError_t wg3_launch_w(const EncdiffGemmArgs& p, const EncdiffGemmArgs& pf, int
 }
 
 hipError_t wg3_launch(const EncdiffGemmArgs& p, int tile, const EncdiffGemmArgs& pf, int nf, hipStream_t s) {
-  return tile == 33 ? wg3_launch_w<8>(p, pf, nf, s) : wg3_launch_w<4>(p, pf, nf, s);
+  if (tile == 33) {
+    // 8-wave workgroups: a riding finalize would reach gemm_finalize's barriers after waves 4-7
+    // returned (a barrier after a divergent exit) -- run it as a launch of its own instead
+    if (nf > 0) {
+      hipLaunchKernelGGL(gemm_finalize_kernel, dim3((unsigned)nf), dim3(256), 0, s, pf);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
+    return wg3_launch_w<8>(p, pf, 0, s);
+  }
+  return wg3_launch_w<4>(p, pf, nf, s);
 }
 
 template <int BM, int BN, int AM, int BMD, int NS = 2, int KB = BK>
@@ -1773,6 +1920,22 @@ hipError_t launch_t(const EncdiffGemmArgs& p, const GemmAux& aux, hipStream_t s)
   if (attr_ok != hipSuccess) return attr_ok;
   dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, p.split_k);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, AM, BMD, NS, KB>), grid, dim3(256), lds, s, p, aux);
+  return hipGetLastError();
+}
+
+// GroupNorm-in-staging forward conv (EncdiffGemmArgs.agn_*): 64x64 tiles, 2-deep ring, the
+// per-(image, channel) coefficient table behind the ring in dynamic LDS
+hipError_t launch_agn(const EncdiffGemmArgs& p, const GemmAux& aux, hipStream_t s) {
+  using G = Gemm<64, 64, A_IM2COL_GN, B_ROWK, 2, BK>;
+  const int hw = p.conv.h * p.conv.w;
+  const int nimg = (63 / hw + 2) < p.conv.batch ? 63 / hw + 2 : p.conv.batch;  // images one 64-row tile reads
+  const size_t lds = (size_t)G::LDS_BYTES + (size_t)nimg * p.conv.cin * 8;
+  static const hipError_t attr_ok = hipFuncSetAttribute((const void*)gemm_kernel<64, 64, A_IM2COL_GN, B_ROWK, 2, BK>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
+  if (attr_ok != hipSuccess) return attr_ok;
+  if (lds > 156 * 1024) return hipErrorInvalidValue;
+  dim3 grid((p.M + 63) / 64, (p.N + 63) / 64, p.split_k);
+  hipLaunchKernelGGL((gemm_kernel<64, 64, A_IM2COL_GN, B_ROWK, 2, BK>), grid, dim3(256), lds, s, p, aux);
   return hipGetLastError();
 }
 
@@ -1971,6 +2134,18 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
     if (!p.aux || p.resid || p.split_k != 1 || p.N % 8 || p.ldc % 8 || p.ld_aux % 8) return ENCDIFF_ERR_ARG;
     if (fwd && (p.a_mode != ENCDIFF_OPA_ROWK || p.b_mode != ENCDIFF_OPB_ROWK || p.N % 128)) return ENCDIFF_ERR_ARG;
   }
+  if (p.agn_gamma) {  // GroupNorm in the A staging: forward 3x3 conv, 64x64 tiles
+    if (p.a_mode != ENCDIFF_OPA_IM2COL || p.b_mode != ENCDIFF_OPB_ROWK || p.c_mode != ENCDIFF_OUT_BF16 ||
+        !p.agn_beta || p.ln_y)
+      return ENCDIFF_ERR_ARG;
+    if (p.conv.resample != ENCDIFF_RESAMPLE_NONE && p.conv.resample != ENCDIFF_RESAMPLE_UP2)
+      return ENCDIFF_ERR_UNSUPPORTED;
+    if (p.conv.cin % 32 || p.conv.cin > 1024 || p.K != 9 * p.conv.cin ||
+        (long)p.M != (long)p.conv.batch * p.conv.h * p.conv.w)
+      return ENCDIFF_ERR_SHAPE;
+    if (p.tile != 0 && p.tile != 4) return ENCDIFF_ERR_UNSUPPORTED;
+    p.tile = 4;
+  }
   g.tile = p.tile ? p.tile : pick_tile(p);
   g.aux.halo = HaloGeom{};
   if (g.tile >= 32 && g.tile <= 34) {  // 3x3 conv weight gradient kernel (WG3)
@@ -2024,7 +2199,8 @@ int launch_one(const GemmPlan& g, hipStream_t s) {
   if (g.tile >= 32 && g.tile <= 34) e = wg3_launch(g.p, g.tile, g.user, 0, s);
   else if (g.tile == 36) e = wgl_launch(g.p, g.user, 0, s);
   else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_ROWK, B_ROWK>(g.p, g.aux, g.tile, s);
-  else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_IM2COL, B_ROWK>(g.p, g.aux, g.tile, s);
+  else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_ROWK)
+    e = g.p.agn_gamma ? launch_agn(g.p, g.aux, s) : launch_modes<A_IM2COL, B_ROWK>(g.p, g.aux, g.tile, s);
   else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWK, B_ROWN>(g.p, g.aux, g.tile, s);
   else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_CONV_DGRAD)
     e = launch_modes<A_IM2COL, B_CONVD>(g.p, g.aux, g.tile, s);

@@ -13,6 +13,9 @@
 
 namespace {
 
+#ifndef ED_GN_BWD_U
+#define ED_GN_BWD_U 4  // backward rows per load batch (code size vs loads in flight)
+#endif
 constexpr int GN_THREADS = 256;
 constexpr int GN_TILE = 1024;      // backward: 16-byte vectors of a slice kept in LDS per operand (16 KB)
 constexpr int GN_TILE_FWD = 6144;  // forward: dynamic LDS tile up to 96 KB (the VQ encoder's 64x64 levels)
@@ -162,6 +165,8 @@ ED_DEV void gn_slab_batch(const float* w, long stride, int z0, int split, float 
 }
 
 ED_DEV uint4 gn_slab_row(const GnSlabs& sl, long row, int c, int cb) {
+  // no FMA contraction: gemm.hip's gemm_finalize does this combine too, bitwise alike
+#pragma clang fp contract(off)
   const float* w = sl.ws + row * c + cb;
   float a[8], v[8][8];
   if (sl.split <= 8) {
@@ -466,6 +471,9 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const EncdiffGroup
   }
 }
 
+// SLAB: dy is combined from its producer's deferred split-K slabs (a separate instantiation: the
+// slab combine unrolled into the plain kernel doubled its code and pushed it past 256 VGPRs)
+template <bool SLAB>
 __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNormArgs p, int cs, const GnSlabs sl) {
   __shared__ uint4 tx[GN_TILE], td[GN_TILE];
   __shared__ float red[4 * 2048], chs[4 * 512], gsh[2 * 64];
@@ -492,6 +500,8 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
     sc1[i] = film ? 1.f + sc1[i] : 1.f;
     sf[i] = film ? sf[i] : 0.f;
   }
+  // gamma of the channel this thread finishes after the reduction, loaded now (off the chain)
+  const float gam0 = threadIdx.x < L.cs ? p.gamma[L.c0 + threadIdx.x] : 0.f;
   // pass 1: per-channel sums of dn, dn*xhat, dz, dz*n
   float acc[4][8];
 #pragma unroll
@@ -499,7 +509,9 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[k][i] = 0.f;
   if (L.active) {
-    constexpr int U1 = 4;  // rows per batch: every load of a batch issued before the first use
+    // rows per batch: every load of a batch issued before the first use (a slab row already
+    // has up to 8 loads in flight)
+    constexpr int U1 = SLAB ? 1 : ED_GN_BWD_U;
     for (int px0 = L.tp; px0 < HW; px0 += U1 * L.np) {
     uint4 bx[U1], bd[U1];
 #pragma unroll
@@ -508,7 +520,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
       bx[u] = bd[u] = (uint4){0u, 0u, 0u, 0u};
       if (px < HW) {
         bx[u] = *(const uint4*)(X + (long)px * p.ldx);
-        if (sl.ws) {  // dy combined from its producer's slabs and written back
+        if constexpr (SLAB) {  // dy combined from its producer's slabs and written back
           bd[u] = gn_slab_row(sl, off + px, p.c, L.cb);
           *(uint4*)(const_cast<bf16_t*>(DY) + (long)px * p.lddy) = bd[u];
         } else {
@@ -543,7 +555,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   float* gch = red;  // [2][cs] (red is free after the reduction)
   for (int cl = threadIdx.x; cl < L.cs; cl += GN_THREADS) {
     const int c = L.c0 + cl;
-    const float gam = p.gamma[c];
+    const float gam = cl == (int)threadIdx.x ? gam0 : p.gamma[c];
     p.dbeta_part[(long)L.b * p.ld_part + c] = chs[cl];
     p.dgamma_part[(long)L.b * p.ld_part + c] = chs[L.cs + cl];
     if (film) {
@@ -576,7 +588,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   const bf16_t* RS = p.resid ? (const bf16_t*)p.resid + off * p.ld_resid + L.cb : nullptr;
   // U rows per thread: the global (resid / accumulate) reads of all U are issued before the
   // first dx store -- one latency per U rows instead of one per row
-  constexpr int U = 4;
+  constexpr int U = ED_GN_BWD_U;
   for (int px0 = L.tp; px0 < HW; px0 += U * L.np) {
     uint4 gr[U];
 #pragma unroll
@@ -823,8 +835,12 @@ extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream
     const int rc = gn_slabs_of(*a->x_from, a->dy, a->lddy, a, sl);
     if (rc != ENCDIFF_OK) return rc;
   }
-  hipLaunchKernelGGL(gn_bwd_kernel, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream, *a, cs,
-                     sl);
+  if (sl.ws)
+    hipLaunchKernelGGL(gn_bwd_kernel<true>, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream,
+                       *a, cs, sl);
+  else
+    hipLaunchKernelGGL(gn_bwd_kernel<false>, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream,
+                       *a, cs, sl);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }

@@ -513,7 +513,51 @@ __global__ __launch_bounds__(256) void st_head_kernel(const EncdiffStHeadArgs p)
   load_b(win, (const bf16_t*)p.w_in, p.ld_in, n0, 0, lane);
   load_b(wq, (const bf16_t*)p.w_qkv, p.ld_w_qkv, n03, 0, lane);
   constexpr int CH = C / 8;
-  if (p.gn_in_stats) {
+  if (!p.gn_in_stats && !p.gn) {
+    // inference: the statistics of the tile's images from x itself (per channel sum / sum of
+    // squares over the image's tokens, thread = (8-channel vector, token lane), lanes and the
+    // group's channels added in order), then the same apply as below
+    constexpr int cpg = C / 32, NP = 256 / CH;
+    float* red = gms + nimg * 64;  // [2][NP][C] scratch behind the statistics (launch_head sizes it)
+    const int tv = tid % CH, tp = tid / CH;
+    for (int i = 0; i < nimg; ++i) {
+      float sa[8], sq[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sa[k] = sq[k] = 0.f;
+      const bf16_t* xb = (const bf16_t*)p.x + (long)(img0 + i) * p.tokens * p.ld_x + tv * 8;
+      for (int px0 = tp; px0 < p.tokens; px0 += 8 * NP) {
+        uint4 u[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int px = px0 + r * NP;
+          u[r] = px < p.tokens ? *(const uint4*)(xb + (long)px * p.ld_x) : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          float v[8];
+          unpack8(u[r], v);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { sa[k] += v[k]; sq[k] += v[k] * v[k]; }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        red[tp * C + tv * 8 + k] = sa[k];
+        red[(NP + tp) * C + tv * 8 + k] = sq[k];
+      }
+      __syncthreads();
+      if (tid < 32) {
+        float a = 0.f, q = 0.f;
+        for (int r = 0; r < NP; ++r)
+          for (int c = tid * cpg; c < (tid + 1) * cpg; ++c) { a += red[r * C + c]; q += red[(NP + r) * C + c]; }
+        const float inv_n = 1.f / ((float)p.tokens * cpg);
+        const float mean = a * inv_n;
+        gms[2 * (i * 32 + tid)] = mean;
+        gms[2 * (i * 32 + tid) + 1] = rsqrtf(fmaxf(q * inv_n - mean * mean, 0.f) + p.gn_eps);
+      }
+      __syncthreads();
+    }
+  } else if (p.gn_in_stats) {
     // per (image, group) statistics from the producer's 64-row segment sums (as gn_fwd_stats_kernel)
     constexpr int cpg = C / 32;
     const int nseg = p.tokens >> 6;
@@ -538,8 +582,11 @@ __global__ __launch_bounds__(256) void st_head_kernel(const EncdiffStHeadArgs p)
       }
     }
     __syncthreads();
+  }
+  if (p.gn_in_stats || !p.gn) {
+    constexpr int cpg = C / 32;
     const bf16_t* xg = (const bf16_t*)p.x + (long)row0 * p.ld_x;
-    bf16_t* gg = (bf16_t*)p.gn + (long)row0 * p.ld_gn;
+    bf16_t* gg = p.gn ? (bf16_t*)p.gn + (long)row0 * p.ld_gn : nullptr;
     for (int e = tid; e < R * CH; e += 256) {
       const int r = e / CH, c8 = (e - r * CH) * 8, i = (row0 + r) / p.tokens - img0;
       float v[8];
@@ -552,7 +599,7 @@ __global__ __launch_bounds__(256) void st_head_kernel(const EncdiffStHeadArgs p)
       }
       const uint4 y = pack8(v);
       *(uint4*)(Xa + r * LDX + c8) = y;
-      *(uint4*)(gg + (long)r * p.ld_gn + c8) = y;
+      if (gg) *(uint4*)(gg + (long)r * p.ld_gn + c8) = y;
     }
   } else {
     rows_to_lds<C, R>(Xa, LDX, (const bf16_t*)p.gn + (long)row0 * p.ld_gn, p.ld_gn, tid);
@@ -603,7 +650,9 @@ int launch_head(const EncdiffStHeadArgs& p, hipStream_t s) {
   constexpr int R = RR;
   if (p.rows % R || (R % p.tokens && p.tokens % R)) return ENCDIFF_ERR_SHAPE;
   const int nimg = R > p.tokens ? R / p.tokens : 1;
-  const size_t lds = (size_t)R * (C + 4) * 4 + (size_t)R * (C + 8) * 2 + (size_t)R * (3 * C + 8) * 2 + nimg * 64 * 4;
+  const bool self_stats = !p.gn_in_stats && !p.gn;  // + the statistics scratch [2][256 / (C / 8)][C] floats
+  const size_t lds = (size_t)R * (C + 4) * 4 + (size_t)R * (C + 8) * 2 + (size_t)R * (3 * C + 8) * 2 + nimg * 64 * 4 +
+                     (self_stats ? 2 * 2048 * 4 : 0);
   if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
   static const hipError_t attr_ok = hipFuncSetAttribute((const void*)st_head_kernel<C, RR>,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -668,13 +717,16 @@ extern "C" int encdiff_st_head_fwd(const EncdiffStHeadArgs* a, void* stream) {
   if (p.tokens < 1 || p.rows < 1 || p.rows % p.tokens) return ENCDIFF_ERR_SHAPE;
   if (p.gn_in_stats && (p.tokens % 64 || p.ld_gn_in_stats < p.c || !p.x || !al16(p.x) || p.ld_x % 8))
     return ENCDIFF_ERR_SHAPE;
-  const void* ptrs[] = {p.gn, p.w_in, p.w_qkv, p.t0, p.qkv};
+  const bool self_stats = !p.gn_in_stats && !p.gn;  // statistics from x in the kernel (no gn output)
+  if (self_stats && (!p.x || !al16(p.x) || p.ld_x % 8 || p.gn_stats)) return ENCDIFF_ERR_ARG;
+  const void* ptrs[] = {self_stats ? p.x : p.gn, p.w_in, p.w_qkv, p.t0, p.qkv};
   for (const void* q : ptrs)
     if (!q || !al16(q)) return ENCDIFF_ERR_ARG;
-  const long lds[] = {p.ld_gn, p.ld_in, p.ld_w_qkv, p.ld_t0, p.ld_qkv};
+  const long lds[] = {self_stats ? p.ld_x : p.ld_gn, p.ld_in, p.ld_w_qkv, p.ld_t0, p.ld_qkv};
   for (long l : lds)
     if (l % 8) return ENCDIFF_ERR_ARG;
-  if (!p.b_in || !p.g1 || !p.be1 || (p.gn_in_stats && (!p.gn_gamma || !p.gn_beta))) return ENCDIFF_ERR_ARG;
+  if (!p.b_in || !p.g1 || !p.be1 || ((p.gn_in_stats || self_stats) && (!p.gn_gamma || !p.gn_beta)))
+    return ENCDIFF_ERR_ARG;
   if ((p.n1 != nullptr) != (p.s1 != nullptr) || (p.n1 && p.ld_n1 % 8)) return ENCDIFF_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   // 64-row tiles at training batches, 16 rows when that leaves most CUs idle (sampling)

@@ -66,13 +66,26 @@ class CrossAttention(nn.Module):
         bf = torch.bfloat16
         # q / k / v projections on the library's GEMM engine (encdiff::linear, autograd through
         # encdiff::linear_bwd), then the MFMA attention
-        q = torch.ops.encdiff.linear(x.to(bf), self.to_q.weight.to(bf))
-        k = torch.ops.encdiff.linear(c.to(bf), self.to_k.weight.to(bf))
-        v = torch.ops.encdiff.linear(c.to(bf), self.to_v.weight.to(bf))
+        q = _linear(x.to(bf), self.to_q.weight.to(bf))
+        k = _linear(c.to(bf), self.to_k.weight.to(bf))
+        v = _linear(c.to(bf), self.to_v.weight.to(bf))
         o, _ = torch.ops.encdiff.attention_fwd(q.contiguous(), k.contiguous(), v.contiguous(), self.heads, False)
         lin, drop = self.to_out[0], self.to_out[1]
-        y = torch.ops.encdiff.linear(o, lin.weight.to(bf)).to(x.dtype)
+        y = _linear(o, lin.weight.to(bf)).to(x.dtype)
         return drop(y + lin.bias if lin.bias is not None else y)
+
+
+def _linear(x, w):
+    """x w^T on the GEMM engine (encdiff::linear).  The engine reads 16-byte rows (K, N multiples
+    of 8): other widths (a context_dim or inner dim not divisible by 8) run zero-padded -- the
+    padded products are exact zeros, the padding is sliced off, autograd flows through both."""
+    N, K = w.shape
+    kp, np_ = (-K) % 8, (-N) % 8
+    if kp or np_:
+        x = torch.nn.functional.pad(x, (0, kp))
+        w = torch.nn.functional.pad(w, (0, kp, 0, np_))
+    y = torch.ops.encdiff.linear(x.contiguous(), w.contiguous())
+    return y[..., :N] if np_ else y
 
 
 class BasicTransformerBlock(nn.Module):

@@ -244,9 +244,13 @@ def wgl_split(M, N, K, lda, ldb, c_mode):
 def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK, c_mode=L.OUT_BF16,
               conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=None, bias=None,
               resid=None, ld_resid=0, bias_grad=None, tile=0, ws_offset=0, aux=None, ld_aux=0,
-              gn_stats=None, ln=None):
+              gn_stats=None, ln=None, agn=None, fold=False):
     """EncdiffGemmArgs with the measured (tile, split) plan; split-K slabs start `ws_offset`
-    floats into this stream's workspace."""
+    floats into this stream's workspace.  agn = (gamma, beta, film or None, eps, silu): GroupNorm of
+    the im2col source applied in the A staging (tile 4); fold: split-K slabs combined in the kernel
+    whenever the plan splits (the output is complete when the launch ends)."""
+    if agn is not None:
+        tile = 4
     if (WG3 and tile == 0 and split_k is None and a_mode == L.OPA_ROWM and b_mode == L.OPB_IM2COL and
             conv is not None and N == 9 * conv.cin and K == conv.batch * conv.h * conv.w):
         sp = wg3_split(conv.batch, conv.h, conv.w, M, conv.cin, conv.resample, lda, conv.ld_src, c_mode)
@@ -273,7 +277,7 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
         # the in-kernel combine indexes one ticket per output tile: only when every tile shape
         # (>= 32 x 32) stays within the ticket array
         if (a_mode != L.OPA_ROWM and math.ceil(M / 32) * math.ceil(N / 32) <= COUNTERS and
-                fold_choice(M, N, K, a_mode, b_mode, c_mode, conv.resample if conv is not None else 0)):
+                (fold or fold_choice(M, N, K, a_mode, b_mode, c_mode, conv.resample if conv is not None else 0))):
             cnt = _counters()
     return L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=b_mode, c_mode=c_mode,
                       a=_p(a), lda=lda, b=_p(b), ldb=ldb, c=_p(c), ldc=ldc,
@@ -284,7 +288,10 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
                       gn_stats=_p(gn_stats), ld_gn_stats=_ld(gn_stats) if gn_stats is not None else 0,
                       split_counters=None if cnt is None else cnt.data_ptr(),
                       **({} if ln is None else dict(ln_gamma=_p(ln[0]), ln_beta=_p(ln[1]), ln_y=_p(ln[2]),
-                                                    ld_ln_y=_ld(ln[2]), ln_stats=_p(ln[3]), ln_eps=ln[4])))
+                                                    ld_ln_y=_ld(ln[2]), ln_stats=_p(ln[3]), ln_eps=ln[4])),
+                      **({} if agn is None else dict(agn_gamma=_p(agn[0]), agn_beta=_p(agn[1]), agn_film=_p(agn[2]),
+                                                     ld_agn_film=_ld(agn[2]) if agn[2] is not None else 0,
+                                                     agn_eps=agn[3], agn_silu=int(agn[4]))))
 
 
 def ws_floats(args) -> int:
@@ -296,14 +303,16 @@ def ws_floats(args) -> int:
     return (n + 3) & ~3
 
 
-_PENDING = {}  # stream -> GemmArgs of a weight gradient whose split-K finalize is deferred
-_HALF = {}     # stream -> workspace half used by the last paired launch
+# Keyed by DEVICE, like the workspace the slabs live in (scratch()): a finalize left pending by a
+# launch on one stream is flushed by the next workspace user on any stream of that device.
+_PENDING = {}  # device -> GemmArgs of a weight gradient whose split-K finalize is deferred
+_HALF = {}     # device -> workspace half used by the last paired launch
 
 
 def flush():
     """Run the deferred weight-gradient finalize of the current stream, if any (the end of a
     backward, or before a GEMM that needs the workspace)."""
-    key = torch.cuda.current_stream().cuda_stream
+    key = torch.cuda.current_device()
     pend = _PENDING.pop(key, None)
     if pend is not None:
         check(lib.encdiff_gemm_finalize(C.byref(pend), _s()), "encdiff_gemm_finalize")
@@ -328,7 +337,7 @@ def gemm_pair(wgrad_fn, dgrad_fn, defer_dx=False):
     last (`flush`).  defer_dx: the input gradient's finalize is skipped too when it has one;
     its GemmArgs are returned for the consumer (groupnorm_bwd(dy_from=...)) or finalize(),
     which must run before the next pair (else None: dx written)."""
-    key = torch.cuda.current_stream().cuda_stream
+    key = torch.cuda.current_device()
     if not PAIR:
         flush()
         w = wgrad_fn(0)
@@ -475,16 +484,18 @@ def linear_bwd_geglu(dy, w, a, f, df, dw, db=None, d_a=None):
 
 # ------------------------------------------------------------------ 3x3 convolutions
 def conv3x3_fwd(x, g: Geom, cin, wf, out, bias=None, resid=None, resample=L.RESAMPLE_NONE, gn_stats=None,
-                out_f32=False, defer=False):
+                out_f32=False, defer=False, agn=None, fold=False):
     """out[pixels][cout] = conv3x3(resample(x)) with packed weights wf [cout][9*cin]
     (gn_stats: as linear_fwd; out_f32: fp32 output).  defer: when the plan leaves split-K slabs
     for a finalize pass, skip it and return the GemmArgs -- the caller hands them to
-    groupnorm_fwd(x_from=...) (which writes `out`) or to finalize(); else None (out written)."""
+    groupnorm_fwd(x_from=...) (which writes `out`) or to finalize(); else None (out written).
+    agn = (gamma, beta, film or None, eps, silu): the conv reads GroupNorm(+FiLM)(+SiLU)(x) -- applied
+    in its A staging, x complete -- instead of a GroupNorm output; fold: see gemm_args."""
     cout = wf.shape[0]
     args = gemm_args(g.pixels, cout, 9 * cin, x, _ld(x), wf, _ld(wf), out, _ld(out), a_mode=L.OPA_IM2COL,
                      c_mode=L.OUT_F32 if out_f32 else L.OUT_BF16, conv=_conv_geom(g, cin, resample, x), bias=bias,
                      resid=resid, ld_resid=_ld(resid) if resid is not None else 0, gn_stats=gn_stats,
-                     split_k=1 if gn_stats is not None else None)
+                     split_k=1 if gn_stats is not None else None, agn=agn, fold=fold)
     if ws_floats(args):
         flush()
     if not defer:
@@ -715,15 +726,19 @@ def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps
 
 
 def st_head_fwd(x, gn, w_in, b_in, g1, be1, w_qkv, t0, qkv, rows, c, tokens, gn_eps, ln_eps, in_stats=None,
-                gn_gamma=None, gn_beta=None, gn_stats=None, n1=None, s1=None) -> bool:
+                gn_gamma=None, gn_beta=None, gn_stats=None, n1=None, s1=None, self_stats=False) -> bool:
     """The row-local head of a SpatialTransformer (attention.py:250-254, 211) as one kernel:
-    gn = GroupNorm32(x) from the producer's segment sums `in_stats` (else `gn` is read, already
-    computed), t0 = proj_in(gn), n1 = LN1(t0) (saved with s1 when given), qkv = n1 Wqkv^T.
+    gn = GroupNorm32(x) from the producer's segment sums `in_stats` (self_stats: from x by the
+    kernel itself, gn not written -- inference; else `gn` is read, already computed),
+    t0 = proj_in(gn), n1 = LN1(t0) (saved with s1 when given), qkv = n1 Wqkv^T.
     Returns False outside the kernel's support (the caller issues the separate launches)."""
     a = L.StHeadArgs(rows=rows, c=c, tokens=tokens, gn_eps=gn_eps, ln_eps=ln_eps, x=_p(x), ld_x=_ld(x),
                      gn=_p(gn), ld_gn=_ld(gn), w_in=_p(w_in), ld_in=_ld(w_in), b_in=_p(b_in), g1=_p(g1), be1=_p(be1),
                      w_qkv=_p(w_qkv), ld_w_qkv=_ld(w_qkv), t0=_p(t0), ld_t0=_ld(t0), qkv=_p(qkv), ld_qkv=_ld(qkv))
-    if in_stats is not None:
+    if self_stats:
+        a.gn, a.ld_gn = None, 0
+        a.gn_gamma, a.gn_beta = _p(gn_gamma), _p(gn_beta)
+    elif in_stats is not None:
         a.gn_in_stats, a.ld_gn_in_stats = _p(in_stats), _ld(in_stats)
         a.gn_gamma, a.gn_beta, a.gn_stats = _p(gn_gamma), _p(gn_beta), _p(gn_stats)
     if n1 is not None:

@@ -47,6 +47,14 @@ LN_EPS = 1e-5      # nn.LayerNorm default (attention.py:206-208)
 # the row-local SpatialTransformer tail (attn1.to_out .. proj_out) as one kernel
 # (encdiff_st_tail_fwd) in no-grad forwards (0: the separate launches, for A/B runs)
 ST_TAIL_FUSED = os.environ.get("ENCDIFF_ST_TAIL", "1") != "0"
+# inference at sampling batches: ResBlock GroupNorms folded into the convs' A staging
+# (_res_fwd_agn); larger batches keep the producer-statistics GroupNorm launches
+AGN = os.environ.get("ENCDIFF_AGN", "1") != "0"
+AGN_MAX_B = int(os.environ.get("ENCDIFF_AGN_MAX_B", "32"))
+# ResBlock convs too (else only the fused ST heads): off by default -- DDIM B=8 measured 500 steps/s
+# with it vs 595 without (the per-workgroup statistics prologue costs more than the launches it saves)
+AGN_RES = os.environ.get("ENCDIFF_AGN_RES", "0") != "0"
+AGN_FOLD = os.environ.get("ENCDIFF_AGN_FOLD", "1") != "0"  # split-K combined in the kernel (else a finalize pass)
 # widest level that uses it: at c = 256 one workgroup streams 2.6 MB of weights through one CU
 # (74 us at B = 8 against ~35 us for the separate launches, tools/st_tail_bench.py)
 ST_TAIL_MAXC = int(os.environ.get("ENCDIFF_ST_TAIL_MAXC", "128"))
@@ -529,6 +537,8 @@ class UNetExecutor:
         S = self.state[r.prefix]
         S["x"] = x
         gi, go = Geom(B, r.hin, r.hin), Geom(B, r.hout, r.hout)
+        if self.infer and AGN and AGN_RES and B <= AGN_MAX_B:
+            return self._res_fwd_agn(r, S, x, gi, go)
         ops.groupnorm_fwd(x, gi, self.P(r.prefix + "in_layers.0.weight"), self.P(r.prefix + "in_layers.0.bias"),
                           S["a1"], S["st1"], GN_EPS, True, in_stats=self._gst(x), x_from=self._take_pend(x))
         a1, rs = self._conv1_input(r, S, go)
@@ -557,6 +567,43 @@ class UNetExecutor:
                                      defer=GN_FIN and self._gst(out) is None)
         return out
 
+    def _res_fwd_agn(self, r: ResSpec, S, x, gi: Geom, go: Geom):
+        """Inference ResBlock with its GroupNorms in the convs' A staging (EncdiffGemmArgs.agn_*):
+        conv1 reads GN1+SiLU(x) (nearest-up through its gather), conv2 reads GN2+FiLM+SiLU(h1); no
+        GroupNorm launch and no normalised activation in memory.  A down block keeps its GN1 launch
+        (the conv reads the 2x2-averaged GroupNorm output).  Each conv combines its split-K slabs in
+        the kernel, so its output is complete for the next conv's statistics."""
+        pre = r.prefix
+        if r.updown == L.RESAMPLE_DOWN2:
+            ops.groupnorm_fwd(x, gi, self.P(pre + "in_layers.0.weight"), self.P(pre + "in_layers.0.bias"), S["a1"],
+                              S["st1"], GN_EPS, True, in_stats=self._gst(x), x_from=self._take_pend(x))
+            a1, rs = self._conv1_input(r, S, go)
+            ops.conv3x3_fwd(a1, go, r.cin, self.W(pre + "in_layers.2.weight"), S["h1"],
+                            bias=self.P(pre + "in_layers.2.bias"), resample=rs, fold=AGN_FOLD)
+        else:
+            p = self._pend  # x complete (a producer that deferred its finalize finalizes now)
+            self._pend = None
+            ops.finalize(p)
+            ops.conv3x3_fwd(x, go, r.cin, self.W(pre + "in_layers.2.weight"), S["h1"],
+                            bias=self.P(pre + "in_layers.2.bias"), resample=r.updown,
+                            agn=(self.P(pre + "in_layers.0.weight"), self.P(pre + "in_layers.0.bias"), None, GN_EPS,
+                                 True), fold=AGN_FOLD)
+        out = S["out"]
+        if r.cin != r.cout:
+            ops.linear_fwd(x, self.W(pre + "skip_connection.weight"), out, bias=self.P(pre + "skip_connection.bias"))
+            resid = out
+        elif r.updown:
+            ops.resample(x, S["xr"], go, r.updown)
+            resid = S["xr"]
+        else:
+            resid = x
+        film = self.E[:, r.film_off:]
+        ops.conv3x3_fwd(S["h1"], go, r.cout, self.W(pre + "out_layers.3.weight"), out,
+                        bias=self.P(pre + "out_layers.3.bias"), resid=resid, gn_stats=self._gst(out),
+                        agn=(self.P(pre + "out_layers.0.weight"), self.P(pre + "out_layers.0.bias"), film, GN_EPS, True),
+                        fold=AGN_FOLD)
+        return out
+
     @staticmethod
     def _conv1_input(r: ResSpec, S, go: Geom):
         """in_layers conv input: the GN1 output, avg-pooled first for a down block
@@ -577,7 +624,9 @@ class UNetExecutor:
         ntok = s.h * s.h
         fused = ST_TAIL_FUSED and c <= ST_TAIL_MAXC and (self.infer or ST_TAIL_TRAIN)
         in_st = self._gst(x)
-        if fused and in_st is None:  # no producer statistics: the GroupNorm kernel reduces them
+        # inference at sampling batches: the fused head computes the GroupNorm statistics itself
+        self_st = fused and in_st is None and self.infer and AGN and B <= AGN_MAX_B
+        if fused and in_st is None and not self_st:  # no producer statistics: the GroupNorm kernel reduces them
             ops.groupnorm_fwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["gn"],
                               S["stg"], ST_GN_EPS, False)
         # GroupNorm (from producer statistics) + proj_in + norm1 + q/k/v as one kernel
@@ -585,9 +634,9 @@ class UNetExecutor:
                 x, S["gn"], self.W(s.prefix + "proj_in.weight"), self.P(s.prefix + "proj_in.bias"),
                 self.P(tb + "norm1.weight"), self.P(tb + "norm1.bias"), self.W(s.prefix + "qkv"), S["t0"], S["qkv"],
                 B * ntok, c, ntok, ST_GN_EPS, LN_EPS, in_stats=in_st, gn_gamma=self.P(s.prefix + "norm.weight"),
-                gn_beta=self.P(s.prefix + "norm.bias"), gn_stats=S["stg"], n1=None if self.infer else S["n1"],
-                s1=None if self.infer else S["s1"])):
-            if not fused or in_st is not None:
+                gn_beta=self.P(s.prefix + "norm.bias"), gn_stats=None if self_st else S["stg"],
+                n1=None if self.infer else S["n1"], s1=None if self.infer else S["s1"], self_stats=self_st)):
+            if not fused or in_st is not None or self_st:
                 ops.groupnorm_fwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["gn"],
                                   S["stg"], ST_GN_EPS, False, in_stats=in_st)
             # proj_in, then norm1 in its epilogue (self-attention input)

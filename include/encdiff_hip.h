@@ -158,6 +158,20 @@ typedef struct EncdiffGemmArgs {
                                 to finish a tile (one int ticket per output tile, zero on entry,
                                 left zero) sums the tile's slabs in split order (reproducible)
                                 and applies alpha/bias/resid; no finalize pass.  NULL: finalize */
+  /* optional (agn_gamma != NULL), forward 3x3 convolutions OPA_IM2COL x OPB_ROWK (resample NONE /
+     UP2, OUT_BF16, tile 0 or 4): the A operand is GroupNorm32(+FiLM)(+SiLU) of the im2col source x
+     -- ResBlock in_layers / out_layers (openaimodel_enc.py:201-205, 225-232, 267-271; util.py:242-244)
+     -- applied to each staged tile in LDS, so the normalised activation never goes to memory.  Every
+     workgroup computes the statistics (fp32 sum / sum of squares per (image, group), 32 groups) of
+     the images its output rows read, from x itself: x must be complete (no deferred slabs).
+     Replaces the encdiff_groupnorm_fwd launch in front of the conv where nothing saves its output
+     (sampling / inference). */
+  const float* agn_gamma;
+  const float* agn_beta;     /* [cin] */
+  const float* agn_film;     /* optional fp32 [batch][ld_agn_film]: scale at [c], shift at [cin + c] */
+  long ld_agn_film;
+  float agn_eps;
+  int agn_silu;
 } EncdiffGemmArgs;
 
 int encdiff_gemm(const EncdiffGemmArgs* args, void* stream);
@@ -577,8 +591,10 @@ int encdiff_st_tail_fwd(const EncdiffStTailArgs* args, void* stream);
 
 /* The row-local head of a SpatialTransformer (attention.py:250-254, 211): gn = GroupNorm32(x)
  * (from the producer's segment sums gn_in_stats, EncdiffGemmArgs.gn_stats layout, when given --
- * then gn and the per-(image, group) mean / rstd gn_stats are written; else gn is read, computed
- * by encdiff_groupnorm_fwd), t0 = proj_in(gn), n1 = LN1(t0), qkv = n1 [Wq; Wk; Wv]^T, as one kernel
+ * then gn and the per-(image, group) mean / rstd gn_stats are written; with gn_in_stats == gn == NULL
+ * the workgroup computes the statistics of its images from x itself and gn is not written
+ * (inference); else gn is read, computed by encdiff_groupnorm_fwd), t0 = proj_in(gn),
+ * n1 = LN1(t0), qkv = n1 [Wq; Wk; Wv]^T, as one kernel
  * (c in {64, 128}).  n1 / s1 optional (training saves).  Replaces up to three launches. */
 typedef struct EncdiffStHeadArgs {
   int rows, c, tokens, pad_;

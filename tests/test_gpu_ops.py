@@ -536,6 +536,35 @@ def test_attention(O, B, heads, sq, sk, dh, cross):
     _attention_case(O, B, heads, sq, sk, dh, cross, fp8=False)
 
 
+@pytest.mark.parametrize("qscale", [1.0, 12.0], ids=["bound", "running_max"])
+@pytest.mark.parametrize("B,heads,sq,sk,dh", [(4, 8, 256, 256, 8), (4, 8, 64, 64, 16), (4, 8, 16, 20, 32),
+                                              (4, 8, 256, 20, 8), (2, 4, 48, 40, 16)])
+def test_attention_fwd_score_bound(O, B, heads, sq, sk, dh, qscale):
+    """Forward softmax offsets: rows whose Cauchy-Schwarz score bound |q| max|k| scale log2e is small
+    use it as a fixed offset (no running max); large scores (q x 12) take the online-max path.  Both:
+    output and natural-log LSE vs torch fp32 (the LSE feeds the backward)."""
+    torch.manual_seed(9)
+    C = heads * dh
+    q = (torch.randn(B * sq, C, device=dev) * qscale).to(torch.bfloat16)
+    kv = bf(B * sk, 2 * C)
+    k, v = kv[:, :C], kv[:, C:]
+    o = torch.empty(B * sq, C, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * heads, sq, device=dev)
+    O.attention_fwd(q, k, v, o, lse, B, heads, sq, sk, dh)
+
+    def split(t, s):
+        return t.float().reshape(B, s, heads, dh).permute(0, 2, 1, 3).reshape(B * heads, s, dh)
+    sc = split(q, sq) @ split(k, sk).transpose(1, 2) * dh ** -0.5
+    ref = (sc.softmax(-1) @ split(v, sk)).reshape(B, heads, sq, dh).permute(0, 2, 1, 3).reshape(B * sq, C)
+    lref = torch.logsumexp(sc, -1)
+    bound = (split(q, sq).norm(dim=-1, keepdim=True) * split(k, sk).norm(dim=-1).amax(-1)[:, None, None]
+             * dh ** -0.5 / math.log(2)).amax().item()
+    print(f"max row score bound (log2) {bound:.1f}: out rel-L2 {rel(o, ref):.3e}, "
+          f"lse max-abs {(lse - lref).abs().max().item():.3e}")
+    assert rel(o, ref) < 1e-2
+    assert (lse - lref).abs().max().item() < 2e-3 * max(1.0, lref.abs().max().item())
+
+
 @pytest.mark.parametrize("B,heads,sq,sk,dh,cross", [(2, 8, 1024, 1024, 16, False), (4, 8, 256, 256, 32, False),
                                                     (4, 8, 64, 64, 64, False), (4, 8, 256, 20, 16, True)])
 def test_attention_fp8_scores(O, B, heads, sq, sk, dh, cross):
@@ -832,6 +861,36 @@ def test_step_prologue(O):
     assert int(pro.counter) == c0 + 2 and int(step) == s0 + 2 and not torch.equal(a, noise)
 
 
+@pytest.mark.parametrize("B,units", [(128, 20), (600, 40), (1100, 20)])
+def test_encoder_head(O, B, units):
+    """Encoder4's flatten + Linear head (openaimodel_enc.py:1012-1013) on HIP vs torch fp32: u, the
+    trunk gradient dr (bf16) and dW / db -- including batches past the old LDS-staging limit
+    (B >= 410 at 40 units), where du is staged in chunks."""
+    from encdiff_amd import _lib as L, ops as P
+    g = torch.Generator().manual_seed(B + units)
+    d = 128
+    r = torch.randn(B * 16, d, generator=g).to(dev)                       # NHWC rows of the 4x4 trunk output
+    W = (torch.randn(units, d * 16, generator=g) * 0.02).to(dev)
+    bias = torch.randn(units, generator=g).to(dev)
+    flat = r.view(B, 16, d).permute(0, 2, 1).reshape(B, d * 16)           # NCHW flatten (k = c * 16 + p)
+    u = torch.empty(B, units, device=dev)
+    L.check(L.lib.encdiff_encoder_head_fwd(r.data_ptr(), r.stride(0), B, d, W.data_ptr(), bias.data_ptr(), units,
+                                           u.data_ptr(), u.stride(0), P._s()), "head_fwd")
+    assert rel(u, flat @ W.t() + bias) < 1e-5
+    du = torch.randn(B, units, generator=g).to(dev)
+    dr = torch.empty(B * 16, d, device=dev, dtype=torch.bfloat16)
+    dW = torch.zeros_like(W)
+    db = torch.zeros_like(bias)
+    L.check(L.lib.encdiff_encoder_head_bwd(r.data_ptr(), r.stride(0), B, d, W.data_ptr(), units, du.data_ptr(),
+                                           du.stride(0), dr.data_ptr(), dr.stride(0), dW.data_ptr(), db.data_ptr(),
+                                           P._s()), "head_bwd")
+    dflat = du @ W
+    want_dr = dflat.view(B, d, 16).permute(0, 2, 1).reshape(B * 16, d)
+    r_dr, r_dw, r_db = rel(dr.float(), want_dr), rel(dW, du.t() @ flat), rel(db, du.sum(0))
+    print(f"head B={B} units={units}: dr {r_dr:.2e} dW {r_dw:.2e} db {r_db:.2e}")
+    assert r_dr < 1e-2 and r_dw < 1e-5 and r_db < 1e-5
+
+
 @pytest.mark.parametrize("B", [128, 50])
 def test_encoder_warp(O, B):
     """Encoder4.warp on HIP (fp32) vs the as-is torch modules (fp32) on the same params:
@@ -1110,14 +1169,17 @@ def test_groupnorm_from_producer_stats(O, H, C, silu, film):
     assert rel(nhwc(outs[1][0], g), ref) < 1e-2
 
 
-@pytest.mark.parametrize("B,H,cin,cout,split,resid,film", [
-    (128, 2, 256, 256, 8, "sep", False), (8, 4, 256, 256, 16, None, True), (16, 8, 128, 128, 2, "inplace", True),
-    (8, 16, 64, 64, 4, None, False), (8, 2, 256, 256, 32, "inplace", False)])
-def test_groupnorm_from_deferred_finalize(O, B, H, cin, cout, split, resid, film):
+@pytest.mark.parametrize("B,H,cin,cout,split,resid,film,alpha", [
+    (128, 2, 256, 256, 8, "sep", False, 1.0), (8, 4, 256, 256, 16, None, True, 1.0),
+    (16, 8, 128, 128, 2, "inplace", True, 1.0), (8, 16, 64, 64, 4, None, False, 1.0),
+    (8, 2, 256, 256, 32, "inplace", False, 1.0), (8, 4, 256, 256, 16, "sep", True, 0.7),
+    (8, 2, 256, 256, 32, None, False, 1.3)])
+def test_groupnorm_from_deferred_finalize(O, B, H, cin, cout, split, resid, film, alpha):
     """encdiff_gemm_ex with the finalize deferred + GroupNorm forward combining the slabs
     (x_from) vs encdiff_gemm (tile kernel + finalize pass) + GroupNorm: the conv output x, the
     normalised output and the saved statistics bitwise equal (<= 8 slabs in one ordered sum,
-    deeper splits in four z-groups, bias, separate and in-place residual)."""
+    deeper splits in four z-groups, alpha != 1 with a bias -- the two combine copies are built
+    without FMA contraction -- separate and in-place residual)."""
     import ctypes as C
     from encdiff_amd import _lib as L
     from encdiff_amd.ops import Geom, _conv_geom
@@ -1139,7 +1201,7 @@ def test_groupnorm_from_deferred_finalize(O, B, H, cin, cout, split, resid, film
             rs = x if resid == "inplace" else (r if resid == "sep" else None)
             args = O.gemm_args(g.pixels, cout, 9 * cin, a, cin, w, 9 * cin, x, cout, a_mode=L.OPA_IM2COL,
                                conv=_conv_geom(g, cin, L.RESAMPLE_NONE, a), bias=bias, resid=rs,
-                               ld_resid=cout if rs is not None else 0, split_k=split, tile=4)
+                               ld_resid=cout if rs is not None else 0, split_k=split, tile=4, alpha=alpha)
             assert args.split_k == split and not args.split_counters
             planned = C.c_int(-1)
             O.check(O.lib.encdiff_gemm_ex(C.byref(args), int(defer), C.byref(planned), O._s()), "gemm_ex")
@@ -1154,7 +1216,8 @@ def test_groupnorm_from_deferred_finalize(O, B, H, cin, cout, split, resid, film
         O.SPLIT_FOLD = fold
     for u, v in zip(outs[0], outs[1]):
         assert torch.equal(u, v)
-    xr = F.conv2d(nhwc(a, g), w.float().reshape(cout, 3, 3, cin).permute(0, 3, 1, 2), bias, padding=1)
+    xr = alpha * F.conv2d(nhwc(a, g), w.float().reshape(cout, 3, 3, cin).permute(0, 3, 1, 2), None, padding=1)
+    xr = xr + bias.view(1, -1, 1, 1)
     if resid:
         xr = xr + nhwc(r, g)
     assert rel(nhwc(outs[1][0], g), xr) < 1e-2
@@ -1240,11 +1303,13 @@ def test_attention_fwd_streamed_kv(O, B, heads, sq, dh):
     assert rel(lse, torch.logsumexp(s, -1)) < 1e-4
 
 
-@pytest.mark.parametrize("dq,dc,heads,dh,sq,sk", [(64, 320, 8, 8, 256, 20), (128, 128, 4, 32, 64, 64)])
+@pytest.mark.parametrize("dq,dc,heads,dh,sq,sk", [(64, 320, 8, 8, 256, 20), (128, 128, 4, 32, 64, 64),
+                                                 (60, 20, 4, 16, 64, 20), (64, 12, 8, 8, 64, 20)])
 def test_cross_attention_module(O, dq, dc, heads, dh, sq, sk):
     """The standalone CrossAttention module (attention.py:152-193): q / k / v / out on encdiff::linear (GEMM
     engine), MFMA attention, to_out -- forward and the gradients of x, context and the projection
-    weights vs a torch fp32 reference on the same bf16-rounded operands."""
+    weights vs a torch fp32 reference on the same bf16-rounded operands.  Widths that are not
+    multiples of 8 (query_dim 60, context_dim 20 / 12) run zero-padded on the same engine."""
     from encdiff_amd.ldm.modules.attention import CrossAttention
     torch.manual_seed(21)
     m = CrossAttention(dq, context_dim=dc, heads=heads, dim_head=dh).cuda()

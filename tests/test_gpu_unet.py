@@ -223,6 +223,9 @@ def test_unet_gn_fin_bitwise(unet, B, train):
     ops.groupnorm_bwd = counted_b
     ops.layernorm_bwd = counted_l
 
+    agn = U.AGN
+    U.AGN = False  # inference at B = 8 would fold these GroupNorms into the convs (test_unet_agn_inference)
+
     def run(on):
         U.GN_FIN = on
         fused.clear()
@@ -243,6 +246,7 @@ def test_unet_gn_fin_bitwise(unet, B, train):
         b, n_off = run(False)
     finally:
         U.GN_FIN = True
+        U.AGN = agn
         ops.groupnorm_fwd, ops.groupnorm_bwd, ops.layernorm_bwd = orig, orig_b, orig_l
     print(f"B={B}: {n_on % 1000} GroupNorm forwards / {n_on // 1000} Group/LayerNorm backwards combined their "
           f"producer's slabs")
@@ -251,6 +255,55 @@ def test_unet_gn_fin_bitwise(unet, B, train):
         assert n_on // 1000 > 0
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("res", [True, False], ids=["resblocks", "st_heads"])
+@pytest.mark.parametrize("B", [2, 8, 32])
+def test_unet_agn_inference(unet, B, res):
+    """Inference at sampling batches folds every non-down ResBlock's GroupNorm32(+FiLM)+SiLU into
+    the A staging of the conv that reads it (EncdiffGemmArgs.agn_*: per-workgroup statistics from
+    x itself, the tile normalised in LDS): eps vs the CPU oracle within the bf16 bound, vs the
+    separate GroupNorm launches within the same bound (two bf16 paths with different rounding
+    points), and only the three down blocks' GN1 (their conv reads the pooled output), the six c = 256
+    transformer GroupNorms
+    (the fused c <= 128 heads compute theirs in the kernel) and the output GroupNorm still launch
+    encdiff_groupnorm_fwd.  res=False (the default, U.AGN_RES: measured faster for DDIM at B = 8) keeps
+    the ResBlock GroupNorm launches and folds only the ten fused transformer heads' statistics."""
+    from encdiff_amd import ops, unet as U
+    from oracle import encdiff_oracle as O
+    g = torch.Generator().manual_seed(B)
+    x = torch.randn(B, 3, 16, 16, generator=g)
+    t = torch.randint(0, 1000, (B,), generator=g)
+    c = torch.randn(B, 320, generator=g) * 0.5
+    calls = []
+    orig = ops.groupnorm_fwd
+
+    def counted(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+    ops.groupnorm_fwd = counted
+    agn_res = U.AGN_RES
+    U.AGN_RES = res
+    try:
+        with torch.no_grad():
+            U.AGN = True
+            e_f = unet(x.cuda(), t.cuda(), context=[c.cuda()]).cpu()
+            n_f = len(calls)
+            calls.clear()
+            U.AGN = False
+            e_u = unet(x.cuda(), t.cuda(), context=[c.cuda()]).cpu()
+            n_u = len(calls)
+    finally:
+        U.AGN = True
+        U.AGN_RES = agn_res
+        ops.groupnorm_fwd = orig
+    P = O.recipe_params(O.param_shapes(O.build_plan()))
+    ref = O.unet_forward(P, O.build_plan(), x, t, [c])
+    r_ref, r_unf, mab = rel(e_f, ref), rel(e_f, e_u), (e_f - ref).abs().max().item()
+    print(f"B={B}: agn eps rel-L2 vs oracle {r_ref:.3e} (max-abs {mab:.3e}), vs GroupNorm launches {r_unf:.3e}; "
+          f"groupnorm_fwd launches {n_f} (without: {n_u})")
+    assert r_ref < EPS_TOL and mab < MAXABS_TOL and r_unf < EPS_TOL
+    assert n_f == (3 + 6 + 1 if res else 28 * 2 + 6 + 1) and n_u == 28 * 2 + 16 + 1
 
 
 def test_st_tail_fused_inference(unet, golden_dir):

@@ -56,10 +56,13 @@ def main():
         fwd = lambda: ops.groupnorm_fwd(x, g, gam, bet, y, st, 1e-5, True, film=film, ld_film=2 * C)
         bwd = lambda: ops.groupnorm_bwd(x, g, gam, bet, st, 1e-5, True, dy, dx, dgp, dbp, film=film, ld_film=2 * C,
                                         dfilm=dfilm, ld_dfilm=2 * C)
+        rs = torch.randn_like(x)
+        bwr = lambda: ops.groupnorm_bwd(x, g, gam, bet, st, 1e-5, True, dy, dx, dgp, dbp, film=film, ld_film=2 * C,
+                                        dfilm=dfilm, ld_dfilm=2 * C, resid=rs)
         cp = lambda: ops.ew(L.EW_COPY, x, y)
-        tf, tb, tc = timed(fwd), timed(bwd), timed(cp)
+        tf, tb, tr, tc = timed(fwd), timed(bwd), timed(bwr), timed(cp)
         print(f"H={H:2d} C={C:3d} MB={x.numel() * 2 / 1e6:6.2f}  gn_fwd {tf:6.2f} us  gn_bwd {tb:6.2f} us  "
-              f"copy {tc:6.2f} us", flush=True)
+              f"+resid {tr:6.2f} us  copy {tc:6.2f} us", flush=True)
 
 
 if __name__ == "__main__":
