@@ -34,8 +34,12 @@ def _headers():
     return hs
 
 
-# per-file extra flags: the attention kernels' softmax max trees need no NaN canonicalisation
-FILE_FLAGS = {"attn_mfma.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]}
+# per-file extra flags: the attention kernels' softmax max trees need no NaN canonicalisation;
+# the norm kernels contract a*b+c only within one source expression (-ffp-contract=on): their
+# template instantiations (GroupNorm backward with / without slab input, the split-K combine
+# restated from gemm.hip) must round identically, and "fast" fuses across statements
+# differently per instantiation (test_unet_gn_fin_bitwise)
+FILE_FLAGS = {"attn_mfma.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"], "norm.hip": ["-ffp-contract=on"]}
 
 
 def _compile(src: str, obj: str, verbose: bool):

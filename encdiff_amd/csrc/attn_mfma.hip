@@ -279,7 +279,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
         for (int kc = 0; kc < KC; ++kc) n2 += bf16_sq4(qf[u][kc]);
         n2 = sum_x32(sum_x16(n2));
         // small relative + absolute slack over the fp32 rounding of the MFMA dot products
-        mb[u] = __builtin_sqrtf(n2 * k2) * sl2 * 1.001f + 1e-6f;
+        mb[u] = __builtin_amdgcn_sqrtf(n2 * k2) * sl2 * 1.001f + 1e-6f;  // raw v_sqrt (bound only)
         ok = ok && mb[u] <= FWD_BOUND_MAX;
       }
       if (!__all(ok)) return false;
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
         lu = l[u];
         lu = sum_x32(sum_x16(lu));
       }
-      const float inv = 1.f / lu;
+      const float inv = __builtin_amdgcn_rcpf(lu);  // v_rcp_f32 (1 ulp; lu >= 1 or a normal bound-path sum)
       if (q[u] < SQ) {
         bf16_t* op = (bf16_t*)p.o + ((long)b * SQ + q[u]) * p.ldo + h * DH;
 #pragma unroll
@@ -533,8 +533,10 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
         *(uint4*)hb = qv;
         *(uint4*)(hb + oG) = gv;
         if (cq == 0) {
-          fls[hq * 2 * SQP + rq] = lq;
-          fls[hq * 2 * SQP + SQP + rq] = d;
+          // both row constants stored NEGATED: -lse2 is the exp argument's addend and -D the dP
+          // accumulator's initial value (no sign flips in the per-score loops)
+          fls[hq * 2 * SQP + rq] = -lq;
+          fls[hq * 2 * SQP + SQP + rq] = -d;
         }
       }
       if (e < nk) {
@@ -598,7 +600,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
         auto qstep = [&](const int qt, const int u) {
           // dP starts from -D (the row constant in the accumulator): dS = P * dP needs no subtraction
           const float4 dv4 = *(const float4*)(Dv + qt * 16 + 4 * g);
-          v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {-dv4.x, -dv4.y, -dv4.z, -dv4.w};
+          v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {dv4.x, dv4.y, dv4.z, dv4.w};
           if constexpr (F8) {
 #pragma unroll
             for (int kc = 0; kc < KC8; ++kc) s = mma8(frag8<DH>(Qs, RP, qt * 16 + l16, kc, g), kf8[kc], s);
@@ -614,7 +616,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
             const v2f sl = {sl2, sl2};
 #pragma unroll
             for (int i = 0; i < 4; i += 2) {
-              const v2f e = __builtin_elementwise_fma((v2f){s[i], s[i + 1]}, sl, (v2f){-lse[q0 + i], -lse[q0 + i + 1]});
+              const v2f e = __builtin_elementwise_fma((v2f){s[i], s[i + 1]}, sl, (v2f){lse[q0 + i], lse[q0 + i + 1]});
               pv[i] = (!MASK || (kv && q0 + i < SQ)) ? ex2(e[0]) : 0.f;
               pv[i + 1] = (!MASK || (kv && q0 + i + 1 < SQ)) ? ex2(e[1]) : 0.f;
             }
@@ -724,7 +726,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
     auto qstep = [&](const int qt, const int u) {
         // dP starts from -D (the row constant in the accumulator): dS = P * dP needs no subtraction
         const float4 dv4 = *(const float4*)(Dv + qt * 16 + 4 * g);
-        v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {-dv4.x, -dv4.y, -dv4.z, -dv4.w};
+        v4f s = {0.f, 0.f, 0.f, 0.f}, dp = {dv4.x, dv4.y, dv4.z, dv4.w};
         if constexpr (F8) {
 #pragma unroll
           for (int kc = 0; kc < KC8; ++kc) s = mma8(frag8<DH>(Qs, RP, qt * 16 + l16, kc, g), kf8[kc], s);
@@ -740,7 +742,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
           const v2f sl = {sl2, sl2};
 #pragma unroll
           for (int i = 0; i < 4; i += 2) {
-            const v2f e = __builtin_elementwise_fma((v2f){s[i], s[i + 1]}, sl, (v2f){-lse[q0 + i], -lse[q0 + i + 1]});
+            const v2f e = __builtin_elementwise_fma((v2f){s[i], s[i + 1]}, sl, (v2f){lse[q0 + i], lse[q0 + i + 1]});
             pv[i] = (!MASK || (kv && q0 + i < SQ)) ? ex2(e[0]) : 0.f;
             pv[i + 1] = (!MASK || (kv && q0 + i + 1 < SQ)) ? ex2(e[1]) : 0.f;
           }
@@ -864,7 +866,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
       }
       if (kt0 < ktiles) kstep(kt0, 0);
     } else {
-      const float lq = lse[q], Dq = Dv[q];
+      const float nlq = lse[q], nDq = Dv[q];  // -lse2, -D (stored negated)
       s4 qf[KC], gf[KC];
       long qf8[KC8];
 #pragma unroll
@@ -877,7 +879,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
         for (int kc = 0; kc < KC8; ++kc) qf8[kc] = frag8<DH>(Qs, RP, q, kc, g);
       }
       auto kstep = [&](const int kt, const int u) {
-        v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {-Dq, -Dq, -Dq, -Dq};  // dP^T - D from the accumulator
+        v4f st = {0.f, 0.f, 0.f, 0.f}, dpt = {nDq, nDq, nDq, nDq};  // dP^T - D from the accumulator
         if constexpr (F8) {
 #pragma unroll
           for (int kc = 0; kc < KC8; ++kc) st = mma8(frag8<DH>(Ks, RP, kt * 16 + l16, kc, g), qf8[kc], st);
@@ -891,7 +893,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int key = kt * 16 + 4 * g + i;
-          const float pr = (!MASK || (qv && key < SK)) ? ex2(__builtin_fmaf(st[i], sl2, -lq)) : 0.f;
+          const float pr = (!MASK || (qv && key < SK)) ? ex2(__builtin_fmaf(st[i], sl2, nlq)) : 0.f;
           ds[i] = pr * dpt[i];
         }
         const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);

@@ -18,6 +18,12 @@ typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
 #define ED_DEV __device__ __forceinline__
 
 ED_DEV float bf2f(bf16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+// Split-K combine epilogue alpha * sum (+ bias): ONE explicit FMA (bias 0 when absent), so every
+// restatement of the combine (finalize pass, in-kernel fold, the GroupNorm / LayerNorm slab
+// combines) rounds alike whatever -ffp-contract=fast does with the surrounding code -- that flag
+// fuses across statements and ignores `#pragma clang fp contract`.  The residual is a plain add
+// of this result (nothing left to contract).
+ED_DEV float splitk_scale(float acc, float alpha, float bias) { return __builtin_fmaf(alpha, acc, bias); }
 ED_DEV bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN preserving
   return __builtin_bit_cast(bf16_t, b);

@@ -1016,12 +1016,15 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
         v[0] += a0.x; v[1] += a0.y; v[2] += a0.z; v[3] += a0.w;
         v[4] += a1.x; v[5] += a1.y; v[6] += a1.z; v[7] += a1.w;
       }
+      {
+        float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (f.bias) {
+          const float4 b0 = *(const float4*)(f.bias + col), b1 = *(const float4*)(f.bias + col + 4);
+          bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+          bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+        }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] *= f.alpha;
-      if (f.bias) {
-        const float4 b0 = *(const float4*)(f.bias + col), b1 = *(const float4*)(f.bias + col + 4);
-        v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
-        v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+        for (int k = 0; k < 8; ++k) v[k] = splitk_scale(v[k], f.alpha, bb[k]);
       }
       if (f.resid) {
         float rr[8];
@@ -1184,8 +1187,7 @@ __device__ __forceinline__ long fin_row(const EncdiffGemmArgs& p, int m) {
 __device__ __forceinline__ void fin_store(const EncdiffGemmArgs& p, const bf16_t* R, const long i, float v) {
   const int row0 = (int)(i / p.N), col = (int)(i - (long)row0 * p.N);
   const long row = fin_row(p, row0);
-  v *= p.alpha;
-  if (p.bias) v += p.bias[col];
+  v = splitk_scale(v, p.alpha, p.bias ? p.bias[col] : 0.f);
   if (R) v += bf2f(R[(long)row * p.ld_resid + col]);
   if (p.c_mode == ENCDIFF_OUT_BF16) ((bf16_t*)p.c)[(long)row * p.ldc + col] = f2bf(v);
   else if (p.c_mode == ENCDIFF_OUT_F32_ACCUM) ((float*)p.c)[(long)row * p.ldc + col] += v;
@@ -1193,8 +1195,7 @@ __device__ __forceinline__ void fin_store(const EncdiffGemmArgs& p, const bf16_t
 }
 
 __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const int bid, const int nblk) {
-  // no FMA contraction: norm.hip's gn_slab_row restates this combine and must round identically
-#pragma clang fp contract(off)
+  // alpha / bias through splitk_scale: norm.hip's gn_slab_row restates this combine bitwise
   __shared__ float4 part[FIN_ZG][64];
   const long total = (long)p.M * p.N;
   const bf16_t* R = (const bf16_t*)p.resid;
@@ -1230,10 +1231,14 @@ __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const in
         const int row0 = total < (1L << 31) ? (int)i / p.N : (int)(i / p.N);
         const int col = (int)(i - (long)row0 * p.N);
         const long row = fin_row(p, row0);
-        float v[4] = {p.alpha * acc.x, p.alpha * acc.y, p.alpha * acc.z, p.alpha * acc.w};
-        if (p.bias) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) v[k] += p.bias[col + k];
+        float v[4];
+        {
+          const float4 bb = p.bias ? make_float4(p.bias[col], p.bias[col + 1], p.bias[col + 2], p.bias[col + 3])
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+          v[0] = splitk_scale(acc.x, p.alpha, bb.x);
+          v[1] = splitk_scale(acc.y, p.alpha, bb.y);
+          v[2] = splitk_scale(acc.z, p.alpha, bb.z);
+          v[3] = splitk_scale(acc.w, p.alpha, bb.w);
         }
         if (R) {
 #pragma unroll

@@ -13,6 +13,9 @@
 
 namespace {
 
+#ifndef ED_GN_SLAB_U
+#define ED_GN_SLAB_U 1  // backward, dy from slabs: rows per load batch
+#endif
 #ifndef ED_GN_BWD_U
 #define ED_GN_BWD_U 4  // backward rows per load batch (code size vs loads in flight)
 #endif
@@ -165,8 +168,7 @@ ED_DEV void gn_slab_batch(const float* w, long stride, int z0, int split, float 
 }
 
 ED_DEV uint4 gn_slab_row(const GnSlabs& sl, long row, int c, int cb) {
-  // no FMA contraction: gemm.hip's gemm_finalize does this combine too, bitwise alike
-#pragma clang fp contract(off)
+  // alpha / bias through splitk_scale: gemm.hip's gemm_finalize does this combine too, bitwise alike
   const float* w = sl.ws + row * c + cb;
   float a[8], v[8][8];
   if (sl.split <= 8) {
@@ -199,12 +201,10 @@ ED_DEV uint4 gn_slab_row(const GnSlabs& sl, long row, int c, int cb) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] = ((g[0][i] + g[1][i]) + g[2][i]) + g[3][i];
   }
+  float bb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (sl.bias) load8f(sl.bias + cb, bb);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) a[i] = sl.alpha * a[i];
-  if (sl.bias) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] += sl.bias[cb + i];
-  }
+  for (int i = 0; i < 8; ++i) a[i] = splitk_scale(a[i], sl.alpha, bb[i]);
   if (sl.resid) {
     float r[8];
     unpack8(*(const uint4*)(sl.resid + row * sl.ld_resid + cb), r);
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const EncdiffGroup
 template <bool SLAB>
 __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNormArgs p, int cs, const GnSlabs sl) {
   __shared__ uint4 tx[GN_TILE], td[GN_TILE];
-  __shared__ float red[4 * 2048], chs[4 * 512], gsh[2 * 64];
+  __shared__ float red[4 * 2048], chs[4 * 512], gam_sh[512];
   const GnSlice L(p, cs);
   const int HW = p.hw;
   const bool film = p.film != nullptr, silu = p.silu;
@@ -500,8 +500,8 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
     sc1[i] = film ? 1.f + sc1[i] : 1.f;
     sf[i] = film ? sf[i] : 0.f;
   }
-  // gamma of the channel this thread finishes after the reduction, loaded now (off the chain)
-  const float gam0 = threadIdx.x < L.cs ? p.gamma[L.c0 + threadIdx.x] : 0.f;
+  // the slice's gamma in LDS for the group terms (published by the reduction's barriers)
+  for (int cl = threadIdx.x; cl < L.cs; cl += GN_THREADS) gam_sh[cl] = p.gamma[L.c0 + cl];
   // pass 1: per-channel sums of dn, dn*xhat, dz, dz*n
   float acc[4][8];
 #pragma unroll
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   if (L.active) {
     // rows per batch: every load of a batch issued before the first use (a slab row already
     // has up to 8 loads in flight)
-    constexpr int U1 = SLAB ? 1 : ED_GN_BWD_U;
+    constexpr int U1 = SLAB ? ED_GN_SLAB_U : ED_GN_BWD_U;
     for (int px0 = L.tp; px0 < HW; px0 += U1 * L.np) {
     uint4 bx[U1], bd[U1];
 #pragma unroll
@@ -555,7 +555,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   float* gch = red;  // [2][cs] (red is free after the reduction)
   for (int cl = threadIdx.x; cl < L.cs; cl += GN_THREADS) {
     const int c = L.c0 + cl;
-    const float gam = cl == (int)threadIdx.x ? gam0 : p.gamma[c];
+    const float gam = gam_sh[cl];
     p.dbeta_part[(long)L.b * p.ld_part + c] = chs[cl];
     p.dgamma_part[(long)L.b * p.ld_part + c] = chs[L.cs + cl];
     if (film) {
@@ -566,6 +566,9 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
     gch[L.cs + cl] = gam * chs[L.cs + cl];
   }
   __syncthreads();
+  // group sums by one thread per group (a per-thread sum over the group's channels instead, with no
+  // barrier, measured slower: a dependent chain of cpg LDS reads per thread, +0.2 .. +1 us)
+  float* gsh = red + 2 * L.cs;  // [2][64]
   if (threadIdx.x < L.gs) {
     float s1 = 0.f, s2 = 0.f;
     for (int cl = threadIdx.x * L.cpg; cl < (threadIdx.x + 1) * L.cpg; ++cl) {

@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 4: attention trims (raw rcp / sqrt, negated row constants) -- op tests, timing, UNet tests, short bench
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-$(pwd)} && mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -x -q -m gpu -k "attention" --timeout 200 --timeout-method thread > gpurun_out/ops16.log 2>&1 || { grep -E "FAIL|Error|assert" gpurun_out/ops16.log | head -20; tail -30 gpurun_out/ops16.log; exit 1; }
+tail -1 gpurun_out/ops16.log
+timeout -k 10 200 python -u tools/attn_bench.py > gpurun_out/attn_bench.txt 2>&1 || { tail -5 gpurun_out/attn_bench.txt; exit 1; }
+grep sq= gpurun_out/attn_bench.txt
+timeout -k 10 600 python -u -m pytest tests/test_gpu_unet.py tests/test_gpu_ldm.py -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/unet16.log 2>&1 || { grep -E "FAIL|Error|assert" gpurun_out/unet16.log | head; tail -20 gpurun_out/unet16.log; exit 1; }
+tail -1 gpurun_out/unet16.log
+timeout -k 10 400 python bench.py --skip-cpu --steps 30 > gpurun_out/b16.log 2>&1 || { tail -5 gpurun_out/b16.log; exit 1; }
+tail -1 gpurun_out/b16.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], d['ddim_steps_per_sec'], d['ddim_steps_per_sec_b128'], d.get('ddim_log_images_s'))"
