@@ -13,6 +13,9 @@
 
 namespace {
 
+#ifndef ED_GN_STAMP
+#define ED_GN_STAMP 0  // diagnostic builds: phase stamps of the GroupNorm backward (tools/gn_stamps.py)
+#endif
 #ifndef ED_GN_SLAB_U
 #define ED_GN_SLAB_U 1  // backward, dy from slabs: rows per load batch
 #endif
@@ -68,8 +71,10 @@ ED_DEV void load8f(const float* p, float* v) {
 // the slice into out[NQ][cs] (LDS).  Power-of-two nvc: xor-shuffles inside each wave, then
 // the wave rows are added in order; otherwise every pixel-lane row goes through LDS and a
 // thread per channel adds the rows in order.  Ends with a barrier.
+// First half of slice_reduce: the per-lane partials reduced across lanes into `rows` partial rows
+// red[(r * NQ + k) * cs + c] (ends with a barrier); returns rows.
 template <int NQ>
-ED_DEV void slice_reduce(float (&q)[NQ][8], const GnSlice& L, float* red, float* out) {
+ED_DEV int slice_partials(float (&q)[NQ][8], const GnSlice& L, float* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool pow2 = (L.nvc & (L.nvc - 1)) == 0;
   int rows;
@@ -125,6 +130,12 @@ ED_DEV void slice_reduce(float (&q)[NQ][8], const GnSlice& L, float* red, float*
     rows = L.np;
   }
   __syncthreads();
+  return rows;
+}
+
+template <int NQ>
+ED_DEV void slice_reduce(float (&q)[NQ][8], const GnSlice& L, float* red, float* out) {
+  const int rows = slice_partials<NQ>(q, L, red);
   for (int e = threadIdx.x; e < NQ * L.cs; e += GN_THREADS) {
     const int k = e / L.cs, c = e - k * L.cs;
     float a = 0.f;
@@ -473,10 +484,30 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const EncdiffGroup
 
 // SLAB: dy is combined from its producer's deferred split-K slabs (a separate instantiation: the
 // slab combine unrolled into the plain kernel doubled its code and pushed it past 256 VGPRs)
+#if ED_GN_STAMP
+// phase stamps of the GroupNorm backward (diagnostic builds only, tools/gn_stamps.py): per block,
+// thread 0: [0] realtime at entry, [1..6] shader clock at entry / after the constants / after pass
+// 1 / after the reduction / after the group terms / at exit, [7] realtime at exit
+__device__ unsigned long long gn_stamps[16384][8];
+#define GN_STAMP(i)                                                                        \
+  do {                                                                                     \
+    if (threadIdx.x == 0 && blockIdx.x < 16384) gn_stamps[blockIdx.x][i] = __builtin_readcyclecounter(); \
+  } while (0)
+#define GN_STAMP_RT(i)                                                                     \
+  do {                                                                                     \
+    if (threadIdx.x == 0 && blockIdx.x < 16384) gn_stamps[blockIdx.x][i] = wall_clock64(); \
+  } while (0)
+#else
+#define GN_STAMP(i) do {} while (0)
+#define GN_STAMP_RT(i) do {} while (0)
+#endif
+
 template <bool SLAB>
 __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNormArgs p, int cs, const GnSlabs sl) {
   __shared__ uint4 tx[GN_TILE], td[GN_TILE];
   __shared__ float red[4 * 2048], chs[4 * 512], gam_sh[512];
+  GN_STAMP_RT(0);
+  GN_STAMP(1);
   const GnSlice L(p, cs);
   const int HW = p.hw;
   const bool film = p.film != nullptr, silu = p.silu;
@@ -500,58 +531,108 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
     sc1[i] = film ? 1.f + sc1[i] : 1.f;
     sf[i] = film ? sf[i] : 0.f;
   }
-  // the slice's gamma in LDS for the group terms (published by the reduction's barriers)
-  for (int cl = threadIdx.x; cl < L.cs; cl += GN_THREADS) gam_sh[cl] = p.gamma[L.c0 + cl];
+  // the slice's gamma for the group terms: loaded now into registers, stored to LDS after pass 1
+  // (a store here would wait for the load before pass 1 issues its own)
+  float gam_r[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int cl = threadIdx.x + j * GN_THREADS;
+    gam_r[j] = cl < L.cs ? p.gamma[L.c0 + cl] : 0.f;
+  }
+  GN_STAMP(2);
+  bf16_t* DX = (bf16_t*)p.dx + off * p.lddx + L.cb;
+  const bool accum = p.accumulate_dx;
+  const bf16_t* RS = p.resid ? (const bf16_t*)p.resid + off * p.ld_resid + L.cb : nullptr;
+  // rows per batch: every load of a batch issued before the first use (a slab row already has up
+  // to 8 loads in flight)
+  constexpr int U1 = SLAB ? ED_GN_SLAB_U : ED_GN_BWD_U;
+  // ONE: the thread's rows are a single batch (every level at B = 128 but 16x16 x 192): pass 1
+  // keeps dn and xhat of its rows in registers and issues pass 2's global operand (skip-branch
+  // gradient / the dx being accumulated) with its own loads, before the reductions, so pass 2 is
+  // three FMAs and a store per element instead of a second load round trip and a recompute of
+  // the SiLU gradient.  (Issuing these loads ahead of the per-channel constants measured no gain.)
+  constexpr bool CACHE = !SLAB;
+  const bool one = CACHE && HW <= U1 * L.np;
+  float cdn[U1][8], cxh[U1][8];
+  uint4 gr0[U1];
   // pass 1: per-channel sums of dn, dn*xhat, dz, dz*n
   float acc[4][8];
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[k][i] = 0.f;
-  if (L.active) {
-    // rows per batch: every load of a batch issued before the first use (a slab row already
-    // has up to 8 loads in flight)
-    constexpr int U1 = SLAB ? ED_GN_SLAB_U : ED_GN_BWD_U;
-    for (int px0 = L.tp; px0 < HW; px0 += U1 * L.np) {
-    uint4 bx[U1], bd[U1];
+  auto row1 = [&](const uint4 ux, const uint4 ud, const int u, const bool keep) {
+    float v[8], d[8];
+    unpack8(ux, v);
+    unpack8(ud, d);
 #pragma unroll
-    for (int u = 0; u < U1; ++u) {
-      const int px = px0 + u * L.np;
-      bx[u] = bd[u] = (uint4){0u, 0u, 0u, 0u};
-      if (px < HW) {
-        bx[u] = *(const uint4*)(X + (long)px * p.ldx);
-        if constexpr (SLAB) {  // dy combined from its producer's slabs and written back
-          bd[u] = gn_slab_row(sl, off + px, p.c, L.cb);
-          *(uint4*)(const_cast<bf16_t*>(DY) + (long)px * p.lddy) = bd[u];
-        } else {
+    for (int i = 0; i < 8; ++i) {
+      const float xh = (v[i] - xm[i]) * xr[i];
+      const float n = xh * ga[i] + be[i];
+      const float z = n * sc1[i] + sf[i];
+      const float dz = silu ? d[i] * silu_grad(z) : d[i];
+      const float dn = dz * sc1[i];
+      acc[0][i] += dn; acc[1][i] += dn * xh;
+      acc[2][i] += dz; acc[3][i] += dz * n;
+      if (keep) { cdn[u][i] = dn; cxh[u][i] = xh; }
+    }
+  };
+  if (L.active) {
+    if (one) {
+      uint4 bx[U1], bd[U1];
+#pragma unroll
+      for (int u = 0; u < U1; ++u) {
+        const int px = L.tp + u * L.np;
+        bx[u] = bd[u] = gr0[u] = (uint4){0u, 0u, 0u, 0u};
+        if (px < HW) {
+          bx[u] = *(const uint4*)(X + (long)px * p.ldx);
           bd[u] = *(const uint4*)(DY + (long)px * p.lddy);
+          if (RS) gr0[u] = *(const uint4*)(RS + (long)px * p.ld_resid);
+          else if (accum) gr0[u] = *(const uint4*)(DX + (long)px * p.lddx);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U1; ++u) {
+        if (L.tp + u * L.np < HW) row1(bx[u], bd[u], u, true);
+      }
+    } else {
+      for (int px0 = L.tp; px0 < HW; px0 += U1 * L.np) {
+        uint4 bx[U1], bd[U1];
+#pragma unroll
+        for (int u = 0; u < U1; ++u) {
+          const int px = px0 + u * L.np;
+          bx[u] = bd[u] = (uint4){0u, 0u, 0u, 0u};
+          if (px < HW) {
+            bx[u] = *(const uint4*)(X + (long)px * p.ldx);
+            if constexpr (SLAB) {  // dy combined from its producer's slabs and written back
+              bd[u] = gn_slab_row(sl, off + px, p.c, L.cb);
+              *(uint4*)(const_cast<bf16_t*>(DY) + (long)px * p.lddy) = bd[u];
+            } else {
+              bd[u] = *(const uint4*)(DY + (long)px * p.lddy);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U1; ++u) {
+          const int px = px0 + u * L.np;
+          if (px >= HW) break;
+          if (L.tiled) { tx[px * L.nvc + L.tv] = bx[u]; td[px * L.nvc + L.tv] = bd[u]; }
+          row1(bx[u], bd[u], u, false);
         }
       }
     }
-#pragma unroll
-    for (int u = 0; u < U1; ++u) {
-      const int px = px0 + u * L.np;
-      if (px >= HW) break;
-      const uint4 ux = bx[u], ud = bd[u];
-      if (L.tiled) { tx[px * L.nvc + L.tv] = ux; td[px * L.nvc + L.tv] = ud; }
-      float v[8], d[8];
-      unpack8(ux, v);
-      unpack8(ud, d);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float xh = (v[i] - xm[i]) * xr[i];
-        const float n = xh * ga[i] + be[i];
-        const float z = n * sc1[i] + sf[i];
-        const float dz = silu ? d[i] * silu_grad(z) : d[i];
-        const float dn = dz * sc1[i];
-        acc[0][i] += dn; acc[1][i] += dn * xh;
-        acc[2][i] += dz; acc[3][i] += dz * n;
-      }
-    }
-    }
   }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int cl = threadIdx.x + j * GN_THREADS;
+    if (cl < L.cs) gam_sh[cl] = gam_r[j];
+  }
+  GN_STAMP(3);
   slice_reduce<4>(acc, L, red, chs);
-  // per-channel outputs + gamma-weighted sums for the group terms
+  GN_STAMP(4);
+  // per-channel outputs + gamma-weighted sums for the group terms.  (Threads owning a whole group
+  // -- channel totals, partials and group terms behind ONE barrier -- measured slower: +0.3 us at
+  // cpg 2, +3.5 us at cpg 16, the few group threads' serial loops outweigh the two barriers.)
   float* gch = red;  // [2][cs] (red is free after the reduction)
   for (int cl = threadIdx.x; cl < L.cs; cl += GN_THREADS) {
     const int c = L.c0 + cl;
@@ -586,52 +667,67 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
     const int g = (L.tv * 8 + i) / L.cpg;
     m1[i] = gsh[g]; m2[i] = gsh[64 + g];
   }
-  bf16_t* DX = (bf16_t*)p.dx + off * p.lddx + L.cb;
-  const bool accum = p.accumulate_dx;
-  const bf16_t* RS = p.resid ? (const bf16_t*)p.resid + off * p.ld_resid + L.cb : nullptr;
-  // U rows per thread: the global (resid / accumulate) reads of all U are issued before the
-  // first dx store -- one latency per U rows instead of one per row
-  constexpr int U = ED_GN_BWD_U;
-  for (int px0 = L.tp; px0 < HW; px0 += U * L.np) {
-    uint4 gr[U];
+  GN_STAMP(5);
+  auto out_row = [&](const int px, const uint4 g, const float (&dn)[8], const float (&xh)[8]) {
+    float o[8];
+    if (RS && accum) {  // both: dx (in place) + resid
+      float rr[8];
+      unpack8(*(const uint4*)(DX + (long)px * p.lddx), o);
+      unpack8(g, rr);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int px = px0 + u * L.np;
-      gr[u] = (uint4){0u, 0u, 0u, 0u};
-      if (px < HW) {
-        if (RS) gr[u] = *(const uint4*)(RS + (long)px * p.ld_resid);
-        else if (accum) gr[u] = *(const uint4*)(DX + (long)px * p.lddx);
-      }
+      for (int i = 0; i < 8; ++i) o[i] += rr[i];
+    } else if (RS || accum) {
+      unpack8(g, o);  // residual-branch gradient (skip connection) or the dx being accumulated
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int px = px0 + u * L.np;
-      if (px >= HW) break;
-      float v[8], d[8], o[8];
-      unpack8(gn_row(L, tx, X, p.ldx, px), v);
-      unpack8(gn_row(L, td, DY, p.lddy, px), d);
-      if (RS && accum) {  // both: dx (in place) + resid
-        float rr[8];
-        unpack8(*(const uint4*)(DX + (long)px * p.lddx), o);
-        unpack8(gr[u], rr);
+    for (int i = 0; i < 8; ++i) {
+      const float r = xr[i] * (dn[i] * ga[i] - m1[i] - xh[i] * m2[i]);
+      o[i] = (accum || RS) ? o[i] + r : r;
+    }
+    *(uint4*)(DX + (long)px * p.lddx) = pack8(o);
+  };
+  if (one) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] += rr[i];
-      } else if (RS || accum) {
-        unpack8(gr[u], o);  // residual-branch gradient (skip connection) or the dx being accumulated
+    for (int u = 0; u < U1; ++u) {
+      const int px = L.tp + u * L.np;
+      if (px < HW) out_row(px, gr0[u], cdn[u], cxh[u]);
+    }
+  } else {
+    // U rows per thread: the global (resid / accumulate) reads of all U are issued before the
+    // first dx store -- one latency per U rows instead of one per row
+    constexpr int U = ED_GN_BWD_U;
+    for (int px0 = L.tp; px0 < HW; px0 += U * L.np) {
+      uint4 gr[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int px = px0 + u * L.np;
+        gr[u] = (uint4){0u, 0u, 0u, 0u};
+        if (px < HW) {
+          if (RS) gr[u] = *(const uint4*)(RS + (long)px * p.ld_resid);
+          else if (accum) gr[u] = *(const uint4*)(DX + (long)px * p.lddx);
+        }
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float xh = (v[i] - xm[i]) * xr[i];
-        const float n = xh * ga[i] + be[i];
-        const float z = n * sc1[i] + sf[i];
-        const float dz = silu ? d[i] * silu_grad(z) : d[i];
-        const float dn = dz * sc1[i];
-        const float r = xr[i] * (dn * ga[i] - m1[i] - xh * m2[i]);
-        o[i] = (accum || RS) ? o[i] + r : r;
+      for (int u = 0; u < U; ++u) {
+        const int px = px0 + u * L.np;
+        if (px >= HW) break;
+        float v[8], d[8], dn[8], xh[8];
+        unpack8(gn_row(L, tx, X, p.ldx, px), v);
+        unpack8(gn_row(L, td, DY, p.lddy, px), d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          xh[i] = (v[i] - xm[i]) * xr[i];
+          const float n = xh[i] * ga[i] + be[i];
+          const float z = n * sc1[i] + sf[i];
+          const float dz = silu ? d[i] * silu_grad(z) : d[i];
+          dn[i] = dz * sc1[i];
+        }
+        out_row(px, gr[u], dn, xh);
       }
-      *(uint4*)(DX + (long)px * p.lddx) = pack8(o);
     }
   }
+  GN_STAMP(6);
+  GN_STAMP_RT(7);
 }
 
 // ---------------------------------------------------------------- LayerNorm
@@ -825,6 +921,13 @@ extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
+
+#if ED_GN_STAMP
+extern "C" int encdiff_debug_gn_stamps(void* dst, int nblocks) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(gn_stamps), (size_t)nblocks * 8 * sizeof(unsigned long long)) == hipSuccess
+             ? 0 : -1;
+}
+#endif
 
 extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream) {
   if (a && a->dtype == ENCDIFF_DT_F32) return ed_groupnorm_bwd_f32(a, (hipStream_t)stream);
