@@ -52,7 +52,9 @@ def parse():
 
 def setup_dist(args):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
-    if ws > 1:
+    # ENCDIFF_DP_FORCE=1 under torch.distributed.run --nproc-per-node 1: a one-rank RCCL group
+    # and the full DP exchange path (trainer.HipTrainer.dp) on a single GPU
+    if ws > 1 or (os.environ.get("ENCDIFF_DP_FORCE", "0") == "1" and "RANK" in os.environ):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # one process per GPU over RCCL ("nccl").  ENCDIFF_DIST_BACKEND=gloo rehearses the
         # DP path with several ranks sharing the GPUs of a smaller box (ranks wrap around).
@@ -339,13 +341,13 @@ def main():
     dt = time_steps(tr, args.steps)
     torch.cuda._sleep(1000)
     dp_info = None
-    if world > 1:  # exchange timing on extra steps (the timed ones carry no extra events)
+    if tr.dp:  # exchange timing on extra steps (the timed ones carry no extra events)
         tr.dp_timing = True
         for _ in range(min(10, args.steps)):
             tr.step()
         tr.dp_timing = False
         dp_info = tr.dp_stats()
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
@@ -387,7 +389,7 @@ def main():
                "loss_simple_last": loss}
         out.update(extra)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

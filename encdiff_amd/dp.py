@@ -74,6 +74,9 @@ class GradBuckets:
         self.max_mb = max_mb
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # ENCDIFF_DP_FORCE=1 (one-rank process group): the collectives are issued anyway, so a
+        # single-GPU box runs the exchange over RCCL exactly as an N-GPU node does
+        self.active = self.world > 1 or (dist.is_initialized() and os.environ.get("ENCDIFF_DP_FORCE", "0") == "1")
         backend = dist.get_backend(group) if dist.is_initialized() else "none"
         self.native_avg = backend == "nccl"
         if grad_dtype is None:
@@ -81,7 +84,7 @@ class GradBuckets:
         self.grad_dtype = grad_dtype
         # bf16 wire format: one staging buffer covering the whole arena (bucket views into it)
         self._wire = torch.empty(flat.numel(), dtype=grad_dtype, device=flat.device) \
-            if grad_dtype != flat.dtype and self.world > 1 else None
+            if grad_dtype != flat.dtype and self.active else None
         self.record = None  # tools/dp_check.py: {bucket: clone of what this rank sends}
         # pieces [lo, hi) of each coarse bucket, at most max_mb MB of wire bytes each (16-element aligned)
         esz = torch.tensor([], dtype=grad_dtype).element_size()
@@ -118,7 +121,7 @@ class GradBuckets:
     def start(self, i: int, async_op: bool = True):
         """Launch bucket i's all-reduces (one per piece) in the calling stream's order; returns
         the works.  With timing on, HIP events bracket them on the calling stream."""
-        if self.world == 1:
+        if not self.active:
             return None
         op = dist.ReduceOp.AVG if self.native_avg else dist.ReduceOp.SUM
         if self.record is not None:
@@ -148,7 +151,7 @@ class GradBuckets:
         for w in works or ():
             if w is not None:
                 w.wait()
-        if self.world > 1:
+        if self.active:
             if self._wire is not None:
                 self.view(i).copy_(self.wire(i))
             if not self.native_avg:

@@ -42,6 +42,11 @@ class HipTrainer:
         self.dev = ldm.device
         self.B = batch_size
         self.rank, self.world = world_info()
+        # the DP exchange path (side-stream bucketed all-reduce, split backward, four graphs) runs
+        # at world > 1, or with ENCDIFF_DP_FORCE=1 on a one-rank process group: a single-GPU box
+        # then exercises the RCCL calls and the split capture exactly as an 8-GPU node does
+        self.dp = self.world > 1 or (os.environ.get("ENCDIFF_DP_FORCE", "0") == "1" and dist.is_available()
+                                     and dist.is_initialized())
         ldm.train()
         arena = ldm.setup_hip_training()
         self.arena = arena
@@ -59,11 +64,11 @@ class HipTrainer:
             self.buckets = GradBuckets(arena.grad, self.buckets.bounds, max_mb=self.bucket_mb)
         self.dp_timing = False  # HIP events around the exchange (dp_stats)
         self._dp_ev = []
-        self._comm = torch.cuda.Stream() if self.world > 1 else None
+        self._comm = torch.cuda.Stream() if self.dp else None
         self.unet = ldm.model.diffusion_model
         # DP: split the UNet backward after the output blocks so their gradient bucket is
         # all-reduced while the middle / input blocks run (ENCDIFF_DP_SPLIT=0 disables)
-        self._split_want = self.world > 1 and os.environ.get("ENCDIFF_DP_SPLIT", "1") != "0"
+        self._split_want = self.dp and os.environ.get("ENCDIFF_DP_SPLIT", "1") != "0"
         self._split_lo: Optional[int] = None
         self._split_checked = False
         self._g_rest = None
@@ -163,7 +168,7 @@ class HipTrainer:
         ops.q_sample(z, noise, t, ldm.sqrt_alphas_cumprod, ldm.sqrt_one_minus_alphas_cumprod, self._xt, x0_scale=sf)
         eps = ex.forward(self._xt, t, c.detach().reshape(self.B, -1).float())
         ops.l1_loss(eps, noise, t, ldm.lvlb_weights, self.loss_buf[:2], grad=self._seed)
-        if self.world == 1:
+        if not self.dp:
             dc = ex.backward(self._seed)
             c.backward(dc.view_as(c))
             return
@@ -177,7 +182,7 @@ class HipTrainer:
         """The reference-API form (LatentDiffusion.p_losses + autograd) for other objectives."""
         ldm = self.ldm
         z = ldm.get_first_stage_encoding(z)
-        if self.world == 1:
+        if not self.dp:
             loss, ld = ldm.p_losses(z, c, t, noise)
             loss.backward()
         else:
@@ -280,7 +285,7 @@ class HipTrainer:
         visits every batch once."""
         self._draw_batch(advance=False)
         self.ldm.init_scale_factor({"image": self.img.permute(0, 2, 3, 1)})
-        if self.world > 1:
+        if self.dp:
             dist.broadcast(self.ldm.scale_factor, 0)
 
     def capture(self, warmup: int = 3):
@@ -300,9 +305,9 @@ class HipTrainer:
             try:
                 with torch.cuda.graph(self._g_fb, stream=s):
                     self._fwd_bwd()
-                    if self.world == 1:
+                    if not self.dp:
                         self.opt.launch()
-                if self.world > 1:
+                if self.dp:
                     pool = self._g_fb.pool()
                     if self._split_lo is not None:
                         self._g_rest = torch.cuda.CUDAGraph()
@@ -325,7 +330,7 @@ class HipTrainer:
         self.opt.stage_hyper()
         try:
             self._fwd_bwd()
-            if self.world > 1:
+            if self.dp:
                 self._exchange(self._cond_bwd, self._unet_rest if self._split_lo is not None else None)
         finally:
             ops.PROLOGUE_STEP = False
@@ -341,7 +346,7 @@ class HipTrainer:
         # parameters were changed in place since the last step (e.g. after an EMA scope)
         self.ldm.refresh_hip_weights()
         self._g_fb.replay()
-        if self.world > 1:
+        if self.dp:
             self._exchange(self._g_cond.replay, self._g_rest.replay if self._g_rest is not None else None)
             self._g_opt.replay()
         self._post()

@@ -67,3 +67,38 @@ def test_dp_two_ranks_equal_single_process_definition(tmp_path):
         # below the O(1) deviation a wrong exchange (a missing bucket, a stale finalize, a wrong
         # scale) produces
         assert rel < 1e-3, k
+
+
+def test_dp_exchange_over_rccl_one_rank(tmp_path):
+    """The RCCL side of the exchange on a one-GPU box: bench.py under torch.distributed.run with
+    ONE rank, backend "nccl" (= RCCL) and ENCDIFF_DP_FORCE=1, so the step runs the full DP path --
+    split backward, the four captured graphs, the bucketed all-reduces (ReduceOp.AVG over the
+    RCCL communicator) on the side stream with the host-issued waits.  A mean over one rank is the
+    identity, so after the same steps the loss must be bitwise the plain single-process step's,
+    and the JSON line must carry the exchange timing (the split engaged)."""
+    import json
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    args = ["bench.py", "--batch", "32", "--steps", "4", "--warmup", "2", "--skip-cpu", "--skip-ddim"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", ENCDIFF_DP_FORCE="1")
+    env.pop("ENCDIFF_DIST_BACKEND", None)
+
+    def run(cmd, log, e):
+        with open(log, "w") as fh:
+            r = subprocess.run(cmd, cwd=REPO, env=e, stdout=fh, stderr=subprocess.STDOUT, timeout=420)
+        out = open(log).read()
+        assert r.returncode == 0, out[-3000:]
+        return json.loads([ln for ln in out.splitlines() if ln.startswith('{"metric"')][-1])
+
+    dp = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+              "--master-addr", "127.0.0.1", "--master-port", "29631", *args], str(tmp_path / "rccl.log"), env)
+    plain_env = dict(os.environ)
+    plain_env.pop("ENCDIFF_DP_FORCE", None)
+    # the DP run takes min(10, steps) extra exchange-timing steps before it reads the loss
+    plain_args = [a if a != "4" else "8" for a in args]
+    plain = run([sys.executable, *plain_args], str(tmp_path / "plain.log"), plain_env)
+    print("RCCL one-rank exchange:", dp.get("dp"), "loss", dp["loss_simple_last"], "plain", plain["loss_simple_last"])
+    assert dp.get("dp") is not None and dp["dp"]["split_backward"], dp.get("dp")
+    # every coarse bucket's all-reduce was issued (timed on the exchange stream)
+    assert all(b["allreduce_ms"] is not None for b in dp["dp"]["buckets"]), dp["dp"]["buckets"]
+    assert dp["loss_simple_last"] == plain["loss_simple_last"]
