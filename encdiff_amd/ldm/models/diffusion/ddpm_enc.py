@@ -63,11 +63,12 @@ class FusedArenaAdamW(torch.optim.Optimizer):
     repacked right after.  Compatible with torch LambdaLR (param_groups[0]['lr'])."""
 
     def __init__(self, params, arena, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, ema=None,
-                 repack=None):
+                 repack=None, repack_parts=None):
         super().__init__(list(params), dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.arena = arena
         self.ema = ema
         self.repack = repack
+        self.repack_parts = repack_parts  # (UNet repack, cond-stage repack) for launch_part
         self.step_count = 0
         # ring of pinned staging rows: a row is rewritten only after the H2D copy that read it
         # has run (its event), so a host running steps ahead of the GPU never changes the
@@ -113,6 +114,22 @@ class FusedArenaAdamW(torch.optim.Optimizer):
                       ema_n=a.ema_numel if ema is not None else 0)
         if self.repack is not None:
             self.repack()
+
+    def launch_part(self, part: int):
+        """The same update in two launches over the arena's two ranges: part 0 = [0, ema_numel)
+        (the UNet, with the EMA) + the UNet's bf16 repack, part 1 = the rest (the cond stage) + its
+        repack.  The trainer runs part 0 on a side stream while the cond stage's backward runs
+        (the UNet gradients are final by then); element-wise, so the result is the one launch's."""
+        a = self.arena
+        mid = (a.ema_numel + 3) // 4 * 4  # float4 lanes: the split on a 4-element boundary (the
+        # elements up to it past ema_numel are the next parameter's alignment padding)
+        lo, hi = (0, mid) if part == 0 else (mid, a.numel)
+        if hi > lo:
+            ema = a.ema if (self.ema is not None and part == 0) else None
+            ops.adamw_ema(a.master[lo:hi], a.grad[lo:hi], a.exp_avg[lo:hi], a.exp_avg_sq[lo:hi], a.hyper, ema=ema,
+                          ema_n=a.ema_numel if ema is not None else 0)
+        if self.repack_parts is not None:
+            self.repack_parts[part]()
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -507,9 +524,10 @@ class LatentDiffusion(DDPM):
         arena = self._arena
         unet = self.model.diffusion_model
         params = [p for _, p in self.hip_trainables()]
+        rp_unet = lambda: (unet.executor().pack.repack(), unet.mark_repacked())  # noqa: E731
+        rp_cond = lambda: getattr(self.cond_stage_model, "repack_hip", lambda: None)()  # noqa: E731
         opt = FusedArenaAdamW(params, arena, lr=lr, ema=self.model_ema if self.use_ema else None,
-                              repack=lambda: (unet.executor().pack.repack(), unet.mark_repacked(),
-                                            getattr(self.cond_stage_model, "repack_hip", lambda: None)()))
+                              repack=lambda: (rp_unet(), rp_cond()), repack_parts=(rp_unet, rp_cond))
         self._optimizer = opt
         if self.use_scheduler:
             sched = instantiate_from_config(self.scheduler_config)
