@@ -178,7 +178,13 @@ constexpr float LN2 = 0.6931471805599453f;
 
 ED_DEV float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-__host__ __device__ constexpr int fwd_tiles_per_task(int dh) { return dh == 8 ? 4 : 2; }
+#ifndef ED_ATTN_NT8
+#define ED_ATTN_NT8 4  // dh 8 forward: 16-query tiles per wave task (A/B switch)
+#endif
+#ifndef ED_ATTN_FWD_UNROLL
+#define ED_ATTN_FWD_UNROLL 2  // forward key loop unroll (32-key steps; A/B switch)
+#endif
+__host__ __device__ constexpr int fwd_tiles_per_task(int dh) { return dh == 8 ? ED_ATTN_NT8 : 2; }
 
 template <bool B>
 struct BoundTag {
@@ -293,7 +299,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
     constexpr bool BOUND = decltype(bnd)::value;
     const bf16_t* kb = Ks + hl * KR * DP;
     const bf16_t* vb = Vs + hl * KR * DP;
-#pragma unroll 2
+#pragma unroll ED_ATTN_FWD_UNROLL
     for (int k0 = 0; k0 < klen; k0 += 32) {
       s4 kf[2][KC];
       long kf8[2][KC8];
