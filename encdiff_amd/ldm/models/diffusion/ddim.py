@@ -27,6 +27,8 @@ ema_scope() samples with the EMA weights inside it.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -40,6 +42,8 @@ GRAPH_MAX_STEPS = 256  # longer loops replay a one-step graph (device step index
 # capture and replay the whole-loop graph.  A one-off call (the first log_images) then costs
 # about its sampling time; repeated sampling (validation, the bench) runs the loop graph.
 LOOP_GRAPH_AFTER = 1
+# whole-loop graph: K / V of the conditioning and the FiLM rows of all steps computed once per loop
+HOIST = os.environ.get("ENCDIFF_DDIM_HOIST", "1") != "0"
 
 
 class DDIMSampler(object):
@@ -233,6 +237,7 @@ class DDIMSampler(object):
             b = img.shape[0]
             steps = np.flip(self.ddim_timesteps)
             st["ts"] = torch.tensor(np.repeat(np.asarray(steps, dtype=np.int64)[:, None], b, axis=1), device=img.device)
+            st["ts_col"] = st["ts"][:, 0].contiguous()  # one timestep per loop step (the FiLM table)
             x0 = st["x"].clone()
             self._loop_body(st, total)  # warm-up: allocations, kernel attributes, GEMM plans
             st["x"].copy_(x0)
@@ -251,12 +256,34 @@ class DDIMSampler(object):
             intermediates["pred_x0"].append(st["log_px0"][j].clone())
         return st["out"].clone(), intermediates
 
+    def _hip_executor(self):
+        """The bf16 HIP UNet executor behind the model (None: another backbone / precision)."""
+        um = getattr(getattr(self.model, "model", None), "diffusion_model", None)
+        if um is None or not hasattr(um, "executor") or getattr(um, "hip_precision", "bf16") == "fp32":
+            return None
+        return um.executor()
+
     def _loop_body(self, st, total):
         x, xn = st["x"], st["x2"]
         logs = st["logs"]
         noise_n = st["noise"].shape[0]
+        # the conditioning is fixed and every row shares t within the loop: the executor computes the
+        # concept-token K / V once and the FiLM rows of all S steps in one pass at step 0
+        # (UNetExecutor.samp_ts / samp_i); ENCDIFF_DDIM_HOIST=0 recomputes them every step
+        ex = self._hip_executor() if HOIST else None
+        if ex is not None:
+            ex.samp_ts, ex.samp_i = st["ts_col"], None
+        try:
+            self._loop_steps(st, total, x, xn, logs, noise_n, ex)
+        finally:
+            if ex is not None:
+                ex.samp_ts = ex.samp_i = None
+
+    def _loop_steps(self, st, total, x, xn, logs, noise_n, ex):
         for i in range(total):
             index = total - i - 1
+            if ex is not None:
+                ex.samp_i = i
             e_t = self.model.apply_model(x, st["ts"][i], st["cond"])
             a_t, a_prev = float(self.ddim_alphas[index]), float(self.ddim_alphas_prev[index])
             sigma, s1 = float(self.ddim_sigmas[index]), float(self.ddim_sqrt_one_minus_alphas[index])

@@ -244,7 +244,7 @@ def wgl_split(M, N, K, lda, ldb, c_mode):
 def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK, c_mode=L.OUT_BF16,
               conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=None, bias=None,
               resid=None, ld_resid=0, bias_grad=None, tile=0, ws_offset=0, aux=None, ld_aux=0,
-              gn_stats=None, ln=None, agn=None, fold=False):
+              gn_stats=None, ln=None, agn=None, fold=False, plan_m=None):
     """EncdiffGemmArgs with the measured (tile, split) plan; split-K slabs start `ws_offset`
     floats into this stream's workspace.  agn = (gamma, beta, film or None, eps, silu): GroupNorm of
     the im2col source applied in the A staging (tile 4); fold: split-K slabs combined in the kernel
@@ -264,8 +264,9 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
         sp = wgl_split(M, N, K, lda, ldb, c_mode)
         if sp is not None and (sp == 1 or sp * M * (N + 1) <= WS_HALF // 2):
             tile, split_k = 36, sp
+    pm = plan_m or M  # the row count whose measured plan is used (linear_fwd plan_m)
     if split_k is None or tile == 0:
-        t, sp = plan(M, N, K, a_mode, b_mode, c_mode, conv.resample if conv is not None else 0)
+        t, sp = plan(pm, N, K, a_mode, b_mode, c_mode, conv.resample if conv is not None else 0)
         tile = tile or FORCE_TILE or t
         split_k = split_k or sp
     ws = None
@@ -277,7 +278,7 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
         # the in-kernel combine indexes one ticket per output tile: only when every tile shape
         # (>= 32 x 32) stays within the ticket array
         if (a_mode != L.OPA_ROWM and math.ceil(M / 32) * math.ceil(N / 32) <= COUNTERS and
-                (fold or fold_choice(M, N, K, a_mode, b_mode, c_mode, conv.resample if conv is not None else 0))):
+                (fold or fold_choice(pm, N, K, a_mode, b_mode, c_mode, conv.resample if conv is not None else 0))):
             cnt = _counters()
     return L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=b_mode, c_mode=c_mode,
                       a=_p(a), lda=lda, b=_p(b), ldb=ldb, c=_p(c), ldc=ldc,
@@ -367,14 +368,16 @@ def gemm_pair(wgrad_fn, dgrad_fn, defer_dx=False):
 
 
 # ------------------------------------------------------------------ linear layers
-def linear_fwd(x, w, out, bias=None, resid=None, alpha=1.0, out_f32=False, gn_stats=None):
+def linear_fwd(x, w, out, bias=None, resid=None, alpha=1.0, out_f32=False, gn_stats=None, plan_m=None):
     """out[M][N] = x[M][K] w[N][K]^T (+bias)(+resid); gn_stats: [2*M/64][ld] fp32 view that
-    receives the per-64-row-segment channel sums of out (the next GroupNorm's statistics)."""
+    receives the per-64-row-segment channel sums of out (the next GroupNorm's statistics).
+    plan_m: take the (tile, split, fold) plan of the same problem with plan_m rows, so every row
+    comes out bitwise as that smaller GEMM computes it (the sampler's per-loop FiLM table)."""
     M, K = x.shape
     N = w.shape[0]
     gemm(M, N, K, x, _ld(x), w, _ld(w), out, _ld(out), c_mode=L.OUT_F32 if out_f32 else L.OUT_BF16,
          bias=bias, resid=resid, ld_resid=_ld(resid) if resid is not None else 0, alpha=alpha,
-         gn_stats=gn_stats, split_k=1 if gn_stats is not None else None)
+         gn_stats=gn_stats, split_k=1 if gn_stats is not None else None, plan_m=plan_m)
 
 
 # LayerNorm in the producing GEMM's epilogue when one tile spans the row (N <= 128):

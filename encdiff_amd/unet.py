@@ -288,6 +288,13 @@ class UNetExecutor:
         self.split_requested = False  # data-parallel trainer: backward(split=True) via autograd
         self.want_dx = False  # backward also writes d x_t (self.d_x): set by _UNetFn when x requires grad
         self.infer = False  # no backward follows the next forward (UNetModel.forward under no_grad)
+        # sampling loops (ddim.DDIMSampler's whole-loop graph): samp_ts = the loop's timesteps
+        # (S,), samp_i = the step being run.  Step 0 fills the loop's FiLM table (the time MLP and
+        # emb_layers for all S timesteps in one pass, one row per step -- every row of a sampling
+        # batch has the same t) and the concept tokens' K / V; later steps skip both
+        self.samp_ts: Optional[torch.Tensor] = None
+        self.samp_i: Optional[int] = None
+        self._samp_tabs: Dict[tuple, dict] = {}  # (S, B) -> buffers; graphs hold their addresses
         self._base_names = set(self.__dict__) | {"_base_names"}
         self.pack.repack()
 
@@ -463,6 +470,35 @@ class UNetExecutor:
                     d_qkv=t(M, 3 * c))
 
     # ---------------------------------------------------------------- forward
+    def _samp_table(self, B: int) -> dict:
+        """The sampling loop's per-step FiLM rows (S, film_total) fp32 and the time-MLP buffers
+        of its S timesteps, per (S, B); kept for the life of the executor."""
+        S = int(self.samp_ts.shape[0])
+        tab = self._samp_tabs.get((S, B))
+        if tab is None:
+            mc, dev = self.mc, self.samp_ts.device
+            bf = dict(device=dev, dtype=torch.bfloat16)
+            tab = dict(temb0=torch.empty(S, mc, **bf), th1=torch.empty(S, 4 * mc, **bf),
+                       ta1=torch.empty(S, 4 * mc, **bf), emb=torch.empty(S, 4 * mc, **bf),
+                       emb_s=torch.empty(S, 4 * mc, **bf),
+                       E=torch.empty(S, self.spec.film_total, device=dev, dtype=torch.float32))
+            self._samp_tabs[(S, B)] = tab
+        return tab
+
+    def _samp_fill(self, tab: dict, B: int):
+        """Time MLP + emb_layers over the loop's S timesteps at once.  Each GEMM takes the plan
+        of the B-row problem a step would run (plan_m=B), so every row is bitwise the FiLM row the
+        step's own forward computes."""
+        mc = self.mc
+        ops.timestep_embedding(self.samp_ts, mc, tab["temb0"])
+        ops.linear_fwd(tab["temb0"], self.W("time_embed.0.weight"), tab["th1"], bias=self.P("time_embed.0.bias"),
+                       plan_m=B)
+        ops.ew(L.EW_SILU, tab["th1"], tab["ta1"])
+        ops.linear_fwd(tab["ta1"], self.W("time_embed.2.weight"), tab["emb"], bias=self.P("time_embed.2.bias"),
+                       plan_m=B)
+        ops.ew(L.EW_SILU, tab["emb"], tab["emb_s"])
+        ops.linear_fwd(tab["emb_s"], self.W("emb_all"), tab["E"], bias=self.emb_bias, out_f32=True, plan_m=B)
+
     def forward(self, x: torch.Tensor, t: torch.Tensor, ctx: torch.Tensor) -> torch.Tensor:
         """x (B,C,H,W) fp32, t (B,) int64, ctx (B, latent_unit*context_dim) fp32 -> eps (B,C,H,W) fp32."""
         B = x.shape[0]
@@ -471,18 +507,28 @@ class UNetExecutor:
         self._pend = None  # GemmArgs of a ResBlock output whose split-K finalize is deferred
         self._x = x.contiguous()
         self._t_in = t.contiguous()
-        # timestep embedding + time MLP (openaimodel_enc.py:726-727)
-        ops.timestep_embedding(self._t_in, mc, self.temb0)
-        ops.linear_fwd(self.temb0, self.W("time_embed.0.weight"), self.th1, bias=self.P("time_embed.0.bias"))
-        ops.ew(L.EW_SILU, self.th1, self.ta1)
-        ops.linear_fwd(self.ta1, self.W("time_embed.2.weight"), self.emb, bias=self.P("time_embed.2.bias"))
-        ops.ew(L.EW_SILU, self.emb, self.emb_s)
-        # all 28 emb_layers at once (fp32 FiLM table)
-        ops.linear_fwd(self.emb_s, self.W("emb_all"), self.E, bias=self.emb_bias, out_f32=True)
-        # concept tokens -> every cross-attention's K/V at once
-        ctx2 = ctx.contiguous().view(B * self.lu, self.cd)
-        ops.ew(L.EW_F32_TO_BF16, ctx2, self.ctx16)
-        ops.linear_fwd(self.ctx16, self.W("kv_all"), self.KV)
+        samp = self.samp_ts is not None and self.samp_i is not None and self.infer
+        if samp:
+            tab = self._samp_table(B)
+            if self.samp_i == 0:
+                self._samp_fill(tab, B)
+            row = tab["E"][self.samp_i]
+            self._E_use, self._E_ld = row.unsqueeze(0).expand(B, row.shape[0]), 0
+        else:
+            # timestep embedding + time MLP (openaimodel_enc.py:726-727)
+            ops.timestep_embedding(self._t_in, mc, self.temb0)
+            ops.linear_fwd(self.temb0, self.W("time_embed.0.weight"), self.th1, bias=self.P("time_embed.0.bias"))
+            ops.ew(L.EW_SILU, self.th1, self.ta1)
+            ops.linear_fwd(self.ta1, self.W("time_embed.2.weight"), self.emb, bias=self.P("time_embed.2.bias"))
+            ops.ew(L.EW_SILU, self.emb, self.emb_s)
+            # all 28 emb_layers at once (fp32 FiLM table)
+            ops.linear_fwd(self.emb_s, self.W("emb_all"), self.E, bias=self.emb_bias, out_f32=True)
+            self._E_use, self._E_ld = self.E, self.E.shape[1]
+        if not samp or self.samp_i == 0:
+            # concept tokens -> every cross-attention's K/V at once
+            ctx2 = ctx.contiguous().view(B * self.lu, self.cd)
+            ops.ew(L.EW_F32_TO_BF16, ctx2, self.ctx16)
+            ops.linear_fwd(self.ctx16, self.W("kv_all"), self.KV)
         # input conv
         g0 = Geom(B, self.H, self.H)
         # input conv on the GEMM engine over channel-padded rows (openaimodel_enc.py:494)
@@ -545,9 +591,9 @@ class UNetExecutor:
         f1 = ops.conv3x3_fwd(a1, go, r.cin, self.W(r.prefix + "in_layers.2.weight"), S["h1"],
                              bias=self.P(r.prefix + "in_layers.2.bias"), resample=rs, gn_stats=self._gst(S["h1"]),
                              defer=GN_FIN and self._gst(S["h1"]) is None)
-        film = self.E[:, r.film_off:]
+        film = self._E_use[:, r.film_off:]
         ops.groupnorm_fwd(S["h1"], go, self.P(r.prefix + "out_layers.0.weight"), self.P(r.prefix + "out_layers.0.bias"),
-                          S["a2"], S["st2"], GN_EPS, True, film=film, ld_film=self.E.shape[1],
+                          S["a2"], S["st2"], GN_EPS, True, film=film, ld_film=self._E_ld,
                           in_stats=self._gst(S["h1"]), x_from=f1)
         # skip path into the output buffer, then conv2 adds onto it
         out = S["out"]
@@ -597,7 +643,7 @@ class UNetExecutor:
             resid = S["xr"]
         else:
             resid = x
-        film = self.E[:, r.film_off:]
+        film = self._E_use[:, r.film_off:]
         ops.conv3x3_fwd(S["h1"], go, r.cout, self.W(pre + "out_layers.3.weight"), out,
                         bias=self.P(pre + "out_layers.3.bias"), resid=resid, gn_stats=self._gst(out),
                         agn=(self.P(pre + "out_layers.0.weight"), self.P(pre + "out_layers.0.bias"), film, GN_EPS, True),

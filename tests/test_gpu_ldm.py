@@ -448,3 +448,23 @@ def test_captured_graphs_follow_ema_scope(ldm, monkeypatch):
     print("graph inside ema_scope vs eager", rel(inside, explicit), "vs base", rel(inside, base))
     assert rel(inside, explicit) < 1e-5 and rel(inside, base) > 1e-3
     assert torch.equal(after, base)
+
+
+def test_ddim_loop_hoisted_film_and_kv_bitwise(ldm, golden_dir, monkeypatch):
+    """The whole-loop DDIM graph computes the conditioning's K / V once and the FiLM rows of all
+    S steps in one pass (UNetExecutor.samp_ts / samp_i, each GEMM on the plan of the per-step
+    B-row problem): the samples are bitwise those of the same loop recomputing both every step."""
+    from encdiff_amd.ldm.models.diffusion import ddim as D
+    from encdiff_amd.ldm.models.diffusion.ddim import DDIMSampler
+    monkeypatch.setattr(D, "LOOP_GRAPH_AFTER", 0)
+    fx = np.load(os.path.join(golden_dir, "ddim.npz"))
+    cond = torch.tensor(fx["cond"]).cuda()
+    xT = torch.tensor(fx["xT"]).cuda()
+    outs = {}
+    with torch.no_grad():
+        for hoist in (True, False):
+            monkeypatch.setattr(D, "HOIST", hoist)
+            o, _ = DDIMSampler(ldm, use_graph=True).sample(10, 2, (3, 16, 16), cond, eta=0.0, verbose=False, x_T=xT)
+            outs[hoist] = o
+    assert torch.equal(outs[True], outs[False])
+    assert rel(outs[True], fx["samples_eta0"]) < 3e-2
