@@ -4,7 +4,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R && mkdir -p gpurun_out
-bash tools/round_profile.sh r04 || exit 1
+bash tools/round_profile.sh ${TAG:-r04} || exit 1
 bash tools/gpu_traffic.sh || exit 1
-cp gpurun_out/gemm_traffic.json gpurun_out/r04_gemm_traffic.json
-python -c "import json; d=json.load(open('gpurun_out/r04_gemm_traffic.json')); print('traffic/alg', d['traffic_over_alg'], 'launches', d['launches'])"
+cp gpurun_out/gemm_traffic.json gpurun_out/${TAG:-r04}_gemm_traffic.json
+python -c "import json; d=json.load(open('gpurun_out/gemm_traffic.json')); print('traffic/alg', d['traffic_over_alg'], 'launches', d['launches'])"
