@@ -45,7 +45,8 @@ class GemmArgs(C.Structure):
                 ("ln_gamma", vp), ("ln_beta", vp), ("ln_y", vp), ("ld_ln_y", C.c_long), ("ln_stats", vp),
                 ("ln_eps", C.c_float), ("pad3_", C.c_int), ("split_counters", vp),
                 ("agn_gamma", vp), ("agn_beta", vp), ("agn_film", vp), ("ld_agn_film", C.c_long),
-                ("agn_eps", C.c_float), ("agn_silu", C.c_int)]
+                ("agn_eps", C.c_float), ("agn_silu", C.c_int),
+                ("lna_gamma", vp), ("lna_beta", vp), ("lna_eps", C.c_float)]
 
 
 class GroupNormArgs(C.Structure):

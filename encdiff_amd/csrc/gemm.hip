@@ -26,7 +26,7 @@ enum { B_ROWK = ENCDIFF_OPB_ROWK, B_ROWN = ENCDIFF_OPB_ROWN, B_CONVD = ENCDIFF_O
 
 // internal A modes: implicit im2col read from a per-workgroup halo image in LDS (tiles >= 16);
 // implicit im2col with GroupNorm(+FiLM)(+SiLU) applied to each staged A tile (EncdiffGemmArgs.agn_*)
-enum { A_HALO = 16, A_IM2COL_GN = 17 };
+enum { A_HALO = 16, A_IM2COL_GN = 17, A_ROWK_LN = 18 };
 
 template <int AM> struct AKInner { static constexpr bool v = AM != A_ROWM; };
 template <int BMd> struct BKInner { static constexpr bool v = BMd == B_ROWK; };
@@ -180,6 +180,7 @@ struct Gemm {
   static constexpr int TN = BN / 32;
   static constexpr bool HALO = AM == A_HALO;
   static constexpr bool AGN = AM == A_IM2COL_GN;  // GroupNorm applied to the staged A tiles
+  static constexpr bool LNA = AM == A_ROWK_LN;    // LayerNorm applied to the staged A tiles (ROWK)
   static constexpr bool IM2 = AM == A_IM2COL || AGN;
   static constexpr int ASTAGE = HALO ? 0 : TA::ELEMS;  // halo mode: the ring holds B only
   static constexpr int STAGE = ASTAGE + TB::ELEMS;     // elements per LDS stage
@@ -341,8 +342,9 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     const int c = tid + 256 * i;
     const int row = c / TA::SLOTS, slot = c % TA::SLOTS;
     const int gs = TA::sw(row, slot);
-    if constexpr (AM == A_ROWK) {
+    if constexpr (AM == A_ROWK || AM == A_ROWK_LN) {
       const int m = m0 + row;
+      a_y[i] = row;  // LNA: the chunk's tile row (its LayerNorm statistics)
       a_k[i] = gs * 8;
       a_off[i] = m < p.M ? ((uint32_t)m * (uint32_t)p.lda + (uint32_t)(gs * 8)) * 2u : OOB;
     } else if constexpr (AM == A_ROWM) {
@@ -432,7 +434,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       const int c = tid + 256 * i;  // LDS chunk position (lane-linear)
       const int k = k0 + a_k[i];
       uint32_t vo;
-      if constexpr (AM == A_ROWK) {
+      if constexpr (AM == A_ROWK || AM == A_ROWK_LN) {
         vo = k < p.K ? a_off[i] + 2u * (uint32_t)k0 : OOB;
       } else if constexpr (AM == A_ROWM) {
         vo = k < p.K ? a_off[i] + (uint32_t)k0 * (uint32_t)p.lda * 2u : OOB;
@@ -758,6 +760,57 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the rewrites land before the barrier publishes them
   };
 
+  // LNA (EncdiffGemmArgs.lna_*): LayerNorm of the A rows over K, folded into the staging.
+  // Prologue: 4 lanes per tile row sum the row (fp32 sum / sum of squares, xor-shuffles over the
+  // 4 lanes), mean / rstd per row and gamma / beta per channel into LDS behind the ring.  Per
+  // k-tile every thread rewrites its own staged chunks in place (as AGN), masked rows / the K
+  // tail left as staged (zeros).
+  float2* lna_row = (float2*)((char*)smem + G::LDS_BYTES);  // [BM] (mean, rstd)
+  float2* lna_gb = lna_row + BM;                             // [K] (gamma, beta)
+  if constexpr (G::LNA) {
+    static_assert(BM * 4 == 256, "LNA: 4 lanes per tile row");
+    const int r = tid >> 2, q = tid & 3;
+    const int m = m0 + r;
+    float sa = 0.f, sq = 0.f;
+    if (m < p.M) {
+      const bf16_t* xr = A + (size_t)m * p.lda;
+      for (int k = 8 * q; k < p.K; k += 32) {
+        float v[8];
+        unpack8(*(const uint4*)(xr + k), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { sa += v[e]; sq += v[e] * v[e]; }
+      }
+    }
+    sa += __shfl_xor(sa, 1, 64); sq += __shfl_xor(sq, 1, 64);
+    sa += __shfl_xor(sa, 2, 64); sq += __shfl_xor(sq, 2, 64);
+    if (q == 0) {
+      const float inv = 1.f / (float)p.K;
+      const float mean = sa * inv, var = fmaxf(sq * inv - mean * mean, 0.f);
+      lna_row[r] = make_float2(mean, rsqrtf(var + p.lna_eps));
+    }
+    for (int k = tid; k < p.K; k += 256) lna_gb[k] = make_float2(p.lna_gamma[k], p.lna_beta[k]);
+    __syncthreads();  // the ring is staged next
+  }
+  auto lna_transform = [&](bf16_t* sa, int kt) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < APT; ++i) {
+      const int k = k0 + a_k[i];
+      if (k >= p.K || m0 + a_y[i] >= p.M) continue;
+      bf16_t* q = sa + (tid + 256 * i) * 8;  // this thread's LDS-DMA chunk (lane-linear)
+      float v[8];
+      unpack8(*(const uint4*)q, v);
+      const float2 st = lna_row[a_y[i]];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float2 gb = lna_gb[k + e];
+        v[e] = (v[e] - st.x) * st.y * gb.x + gb.y;
+      }
+      *(uint4*)q = pack8(v);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+
   // NSTAGE-deep LDS ring: tiles it+1 .. it+NSTAGE-2 stay in flight while tile it is
   // multiplied, so the K loop is bound by MFMA / bandwidth rather than by one load latency
   // per k-tile.  Per iteration: wait for tile it (vmcnt = loads issued after it), one
@@ -775,6 +828,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     for (int it = 0; it < nkt; ++it) {
       vm_wait_stages<G::LPS, D - 2>(min(D - 2, nkt - 1 - it));
       if constexpr (G::AGN) agn_transform(ring + rd * G::STAGE, kt_begin + it);
+      if constexpr (G::LNA) lna_transform(ring + rd * G::STAGE, kt_begin + it);
       asm volatile("s_barrier" ::: "memory");  // (asm: the compiler may not move LDS-DMA issue across it)
       if (it + D - 1 < nkt) stage(ring + wr * G::STAGE, kt_begin + it + D - 1);
       compute(ring + rd * G::STAGE, kt_begin + it);
@@ -1944,6 +1998,20 @@ hipError_t launch_agn(const EncdiffGemmArgs& p, const GemmAux& aux, hipStream_t 
   return hipGetLastError();
 }
 
+// LayerNorm-in-staging linear (EncdiffGemmArgs.lna_*): 64x64 tiles, 2-deep ring, row statistics
+// and gamma / beta behind the ring in dynamic LDS
+hipError_t launch_lna(const EncdiffGemmArgs& p, const GemmAux& aux, hipStream_t s) {
+  using G = Gemm<64, 64, A_ROWK_LN, B_ROWK, 2, BK>;
+  const size_t lds = (size_t)G::LDS_BYTES + 64 * 8 + (size_t)p.K * 8;
+  static const hipError_t attr_ok = hipFuncSetAttribute((const void*)gemm_kernel<64, 64, A_ROWK_LN, B_ROWK, 2, BK>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
+  if (attr_ok != hipSuccess) return attr_ok;
+  if (lds > 156 * 1024) return hipErrorInvalidValue;
+  dim3 grid((p.M + 63) / 64, (p.N + 63) / 64, p.split_k);
+  hipLaunchKernelGGL((gemm_kernel<64, 64, A_ROWK_LN, B_ROWK, 2, BK>), grid, dim3(256), lds, s, p, aux);
+  return hipGetLastError();
+}
+
 // halo tiles: ids 16.. (tile_halo_bm / tile_halo_bn), 3-deep B ring, window + ring in dynamic LDS
 constexpr int HALO_NS = 3;
 constexpr int HALO_LDS_MAX = 156 * 1024;  // 160 KiB less the paired kernel's static finalize scratch
@@ -2151,6 +2219,14 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
     if (p.tile != 0 && p.tile != 4) return ENCDIFF_ERR_UNSUPPORTED;
     p.tile = 4;
   }
+  if (p.lna_gamma) {  // LayerNorm in the A staging: linear forward, 64x64 tiles, no split
+    if (p.a_mode != ENCDIFF_OPA_ROWK || p.b_mode != ENCDIFF_OPB_ROWK || p.c_mode != ENCDIFF_OUT_BF16 ||
+        !p.lna_beta || p.ln_y || p.agn_gamma || p.split_k != 1)
+      return ENCDIFF_ERR_ARG;
+    if (p.K % 8 || p.K > 1024 || p.lda % 8 || ((uintptr_t)p.a & 15)) return ENCDIFF_ERR_SHAPE;
+    if (p.tile != 0 && p.tile != 4) return ENCDIFF_ERR_UNSUPPORTED;
+    p.tile = 4;
+  }
   g.tile = p.tile ? p.tile : pick_tile(p);
   g.aux.halo = HaloGeom{};
   if (g.tile >= 32 && g.tile <= 34) {  // 3x3 conv weight gradient kernel (WG3)
@@ -2203,7 +2279,8 @@ int launch_one(const GemmPlan& g, hipStream_t s) {
   hipError_t e;
   if (g.tile >= 32 && g.tile <= 34) e = wg3_launch(g.p, g.tile, g.user, 0, s);
   else if (g.tile == 36) e = wgl_launch(g.p, g.user, 0, s);
-  else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWK) e = launch_modes<A_ROWK, B_ROWK>(g.p, g.aux, g.tile, s);
+  else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWK)
+    e = g.p.lna_gamma ? launch_lna(g.p, g.aux, s) : launch_modes<A_ROWK, B_ROWK>(g.p, g.aux, g.tile, s);
   else if (am == ENCDIFF_OPA_IM2COL && bm == ENCDIFF_OPB_ROWK)
     e = g.p.agn_gamma ? launch_agn(g.p, g.aux, s) : launch_modes<A_IM2COL, B_ROWK>(g.p, g.aux, g.tile, s);
   else if (am == ENCDIFF_OPA_ROWK && bm == ENCDIFF_OPB_ROWN) e = launch_modes<A_ROWK, B_ROWN>(g.p, g.aux, g.tile, s);

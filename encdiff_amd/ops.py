@@ -244,13 +244,15 @@ def wgl_split(M, N, K, lda, ldb, c_mode):
 def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK, c_mode=L.OUT_BF16,
               conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=None, bias=None,
               resid=None, ld_resid=0, bias_grad=None, tile=0, ws_offset=0, aux=None, ld_aux=0,
-              gn_stats=None, ln=None, agn=None, fold=False, plan_m=None):
+              gn_stats=None, ln=None, agn=None, fold=False, plan_m=None, lna=None):
     """EncdiffGemmArgs with the measured (tile, split) plan; split-K slabs start `ws_offset`
     floats into this stream's workspace.  agn = (gamma, beta, film or None, eps, silu): GroupNorm of
     the im2col source applied in the A staging (tile 4); fold: split-K slabs combined in the kernel
     whenever the plan splits (the output is complete when the launch ends)."""
     if agn is not None:
         tile = 4
+    if lna is not None:  # LayerNorm of the A rows in the staging: 64x64 tiles, no split
+        tile, split_k = 4, 1
     if (WG3 and tile == 0 and split_k is None and a_mode == L.OPA_ROWM and b_mode == L.OPB_IM2COL and
             conv is not None and N == 9 * conv.cin and K == conv.batch * conv.h * conv.w):
         sp = wg3_split(conv.batch, conv.h, conv.w, M, conv.cin, conv.resample, lda, conv.ld_src, c_mode)
@@ -292,7 +294,8 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
                                                     ld_ln_y=_ld(ln[2]), ln_stats=_p(ln[3]), ln_eps=ln[4])),
                       **({} if agn is None else dict(agn_gamma=_p(agn[0]), agn_beta=_p(agn[1]), agn_film=_p(agn[2]),
                                                      ld_agn_film=_ld(agn[2]) if agn[2] is not None else 0,
-                                                     agn_eps=agn[3], agn_silu=int(agn[4]))))
+                                                     agn_eps=agn[3], agn_silu=int(agn[4]))),
+                      **({} if lna is None else dict(lna_gamma=_p(lna[0]), lna_beta=_p(lna[1]), lna_eps=lna[2])))
 
 
 def ws_floats(args) -> int:
@@ -368,16 +371,19 @@ def gemm_pair(wgrad_fn, dgrad_fn, defer_dx=False):
 
 
 # ------------------------------------------------------------------ linear layers
-def linear_fwd(x, w, out, bias=None, resid=None, alpha=1.0, out_f32=False, gn_stats=None, plan_m=None):
+def linear_fwd(x, w, out, bias=None, resid=None, alpha=1.0, out_f32=False, gn_stats=None, plan_m=None,
+               ln_in=None):
     """out[M][N] = x[M][K] w[N][K]^T (+bias)(+resid); gn_stats: [2*M/64][ld] fp32 view that
     receives the per-64-row-segment channel sums of out (the next GroupNorm's statistics).
     plan_m: take the (tile, split, fold) plan of the same problem with plan_m rows, so every row
-    comes out bitwise as that smaller GEMM computes it (the sampler's per-loop FiLM table)."""
+    comes out bitwise as that smaller GEMM computes it (the sampler's per-loop FiLM table).
+    ln_in = (gamma, beta, eps): out = LayerNorm(x) w^T (+bias)(+resid), the LayerNorm applied to
+    the staged A tiles (EncdiffGemmArgs.lna_*; inference: no normalised rows materialised)."""
     M, K = x.shape
     N = w.shape[0]
     gemm(M, N, K, x, _ld(x), w, _ld(w), out, _ld(out), c_mode=L.OUT_F32 if out_f32 else L.OUT_BF16,
          bias=bias, resid=resid, ld_resid=_ld(resid) if resid is not None else 0, alpha=alpha,
-         gn_stats=gn_stats, split_k=1 if gn_stats is not None else None, plan_m=plan_m)
+         gn_stats=gn_stats, split_k=1 if gn_stats is not None else None, plan_m=plan_m, lna=ln_in)
 
 
 # LayerNorm in the producing GEMM's epilogue when one tile spans the row (N <= 128):

@@ -50,6 +50,11 @@ ST_TAIL_FUSED = os.environ.get("ENCDIFF_ST_TAIL", "1") != "0"
 # inference at sampling batches: ResBlock GroupNorms folded into the convs' A staging
 # (_res_fwd_agn); larger batches keep the producer-statistics GroupNorm launches
 AGN = os.environ.get("ENCDIFF_AGN", "1") != "0"
+# LayerNorm applied in the consuming linear's A staging at inference (c > 128 transformer blocks):
+# off by default -- DDIM B=8 606 / 611 -> 600 / 600 steps/s with it (profiles/r04_lna_ab.txt): every
+# workgroup re-reduces its rows' statistics and rewrites each staged tile, which costs more than
+# the LayerNorm launch it saves at these sizes (the same finding as AGN for the ResBlock convs)
+LNA_IN = os.environ.get("ENCDIFF_LNA", "0") == "1"
 AGN_MAX_B = int(os.environ.get("ENCDIFF_AGN_MAX_B", "32"))
 # ResBlock convs too (else only the fused ST heads): off by default -- DDIM B=8 measured 500 steps/s
 # with it vs 595 without (the per-workgroup statistics prologue costs more than the launches it saves)
@@ -669,6 +674,9 @@ class UNetExecutor:
         tb = s.prefix + "transformer_blocks.0."
         ntok = s.h * s.h
         fused = ST_TAIL_FUSED and c <= ST_TAIL_MAXC and (self.infer or ST_TAIL_TRAIN)
+        # inference, blocks whose LayerNorms would be launches of their own (c > 128: the GEMM
+        # epilogue form needs the tile to span the row): norm1 / norm2 in the consumer's A staging
+        lna = self.infer and LNA_IN and 128 < c <= 1024
         in_st = self._gst(x)
         # inference at sampling batches: the fused head computes the GroupNorm statistics itself
         self_st = fused and in_st is None and self.infer and AGN and B <= AGN_MAX_B
@@ -685,10 +693,17 @@ class UNetExecutor:
             if not fused or in_st is not None or self_st:
                 ops.groupnorm_fwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["gn"],
                                   S["stg"], ST_GN_EPS, False, in_stats=in_st)
-            # proj_in, then norm1 in its epilogue (self-attention input)
-            ops.linear_fwd_ln(S["gn"], self.W(s.prefix + "proj_in.weight"), S["t0"], self.P(tb + "norm1.weight"),
-                              self.P(tb + "norm1.bias"), S["n1"], S["s1"], LN_EPS, bias=self.P(s.prefix + "proj_in.bias"))
-            ops.linear_fwd(S["n1"], self.W(s.prefix + "qkv"), S["qkv"])
+            if lna:  # norm1 applied in q/k/v's A staging (no LayerNorm launch)
+                ops.linear_fwd(S["gn"], self.W(s.prefix + "proj_in.weight"), S["t0"],
+                               bias=self.P(s.prefix + "proj_in.bias"))
+                ops.linear_fwd(S["t0"], self.W(s.prefix + "qkv"), S["qkv"],
+                               ln_in=(self.P(tb + "norm1.weight"), self.P(tb + "norm1.bias"), LN_EPS))
+            else:
+                # proj_in, then norm1 in its epilogue (self-attention input)
+                ops.linear_fwd_ln(S["gn"], self.W(s.prefix + "proj_in.weight"), S["t0"], self.P(tb + "norm1.weight"),
+                                  self.P(tb + "norm1.bias"), S["n1"], S["s1"], LN_EPS,
+                                  bias=self.P(s.prefix + "proj_in.bias"))
+                ops.linear_fwd(S["n1"], self.W(s.prefix + "qkv"), S["qkv"])
         q, k, v = S["qkv"][:, :c], S["qkv"][:, c:2 * c], S["qkv"][:, 2 * c:]
         ops.attention_fwd(q, k, v, S["o1"], S["lse1"], B, s.heads, ntok, ntok, s.dh, fp8=s.fp8)
         k2 = self.KV[:, s.kv_off:s.kv_off + c]
@@ -701,11 +716,18 @@ class UNetExecutor:
             if ops.st_tail_fwd(S["o1"], S["t0"], x, k2, v2, self._tail_weights(s), S["out"], B * ntok, c, ntok,
                                s.heads, self.lu, LN_EPS, save=save, gn_stats=self._gst(S["out"])):
                 return S["out"]
-        # cross-attention to the concept tokens (norm2 in the to_out epilogue)
-        ops.linear_fwd_ln(S["o1"], self.W(tb + "attn1.to_out.0.weight"), S["t1"], self.P(tb + "norm2.weight"),
-                          self.P(tb + "norm2.bias"), S["n2"], S["s2"], LN_EPS,
-                          bias=self.P(tb + "attn1.to_out.0.bias"), resid=S["t0"])
-        ops.linear_fwd(S["n2"], self.W(tb + "attn2.to_q.weight"), S["q2"])
+        # cross-attention to the concept tokens (norm2 in the to_out epilogue, or at inference for
+        # wide blocks in to_q's A staging)
+        if lna:
+            ops.linear_fwd(S["o1"], self.W(tb + "attn1.to_out.0.weight"), S["t1"],
+                           bias=self.P(tb + "attn1.to_out.0.bias"), resid=S["t0"])
+            ops.linear_fwd(S["t1"], self.W(tb + "attn2.to_q.weight"), S["q2"],
+                           ln_in=(self.P(tb + "norm2.weight"), self.P(tb + "norm2.bias"), LN_EPS))
+        else:
+            ops.linear_fwd_ln(S["o1"], self.W(tb + "attn1.to_out.0.weight"), S["t1"], self.P(tb + "norm2.weight"),
+                              self.P(tb + "norm2.bias"), S["n2"], S["s2"], LN_EPS,
+                              bias=self.P(tb + "attn1.to_out.0.bias"), resid=S["t0"])
+            ops.linear_fwd(S["n2"], self.W(tb + "attn2.to_q.weight"), S["q2"])
         ops.attention_fwd(S["q2"], k2, v2, S["o2"], S["lse2"], B, s.heads, ntok, self.lu, s.dh)
         # GEGLU feed-forward (norm3 in the to_out epilogue)
         ops.linear_fwd_ln(S["o2"], self.W(tb + "attn2.to_out.0.weight"), S["t2"], self.P(tb + "norm3.weight"),

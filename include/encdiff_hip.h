@@ -172,6 +172,15 @@ typedef struct EncdiffGemmArgs {
   long ld_agn_film;
   float agn_eps;
   int agn_silu;
+  /* optional (lna_gamma != NULL), linear forwards OPA_ROWK x OPB_ROWK (bf16 / GEGLU output, tile 0
+     or 4, split 1, K <= 1024, K % 8 == 0): the A operand is LayerNorm(A) over its K channels --
+     BasicTransformerBlock norm1 / norm2 / norm3 (attention.py:210-230) -- applied to each staged
+     tile in LDS.  Every workgroup reduces the mean / rstd (fp32, one pass) of its rows from A in a
+     prologue.  Replaces the encdiff_layernorm_fwd launch in front of the linear where nothing
+     saves the normalised rows (sampling / inference). */
+  const float* lna_gamma;
+  const float* lna_beta;     /* [K] */
+  float lna_eps;
 } EncdiffGemmArgs;
 
 int encdiff_gemm(const EncdiffGemmArgs* args, void* stream);

@@ -1336,3 +1336,30 @@ def test_cross_attention_module(O, dq, dc, heads, dh, sq, sk):
         r = rel(a_, b_)
         print(name, r)
         assert r < 3e-2, (name, r)
+
+
+@pytest.mark.parametrize("M,K,N,resid", [(128, 256, 256, False), (2048, 256, 768, True), (100, 512, 256, False),
+                                         (512, 512, 128, True)])
+def test_linear_layernorm_in_staging(O, M, K, N, resid):
+    """out = LayerNorm(x) w^T + b (+ r) with the LayerNorm applied to the staged A tiles
+    (EncdiffGemmArgs.lna_*, row statistics reduced per workgroup): vs torch fp32, and vs the
+    LayerNorm launch + plain GEMM it replaces at inference (c > 128 transformer blocks)."""
+    torch.manual_seed(41)
+    x = (torch.randn(M, K, device=dev) * 1.5 + 0.3).to(torch.bfloat16)
+    w = bf(N, K, scale=K ** -0.5)
+    b = torch.randn(N, device=dev) * 0.1
+    g = 1 + 0.1 * torch.randn(K, device=dev)
+    be = 0.1 * torch.randn(K, device=dev)
+    r = bf(M, N) if resid else None
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    O.linear_fwd(x, w, out, bias=b, resid=r, ln_in=(g, be, 1e-5))
+    ref = F.layer_norm(x.float(), (K,), g, be, 1e-5) @ w.float().t() + b
+    if resid:
+        ref = ref + r.float()
+    assert rel(out, ref) < 1e-2
+    n = torch.empty_like(x)
+    st = torch.empty(M, 2, device=dev)
+    O.layernorm_fwd(x, g, be, n, st, 1e-5)
+    two = torch.empty_like(out)
+    O.linear_fwd(n, w, two, bias=b, resid=r)
+    assert rel(out, two.float()) < 1e-2
