@@ -196,7 +196,7 @@ def kernel_roofline(tr, reps=10):
     with torch.cuda.stream(s):
         replay_gemms(calls)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
             replay_gemms(calls)
         g.replay()
         s.synchronize()

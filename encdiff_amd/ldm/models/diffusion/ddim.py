@@ -245,7 +245,7 @@ class DDIMSampler(object):
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s):
+                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                     self._loop_body(st, total)
             torch.cuda.current_stream().wait_stream(s)
             st["graph"] = g
@@ -317,7 +317,7 @@ class DDIMSampler(object):
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                with torch.cuda.graph(g, stream=s):
+                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                     self._step_body(st)
             torch.cuda.current_stream().wait_stream(s)
             st["graph"] = g

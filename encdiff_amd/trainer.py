@@ -321,9 +321,14 @@ class HipTrainer:
         self._g_fb = torch.cuda.CUDAGraph()
         from . import ops
         self._prologue_regions()
+        # capture_error_mode "thread_local" (every capture in the package): under the default
+        # "global" mode ANY thread's unsafe HIP call invalidates the capture, and with RCCL the
+        # process-group watchdog thread polls the earlier all-reduces' events (hipEventQuery)
+        # at arbitrary moments -- a one-rank RCCL run lost its step capture to that
+        # (hipErrorStreamCaptureInvalidated, then the watchdog aborts the process)
         with torch.cuda.stream(s):
             try:
-                with torch.cuda.graph(self._g_fb, stream=s):
+                with torch.cuda.graph(self._g_fb, stream=s, capture_error_mode="thread_local"):
                     self._opt_in_fb = False
                     self._fwd_bwd()
                     if not self.dp and not self._opt_in_fb:
@@ -332,13 +337,13 @@ class HipTrainer:
                     pool = self._g_fb.pool()
                     if self._split_lo is not None:
                         self._g_rest = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(self._g_rest, stream=s, pool=pool):
+                        with torch.cuda.graph(self._g_rest, stream=s, pool=pool, capture_error_mode="thread_local"):
                             self._unet_rest()
                     self._g_cond = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(self._g_cond, stream=s, pool=pool):
+                    with torch.cuda.graph(self._g_cond, stream=s, pool=pool, capture_error_mode="thread_local"):
                         self._cond_bwd()
                     self._g_opt = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(self._g_opt, stream=s, pool=pool):
+                    with torch.cuda.graph(self._g_opt, stream=s, pool=pool, capture_error_mode="thread_local"):
                         self.opt.launch()
             finally:
                 ops.PROLOGUE_STEP = False

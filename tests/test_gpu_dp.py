@@ -69,7 +69,8 @@ def test_dp_two_ranks_equal_single_process_definition(tmp_path):
         assert rel < 1e-3, k
 
 
-def test_dp_exchange_over_rccl_one_rank(tmp_path):
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_dp_exchange_over_rccl_one_rank(tmp_path, wire):
     """The RCCL side of the exchange on a one-GPU box: bench.py under torch.distributed.run with
     ONE rank, backend "nccl" (= RCCL) and ENCDIFF_DP_FORCE=1, so the step runs the full DP path --
     split backward, the four captured graphs, the bucketed all-reduces (ReduceOp.AVG over the
@@ -82,6 +83,8 @@ def test_dp_exchange_over_rccl_one_rank(tmp_path):
     args = ["bench.py", "--batch", "32", "--steps", "4", "--warmup", "2", "--skip-cpu", "--skip-ddim"]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", ENCDIFF_DP_FORCE="1")
     env.pop("ENCDIFF_DIST_BACKEND", None)
+    if wire == "bf16":  # the bf16 wire format (ENCDIFF_DP_GRAD_BF16): staged, all-reduced, cast back
+        env["ENCDIFF_DP_GRAD_BF16"] = "1"
 
     def run(cmd, log, e):
         with open(log, "w") as fh:
@@ -91,7 +94,8 @@ def test_dp_exchange_over_rccl_one_rank(tmp_path):
         return json.loads([ln for ln in out.splitlines() if ln.startswith('{"metric"')][-1])
 
     dp = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-              "--master-addr", "127.0.0.1", "--master-port", "29631", *args], str(tmp_path / "rccl.log"), env)
+              "--master-addr", "127.0.0.1", "--master-port", "29631" if wire == "fp32" else "29633", *args],
+             str(tmp_path / "rccl.log"), env)
     plain_env = dict(os.environ)
     plain_env.pop("ENCDIFF_DP_FORCE", None)
     # the DP run takes min(10, steps) extra exchange-timing steps before it reads the loss
@@ -101,4 +105,8 @@ def test_dp_exchange_over_rccl_one_rank(tmp_path):
     assert dp.get("dp") is not None and dp["dp"]["split_backward"], dp.get("dp")
     # every coarse bucket's all-reduce was issued (timed on the exchange stream)
     assert all(b["allreduce_ms"] is not None for b in dp["dp"]["buckets"]), dp["dp"]["buckets"]
-    assert dp["loss_simple_last"] == plain["loss_simple_last"]
+    if wire == "fp32":
+        assert dp["loss_simple_last"] == plain["loss_simple_last"]
+    else:  # gradients rounded to bf16 before the (identity) mean: close, not bitwise
+        assert all(abs(b["wire_mb"] * 2 - b["params"] * 4 / 2 ** 20) < 0.05 for b in dp["dp"]["buckets"])
+        assert abs(dp["loss_simple_last"] - plain["loss_simple_last"]) < 1e-2 * plain["loss_simple_last"]
