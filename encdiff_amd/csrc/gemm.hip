@@ -107,6 +107,7 @@ struct GemmAux {
   FDiv w;     // in-image index -> (y, x)
   HaloGeom halo;
   SplitFold fold;
+  int xcd;    // XCD-aware tile order (gemm_kernel / gemm2_kernel): see xcd_remap
 };
 
 // Implicit im2col, branch-free.  The launch's resample mode is folded into uniform
@@ -1178,10 +1179,29 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   }
 }
 
+// Bijective XCD remap of a 1-D block id: the dispatcher deals workgroups round-robin over the 8
+// XCDs (block b runs on XCD b % 8), so blocks b and b + 8 share an L2; the remap gives the blocks
+// of one XCD CONSECUTIVE logical ids, i.e. neighbouring tiles: the same weight columns / k-slice
+// (and, for implicit im2col, the neighbouring image rows the 3x3 taps reach) stay in one L2
+// instead of being fetched by all eight.
+ED_DEV int xcd_remap(int b, int n) {
+  const int q = n >> 3, r = n & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
 template <int BM, int BN, int AM, int BMD, int NS, int KB>
 __global__ __launch_bounds__(256) void gemm_kernel(const EncdiffGemmArgs p, const GemmAux aux) {
   extern __shared__ __attribute__((aligned(16))) bf16_t smem[];
-  gemm_tile<BM, BN, AM, BMD, NS, KB>(p, aux, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (aux.xcd) {  // logical tile order x (M tiles) fastest, then y (N tiles), then z (k-slices)
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int l = xcd_remap(bx + gx * (by + gy * bz), gx * gy * (int)gridDim.z);
+    bx = l % gx;
+    const int t = l / gx;
+    by = t % gy;
+    bz = t / gy;
+  }
+  gemm_tile<BM, BN, AM, BMD, NS, KB>(p, aux, bx, by, bz, smem);
 }
 
 __device__ __forceinline__ void gemm_finalize(const EncdiffGemmArgs& p, const int bid, const int nblk);
@@ -1202,10 +1222,14 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const EncdiffGemmArgs p1, co
   const int n2 = gx2 * gy2 * p2.split_k;
   int i = blockIdx.x;
   if (i < n1) {
+    // XCD of block i is i % 8 in both ranges (a rotation of the labels in the second): the remap
+    // over each range keeps it bijective and XCD-grouped
+    if (aux1.xcd) i = xcd_remap(i, n1);
     const int bx = i % gx1, t = i / gx1;
     gemm_tile<64, 64, AM1, BMD1, NS1, KB1>(p1, aux1, bx, t % gy1, t / gy1, smem);
   } else if (i < n1 + n2) {
     i -= n1;
+    if (aux2.xcd) i = xcd_remap(i, n2);
     const int bx = i % gx2, t = i / gx2;
     gemm_tile<BM2, BN2, AM2, BMD2, NS2, KB2>(p2, aux2, bx, t % gy2, t / gy2, smem);
   } else {
@@ -1420,11 +1444,6 @@ ED_DEV v8bf cat8(v4s lo, v4s hi) {
 ED_DEV uint32_t lds_addr(const void* p) {
   typedef __attribute__((address_space(3))) const char lds_char;
   return (uint32_t)(uintptr_t)(lds_char*)p;
-}
-// bijective XCD remap: blocks b and b + 8 run on one XCD; consecutive logical ids share it
-ED_DEV int xcd_remap(int b, int n) {
-  const int q = n >> 3, r = n & 7, x = b & 7;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
 }
 
 template <int W, int NS>
@@ -2155,6 +2174,21 @@ struct GemmPlan {
   bool fold;  // split-K slabs combined in the kernel (no finalize pass)
 };
 
+// XCD-aware tile order (xcd_remap) per problem.  Measured per call over the step's GEMMs
+// (tools/gemm_calls_time.py, round 4): it pays for the weight gradients whose A operand is
+// k-outer (dY^T, deep split-K over pixels: the x / dY k-slices of 8 split-K parts and 8 M tiles
+// stay in one L2; the 512x64x32768 linear pairs 22.4 -> 16.9 us) and LOSES for the forward /
+// input-gradient convs (M = 2048 split-4 3x3 convs 14.6 -> 21.7 us: one XCD's 64 workgroups then
+// start on the same two weight tiles at once).  ENCDIFF_GEMM_XCD: 0 off, 1 every GEMM, 2 (default)
+// the k-outer-A GEMMs only.
+int gemm_xcd_order(const EncdiffGemmArgs& p) {
+  static const int v = [] {
+    const char* e = getenv("ENCDIFF_GEMM_XCD");
+    return e ? atoi(e) : 2;
+  }();
+  return v == 1 || (v == 2 && p.a_mode == ENCDIFF_OPA_ROWM);
+}
+
 int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
   if (!pa || pa->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_ARG;  // fp32: encdiff_gemm only
   EncdiffGemmArgs p = *pa;
@@ -2258,6 +2292,7 @@ int prepare(const EncdiffGemmArgs* pa, GemmPlan& g) {
                            (const bf16_t*)g.user.resid, g.user.ld_resid};
   }
   g.p = p;
+  g.aux.xcd = gemm_xcd_order(p);
   g.aux.cin = make_fdiv(p.conv.cin);
   g.aux.cout = make_fdiv(p.conv_cout);
   const bool tp = im2col && p.conv.resample == ENCDIFF_RESAMPLE_K4S2_TP;

@@ -47,14 +47,25 @@ def run(batch: int):
     torch.cuda.synchronize()
     torch.cuda._sleep(1000)
     ops.ew(0, src, dst)                      # calibration: ENCDIFF_EW_COPY
-    bench.replay_gemms(calls)
+    for c in calls:                          # a spin marker before every call: per-call segments
+        torch.cuda._sleep(1)
+        bench.replay_gemms([c])
     torch.cuda._sleep(1000)
     torch.cuda.synchronize()
     probs = bench.gemm_problems(calls)
     alg = sum(bench.gemm_alg_bytes(a) for a in probs)
+
+    def desc(a):
+        return {"M": a.M, "N": a.N, "K": a.K, "a_mode": a.a_mode, "b_mode": a.b_mode, "c_mode": a.c_mode,
+                "tile": a.tile, "split_k": a.split_k, "hw": [a.conv.h, a.conv.w], "cin": a.conv.cin,
+                "resample": a.conv.resample, "alg_bytes": bench.gemm_alg_bytes(a), "flops": 2.0 * a.M * a.N * a.K}
+    per_call = []
+    for c in calls:
+        ps = [c[1]] if c[0] == "gemm" else ([c[1], c[2]] if c[0] == "pair_ex" else [])
+        per_call.append({"kind": c[0], "problems": [desc(a) for a in ps]})
     with open(os.path.join(REPO, "gpurun_out", "gemm_traffic_calls.json"), "w") as f:
         json.dump({"launches": len(calls), "alg_bytes": alg,
-                   "flops": sum(2.0 * a.M * a.N * a.K for a in probs)}, f)
+                   "flops": sum(2.0 * a.M * a.N * a.K for a in probs), "calls": per_call}, f)
     print(f"replayed {len(calls)} gemm launches")
 
 
@@ -70,21 +81,32 @@ def _rows(d):
     return out
 
 
-def _window(rows, counter):
+def _segments(rows, counter):
+    """rows between the first and the last spin marker, split at every marker: segment 0 is the
+    calibration copy, segment i + 1 the dispatches of recorded call i."""
     marks = [i for i, r in enumerate(rows) if "spin_kernel" in r[1]]
-    assert len(marks) >= 2, "markers missing"
-    win = rows[marks[-2] + 1:marks[-1]]
-    cal = [r for r in win if "ew_kernel" in r[1] and r[2] == counter]
+    assert len(marks) >= 3, "markers missing"
+    segs = []
+    for a, b in zip(marks[:-1], marks[1:]):
+        segs.append([r for r in rows[a + 1:b] if r[2] == counter])
+    return segs
+
+
+FAM = ("gemm_kernel", "gemm2_kernel", "gemm_finalize", "wgrad3x3_kernel", "wgradlin_kernel")
+
+
+def _window(rows, counter):
+    segs = _segments(rows, counter)
+    cal = [r for r in segs[0] if "ew_kernel" in r[1]]
     # single, paired, split-K finalize kernels, and the weight-gradient kernels (WG3 3x3 conv, WGL linear)
-    fam = ("gemm_kernel", "gemm2_kernel", "gemm_finalize", "wgrad3x3_kernel", "wgradlin_kernel")
-    gem = [r for r in win if any(k in r[1] for k in fam) and r[2] == counter]
-    launches = len({r[0] for r in win if any(k in r[1] for k in fam)})
-    return sum(r[3] for r in cal), sum(r[3] for r in gem), launches
+    gem = [r for s in segs[1:] for r in s if any(k in r[1] for k in FAM)]
+    launches = len({r[0] for r in gem})
+    return sum(r[3] for r in cal), sum(r[3] for r in gem), launches, segs
 
 
 def summarize(fdir, wdir, out):
-    f_cal, f_gemm, n1 = _window(_rows(fdir), "FETCH_SIZE")
-    w_cal, w_gemm, n2 = _window(_rows(wdir), "WRITE_SIZE")
+    f_cal, f_gemm, n1, fseg = _window(_rows(fdir), "FETCH_SIZE")
+    w_cal, w_gemm, n2, wseg = _window(_rows(wdir), "WRITE_SIZE")
     assert n1 == n2, (n1, n2)
     rd = f_gemm * CAL_BYTES / f_cal        # calibrated: units of the counter -> bytes
     wr = w_gemm * CAL_BYTES / w_cal
@@ -96,8 +118,30 @@ def summarize(fdir, wdir, out):
            "fetch_units_per_cal_byte": f_cal / CAL_BYTES, "write_units_per_cal_byte": w_cal / CAL_BYTES,
            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of tools/gemm_traffic.py run (B=128), "
                      "calibrated on a 256 MiB 16-B-lane copy"}
+    # per call: measured read / write bytes beside the algorithmic bytes, and per kernel name
+    calls = meta.get("calls", [])
+    if len(calls) == len(fseg) - 1 == len(wseg) - 1:
+        rows, byk = [], {}
+        for i, c in enumerate(calls):
+            fr = [r for r in fseg[i + 1] if any(k in r[1] for k in FAM)]
+            r_b = sum(r[3] for r in fr) * CAL_BYTES / f_cal
+            w_b = sum(r[3] for r in wseg[i + 1] if any(k in r[1] for k in FAM)) * CAL_BYTES / w_cal
+            alg = sum(p["alg_bytes"] for p in c["problems"])
+            ks = sorted({r[1].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0] for r in fr})
+            rows.append({"i": i, "kind": c["kind"], "kernels": ks, "read": r_b, "write": w_b, "alg": alg,
+                         "ratio": (r_b + w_b) / alg if alg else None,
+                         "problems": [{k: p[k] for k in ("M", "N", "K", "a_mode", "b_mode", "c_mode", "tile",
+                                                         "split_k", "hw", "cin")} for p in c["problems"]]})
+            for k in ks:
+                e = byk.setdefault(k, {"calls": 0, "read": 0.0, "write": 0.0, "alg": 0.0})
+                e["calls"] += 1
+                e["read"] += r_b / len(ks)
+                e["write"] += w_b / len(ks)
+                e["alg"] += alg / len(ks)
+        res["by_kernel"] = dict(sorted(byk.items(), key=lambda kv: -(kv[1]["read"] + kv[1]["write"])))
+        res["worst_calls"] = sorted(rows, key=lambda r: -(r["read"] + r["write"] - r["alg"]))[:25]
     json.dump(res, open(out, "w"), indent=1)
-    print(json.dumps(res, indent=1))
+    print(json.dumps({k: v for k, v in res.items() if k not in ("worst_calls",)}, indent=1))
 
 
 def main():
