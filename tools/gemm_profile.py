@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--pairs", type=int, default=1, help="choose paired wgrad/dgrad tiles by timing the pair")
+    ap.add_argument("--wg", type=int, default=1, help="sweep the WG3 / WGL weight-gradient kernels' splits too")
     ap.add_argument("--write-table", default="", help="path for the measured (tile, split) table, e.g. "
                     "gpurun_out/gemm_tiles.json (copy it to encdiff_amd/gemm_tiles.json)")
     args = ap.parse_args()
@@ -144,13 +145,15 @@ def main():
         dgrad = a.b_mode in (L.OPB_ROWN, L.OPB_CONV_DGRAD) and not wgrad
         cands = (1, 2, 3, 4, 5, 7, 9, 10) if wgrad else ((1, 2, 3, 4, 5, 9, 10) if dgrad else
                                                       (1, 2, 3, 4, 5, 6, 7, 8, 9, 10))
+        if wgrad and args.wg:  # the weight-gradient kernels with their own split sweep: WG3 (3x3), WGL (linear)
+            cands += (32,) if a.b_mode == L.OPB_IM2COL else ((36,) if a.b_mode == L.OPB_ROWN else ())
         if a.a_mode == L.OPA_IM2COL and a.b_mode in (L.OPB_ROWK, L.OPB_CONV_DGRAD):
             # halo tiles (window staged once; split-K 1); paired input gradients: 16, 17, 18, 22
             halo = (16, 17, 18, 22) if dgrad else tuple(ops.HALO_TILES)
             cands += tuple(t for t in halo if ops.halo_fits(t, a.conv.batch, a.conv.h, a.conv.w, a.conv.cin,
                                                             a.conv.resample))
         for tile in cands:
-            for split in ((1,) if tile >= 16 else (1, 2, 4, 8, 16, 32, 64, 128, 256)):
+            for split in ((1,) if 16 <= tile < 32 else (1, 2, 4, 8, 16, 32, 64, 128, 256)):
                 if split > 1 and a.K // split < 64:
                     continue
                 if wgrad and split > 1 and split * a.M * (a.N + 1) > ops.WS_HALF // 2:
