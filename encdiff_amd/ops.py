@@ -141,27 +141,37 @@ def halo_fits(tile, batch, h, w, cin, resample):
     return max(chunks * 16 + 3 * bn * 64 * 2, bm * (bn + 4) * 4) <= HALO_LDS_MAX
 
 
-def plan_key(M, N, K, a_mode, b_mode, c_mode, resample=0):
+def plan_key(M, N, K, a_mode, b_mode, c_mode, resample=0, h=0):
+    """Tile-table key.  h (the conv geometry's h, implicit-im2col problems): the same (M, N, K) is a
+    different conv at another batch (B=512 at 8x8 has B=128 16x16's pixel count), and the halo
+    and WG3 tiles are valid only for the geometry they were measured on -- keys written with h
+    are looked up first, plain keys (older tables) after them."""
     key = f"{a_mode},{b_mode},{c_mode},{M},{N},{K}"
-    return key + (f",r{resample}" if resample else "")
+    return key + (f",r{resample}" if resample else "") + (f",h{h}" if h else "")
 
 
-def fold_choice(M, N, K, a_mode, b_mode, c_mode, resample=0) -> bool:
+def _table_hit(M, N, K, a_mode, b_mode, c_mode, resample, h):
+    t = _tile_table()
+    for cm in ((c_mode, L.OUT_BF16) if c_mode == L.OUT_F32 else (c_mode,)):  # f32 output: the bf16 plan
+        for hh in ((h, 0) if h else (0,)):
+            hit = t.get(plan_key(M, N, K, a_mode, b_mode, cm, resample, hh))
+            if hit is not None:
+                return hit
+    return None
+
+
+def fold_choice(M, N, K, a_mode, b_mode, c_mode, resample=0, h=0) -> bool:
     """Whether a split-K GEMM combines its slabs in the kernel (measured per problem)."""
     if SPLIT_FOLD != 1:
         return SPLIT_FOLD == 2
-    hit = _tile_table().get(plan_key(M, N, K, a_mode, b_mode, c_mode, resample))
-    if hit is None and c_mode == L.OUT_F32:
-        hit = _tile_table().get(plan_key(M, N, K, a_mode, b_mode, L.OUT_BF16, resample))
+    hit = _table_hit(M, N, K, a_mode, b_mode, c_mode, resample, h)
     return hit is not None and len(hit) > 3 and bool(hit[3])
 
 
-def plan(M, N, K, a_mode, b_mode, c_mode, resample=0):
+def plan(M, N, K, a_mode, b_mode, c_mode, resample=0, h=0):
     """(tile, split_k) for a GEMM: measured table (tools/gemm_profile.py --write-table) first,
     else a heuristic aiming at >= 256 workgroups with bounded split-K traffic."""
-    hit = _tile_table().get(plan_key(M, N, K, a_mode, b_mode, c_mode, resample))
-    if hit is None and c_mode == L.OUT_F32:  # same problem with a bf16 output: same tile plan
-        hit = _tile_table().get(plan_key(M, N, K, a_mode, b_mode, L.OUT_BF16, resample))
+    hit = _table_hit(M, N, K, a_mode, b_mode, c_mode, resample, h)
     if hit is not None:
         tile, split = int(hit[0]), min(int(hit[1]), MAX_SPLIT)
         if split == 1 or c_mode in (L.OUT_F32_ATOMIC, L.OUT_F32_ATOMIC_CONVW) or split * M * (N + 1) <= WS_FLOATS:
@@ -267,8 +277,10 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
         if sp is not None and (sp == 1 or sp * M * (N + 1) <= WS_HALF // 2):
             tile, split_k = 36, sp
     pm = plan_m or M  # the row count whose measured plan is used (linear_fwd plan_m)
+    rs = conv.resample if conv is not None else 0
+    hk = conv.h if conv is not None and (a_mode == L.OPA_IM2COL or b_mode == L.OPB_IM2COL) else 0
     if split_k is None or tile == 0:
-        t, sp = plan(pm, N, K, a_mode, b_mode, c_mode, conv.resample if conv is not None else 0)
+        t, sp = plan(pm, N, K, a_mode, b_mode, c_mode, rs, hk)
         tile = tile or FORCE_TILE or t
         split_k = split_k or sp
     ws = None
@@ -280,7 +292,7 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
         # the in-kernel combine indexes one ticket per output tile: only when every tile shape
         # (>= 32 x 32) stays within the ticket array
         if (a_mode != L.OPA_ROWM and math.ceil(M / 32) * math.ceil(N / 32) <= COUNTERS and
-                (fold or fold_choice(pm, N, K, a_mode, b_mode, c_mode, conv.resample if conv is not None else 0))):
+                (fold or fold_choice(pm, N, K, a_mode, b_mode, c_mode, rs, hk))):
             cnt = _counters()
     return L.GemmArgs(M=M, N=N, K=K, a_mode=a_mode, b_mode=b_mode, c_mode=c_mode,
                       a=_p(a), lda=lda, b=_p(b), ldb=ldb, c=_p(c), ldc=ldc,

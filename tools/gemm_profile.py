@@ -120,13 +120,17 @@ def main():
         return {(1, 0): "conv_fwd", (1, 2): "conv_dgrad", (2, 3): "conv_wgrad", (0, 0): "lin_fwd",
                 (0, 1): "lin_dgrad", (2, 1): "lin_wgrad"}.get(modes, str(modes))
 
+    def key_of(a):  # implicit-im2col problems keyed with their geometry (ops.plan_key)
+        im2 = a.a_mode == L.OPA_IM2COL or a.b_mode == L.OPB_IM2COL
+        return ops.plan_key(a.M, a.N, a.K, a.a_mode, a.b_mode, a.c_mode, a.conv.resample, a.conv.h if im2 else 0)
+
     tot_cur, tot_best = defaultdict(float), defaultdict(float)
     flops = defaultdict(float)
     table = {}
     rows = []
     done = {}
     for a in calls:
-        key = ops.plan_key(a.M, a.N, a.K, a.a_mode, a.b_mode, a.c_mode, a.conv.resample)
+        key = key_of(a)
         if key in done:  # same problem already swept: reuse
             cur, best_tile, best_split, best_t, best_fold = done[key]
             k = cat(a)
@@ -209,7 +213,6 @@ def main():
             torch.cuda.synchronize()
             return s.elapsed_time(f) / args.reps * 1e3
 
-        key_of = lambda a: ops.plan_key(a.M, a.N, a.K, a.a_mode, a.b_mode, a.c_mode, a.conv.resample)
         for rec in recs:
             if rec[0] != "pair_ex":
                 continue
