@@ -168,10 +168,10 @@ def fold_choice(M, N, K, a_mode, b_mode, c_mode, resample=0, h=0) -> bool:
     return hit is not None and len(hit) > 3 and bool(hit[3])
 
 
-def plan(M, N, K, a_mode, b_mode, c_mode, resample=0, h=0):
+def plan(M, N, K, a_mode, b_mode, c_mode, resample=0, h=0, table=True):
     """(tile, split_k) for a GEMM: measured table (tools/gemm_profile.py --write-table) first,
     else a heuristic aiming at >= 256 workgroups with bounded split-K traffic."""
-    hit = _table_hit(M, N, K, a_mode, b_mode, c_mode, resample, h)
+    hit = _table_hit(M, N, K, a_mode, b_mode, c_mode, resample, h) if table else None
     if hit is not None:
         tile, split = int(hit[0]), min(int(hit[1]), MAX_SPLIT)
         if split == 1 or c_mode in (L.OUT_F32_ATOMIC, L.OUT_F32_ATOMIC_CONVW) or split * M * (N + 1) <= WS_FLOATS:
@@ -281,6 +281,8 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
     hk = conv.h if conv is not None and (a_mode == L.OPA_IM2COL or b_mode == L.OPB_IM2COL) else 0
     if split_k is None or tile == 0:
         t, sp = plan(pm, N, K, a_mode, b_mode, c_mode, rs, hk)
+        if (t in (32, 33, 34) and not WG3) or (t == 36 and not WGL):  # kernel switched off: generic plan
+            t, sp = plan(pm, N, K, a_mode, b_mode, c_mode, rs, hk, table=False)
         tile = tile or FORCE_TILE or t
         split_k = split_k or sp
     ws = None
