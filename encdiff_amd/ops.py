@@ -231,6 +231,10 @@ def wg3_split(batch, h, w, cout, cin, resample, lda, ld_src, c_mode, tile=None):
     return best or 1
 
 
+# tuned table entries for weight gradients over the WG3 / WGL heuristics (gemm_args): 0 off, 1 entries
+# naming WG3 / WGL, 2 any entry
+TABLE_WG = int(os.environ.get("ENCDIFF_TABLE_WG", "0"))
+
 # linear weight gradients on the WGL kernel (tile 36): 0 off, 1 square c x c layers only, 2 every eligible one
 WGL = int(os.environ.get("ENCDIFF_WGL", "1"))
 
@@ -263,6 +267,16 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
         tile = 4
     if lna is not None:  # LayerNorm of the A rows in the staging: 64x64 tiles, no split
         tile, split_k = 4, 1
+    if TABLE_WG and tile == 0 and split_k is None and a_mode == L.OPA_ROWM:
+        # a tuned table entry for this exact weight gradient (conv: keyed with its geometry) overrides
+        # the WG3 / WGL split heuristics (1: entries naming those kernels, 2: any entry)
+        im2 = conv is not None and b_mode == L.OPB_IM2COL
+        hit = _tile_table().get(plan_key(M, N, K, a_mode, b_mode, c_mode, conv.resample if im2 else 0,
+                                         conv.h if im2 else 0))
+        if hit is not None and (TABLE_WG == 2 or int(hit[0]) in (32, 33, 34, 36)):
+            t, sp = int(hit[0]), int(hit[1])
+            if (t not in (32, 33, 34) or WG3) and (t != 36 or WGL) and (sp == 1 or sp * M * (N + 1) <= WS_HALF // 2):
+                tile, split_k = t, sp
     if (WG3 and tile == 0 and split_k is None and a_mode == L.OPA_ROWM and b_mode == L.OPB_IM2COL and
             conv is not None and N == 9 * conv.cin and K == conv.batch * conv.h * conv.w):
         sp = wg3_split(conv.batch, conv.h, conv.w, M, conv.cin, conv.resample, lda, conv.ld_src, c_mode)
