@@ -233,7 +233,7 @@ def wg3_split(batch, h, w, cout, cin, resample, lda, ld_src, c_mode, tile=None):
 
 # tuned table entries for weight gradients over the WG3 / WGL heuristics (gemm_args): 0 off, 1 entries
 # naming WG3 / WGL, 2 any entry
-TABLE_WG = int(os.environ.get("ENCDIFF_TABLE_WG", "0"))
+TABLE_WG = int(os.environ.get("ENCDIFF_TABLE_WG", "1"))
 
 # linear weight gradients on the WGL kernel (tile 36): 0 off, 1 square c x c layers only, 2 every eligible one
 WGL = int(os.environ.get("ENCDIFF_WGL", "1"))
