@@ -363,10 +363,12 @@ def test_conv3x3(O, B, H, cin, cout, mode):
                                                 (128, 8, 128, 128, 0), (64, 8, 384, 128, 0), (128, 4, 256, 256, 0),
                                                 (16, 4, 512, 256, 2), (8, 8, 64, 32, 0)])
 @pytest.mark.parametrize("tile", [32, 33, 34])
-def test_conv3x3_wgrad_wg3(O, B, H, cin, cout, mode, tile):
+def test_conv3x3_wgrad_wg3(O, B, H, cin, cout, mode, tile, monkeypatch):
     """The 3x3 weight-gradient kernel (gemm.hip WG3, tile 32) vs a torch fp32 reference and vs the
     split-K GEMM form: dW (channels-last, accumulated onto a nonzero dW) and the bias gradient;
-    then two paired backward launches in a row (the first's finalize deferred into the second)."""
+    then two paired backward launches in a row (the first's finalize deferred into the second).
+    The heuristic WG3 plan is what is tested here (no tuned-table override, ops.TABLE_WG)."""
+    monkeypatch.setattr(O, "TABLE_WG", 0)
     from encdiff_amd.ops import Geom
     from encdiff_amd import _lib as L
     torch.manual_seed(11)
@@ -416,10 +418,11 @@ def test_conv3x3_wgrad_wg3(O, B, H, cin, cout, mode, tile):
 
 @pytest.mark.parametrize("T,cout,cin", [(32768, 64, 64), (8192, 128, 128), (2048, 256, 256), (32768, 512, 64),
                                          (8192, 1024, 128), (2048, 2048, 256), (256, 64, 128), (2048, 192, 64)])
-def test_linear_wgrad_wgl(O, T, cout, cin):
+def test_linear_wgrad_wgl(O, T, cout, cin, monkeypatch):
     """The linear weight-gradient kernel (gemm.hip WGL, tile 36) vs a torch fp32 reference and vs
     the split-K GEMM form (dW accumulated onto a nonzero dW, bias gradient), then two paired
     backward launches in a row (input gradient in the same grid, the first finalize deferred)."""
+    monkeypatch.setattr(O, "TABLE_WG", 0)  # the heuristic WGL plan (no tuned-table override)
     torch.manual_seed(12)
     dy, x = bf(T, cout), bf(T, cin)
     sp = O.wgl_split(cout, cin, T, cout, cin, O.L.OUT_F32_ACCUM)
