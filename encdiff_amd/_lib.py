@@ -148,6 +148,9 @@ _PROTOS = {
     "encdiff_gemm_pair": [C.POINTER(GemmArgs), C.POINTER(GemmArgs), vp],
     "encdiff_gemm_pair_ex": [C.POINTER(GemmArgs), C.POINTER(GemmArgs), C.POINTER(GemmArgs), C.c_int, vp],
     "encdiff_gemm_finalize": [C.POINTER(GemmArgs), vp],
+    "encdiff_wgrad_group_plan": [C.POINTER(GemmArgs), C.c_int, vp, C.c_long, vp, C.c_int, vp, C.c_long,
+                                 C.POINTER(C.c_long)],
+    "encdiff_wgrad_group_launch": [vp, vp, vp],
     "encdiff_gemm_ex": [C.POINTER(GemmArgs), C.c_int, C.POINTER(C.c_int), vp],
     "encdiff_gemm_pair_dx": [C.POINTER(GemmArgs), C.POINTER(GemmArgs), C.POINTER(GemmArgs), C.c_int, C.c_int,
                              C.POINTER(C.c_int), vp],
@@ -169,6 +172,7 @@ _PROTOS = {
     "encdiff_ddim_step": [vp, vp, vp, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, vp, vp, vp],
     "encdiff_ddim_step_indexed": [vp, vp, vp, C.c_int, vp, vp, C.c_int, vp, vp, vp],
     "encdiff_adamw_ema": [vp, vp, vp, vp, vp, C.c_longlong, vp, C.c_longlong, vp],
+    "encdiff_adamw_ema_mirror": [vp, vp, vp, vp, vp, C.c_longlong, vp, C.c_longlong, vp, vp],
     "encdiff_pack_weights": [vp, vp, vp, C.c_int, vp],
     "encdiff_reduce_partials": [vp, C.c_long, C.c_int, C.c_int, vp, vp, vp],
     "encdiff_grad_fold": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp],

@@ -16,6 +16,8 @@ each self-attention's to_q/to_k/to_v one [3C][C] matrix.
 """
 from __future__ import annotations
 
+import os
+
 import ctypes as C
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -67,6 +69,11 @@ class ParamArena:
                 p.grad = self.view_in(self.grad, name)
         self.step = 0
         self.hyper = torch.zeros(8, device=self.device, dtype=torch.float32)
+        # bf16 shadow of the arena, index for index (enable_mirror): the GEMM operand copy of every
+        # weight whose compute layout is its arena layout.  The fused optimizer writes it with the
+        # update (encdiff_adamw_ema_mirror); mirror_fresh tells the packs it was just written.
+        self.mirror: Optional[torch.Tensor] = None
+        self.mirror_fresh = False
         # bumped by every host-side write of parameter values (EMA swap, load_state_dict):
         # consumers of bf16 weight copies (UNet / Encoder4 packs) repack when it moves.
         # Writes through a parameter's .data do not bump master._version (p.data is a view
@@ -138,23 +145,41 @@ class ParamArena:
         self.attach_grads()
         self.grad.zero_()
 
+    def enable_mirror(self) -> torch.Tensor:
+        if self.mirror is None:
+            self.mirror = self.master.to(torch.bfloat16)
+        return self.mirror
+
     def enable_ema(self):
         if self.ema is None:
             self.ema = self.master[: self.ema_numel].clone()
         return self.ema
 
 
+# plain-cast weights live in the arena's bf16 mirror, written by the optimizer with the update
+# (0: every weight packed into the table's own buffer by encdiff_pack_weights, A/B runs)
+MIRROR = os.environ.get("ENCDIFF_PACK_MIRROR", "1") != "0"
+
+
 class PackTable:
-    """bf16 compute copies of the GEMM weights, refreshed from the fp32 arena by one
-    kernel (encdiff_pack_weights) after every optimizer step."""
+    """bf16 compute copies of the GEMM weights.  Weights whose compute layout is their arena layout
+    (kind 0: a plain cast) are views of the arena's bf16 mirror, which the fused optimizer writes
+    with the update; the rest (permuted / padded / split-bf16 layouts) are packed from the fp32
+    arena into this table's buffer by one kernel (encdiff_pack_weights) after every step."""
 
     def __init__(self, arena: ParamArena):
         self.arena = arena
         self.jobs: List[L.PackJob] = []
+        self.mjobs: List[L.PackJob] = []  # mirror ranges (refreshed here only outside the optimizer)
         self.views: Dict[str, Tuple[int, int, int]] = {}  # key -> (dst_off, rows, cols)
+        self.mviews: Dict[str, Tuple[int, int, int]] = {}  # key -> (arena offset, rows, cols)
         self.numel = 0
 
     def add(self, key: str, src_off: int, rows: int, cols: int, kind: int = 0, cin: int = 0):
+        if MIRROR and kind == 0 and src_off % 8 == 0:
+            self.mjobs.append(L.PackJob(src_off=src_off, dst_off=src_off, rows=rows, cols=cols, kind=0, cin=0))
+            self.mviews[key] = (src_off, rows, cols)
+            return
         off = (self.numel + 7) // 8 * 8
         self.jobs.append(L.PackJob(src_off=src_off, dst_off=off, rows=rows, cols=cols, kind=kind, cin=cin))
         self.views[key] = (off, rows, cols)
@@ -163,17 +188,34 @@ class PackTable:
     def finalize(self):
         dev = self.arena.device
         self.buf = torch.zeros(max(self.numel, 8), device=dev, dtype=torch.bfloat16)
-        arr = (L.PackJob * len(self.jobs))(*self.jobs)
-        self.jobs_dev = torch.frombuffer(bytearray(arr), dtype=torch.uint8).to(dev)
-        self.njobs = len(self.jobs)
+
+        def table(jobs):
+            arr = (L.PackJob * max(len(jobs), 1))(*jobs)
+            return torch.frombuffer(bytearray(arr), dtype=torch.uint8).to(dev), len(jobs)
+        self.jobs_dev, self.njobs = table(self.jobs)
+        self.mjobs_dev, self.nmjobs = table(self.mjobs)
+        if self.mjobs:
+            self.arena.enable_mirror()
 
     def view(self, key: str) -> torch.Tensor:
+        if key in self.mviews:
+            off, rows, cols = self.mviews[key]
+            return self.arena.mirror[off:off + rows * cols].view(rows, cols)
         off, rows, cols = self.views[key]
         return self.buf[off:off + rows * cols].view(rows, cols)
 
+    def snapshot(self) -> torch.Tensor:
+        """Every packed weight, concatenated (tests: did a repack happen)."""
+        return torch.cat([self.buf] + [self.view(k).reshape(-1) for k in self.mviews])
+
     def repack(self):
+        """Refresh every bf16 copy from the fp32 arena -- the mirror ranges too, unless the
+        optimizer has just written them (arena.mirror_fresh)."""
         from . import ops
-        ops.pack_weights(self.arena.master, self.buf, self.jobs_dev, self.njobs)
+        if self.nmjobs and not self.arena.mirror_fresh:
+            ops.pack_weights(self.arena.master, self.arena.mirror, self.mjobs_dev, self.nmjobs)
+        if self.njobs:
+            ops.pack_weights(self.arena.master, self.buf, self.jobs_dev, self.njobs)
 
 
 class NormPartials:

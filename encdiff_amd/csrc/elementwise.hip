@@ -528,21 +528,29 @@ __global__ __launch_bounds__(256) void step_prologue_kernel(const EncdiffStepPro
   for (int j = 0; j < a.njobs; ++j) {
     const EncdiffZeroJob z = a.jobs[j];
     const long long per = z.row_bytes >> 4, n = z.rows * per;
-    for (long long i = gid; i < n; i += gs) {
-      const long long r = i / per, cc = i - r * per;
-      *(uint4*)((char*)z.ptr + r * z.ld_bytes + cc * 16) = make_uint4(0u, 0u, 0u, 0u);
+    if (z.ld_bytes == z.row_bytes || z.rows == 1) {  // contiguous: a flat 16-B sweep (the gradient arena)
+      uint4* p = (uint4*)z.ptr;
+      for (long long i = gid; i < n; i += gs) p[i] = make_uint4(0u, 0u, 0u, 0u);
+    } else {  // strided rows: 32-bit row / column split (the host keeps rows and per < 2^31)
+      for (long long i = gid; i < n; i += gs) {
+        const uint32_t r = (uint32_t)i / (uint32_t)per, cc = (uint32_t)i - r * (uint32_t)per;
+        *(uint4*)((char*)z.ptr + (long long)r * z.ld_bytes + (long long)cc * 16) = make_uint4(0u, 0u, 0u, 0u);
+      }
     }
   }
-  // the last workgroup advances the counters (every workgroup read *rng_counter before its ticket)
+  // the last workgroup advances the counters (every workgroup read *rng_counter before its ticket).
+  // Only that read must be complete before the ticket: a wait on this wave's memory operations,
+  // not a __threadfence (an agent release writes back the XCD L2's dirty lines -- here the freshly
+  // zeroed arena, 2048 times: it was most of the kernel's time).  The counters reach the next
+  // kernels at the kernel boundary.
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int tk = atomicAdd(a.done, 1);
     if (tk == (int)gridDim.x - 1) {
       *a.rng_counter = ctr + 1;
       if (a.data_step) *a.data_step += 1;
       *a.done = 0;
-      __threadfence();
     }
   }
 }
@@ -552,7 +560,8 @@ __global__ __launch_bounds__(256) void step_prologue_kernel(const EncdiffStepPro
 __global__ __launch_bounds__(256) void adamw_ema_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         float* __restrict__ ema, long long n,
-                                                        const float* __restrict__ hyper, long long ema_n) {
+                                                        const float* __restrict__ hyper, long long ema_n,
+                                                        bf16_t* __restrict__ mirror) {
   const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
   const float step_size = hyper[5], inv_bc2_sqrt = hyper[6], omd = hyper[7];
   const long long n4 = n >> 2;
@@ -569,6 +578,7 @@ __global__ __launch_bounds__(256) void adamw_ema_kernel(float* __restrict__ p, c
       pa[k] -= step_size * ma[k] / denom;
     }
     ((float4*)p)[i] = pp; ((float4*)m)[i] = mm; ((float4*)v)[i] = vv;
+    if (mirror) ((uint2*)mirror)[i] = make_uint2(pack2(pa[0], pa[1]), pack2(pa[2], pa[3]));  // bf16 GEMM copy
     if (ema && 4 * i < ema_n) {  // LitEma.forward (ema.py:37-42): s -= (1 - decay) (s - p)
       float4 ee = ((float4*)ema)[i];
       float* ea = &ee.x;
@@ -840,9 +850,14 @@ extern "C" int encdiff_step_prologue(const EncdiffStepPrologueArgs* a, void* str
 
 extern "C" int encdiff_adamw_ema(float* p, const float* g, float* m, float* v, float* ema, long long n,
                                  const float* hyper, long long ema_n, void* stream) {
-  if (!p || !g || !m || !v || !hyper || n % 4) return ENCDIFF_ERR_ARG;
+  return encdiff_adamw_ema_mirror(p, g, m, v, ema, n, hyper, ema_n, nullptr, stream);
+}
+
+extern "C" int encdiff_adamw_ema_mirror(float* p, const float* g, float* m, float* v, float* ema, long long n,
+                                        const float* hyper, long long ema_n, void* mirror, void* stream) {
+  if (!p || !g || !m || !v || !hyper || n % 4 || ((uintptr_t)mirror & 7)) return ENCDIFF_ERR_ARG;
   hipLaunchKernelGGL(adamw_ema_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, ema, n,
-                     hyper, ema_n);
+                     hyper, ema_n, (bf16_t*)mirror);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }

@@ -16,6 +16,10 @@
 // 43,58,233-259 (every Conv2d / Linear forward and their autograd backward).
 #include "common.h"
 
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
 namespace {
 
 constexpr int BK = 64;
@@ -269,7 +273,29 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
   const int kt_per = (ktiles_total + p.split_k - 1) / p.split_k;
   const int kt_begin = bz * kt_per;
   const int kt_end = min(ktiles_total, kt_begin + kt_per);
-  const int nkt = kt_end - kt_begin;
+  int nkt = kt_end - kt_begin;
+  // halo tiles with split-K: split bz owns the source channels [hcb, hcb + 8 h.ch) of every tap
+  // (the window holds that slice only); its k-tiles run tap by tap over the slice's 64-channel
+  // groups, k-tile (tap, g) = tap * cin / 64 + bz * ncc + g
+  uint32_t hcb = 0;
+  int kt_ncc = 0, kt_c64 = 0;
+  if constexpr (G::HALO) {
+    if (p.split_k > 1) {
+      kt_ncc = aux.halo.ch >> 3;
+      kt_c64 = p.conv.cin >> 6;
+      hcb = (uint32_t)(bz * aux.halo.ch * 8);
+      nkt = aux.halo.kt * aux.halo.kt * kt_ncc;
+    }
+  }
+  auto ktile = [&](int it) -> int {
+    if constexpr (G::HALO) {
+      if (kt_ncc) {
+        const int tap = it / kt_ncc;
+        return tap * kt_c64 + bz * kt_ncc + (it - tap * kt_ncc);
+      }
+    }
+    return kt_begin + it;
+  };
 
   const bf16_t* __restrict__ A = (const bf16_t*)p.a;
   const bf16_t* __restrict__ B = (const bf16_t*)p.b;
@@ -308,7 +334,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
       const int cy = cy0 + (int)hy, cx = h.off + (int)(r - hy * (uint32_t)h.hc);
       const bool ok = (int)px < h.npix && (unsigned)cy < (unsigned)h.lh && (unsigned)cx < (unsigned)h.lw;
       const uint32_t row = ((b0 + j) * (uint32_t)h.hs + (uint32_t)(cy >> h.ush)) * (uint32_t)h.ws + (uint32_t)(cx >> h.ush);
-      const void* src = ok ? (const void*)(A + (size_t)row * p.conv.ld_src + gch * 8) : (const void*)&g_zero16;
+      const void* src = ok ? (const void*)(A + (size_t)row * p.conv.ld_src + hcb + gch * 8) : (const void*)&g_zero16;
       __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(smem + (c & ~63) * 8), 16, 0, 0);
     }
   };
@@ -547,7 +573,7 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     const HaloGeom& h = aux.halo;
     uint32_t k = (uint32_t)(kt * BK + kk * 32 + g4 * 8);
     if (k >= (uint32_t)p.K) k = 0;  // tail of the last k-tile: B is zero there, keep A finite
-    const uint32_t tap = fdiv(k, aux.cin), ci = k - tap * (uint32_t)p.conv.cin;
+    const uint32_t tap = fdiv(k, aux.cin), ci = k - tap * (uint32_t)p.conv.cin - hcb;
     const uint32_t ty = h.kt == 4 ? tap >> 2 : (tap * 11u) >> 5;
     const uint32_t hp = hpb[i] + ty * (uint32_t)h.hc + (tap - (uint32_t)h.kt * ty);
     const uint32_t slot = (ci >> 3) ^ ((hp >> h.xsh) & (uint32_t)h.xmsk);
@@ -824,15 +850,15 @@ __device__ __forceinline__ void gemm_tile(const EncdiffGemmArgs& p, const GemmAu
     if constexpr (G::HALO) stage_halo();
 #pragma unroll
     for (int st = 0; st < D - 1; ++st)
-      if (st < nkt) stage(ring + st * G::STAGE, kt_begin + st);
+      if (st < nkt) stage(ring + st * G::STAGE, ktile(st));
     int rd = 0, wr = D - 1;  // ring slots of the tile read now / the tile issued next
     for (int it = 0; it < nkt; ++it) {
       vm_wait_stages<G::LPS, D - 2>(min(D - 2, nkt - 1 - it));
       if constexpr (G::AGN) agn_transform(ring + rd * G::STAGE, kt_begin + it);
       if constexpr (G::LNA) lna_transform(ring + rd * G::STAGE, kt_begin + it);
       asm volatile("s_barrier" ::: "memory");  // (asm: the compiler may not move LDS-DMA issue across it)
-      if (it + D - 1 < nkt) stage(ring + wr * G::STAGE, kt_begin + it + D - 1);
-      compute(ring + rd * G::STAGE, kt_begin + it);
+      if (it + D - 1 < nkt) stage(ring + wr * G::STAGE, ktile(it + D - 1));
+      compute(ring + rd * G::STAGE, ktile(it));
       // this wave's fragment reads of slot rd retire before it reaches the next barrier
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       rd = rd + 1 == D ? 0 : rd + 1;
@@ -1485,16 +1511,48 @@ struct Wg3Stage {
 // (the body is a __device__ function, as gemm_tile: a kernel template whose own body calls a lambda
 // holding device builtins loses its host launch stub.  TAG: one body specialization per kernel --
 // hipcc's host pass rejects a second kernel instantiation calling the same one)
+// Split-K combine of a grouped weight gradient (wgrad_group_kernel; the SplitFold that wg_prepare
+// sets): the workgroup's slab stores were write-through (sc1); after draining them, one lane takes
+// the output part's ticket (relaxed, agent scope), and the chunk that draws split - 1 acquires and
+// returns true -- it then sums the part's slabs in chunk order (bitwise reproducible, independent
+// of which chunk arrives last or where it runs) -- and leaves the ticket at zero for the next launch.
+// The guide's write-through ticket recipe, as the GEMM tiles' in-kernel combine.
+ED_DEV bool wg_last_chunk(int* cnt, int split, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int tk = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = tk == split - 1;
+  }
+  __syncthreads();
+  if (!flag[0]) return false;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return true;
+}
+constexpr int WG3_PART = 32 * 9 * 16, WGL_PART = 64 * 64;  // floats of one output part
+ED_DEV float4 f4add(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+// the combined part written to the user's output: alpha, then += the output (F32_ACCUM)
+ED_DEV void wg_fold_store(const SplitFold& f, float* o, float4 v) {
+  v.x *= f.alpha; v.y *= f.alpha; v.z *= f.alpha; v.w *= f.alpha;
+  if (f.mode == ENCDIFF_OUT_F32_ACCUM) v = f4add(v, *(const float4*)o);
+  *(float4*)o = v;
+}
+
 template <int W, bool UP, int NS, int WPG, int TAG = 0>
-__device__ __forceinline__ void wgrad3x3_body(const EncdiffGemmArgs& p, const int nblk, char* wsm) {
+__device__ __forceinline__ void wgrad3x3_body(const EncdiffGemmArgs& p, const int bid, char* wsm,
+                                              const SplitFold* fold = nullptr) {
   using G = Wg3<W>;
   constexpr int H = W;
   constexpr uint32_t OOB = 0x80000000u;
   typedef __attribute__((address_space(3))) void lds_void;
   const int cin = p.conv.cin, cout = p.M;
   const int ncit = cin >> 4, nparts = (cout >> 5) * ncit;
-  const int bid = xcd_remap(blockIdx.x, nblk);  // a chunk's parts (sharing dY / x rows) on one XCD
-  const int z = bid / nparts, part = bid - z * nparts;
+  const int z = bid / nparts, part = bid - z * nparts;  // bid: the caller's logical block
   const int cot = part / ncit, cit = part - cot * ncit;
   const int co0 = cot * 32, ci0 = cit * 16;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1603,6 +1661,7 @@ __device__ __forceinline__ void wgrad3x3_body(const EncdiffGemmArgs& p, const in
   float* out = (float*)p.c + (slab ? (long)z * MN : 0);
   const long ldo = slab ? p.N : p.ldc;
   const auto rso = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, 0x7FFFFFF0, 0x00020000);
+  const auto rsp = __builtin_amdgcn_make_buffer_rsrc((void*)p.c, 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     __syncthreads();  // ring (m = 0) / the previous half's image (m = 1) no longer read
@@ -1629,7 +1688,10 @@ __device__ __forceinline__ void wgrad3x3_body(const EncdiffGemmArgs& p, const in
       }
       const int c4 = f & 3, ct = f >> 2, t = ct % 9, co = co0 + m * 16 + ct / 9;
       const long off = (long)co * ldo + t * cin + ci0 + 4 * c4;
-      if (slab) {
+      if (slab && fold) {  // part-major slab [z][part][32 co][9 tap][16 ci]: no cache line shared by two parts
+        const long po = ((long)z * nparts + part) * WG3_PART + (m * 16 + ct / 9) * 144 + t * 16 + 4 * c4;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rsp, (int)(po * 4), 0, 16);
+      } else if (slab) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rso, (int)(off * 4), 0, 16);
       } else {
         float4* o = (float4*)(out + off);
@@ -1647,8 +1709,33 @@ __device__ __forceinline__ void wgrad3x3_body(const EncdiffGemmArgs& p, const in
 #pragma unroll
     for (int w = 1; w < WPG; ++w) v += bred[w * 32 + threadIdx.x];
     const int co = co0 + threadIdx.x;
-    if (slab) p.workspace[(long)p.split_k * MN + (long)z * p.M + co] = v;
-    else p.bias_grad[co] += v;
+    if (slab && fold) {  // write-through, as the slab, at [cout tile][z][32]: read by the combining chunk
+      const auto rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.workspace, 0, 0x7FFFFFF0, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(
+          __builtin_bit_cast(uint32_t, v), rsw,
+          (int)(((long)p.split_k * MN + ((long)cot * p.split_k + z) * 32 + threadIdx.x) * 4), 0, 16);
+    } else if (slab) {
+      p.workspace[(long)p.split_k * MN + (long)z * p.M + co] = v;
+    } else {
+      p.bias_grad[co] += v;
+    }
+  }
+  if (!(slab && fold) || !wg_last_chunk(fold->cnt + part, p.split_k, (int*)wsm)) return;
+  // the combining chunk: the part's [32 co][9 tap][16 ci] summed over the chunks in order
+  const float* s0 = (const float*)p.c + (long)part * WG3_PART;
+  const long zs = (long)nparts * WG3_PART;
+  for (int f = threadIdx.x; f < 32 * 9 * 4; f += WPG * 64) {
+    const int cl = f / 36, r = f % 36, t = r >> 2, c4 = r & 3;
+    const int lo = cl * 144 + t * 16 + 4 * c4;
+    float4 v = *(const float4*)(s0 + lo);
+    for (int zz = 1; zz < p.split_k; ++zz) v = f4add(v, *(const float4*)(s0 + zz * zs + lo));
+    wg_fold_store(*fold, (float*)fold->c + (long)(co0 + cl) * fold->ldc + t * cin + ci0 + 4 * c4, v);
+  }
+  if (bg && threadIdx.x < 32) {
+    const float* bz = p.workspace + (long)p.split_k * MN + (long)cot * p.split_k * 32 + threadIdx.x;
+    float v = bz[0];
+    for (int zz = 1; zz < p.split_k; ++zz) v += bz[zz * 32];
+    p.bias_grad[co0 + threadIdx.x] += v;
   }
 }
 
@@ -1662,7 +1749,8 @@ __global__ __launch_bounds__(WPG * 64) void wgrad3x3_kernel(const EncdiffGemmArg
   extern __shared__ __attribute__((aligned(16))) char wsm[];
   int i = blockIdx.x;
   if (i < nblk) {
-    wgrad3x3_body<W, UP, NS, WPG, BM2 * 1000 + BN2 * 10 + AM2>(p, nblk, wsm);
+    // a chunk's parts (sharing dY / x rows) on one XCD
+    wgrad3x3_body<W, UP, NS, WPG, BM2 * 1000 + BN2 * 10 + AM2>(p, xcd_remap(i, nblk), wsm);
     return;
   }
   i -= nblk;
@@ -1744,11 +1832,11 @@ struct WglStage {
 };
 
 template <int NS, int TAG = 0>
-__device__ __forceinline__ void wgradlin_body(const EncdiffGemmArgs& p, const int nblk, char* wsm) {
+__device__ __forceinline__ void wgradlin_body(const EncdiffGemmArgs& p, const int bid, char* wsm,
+                                              const SplitFold* fold = nullptr) {
   typedef __attribute__((address_space(3))) void lds_void;
   const int ntn = p.N >> 6, nparts = (p.M >> 6) * ntn;
-  const int bid = xcd_remap(blockIdx.x, nblk);  // a chunk's parts (sharing dY / x rows) on one XCD
-  const int z = bid / nparts, part = bid - z * nparts;
+  const int z = bid / nparts, part = bid - z * nparts;  // bid: the caller's logical block
   const int mt = part / ntn, nt = part - mt * ntn;
   const int m0 = mt * 64, n0 = nt * 64;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1832,6 +1920,7 @@ __device__ __forceinline__ void wgradlin_body(const EncdiffGemmArgs& p, const in
   float* out = (float*)p.c + (slab ? (long)z * MN : 0);
   const long ldo = slab ? p.N : p.ldc;
   const auto rso = __builtin_amdgcn_make_buffer_rsrc((void*)out, 0, 0x7FFFFFF0, 0x00020000);
+  const auto rsp = __builtin_amdgcn_make_buffer_rsrc((void*)p.c, 0, 0x7FFFFFF0, 0x00020000);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     __syncthreads();
@@ -1860,7 +1949,10 @@ __device__ __forceinline__ void wgradlin_body(const EncdiffGemmArgs& p, const in
       }
       const int row = m0 + h * 32 + (f >> 4), col = n0 + 4 * (f & 15);
       const long off = (long)row * ldo + col;
-      if (slab) {
+      if (slab && fold) {  // part-major slab [z][part][64][64]: no cache line shared by two parts
+        const long po = ((long)z * nparts + part) * WGL_PART + (h * 32 + (f >> 4)) * 64 + 4 * (f & 15);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rsp, (int)(po * 4), 0, 16);
+      } else if (slab) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rso, (int)(off * 4), 0, 16);
       } else {
         float4* o = (float4*)(out + off);
@@ -1878,8 +1970,32 @@ __device__ __forceinline__ void wgradlin_body(const EncdiffGemmArgs& p, const in
 #pragma unroll
     for (int w = 1; w < 4; ++w) v += bred[w * 64 + threadIdx.x];
     const int m = m0 + threadIdx.x;
-    if (slab) p.workspace[(long)p.split_k * MN + (long)z * p.M + m] = v;
-    else p.bias_grad[m] += v;
+    if (slab && fold) {  // write-through, as the slab, at [row tile][z][64]: read by the combining chunk
+      const auto rsw = __builtin_amdgcn_make_buffer_rsrc((void*)p.workspace, 0, 0x7FFFFFF0, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(
+          __builtin_bit_cast(uint32_t, v), rsw,
+          (int)(((long)p.split_k * MN + ((long)mt * p.split_k + z) * 64 + threadIdx.x) * 4), 0, 16);
+    } else if (slab) {
+      p.workspace[(long)p.split_k * MN + (long)z * p.M + m] = v;
+    } else {
+      p.bias_grad[m] += v;
+    }
+  }
+  if (!(slab && fold) || !wg_last_chunk(fold->cnt + part, p.split_k, (int*)wsm)) return;
+  // the combining chunk: the 64 x 64 part summed over the chunks in order, 16 B per lane
+  const float* s0 = (const float*)p.c + (long)part * WGL_PART;
+  const long zs = (long)nparts * WGL_PART;
+  for (int f = threadIdx.x; f < 64 * 16; f += 256) {
+    const int lo = (f >> 4) * 64 + 4 * (f & 15);
+    float4 v = *(const float4*)(s0 + lo);
+    for (int zz = 1; zz < p.split_k; ++zz) v = f4add(v, *(const float4*)(s0 + zz * zs + lo));
+    wg_fold_store(*fold, (float*)fold->c + (long)(m0 + (f >> 4)) * fold->ldc + n0 + 4 * (f & 15), v);
+  }
+  if (bg && threadIdx.x < 64) {
+    const float* bz = p.workspace + (long)p.split_k * MN + (long)mt * p.split_k * 64 + threadIdx.x;
+    float v = bz[0];
+    for (int zz = 1; zz < p.split_k; ++zz) v += bz[zz * 64];
+    p.bias_grad[m0 + threadIdx.x] += v;
   }
 }
 
@@ -1891,7 +2007,8 @@ __global__ __launch_bounds__(256) void wgradlin_kernel(const EncdiffGemmArgs p, 
   extern __shared__ __attribute__((aligned(16))) char wsm[];
   int i = blockIdx.x;
   if (i < nblk) {
-    wgradlin_body<NS, BM2 * 100000 + BN2 * 100 + NS2 * 10 + (KB2 == BK ? 0 : 1)>(p, nblk, wsm);
+    // a chunk's parts (sharing dY / x rows) on one XCD
+    wgradlin_body<NS, BM2 * 100000 + BN2 * 100 + NS2 * 10 + (KB2 == BK ? 0 : 1)>(p, xcd_remap(i, nblk), wsm);
     return;
   }
   i -= nblk;
@@ -2051,7 +2168,7 @@ hipError_t launch_halo_t(const EncdiffGemmArgs& p, const GemmAux& aux, hipStream
   static const hipError_t attr_ok = hipFuncSetAttribute(
       (const void*)gemm_kernel<BM, BN, A_HALO, BMD, HALO_NS, BK>, hipFuncAttributeMaxDynamicSharedMemorySize, HALO_LDS_MAX);
   if (attr_ok != hipSuccess) return attr_ok;
-  dim3 grid(p.M / BM, (p.N + BN - 1) / BN, 1);
+  dim3 grid(p.M / BM, (p.N + BN - 1) / BN, p.split_k);
   hipLaunchKernelGGL((gemm_kernel<BM, BN, A_HALO, BMD, HALO_NS, BK>), grid, dim3(256), halo_lds_bytes(aux.halo, BM, BN), s,
                      p, aux);
   return hipGetLastError();
@@ -2125,8 +2242,9 @@ int prepare_halo(const EncdiffGemmArgs& p, int tile, HaloGeom& h) {
   } else if (p.b_mode != ENCDIFF_OPB_CONV_DGRAD || rs != ENCDIFF_RESAMPLE_NONE) {
     return ENCDIFF_ERR_UNSUPPORTED;
   }
-  if (p.split_k != 1 || p.c_mode == ENCDIFF_OUT_F32_ATOMIC || p.c_mode == ENCDIFF_OUT_F32_ATOMIC_CONVW)
-    return ENCDIFF_ERR_UNSUPPORTED;
+  if (p.c_mode == ENCDIFF_OUT_F32_ATOMIC || p.c_mode == ENCDIFF_OUT_F32_ATOMIC_CONVW) return ENCDIFF_ERR_UNSUPPORTED;
+  // split-K: each split stages and contracts its own slice of the source channels (gemm_tile)
+  if (p.split_k > 1 && (p.conv.cin % (64 * p.split_k) || p.K % 64)) return ENCDIFF_ERR_SHAPE;
   const int bm = halo_bm(tile), bn = halo_bn(tile);
   const int H = p.conv.h, W = p.conv.w, HW = H * W, cin = p.conv.cin;
   if ((long)p.M != (long)p.conv.batch * HW || p.M % bm || bm % W || (HW % bm && bm % HW)) return ENCDIFF_ERR_SHAPE;
@@ -2145,7 +2263,7 @@ int prepare_halo(const EncdiffGemmArgs& p, int tile, HaloGeom& h) {
   h.ni = bm > HW ? bm / HW : 1;
   h.hr = h.s * (rows - 1) + h.kt;
   h.hc = h.s * (W - 1) + h.kt;
-  h.ch = cin / 8;
+  h.ch = cin / 8 / p.split_k;  // the split's channel slice
   h.npix = h.ni * h.hr * h.hc;
   h.chunks = (h.npix * h.ch + 255) & ~255;
   // bank swizzle: consecutive pixels advance q 16-B slots in the 16-slot bank row; g pixels share a
@@ -2361,7 +2479,7 @@ hipError_t launch_pair_halo_t(const GemmPlan& g1, const GemmPlan& g2, const Encd
   if ((size_t)G1::LDS_BYTES > lds) lds = G1::LDS_BYTES;
   const int gx1 = (g1.p.M + 63) / 64, gy1 = (g1.p.N + 63) / 64;
   const int gx2 = g2.p.M / BM2, gy2 = (g2.p.N + BN2 - 1) / BN2;
-  const long nb = (long)gx1 * gy1 * g1.p.split_k + (long)gx2 * gy2 + nf;
+  const long nb = (long)gx1 * gy1 * g1.p.split_k + (long)gx2 * gy2 * g2.p.split_k + nf;
   hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), lds, s, g1.p, g1.aux, g2.p, g2.aux, gx1, gy1, gx2, gy2, pf, nf);
   return hipGetLastError();
 }
@@ -2502,7 +2620,262 @@ hipError_t launch_finalize(const EncdiffGemmArgs& u, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Grouped weight gradients (encdiff_wgrad_group_plan / _launch): the weight gradients of a whole
+// backward region -- every nn.Linear / 3x3 conv / skip conv of the output blocks, or of the rest
+// of the UNet (openaimodel_enc.py:255-275, attention.py:159-167, 211-261) -- in ONE grid, after
+// the region's input-gradient chain has produced every dY.  Alone, each of these problems (output
+// a few KB, K = 2 048 .. 32 768 pixels) fills the chip only through split-K, whose fp32 slabs and
+// finalize passes were half the GEMM family's excess traffic; together there are thousands of
+// output parts, so every problem runs WHOLE (split_k 1): each output element is produced by one
+// workgroup in one ordered sum (reproducible), no slabs, no finalize.  The workgroup bodies are
+// the WG3 (3x3 conv, h in {4, 8, 16}) and WGL (linear, 64 x 64 parts) kernels' and the generic
+// 64 x 64 tile for the rest (2x2 convs, narrow / short-K linears).  Work items are ordered by
+// cost, longest first, so the list scheduling of the dispatcher balances the CUs.
+struct WgProb {
+  EncdiffGemmArgs p;
+  GemmAux aux;
+  int kind, gx, nblk, pad_;
+};
+struct WgBlobHead {
+  int magic, n_probs, n_items, lds;
+  long probs_off, items_off, bytes, pad_;
+};
+constexpr int WGG_MAGIC = 0x57474731;  // "WGG1"
+constexpr int WGG_WG3_NS = 3, WGG_WGL_NS = 2;
+// kinds: 0..5 WG3 (w 16 / 8 / 4) x (resample none / up2), 6 WGL, 7 generic linear, 8 generic conv
+enum { WGK_WGL = 6, WGK_GEN_LIN = 7, WGK_GEN_CONV = 8 };
+constexpr size_t cmax(size_t a, size_t b) { return a > b ? a : b; }
+constexpr size_t WGG_LDS =
+    cmax(cmax(cmax(wg3_lds<16, WGG_WG3_NS, 4>(), wg3_lds<8, WGG_WG3_NS, 4>()), cmax(wg3_lds<4, WGG_WG3_NS, 4>(),
+         wgl_lds<WGG_WGL_NS>())), cmax((size_t)Gemm<64, 64, A_ROWM, B_ROWN, 2, BK>::LDS_BYTES,
+                                       (size_t)Gemm<64, 64, A_ROWM, B_IM2COL, 2, BK>::LDS_BYTES));
+
+__global__ __launch_bounds__(256) void wgrad_group_kernel(const WgProb* __restrict__ probs,
+                                                          const int* __restrict__ items) {
+  extern __shared__ __attribute__((aligned(16))) char wsm[];
+  const int it = items[blockIdx.x];
+  if (it < 0) return;
+  const int pi = it >> 20, loc = it & 0xFFFFF;
+  const int kind = probs[pi].kind;
+  const EncdiffGemmArgs p = probs[pi].p;  // read before any store: scalar loads
+  const SplitFold fold = probs[pi].aux.fold;
+  const SplitFold* fp = fold.cnt ? &fold : nullptr;  // chunks combined in the kernel
+  switch (kind) {
+    case 0: wgrad3x3_body<16, false, WGG_WG3_NS, 4, 9001>(p, loc, wsm, fp); return;
+    case 1: wgrad3x3_body<16, true, WGG_WG3_NS, 4, 9002>(p, loc, wsm, fp); return;
+    case 2: wgrad3x3_body<8, false, WGG_WG3_NS, 4, 9003>(p, loc, wsm, fp); return;
+    case 3: wgrad3x3_body<8, true, WGG_WG3_NS, 4, 9004>(p, loc, wsm, fp); return;
+    case 4: wgrad3x3_body<4, false, WGG_WG3_NS, 4, 9005>(p, loc, wsm, fp); return;
+    case 5: wgrad3x3_body<4, true, WGG_WG3_NS, 4, 9006>(p, loc, wsm, fp); return;
+    case WGK_WGL: wgradlin_body<WGG_WGL_NS, 9007>(p, loc, wsm, fp); return;
+    default: {
+      const GemmAux aux = probs[pi].aux;
+      const int gx = probs[pi].gx;
+      if (kind == WGK_GEN_LIN)
+        gemm_tile<64, 64, A_ROWM, B_ROWN, 2, BK>(p, aux, loc % gx, loc / gx, 0, (bf16_t*)wsm);
+      else
+        gemm_tile<64, 64, A_ROWM, B_IM2COL, 2, BK>(p, aux, loc % gx, loc / gx, 0, (bf16_t*)wsm);
+      return;
+    }
+  }
+}
+
+// Scratch the group's split-K chunks use: fp32 slabs (their own region of the caller's workspace)
+// and one ticket per split output part (the caller's zeroed counter array; left zero).
+struct WgScratch {
+  float* ws;
+  long ws_floats, ws_used;
+  int* cnt;
+  int n_cnt, cnt_used;
+};
+
+// 32-pixel / 32-token stages one wave of a group workgroup may run in sequence: deeper problems are
+// cut into chunks of whole images / token ranges, combined in the kernel (wg_last_chunk).  At one
+// or two waves per SIMD a wave's stage loop is latency-bound, so a long sequence would be the
+// group's critical path (a whole 16x16 problem: 256 stages, ~120 us).  ENCDIFF_WGG_STAGES.
+int wgg_stages() {
+  static const int v = [] {
+    const char* e = getenv("ENCDIFF_WGG_STAGES");
+    return e ? atoi(e) : 32;
+  }();
+  return v;
+}
+
+// one problem of a group: the first body that accepts it (WG3, WGL, generic 64 x 64 tile), with
+// the chunk count (split_k) that keeps each wave's stage sequence within wgg_stages()
+int wg_prepare(const EncdiffGemmArgs& in, WgProb& w, double& block_flops, WgScratch& sc) {
+  if (in.dtype != ENCDIFF_DT_BF16 || in.a_mode != ENCDIFF_OPA_ROWM) return ENCDIFF_ERR_ARG;
+  if (in.c_mode != ENCDIFF_OUT_F32 && in.c_mode != ENCDIFF_OUT_F32_ACCUM) return ENCDIFF_ERR_UNSUPPORTED;
+  if (in.b_mode != ENCDIFF_OPB_IM2COL && in.b_mode != ENCDIFF_OPB_ROWN) return ENCDIFF_ERR_UNSUPPORTED;
+  EncdiffGemmArgs q = in;
+  q.split_k = 1;
+  q.workspace = nullptr;
+  q.split_counters = nullptr;
+  GemmPlan g;
+  const bool conv = q.b_mode == ENCDIFF_OPB_IM2COL;
+  q.tile = conv ? 32 : 36;
+  if (prepare(&q, g) == ENCDIFF_OK) {
+    int nparts, split = 1;
+    if (conv) {
+      const int wi = q.conv.w == 16 ? 0 : (q.conv.w == 8 ? 1 : 2);
+      w.kind = 2 * wi + (q.conv.resample == ENCDIFF_RESAMPLE_UP2 ? 1 : 0);
+      nparts = (q.M / 32) * (q.conv.cin / 16);
+      const int ni = q.conv.w == 16 ? 1 : 2, rows = q.conv.w == 4 ? 4 : 2;
+      auto spw = [&](int sp) {  // stages per wave, 0 when the chunking does not divide
+        if (q.conv.batch % (sp * ni)) return 0;
+        const int nst = (q.conv.batch / sp / ni) * (q.conv.h / rows);
+        return nst % 4 ? 0 : nst / 4;
+      };
+      while (spw(split) > wgg_stages() && spw(2 * split) > 0) split *= 2;
+      block_flops = 2.0 * 32 * 9 * 16 * (double)q.K / split;
+    } else {
+      w.kind = WGK_WGL;
+      nparts = (q.M / 64) * (q.N / 64);
+      while (q.K / (split * 128) > wgg_stages() && q.K % (2 * split * 128) == 0) split *= 2;
+      block_flops = 2.0 * 64 * 64 * (double)q.K / split;
+    }
+    if (split > 1) {  // slabs + tickets, or whole when the scratch is exhausted
+      // (regions 128-B aligned: a cache line never holds two problems' chunks -- see wg_last_chunk)
+      const long need = ((long)split * q.M * q.N + (q.bias_grad ? (long)split * q.M : 0) + 31) & ~31L;
+      if (sc.ws && sc.cnt && sc.ws_used + need <= sc.ws_floats && sc.cnt_used + nparts <= sc.n_cnt) {
+        EncdiffGemmArgs qs = q;
+        qs.split_k = split;
+        qs.workspace = sc.ws + sc.ws_used;
+        if (prepare(&qs, g) == ENCDIFF_OK) {
+          g.aux.fold = SplitFold{sc.cnt + sc.cnt_used, g.user.c, g.user.ldc, g.user.c_mode, g.user.alpha,
+                                 nullptr, nullptr, 0};
+          sc.ws_used += need;
+          sc.cnt_used += nparts;
+        } else {
+          split = 1;
+        }
+      } else {
+        split = 1;
+      }
+      if (split == 1 && prepare(&q, g) != ENCDIFF_OK) return ENCDIFF_ERR_SHAPE;
+    }
+    if (split == 1) block_flops = (conv ? 2.0 * 32 * 9 * 16 : 2.0 * 64 * 64) * (double)q.K;
+    w.nblk = nparts * split;
+    w.gx = 0;
+  } else {
+    q.tile = 4;
+    const int rc = prepare(&q, g);
+    if (rc != ENCDIFF_OK) return rc;
+    if (g.ws_path) return ENCDIFF_ERR_ARG;
+    w.kind = conv ? WGK_GEN_CONV : WGK_GEN_LIN;
+    w.gx = (q.M + 63) / 64;
+    w.nblk = w.gx * ((q.N + 63) / 64);
+    block_flops = 2.0 * 64 * 64 * (double)q.K;
+  }
+  w.p = g.p;
+  w.aux = g.aux;
+  w.aux.xcd = 0;
+  w.pad_ = 0;
+  return ENCDIFF_OK;
+}
+
 }  // namespace
+
+// Work-item order of a group.  Blocks of one problem read the same dY / x rows (the whole K range:
+// nothing is split), so they are kept on one XCD, whose L2 then serves the re-reads; problems go
+// to the least-loaded XCD, largest first (those with more blocks than an XCD holds at once are
+// cut into runs of consecutive blocks -- consecutive parts share their dY columns), and each XCD
+// runs its blocks longest first.  Blocks are dealt round-robin over the XCDs by index (MI355X
+// microarch guide: b and b + 8 share an XCD), so XCD x's list occupies indices x, x + 8, ...;
+// shorter lists are padded with empty items.  ENCDIFF_WGG_ORDER=0: one global longest-first list.
+static std::vector<int> wg_items(const std::vector<WgProb>& w, const std::vector<double>& cost) {
+  const int n = (int)w.size();
+  static const int order_mode = [] {
+    const char* e = getenv("ENCDIFF_WGG_ORDER");
+    return e ? atoi(e) : 1;
+  }();
+  std::vector<int> order((size_t)n);
+  for (int i = 0; i < n; ++i) order[i] = i;
+  std::vector<int> items;
+  if (order_mode == 0) {
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+    for (int i : order)
+      for (int b = 0; b < w[i].nblk; ++b) items.push_back((i << 20) | b);
+    return items;
+  }
+  constexpr int NX = 8, RUN = 64;  // XCDs; blocks of one problem per XCD run (32 CUs x 2 workgroups)
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int a, int b) { return cost[a] * w[a].nblk > cost[b] * w[b].nblk; });
+  std::vector<std::vector<int>> q(NX);
+  double load[NX] = {0};
+  for (int i : order) {
+    for (int b0 = 0; b0 < w[i].nblk; b0 += RUN) {
+      const int b1 = std::min(w[i].nblk, b0 + RUN);
+      int x = 0;
+      for (int k = 1; k < NX; ++k)
+        if (load[k] < load[x]) x = k;
+      load[x] += cost[i] * (b1 - b0);
+      for (int b = b0; b < b1; ++b) q[x].push_back((i << 20) | b);
+    }
+  }
+  size_t len = 0;
+  for (auto& v : q) {
+    std::stable_sort(v.begin(), v.end(), [&](int a, int b) { return cost[a >> 20] > cost[b >> 20]; });
+    len = std::max(len, v.size());
+  }
+  items.assign(len * NX, -1);
+  for (int x = 0; x < NX; ++x)
+    for (size_t j = 0; j < q[x].size(); ++j) items[j * NX + x] = q[x][j];
+  return items;
+}
+
+extern "C" int encdiff_wgrad_group_plan(const EncdiffGemmArgs* probs, int n, float* workspace, long ws_floats,
+                                        int* counters, int n_counters, void* blob, long capacity, long* blob_bytes) {
+  if (!probs || n <= 0 || n > 2047 || !blob_bytes || ws_floats < 0 || n_counters < 0) return ENCDIFF_ERR_ARG;
+  if ((uintptr_t)workspace & 127) return ENCDIFF_ERR_ARG;
+  std::vector<WgProb> w((size_t)n);
+  std::vector<double> cost((size_t)n);
+  WgScratch sc{workspace, workspace ? ws_floats : 0, 0, counters, counters ? n_counters : 0, 0};
+  for (int i = 0; i < n; ++i) {
+    std::memset(&w[i], 0, sizeof(WgProb));
+    const int rc = wg_prepare(probs[i], w[i], cost[i], sc);
+    if (rc != ENCDIFF_OK) return rc;
+    if (w[i].nblk <= 0 || w[i].nblk >= (1 << 20)) return ENCDIFF_ERR_SHAPE;
+  }
+  const std::vector<int> items = wg_items(w, cost);
+  if (items.size() >= (size_t)1 << 30) return ENCDIFF_ERR_SHAPE;
+  const long probs_off = (long)((sizeof(WgBlobHead) + 63) & ~(size_t)63);
+  const long items_off = probs_off + (long)(sizeof(WgProb) * (size_t)n);
+  const long bytes = items_off + (long)items.size() * 4;
+  *blob_bytes = bytes;
+  if (!blob) return ENCDIFF_OK;
+  if (capacity < bytes || ((uintptr_t)blob & 7)) return ENCDIFF_ERR_ARG;
+  char* out = (char*)blob;
+  WgBlobHead h{};
+  h.magic = WGG_MAGIC;
+  h.n_probs = n;
+  h.n_items = (int)items.size();
+  h.lds = (int)WGG_LDS;
+  h.probs_off = probs_off;
+  h.items_off = items_off;
+  h.bytes = bytes;
+  std::memset(out, 0, (size_t)probs_off);
+  std::memcpy(out, &h, sizeof(h));
+  std::memcpy(out + probs_off, w.data(), sizeof(WgProb) * (size_t)n);
+  std::memcpy(out + items_off, items.data(), items.size() * 4);
+  return ENCDIFF_OK;
+}
+
+extern "C" int encdiff_wgrad_group_launch(const void* host_blob, const void* dev_blob, void* stream) {
+  if (!host_blob || !dev_blob) return ENCDIFF_ERR_ARG;
+  WgBlobHead h;
+  std::memcpy(&h, host_blob, sizeof(h));
+  if (h.magic != WGG_MAGIC || h.n_items <= 0 || h.lds > HALO_LDS_MAX) return ENCDIFF_ERR_ARG;
+  static const hipError_t attr_ok = hipFuncSetAttribute((const void*)wgrad_group_kernel,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)WGG_LDS);
+  if (attr_ok != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)attr_ok;
+  const char* d = (const char*)dev_blob;
+  hipLaunchKernelGGL(wgrad_group_kernel, dim3((unsigned)h.n_items), dim3(256), (size_t)h.lds, (hipStream_t)stream,
+                     (const WgProb*)(d + h.probs_off), (const int*)(d + h.items_off));
+  const hipError_t e = hipGetLastError();
+  return e != hipSuccess ? ENCDIFF_ERR_LAUNCH - (int)e : ENCDIFF_OK;
+}
 
 extern "C" int encdiff_gemm(const EncdiffGemmArgs* pa, void* stream) {
   if (pa && pa->dtype == ENCDIFF_DT_F32) return ed_gemm_f32(pa, (hipStream_t)stream);

@@ -111,9 +111,13 @@ class FusedArenaAdamW(torch.optim.Optimizer):
         a = self.arena
         ema = a.ema if self.ema is not None else None
         ops.adamw_ema(a.master, a.grad, a.exp_avg, a.exp_avg_sq, a.hyper, ema=ema,
-                      ema_n=a.ema_numel if ema is not None else 0)
+                      ema_n=a.ema_numel if ema is not None else 0, mirror=a.mirror)
         if self.repack is not None:
-            self.repack()
+            a.mirror_fresh = a.mirror is not None  # the update wrote the bf16 mirror: packs skip it
+            try:
+                self.repack()
+            finally:
+                a.mirror_fresh = False
 
     def launch_part(self, part: int):
         """The same update in two launches over the arena's two ranges: part 0 = [0, ema_numel)
@@ -127,9 +131,14 @@ class FusedArenaAdamW(torch.optim.Optimizer):
         if hi > lo:
             ema = a.ema if (self.ema is not None and part == 0) else None
             ops.adamw_ema(a.master[lo:hi], a.grad[lo:hi], a.exp_avg[lo:hi], a.exp_avg_sq[lo:hi], a.hyper, ema=ema,
-                          ema_n=a.ema_numel if ema is not None else 0)
+                          ema_n=a.ema_numel if ema is not None else 0,
+                          mirror=a.mirror[lo:hi] if a.mirror is not None else None)
         if self.repack_parts is not None:
-            self.repack_parts[part]()
+            a.mirror_fresh = a.mirror is not None and hi > lo
+            try:
+                self.repack_parts[part]()
+            finally:
+                a.mirror_fresh = False
 
     @torch.no_grad()
     def step(self, closure=None):

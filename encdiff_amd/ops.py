@@ -123,11 +123,16 @@ HALO_TILES = {16: (64, 64), 17: (128, 64), 18: (128, 128), 19: (256, 32), 20: (1
 HALO_LDS_MAX = 156 * 1024  # gemm.hip: 160 KiB less the paired kernel's static scratch
 
 
-def halo_fits(tile, batch, h, w, cin, resample):
+def halo_fits(tile, batch, h, w, cin, resample, split=1):
     """Host mirror of gemm.hip prepare_halo's geometry checks: the tile's BM pixels are whole
-    rows of one image (or whole images) and window + 3-deep B ring + epilogue fit the LDS."""
+    rows of one image (or whole images) and window + 3-deep B ring + epilogue fit the LDS.
+    split > 1: split-K by source-channel slices (cin / split channels per split, 64 | slice)."""
     if tile not in HALO_TILES or cin % 8 or resample not in (0, 2, 3, 4):
         return False
+    if split > 1:
+        if cin % (64 * split):
+            return False
+        cin //= split
     bm, bn = HALO_TILES[tile]
     hw = h * w
     if (batch * hw) % bm or bm % w or (hw % bm and bm % hw) or (resample == 2 and (h | w) & 1):
@@ -255,6 +260,27 @@ def wgl_split(M, N, K, lda, ldb, c_mode):
     return best
 
 
+def _plan_ok(tile, split, M, N, K, c_mode, conv, lda, ldb, a_mode=None) -> bool:
+    """Whether a (tile, split) plan -- a table entry measured on some geometry -- is valid for THIS
+    problem: halo tiles need the conv's window to fit (halo_fits), WG3 / WGL tiles their kernel's
+    eligibility and a chunking that divides (wg3_check / wgl_check on the device side would raise
+    ENCDIFF_ERR_SHAPE).  Keys carry (M, N, K, h) but not the batch, strides or alignment."""
+    if tile in HALO_TILES:
+        return (conv is not None and a_mode == L.OPA_IM2COL and
+                halo_fits(tile, conv.batch, conv.h, conv.w, conv.cin, conv.resample, split))
+    if tile in (32, 33, 34):
+        if conv is None or wg3_split(conv.batch, conv.h, conv.w, M, conv.cin, conv.resample, lda, conv.ld_src,
+                                     c_mode, tile=tile) is None:
+            return False
+        ni, rows = (1 if conv.h == 16 else 2), (4 if conv.h == 4 else 2)
+        if conv.batch % (split * ni):
+            return False
+        return ((conv.batch // split // ni) * (conv.h // rows)) % (8 if tile == 33 else 4) == 0
+    if tile == 36:
+        return wgl_split(M, N, K, lda, ldb, c_mode) is not None and K % (split * 128) == 0
+    return True
+
+
 def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OPB_ROWK, c_mode=L.OUT_BF16,
               conv: Optional[L.ConvGeom] = None, conv_cout=0, convw_cin=0, alpha=1.0, split_k=None, bias=None,
               resid=None, ld_resid=0, bias_grad=None, tile=0, ws_offset=0, aux=None, ld_aux=0,
@@ -267,6 +293,8 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
         tile = 4
     if lna is not None:  # LayerNorm of the A rows in the staging: 64x64 tiles, no split
         tile, split_k = 4, 1
+    if _WG_WHOLE:  # a WgradGroup member: whole problem, the group picks the body
+        split_k = 1
     if TABLE_WG and tile == 0 and split_k is None and a_mode == L.OPA_ROWM:
         # a tuned table entry for this exact weight gradient (conv: keyed with its geometry) overrides
         # the WG3 / WGL split heuristics (1: entries naming those kernels, 2: any entry)
@@ -275,7 +303,8 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
                                          conv.h if im2 else 0))
         if hit is not None and (TABLE_WG == 2 or int(hit[0]) in (32, 33, 34, 36)):
             t, sp = int(hit[0]), int(hit[1])
-            if (t not in (32, 33, 34) or WG3) and (t != 36 or WGL) and (sp == 1 or sp * M * (N + 1) <= WS_HALF // 2):
+            if ((t not in (32, 33, 34) or WG3) and (t != 36 or WGL) and (sp == 1 or sp * M * (N + 1) <= WS_HALF // 2)
+                    and _plan_ok(t, sp, M, N, K, c_mode, conv, lda, ldb, a_mode)):
                 tile, split_k = t, sp
     if (WG3 and tile == 0 and split_k is None and a_mode == L.OPA_ROWM and b_mode == L.OPB_IM2COL and
             conv is not None and N == 9 * conv.cin and K == conv.batch * conv.h * conv.w):
@@ -295,7 +324,8 @@ def gemm_args(M, N, K, a, lda, b, ldb, c, ldc, *, a_mode=L.OPA_ROWK, b_mode=L.OP
     hk = conv.h if conv is not None and (a_mode == L.OPA_IM2COL or b_mode == L.OPB_IM2COL) else 0
     if split_k is None or tile == 0:
         t, sp = plan(pm, N, K, a_mode, b_mode, c_mode, rs, hk)
-        if (t in (32, 33, 34) and not WG3) or (t == 36 and not WGL):  # kernel switched off: generic plan
+        if ((t in (32, 33, 34) and not WG3) or (t == 36 and not WGL) or  # kernel switched off, or a table
+                not _plan_ok(t, sp, M, N, K, c_mode, conv, lda, ldb, a_mode)):  # plan invalid here: generic plan
             t, sp = plan(pm, N, K, a_mode, b_mode, c_mode, rs, hk, table=False)
         tile = tile or FORCE_TILE or t
         split_k = split_k or sp
@@ -359,6 +389,108 @@ def gemm(M, N, K, a, lda, b, ldb, c, ldc, **kw):
 
 PAIR = True  # fuse a layer's weight- and input-gradient GEMMs into one launch (encdiff_gemm_pair_ex)
 
+# Grouped weight gradients (encdiff_wgrad_group_*): while a WgradGroup is active, gemm_pair and
+# linear_wgrad launch only the input gradient and hand the weight gradient (whole: split_k 1) to
+# the group, which runs all of them as ONE grid at group_end().  ENCDIFF_WG_GROUP=0: paired launches.
+WG_GROUP = int(os.environ.get("ENCDIFF_WG_GROUP", "0"))  # measured slower than the pairs: DESIGN.md §5
+# only weight gradients with K (pixels / tokens) <= WG_MAXK join the group; deeper ones stay paired
+# with their input gradient (their grid overlaps the input gradient's latency-bound tiles)
+WG_MAXK = int(os.environ.get("ENCDIFF_WG_MAXK", str(1 << 30)))
+_GROUP = None      # the active WgradGroup
+_WG_WHOLE = False  # gemm_args: build a weight gradient for the group (split_k 1, no slabs)
+
+
+class WgradGroup:
+    """The weight-gradient GEMMs of a backward region, launched together.  Launch descriptions
+    are planned once per distinct problem list (the executors' buffers are static per batch size,
+    so a list recurs bit for bit every step) and kept in device memory for the life of the group:
+    captured graphs read them at replay."""
+
+    def __init__(self):
+        self.probs = []
+        self._plans = {}
+
+    def add(self, args):
+        self.probs.append(args)
+
+    def launch(self):
+        probs, self.probs = self.probs, []
+        if not probs:
+            return
+        arr = (L.GemmArgs * len(probs))(*probs)
+        key = bytes(arr)
+        ent = self._plans.get(key)
+        if ent is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("encdiff weight-gradient group first planned inside a graph capture: run an "
+                                   "eager step before capturing")
+            # chunk slabs in the workspace's second half (the first holds deferred input-gradient
+            # slabs until their norms consume them -- all before the group runs)
+            sc = (_workspace().data_ptr() + 4 * WS_HALF, WS_HALF, _counters().data_ptr(), COUNTERS)
+            nb = C.c_long(0)
+            check(lib.encdiff_wgrad_group_plan(arr, len(probs), *sc, None, 0, C.byref(nb)), "encdiff_wgrad_group_plan")
+            host = (C.c_longlong * ((nb.value + 7) // 8))()
+            check(lib.encdiff_wgrad_group_plan(arr, len(probs), *sc, C.addressof(host), C.sizeof(host), C.byref(nb)),
+                  "encdiff_wgrad_group_plan")
+            dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(torch.cuda.current_device())
+            ent = self._plans[key] = (host, dev, probs)  # (the problems: tools / tests re-plan subsets)
+        check(lib.encdiff_wgrad_group_launch(C.addressof(ent[0]), ent[1].data_ptr(), _s()), "encdiff_wgrad_group_launch")
+
+
+def group_begin(group: Optional[WgradGroup]):
+    """Route the following weight gradients into `group` (None: launch them as before)."""
+    global _GROUP
+    _GROUP = group
+
+
+def group_flush():
+    """Launch the weight gradients collected so far; the group stays active (windowed groups: the
+    dY / x operands of the last few blocks are still resident in the 256 MB Infinity Cache)."""
+    if _GROUP is not None:
+        flush()  # a paired launch's deferred finalize: its slabs share the group's workspace half
+        _GROUP.launch()
+
+
+def group_end():
+    """Launch the active group's weight gradients and deactivate it."""
+    global _GROUP
+    g, _GROUP = _GROUP, None
+    if g is not None:
+        flush()
+        g.launch()
+
+
+def _grouped(wgrad_fn):
+    """The whole-problem weight gradient of `wgrad_fn` added to the active group, or None when
+    no group is active or the problem is deeper than WG_MAXK (it runs paired / alone)."""
+    if _GROUP is None:
+        return None
+    w = _whole_wgrad(wgrad_fn)
+    if w.K > WG_MAXK:
+        return None
+    _GROUP.add(w)
+    return w
+
+
+def _whole_wgrad(wgrad_fn):
+    global _WG_WHOLE
+    _WG_WHOLE = True
+    try:
+        return wgrad_fn(0)
+    finally:
+        _WG_WHOLE = False
+
+
+def _dgrad_alone(d, defer_dx):
+    if ws_floats(d):
+        flush()
+    if not defer_dx:
+        check(lib.encdiff_gemm(C.byref(d), _s()), "encdiff_gemm")
+        return None
+    planned = C.c_int(0)
+    check(lib.encdiff_gemm_ex(C.byref(d), 1, C.byref(planned), _s()), "encdiff_gemm_ex")
+    return d if planned.value else None
+
 
 def gemm_pair(wgrad_fn, dgrad_fn, defer_dx=False):
     """Launch a layer's weight-gradient and input-gradient GEMMs together (`wgrad_fn(off)`,
@@ -368,7 +500,11 @@ def gemm_pair(wgrad_fn, dgrad_fn, defer_dx=False):
     half), so a backward of N layers needs no finalize launches for weight gradients but the
     last (`flush`).  defer_dx: the input gradient's finalize is skipped too when it has one;
     its GemmArgs are returned for the consumer (groupnorm_bwd(dy_from=...)) or finalize(),
-    which must run before the next pair (else None: dx written)."""
+    which must run before the next pair (else None: dx written).
+    With a WgradGroup active the weight gradient goes to the group and only the input gradient
+    is launched here."""
+    if _grouped(wgrad_fn) is not None:
+        return _dgrad_alone(dgrad_fn(0), defer_dx)
     key = torch.cuda.current_device()
     if not PAIR:
         flush()
@@ -472,6 +608,8 @@ def linear_wgrad_args(dy, x, dw, db=None, ws_offset=0):
 def linear_wgrad(dy, x, dw, db=None):
     """dw[N][K] += dy[M][N]^T x[M][K] (split-K slabs summed in order: reproducible);
     db[N] += sum_m dy[m][n]."""
+    if _grouped(lambda off: linear_wgrad_args(dy, x, dw, db, off)) is not None:
+        return
     args = linear_wgrad_args(dy, x, dw, db)
     if ws_floats(args):
         flush()
@@ -576,6 +714,8 @@ def conv3x3_wgrad_cl_args(dy, x, g: Geom, cin, dw_cl, db=None, resample=L.RESAMP
 def conv3x3_wgrad_cl(dy, x, g: Geom, cin, dw_cl, db=None, resample=L.RESAMPLE_NONE):
     """dw_cl[cout][9*cin] (fp32, channels-last [co][kh][kw][ci]) += dy^T im2col(resample(x))
     (split-K slabs summed in order: reproducible)."""
+    if _grouped(lambda off: conv3x3_wgrad_cl_args(dy, x, g, cin, dw_cl, db, resample, off)) is not None:
+        return
     args = conv3x3_wgrad_cl_args(dy, x, g, cin, dw_cl, db, resample)
     if ws_floats(args):
         flush()
@@ -896,9 +1036,10 @@ def ddim_step_indexed(x, e, noise, coef, index, x_prev, pred_x0=None, advance=Tr
                                         _p(x_prev), _p(pred_x0), _s()), "encdiff_ddim_step_indexed")
 
 
-def adamw_ema(p, g, m, v, hyper, ema=None, ema_n=0):
-    check(lib.encdiff_adamw_ema(_p(p), _p(g), _p(m), _p(v), _p(ema), p.numel(), _p(hyper), ema_n, _s()),
-          "encdiff_adamw_ema")
+def adamw_ema(p, g, m, v, hyper, ema=None, ema_n=0, mirror=None):
+    """mirror: bf16 buffer of p's size that receives the updated weights (arena.mirror)."""
+    check(lib.encdiff_adamw_ema_mirror(_p(p), _p(g), _p(m), _p(v), _p(ema), p.numel(), _p(hyper), ema_n, _p(mirror),
+                                       _s()), "encdiff_adamw_ema_mirror")
 
 
 def adamw_hyper(lr, step, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=1e-2, ema_one_minus_decay=0.0):

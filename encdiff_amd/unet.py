@@ -43,6 +43,9 @@ GN_FROM_PRODUCER = os.environ.get("ENCDIFF_GN_FROM_PRODUCER", "1") != "0"
 # -> GN2 / GN1 backward, transformer linears -> the LayerNorm / GroupNorm backward reading their
 # input gradient.  One launch instead of two (0: separate finalize launches, A/B runs)
 GN_FIN = os.environ.get("ENCDIFF_GN_FIN", "1") != "0"
+# grouped weight gradients (ops.WgradGroup): one grid per WG_WINDOW UNet blocks of the backward
+# (0: one grid per DP bucket region)
+WG_WINDOW = int(os.environ.get("ENCDIFF_WG_WINDOW", "1"))
 LN_EPS = 1e-5      # nn.LayerNorm default (attention.py:206-208)
 # the row-local SpatialTransformer tail (attn1.to_out .. proj_out) as one kernel
 # (encdiff_st_tail_fwd) in no-grad forwards (0: the separate launches, for A/B runs)
@@ -300,6 +303,7 @@ class UNetExecutor:
         self.samp_ts: Optional[torch.Tensor] = None
         self.samp_i: Optional[int] = None
         self._samp_tabs: Dict[tuple, dict] = {}  # (S, B) -> buffers; graphs hold their addresses
+        self._wgg = ops.WgradGroup()  # the backward's grouped weight gradients (planned per batch size)
         self._base_names = set(self.__dict__) | {"_base_names"}
         self.pack.repack()
 
@@ -809,22 +813,40 @@ class UNetExecutor:
         middle / input blocks and the batched emb / K,V GEMMs and fills the returned d_context
         buffer.  Launch for launch the same work as the unsplit backward (the last deferred
         finalize and the norm partial fold are issued in two parts)."""
-        out = self._bwd_outputs(d_eps)
-        if split and self._split:
-            _, gcol, lcol = self._split
-            ops.flush()
-            self.gn.reduce(gcol)
-            self.ln.reduce(lcol)
-            self._cont = out
-            return self.d_ctx
-        self._cont = None
-        return self._bwd_rest(out, self.gn.cols, self.ln.cols)
+        ops.group_begin(self._wgg if ops.WG_GROUP else None)
+        self._wg_blocks = 0
+        try:
+            out = self._bwd_outputs(d_eps)
+            if split and self._split:
+                ops.group_end()  # the output blocks' weight gradients, one grid
+                _, gcol, lcol = self._split
+                ops.flush()
+                self.gn.reduce(gcol)
+                self.ln.reduce(lcol)
+                self._cont = out
+                return self.d_ctx
+            self._cont = None
+            return self._bwd_rest(out, self.gn.cols, self.ln.cols)
+        finally:
+            ops.group_begin(None)
+
+    def _wg_block_done(self):
+        """A UNet block's backward is issued: every WG_WINDOW blocks the collected weight gradients
+        run as one grid while their operands are hot."""
+        self._wg_blocks += 1
+        if WG_WINDOW > 0 and self._wg_blocks % WG_WINDOW == 0:
+            ops.group_flush()
 
     def backward_rest(self) -> torch.Tensor:
         assert self._cont is not None, "backward_rest() follows backward(split=True)"
         out, self._cont = self._cont, None
         _, gcol, lcol = self._split
-        return self._bwd_rest(out, gcol, lcol)
+        self._wg_blocks = 0
+        ops.group_begin(self._wgg if ops.WG_GROUP else None)
+        try:
+            return self._bwd_rest(out, gcol, lcol)
+        finally:
+            ops.group_begin(None)
 
     def _bwd_outputs(self, d_eps: torch.Tensor):
         B = self.B
@@ -864,6 +886,7 @@ class UNetExecutor:
             c1 = blk[0].cin - sp.skip_ch[nhs - 1 - j]
             g_hs[nhs - 1 - j] = self.dxcat[j][:, c1:]
             dout = self.dxcat[j][:, :c1]
+            self._wg_block_done()
         return dout, g_hs
 
     def _bwd_rest(self, state, gcol: int, lcol: int) -> torch.Tensor:
@@ -881,6 +904,7 @@ class UNetExecutor:
                 dx_target, acc = self.state[layer.prefix]["d_in"], False
             self._layer_bwd(layer, dout, dx_target, acc)
             dout = dx_target
+        self._wg_block_done()
         # input blocks 11..1: output grad = g_hs[i] (complete), input grad accumulates into g_hs[i-1]
         for i in range(len(sp.input_blocks) - 1, 0, -1):
             blk = sp.input_blocks[i]
@@ -893,6 +917,7 @@ class UNetExecutor:
                     dx_target, acc = self.state[layer.prefix]["d_in"], False
                 self._layer_bwd(layer, dout, dx_target, acc)
                 dout = dx_target
+            self._wg_block_done()
         # input conv weight grad (no input grad: x_t carries no gradient)
         dy0 = g_hs[0]
         ops.gemm(self.mc, 72, g0.pixels, dy0, dy0.stride(0), self.x8, 8, self.dw_in, 72, a_mode=L.OPA_ROWM,
@@ -924,7 +949,8 @@ class UNetExecutor:
         ops.gemm(B * self.lu, self.cd, sp.kv_total, self.dKV, self.dKV.stride(0), self.W("kv_all"), self.cd,
                  self.d_ctx, self.cd, b_mode=L.OPB_ROWN, c_mode=L.OUT_F32)
         ops.linear_wgrad(self.dKV, self.ctx16, self.kv_w_grad)
-        ops.flush()  # the last deferred weight-gradient finalize
+        ops.group_end()  # every weight gradient since group_begin, one grid
+        ops.flush()  # the last deferred weight-gradient finalize (paired launches)
         # fold the norm affine partial sums into the arena (all of them, or what the split
         # backward left: the columns before the output blocks' suffix)
         self.gn.reduce(0, gcol)

@@ -210,6 +210,26 @@ int encdiff_gemm_pair_dx(const EncdiffGemmArgs* wgrad, const EncdiffGemmArgs* dg
                          const EncdiffGemmArgs* prev_wgrad, int defer, int defer_dgrad, int* dgrad_deferred,
                          void* stream);
 
+/* Grouped weight gradients: n weight-gradient GEMMs (a_mode OPA_ROWM, b_mode OPB_ROWN or
+ * OPB_IM2COL, c_mode OUT_F32 / OUT_F32_ACCUM, optional bias_grad) in ONE launch (split_k /
+ * workspace / tile of the problems are ignored).  Replaces the autograd weight gradients of every
+ * nn.Linear / nn.Conv2d of a backward region (openaimodel_enc.py:230, 237-241, 255-275;
+ * attention.py:159-167, 211-261) once their dY tensors exist.  Deep problems are cut into chunks
+ * whose fp32 partials go to `workspace` (ws_floats floats, 16-byte aligned, this group's alone
+ * while it runs) and are combined in the kernel by the chunk that finishes last (one ticket per
+ * output part in `counters`, n_counters zeroed ints, left zero); every output element is one sum
+ * in a fixed order, so results are reproducible run to run.  workspace / counters NULL: every
+ * problem runs whole.
+ * encdiff_wgrad_group_plan validates the problems and writes the launch description into `blob`
+ * (8-byte aligned host memory of `capacity` bytes; blob == NULL: only *blob_bytes is set).  The
+ * caller copies the blob byte for byte into device memory it owns and keeps (a captured graph
+ * reads it at every replay), then encdiff_wgrad_group_launch(host copy, device copy, stream)
+ * enqueues the grid.  Every pointer inside the problems, the workspace and the counters must
+ * stay valid for as long as the blob is launched. */
+int encdiff_wgrad_group_plan(const EncdiffGemmArgs* probs, int n, float* workspace, long ws_floats, int* counters,
+                             int n_counters, void* blob, long capacity, long* blob_bytes);
+int encdiff_wgrad_group_launch(const void* host_blob, const void* dev_blob, void* stream);
+
 /* The split-K finalize of a GEMM launched with a deferred finalize (no-op without slabs). */
 int encdiff_gemm_finalize(const EncdiffGemmArgs* args, void* stream);
 
@@ -435,6 +455,11 @@ int encdiff_ddim_step_indexed(const float* x, const float* e, const float* noise
  * The EMA covers the first ema_n elements of the arena (the UNet parameters). */
 int encdiff_adamw_ema(float* p, const float* g, float* m, float* v, float* ema, long long n,
                       const float* hyper, long long ema_n, void* stream);
+/* encdiff_adamw_ema that also writes the updated weights as bf16 into `mirror` (n elements,
+ * 8-byte aligned, index for index with p; NULL: none): the GEMM operand copies of every weight
+ * whose compute layout is its arena layout, so no separate repack pass reads the arena again. */
+int encdiff_adamw_ema_mirror(float* p, const float* g, float* m, float* v, float* ema, long long n,
+                             const float* hyper, long long ema_n, void* mirror, void* stream);
 
 /* Pack fp32 master weights into bf16 compute layouts.  Each job copies `rows x cols`
  * elements: dst[r*dst_ld + c] = src[src_index(r, c)], kind 0: src[r*cols + c]

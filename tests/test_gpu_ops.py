@@ -285,6 +285,49 @@ def test_conv_halo_tiles(O, tile, B, H, cin, cout, mode):
         assert torch.equal(dx, drun(HALO_TWIN[tile]))
 
 
+@pytest.mark.parametrize("tile", [16, 17, 22])
+@pytest.mark.parametrize("split", [2, 4])
+@pytest.mark.parametrize("B,H,cin,cout,mode", [(32, 4, 256, 256, 0), (32, 4, 512, 256, 0), (64, 2, 512, 256, 0),
+                                               (16, 8, 256, 128, 0), (32, 4, 256, 256, 2), (16, 2, 768, 256, 0)])
+def test_conv_halo_split_k(O, tile, split, B, H, cin, cout, mode):
+    """Halo tiles with split-K over source-channel slices (the small-image convs: a 64-row tile is
+    whole 4x4 / 2x2 images, each split stages its channel slice of their windows once and runs all
+    9 taps over it): forward (bf16 out through the slab finalize, and the in-kernel combine) and the
+    input gradient vs torch fp32; bitwise equal to the same split on the LDS-ring tile is not
+    expected (different k order), so the bound is the fp32 one."""
+    import encdiff_amd._lib as L
+    from encdiff_amd.ops import Geom
+    torch.manual_seed(19)
+    g = Geom(B, H, H)
+    gs = Geom(B, H // 2, H // 2) if mode == 2 else g
+    x = bf(gs.pixels, cin)
+    wf = bf(cout, 9 * cin, scale=(9 * cin) ** -0.5)
+    wq = wf.float().reshape(cout, 3, 3, cin).permute(0, 3, 1, 2)
+    bias = torch.randn(cout, device=dev)
+    cg = L.ConvGeom(batch=B, h=H, w=H, cin=cin, resample=mode, ld_src=cin)
+    if not O.halo_fits(tile, B, H, H, cin, mode, split):
+        pytest.skip("window does not fit")
+    xin = nhwc(x, gs)
+    if mode == 2:
+        xin = F.interpolate(xin, scale_factor=2, mode="nearest")
+    ref = F.conv2d(xin, wq, bias, padding=1)
+    for c_mode, fold, tol in ((L.OUT_F32, False, 1e-4), (L.OUT_BF16, False, 1e-2), (L.OUT_BF16, True, 1e-2)):
+        out = torch.empty(g.pixels, cout, device=dev, dtype=torch.bfloat16 if c_mode == L.OUT_BF16 else torch.float32)
+        O.gemm(g.pixels, cout, 9 * cin, x, cin, wf, 9 * cin, out, cout, a_mode=L.OPA_IM2COL, c_mode=c_mode,
+               conv=cg, bias=bias, split_k=split, tile=tile, fold=fold)
+        assert rel(nhwc(out, g), ref) < tol, (c_mode, fold)
+    if mode != 0 or not O.halo_fits(tile, B, H, H, cout, 0, split):
+        return
+    dy = bf(g.pixels, cout)
+    cgd = L.ConvGeom(batch=B, h=H, w=H, cin=cout, resample=0, ld_src=cout)
+    dx = torch.empty(g.pixels, cin, device=dev)
+    O.gemm(g.pixels, cin, 9 * cout, dy, cout, wf, 9 * cin, dx, cin, a_mode=L.OPA_IM2COL, b_mode=L.OPB_CONV_DGRAD,
+           c_mode=L.OUT_F32, conv=cgd, conv_cout=cout, split_k=split, tile=tile)
+    xr = nhwc(x, gs).requires_grad_(True)
+    F.conv2d(xr, wq, None, padding=1).backward(nhwc(dy, g))
+    assert rel(nhwc(dx, g), xr.grad) < 1e-4
+
+
 def test_linear_strided_views(O):
     """q/k/v slices of a fused [M][3C] projection output are strided views."""
     torch.manual_seed(1)
@@ -460,6 +503,63 @@ def test_linear_wgrad_wgl(O, T, cout, cin, monkeypatch):
     for i in range(2):
         assert torch.equal(dws[i], got[1][0]) or rel(dws[i], got[1][0]) < 1e-6
         assert rel(dxs[i], dy.float() @ w.float()) < 1e-2
+
+
+def test_wgrad_group(O):
+    """Grouped weight gradients (encdiff_wgrad_group_*): one grid over every body the group has --
+    WG3 at 16 / 8 / 4 (resample none and nearest-up), WGL, the generic 64x64 tile for 2x2 convs and
+    for narrow / short-K linears -- each problem whole (no split-K), vs torch fp32 references;
+    dW and the bias gradient accumulate onto nonzero values; a second launch of the same planned
+    group is bitwise the first (one ordered sum per output element)."""
+    from encdiff_amd.ops import Geom
+    torch.manual_seed(21)
+    convs = [(64, 16, 64, 64, 0), (16, 16, 128, 64, 2), (32, 8, 128, 128, 0), (16, 8, 256, 128, 2),
+             (32, 4, 256, 256, 0), (16, 4, 512, 256, 2), (32, 2, 256, 256, 0), (8, 2, 512, 256, 2)]
+    lins = [(8192, 64, 64), (2048, 512, 128), (4096, 256, 1024), (128, 1024, 256), (2560, 64, 16), (384, 200, 72)]
+    grp = O.WgradGroup()
+    cases, keep = [], []  # keep: operands stay alive until the deferred group launch
+    O.group_begin(grp)
+    try:
+        for B, H, cin, cout, mode in convs:
+            g = Geom(B, H, H)
+            gs = Geom(B, H // 2, H // 2) if mode == 2 else g
+            x, dy = bf(gs.pixels, cin), bf(g.pixels, cout)
+            xin = nhwc(x, gs)
+            if mode == 2:
+                xin = F.interpolate(xin, scale_factor=2, mode="nearest")
+            w0 = torch.zeros(cout, cin, 3, 3, device=dev, requires_grad=True)
+            F.conv2d(xin, w0, padding=1).backward(nhwc(dy, g))
+            ref = w0.grad.permute(0, 2, 3, 1).reshape(cout, 9 * cin)
+            dw, db = torch.randn(cout, 9 * cin, device=dev), torch.randn(cout, device=dev)
+            cases.append((dw, dw.clone(), ref, db, db.clone(), nhwc(dy, g).sum((0, 2, 3))))
+            keep += [x, dy]
+            O.conv3x3_wgrad_cl(dy, x, g, cin, dw, db, resample=mode)
+        for T, cout, cin in lins:
+            dy, x = bf(T, cout), bf(T, cin)
+            dw, db = torch.randn(cout, cin, device=dev), torch.randn(cout, device=dev)
+            cases.append((dw, dw.clone(), dy.float().t() @ x.float(), db, db.clone(), dy.float().sum(0)))
+            keep += [x, dy]
+            O.linear_wgrad(dy, x, dw, db)
+        assert len(grp.probs) == len(cases)
+        O.group_end()
+    finally:
+        O.group_begin(None)
+    torch.cuda.synchronize()
+    for i, (dw, w0, ref, db, b0, rb) in enumerate(cases):
+        assert rel(dw - w0, ref) < 2e-3, (i, rel(dw - w0, ref))
+        assert rel(db - b0, rb) < 2e-3, (i, rel(db - b0, rb))
+    first = [(c[0].clone(), c[3].clone()) for c in cases]
+    # relaunch the same planned group (the executors replay it every step): identical sums
+    for dw, w0, _, db, b0, _ in cases:
+        dw.copy_(w0)
+        db.copy_(b0)
+    arr = list(grp._plans.values())
+    assert len(arr) == 1
+    host, devb = arr[0][:2]
+    O.check(O.lib.encdiff_wgrad_group_launch(O.C.addressof(host), devb.data_ptr(), O._s()), "group")
+    torch.cuda.synchronize()
+    for (dw, _, _, db, _, _), (f_dw, f_db) in zip(cases, first):
+        assert torch.equal(dw, f_dw) and torch.equal(db, f_db)
 
 
 @pytest.mark.parametrize("C,H,film,silu,eps", [(64, 16, True, True, 1e-5), (192, 16, False, True, 1e-5),

@@ -72,12 +72,12 @@ def test_graph_step_after_ema_scope(rig):
     ldm, a = rig.ldm, rig.tr.arena
     ex = ldm.model.diffusion_model._ex
     saved_ema = a.ema.clone()
-    packed = ex.pack.buf.clone()
+    packed = ex.pack.snapshot()
     a.ema.copy_(a.master[: a.ema.numel()] * 0.9)
     x = torch.randn(2, 3, 16, 16, device="cuda")
     with torch.no_grad(), ldm.ema_scope():
         ldm.apply_model(x, torch.tensor([5, 500], device="cuda"), torch.randn(2, 320, device="cuda"))
-        assert not torch.equal(ex.pack.buf, packed), "EMA scope did not repack"
+        assert not torch.equal(ex.pack.snapshot(), packed), "EMA scope did not repack"
     a.ema.copy_(saved_ema)
     ldm.train()
     r = rig.check()

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--wg", type=int, default=1, help="sweep the WG3 / WGL weight-gradient kernels' splits too")
     ap.add_argument("--write-table", default="", help="path for the measured (tile, split) table, e.g. "
                     "gpurun_out/gemm_tiles.json (copy it to encdiff_amd/gemm_tiles.json)")
+    ap.add_argument("--only-h", default="", help="comma list of conv sizes h: sweep only the implicit-im2col "
+                    "problems (and their pairs) at those sizes, keeping every other entry of the current table")
     args = ap.parse_args()
     import encdiff_amd  # noqa: F401
     from encdiff_amd import _lib as L
@@ -124,13 +126,20 @@ def main():
         im2 = a.a_mode == L.OPA_IM2COL or a.b_mode == L.OPB_IM2COL
         return ops.plan_key(a.M, a.N, a.K, a.a_mode, a.b_mode, a.c_mode, a.conv.resample, a.conv.h if im2 else 0)
 
+    only_h = {int(x) for x in args.only_h.split(",") if x}
+
+    def selected(a):
+        return not only_h or ((a.a_mode == L.OPA_IM2COL or a.b_mode == L.OPB_IM2COL) and a.conv.h in only_h)
+
     tot_cur, tot_best = defaultdict(float), defaultdict(float)
     flops = defaultdict(float)
-    table = {}
+    table = dict(ops._tile_table()) if only_h else {}
     rows = []
     done = {}
     for a in calls:
         key = key_of(a)
+        if not selected(a):
+            continue
         if key in done:  # same problem already swept: reuse
             cur, best_tile, best_split, best_t, best_fold = done[key]
             k = cat(a)
@@ -152,13 +161,17 @@ def main():
         if wgrad and args.wg:  # the weight-gradient kernels with their own split sweep: WG3 (3x3), WGL (linear)
             cands += (32,) if a.b_mode == L.OPB_IM2COL else ((36,) if a.b_mode == L.OPB_ROWN else ())
         if a.a_mode == L.OPA_IM2COL and a.b_mode in (L.OPB_ROWK, L.OPB_CONV_DGRAD):
-            # halo tiles (window staged once; split-K 1); paired input gradients: 16, 17, 18, 22
+            # halo tiles (window staged once; split-K by source-channel slices); paired input gradients:
+            # 16, 17, 18, 22
             halo = (16, 17, 18, 22) if dgrad else tuple(ops.HALO_TILES)
             cands += tuple(t for t in halo if ops.halo_fits(t, a.conv.batch, a.conv.h, a.conv.w, a.conv.cin,
                                                             a.conv.resample))
         for tile in cands:
-            for split in ((1,) if 16 <= tile < 32 else (1, 2, 4, 8, 16, 32, 64, 128, 256)):
+            for split in ((1, 2, 4, 8) if 16 <= tile < 32 else (1, 2, 4, 8, 16, 32, 64, 128, 256)):
                 if split > 1 and a.K // split < 64:
+                    continue
+                if 16 <= tile < 32 and not ops.halo_fits(tile, a.conv.batch, a.conv.h, a.conv.w, a.conv.cin,
+                                                         a.conv.resample, split):
                     continue
                 if wgrad and split > 1 and split * a.M * (a.N + 1) > ops.WS_HALF // 2:
                     continue
@@ -218,7 +231,7 @@ def main():
                 continue
             w, d = rec[1], rec[2]
             wk, dk = key_of(w), key_of(d)
-            if (wk, dk) in seen_p or wk not in table or dk not in table:
+            if (wk, dk) in seen_p or wk not in table or dk not in table or not selected(d):
                 continue
             seen_p.add((wk, dk))
             w_split = table[wk][1]
@@ -226,8 +239,8 @@ def main():
             dc = {(table[dk][0], table[dk][1])} | {(t, s) for t in (1, 2, 3, 4, 5, 9, 10) for s in (1, 2, 4, 8)
                                                    if d.K // s >= 64}
             if conv:
-                dc |= {(t, 1) for t in (16, 17, 18, 22)
-                       if ops.halo_fits(t, d.conv.batch, d.conv.h, d.conv.w, d.conv.cin, d.conv.resample)}
+                dc |= {(t, sp) for t in (16, 17, 18, 22) for sp in (1, 2, 4, 8)
+                       if ops.halo_fits(t, d.conv.batch, d.conv.h, d.conv.w, d.conv.cin, d.conv.resample, sp)}
             best = None
             for wt in sorted({4, 5, 7, 9, 10, table[wk][0]}):  # tiles 1-3: unpaired (back to back)
                 wa = copy_args(w, wt, w_split, 0)
