@@ -338,8 +338,10 @@ def main():
     # marker kernels (torch's spin_kernel) bracket the timed region so a kernel trace can
     # be cut to it (tools/trace_window.py); they run outside the timed region
     torch.cuda._sleep(1000)
-    dt = time_steps(tr, args.steps)
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    dt = time_steps(tr, args.steps, events=ev)
     torch.cuda._sleep(1000)
+    local_ms = ev[0].elapsed_time(ev[1]) / args.steps  # this rank's GPU time per step
     dp_info = None
     if tr.dp:  # exchange timing on extra steps (the timed ones carry no extra events)
         tr.dp_timing = True
@@ -347,10 +349,20 @@ def main():
             tr.step()
         tr.dp_timing = False
         dp_info = tr.dp_stats()
+    dist_info = None
     if dist.is_initialized():
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
+        # self-verifying multi-GPU line: what the process group itself reports (not the launcher's
+        # WORLD_SIZE), and every rank's own GPU time per step (before the closing barrier)
+        dvc = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        per = [torch.zeros(1, device=dvc) for _ in range(dist.get_world_size())]
+        dist.all_gather(per, torch.tensor([local_ms], device=dvc))
+        per = [round(float(x), 4) for x in per]
+        dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                     "rank_gpu_ms_per_step": per, "rank_spread_ms": round(max(per) - min(per), 4),
+                     "wall_ms_per_step_max_over_ranks": round(dt / args.steps * 1e3, 4)}
     imgs = args.batch * world * args.steps
     value = imgs / dt
     loss = tr.loss()
@@ -360,6 +372,8 @@ def main():
         extra["roofline"] = roof
         if dp_info is not None:
             extra["dp"] = dp_info
+        if dist_info is not None:
+            extra["dist"] = dist_info
         f_step = 3 * F_UNET_FWD_PER_IMG * args.batch  # configs[1]'s UNet; other configs: see the GEMM roofline
         if args.config == "shapes3d":
             extra["step_roofline"] = {"bound": "mfma", "unit": "TFLOP/s",

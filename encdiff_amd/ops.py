@@ -367,15 +367,28 @@ def ws_floats(args) -> int:
 
 # Keyed by DEVICE, like the workspace the slabs live in (scratch()): a finalize left pending by a
 # launch on one stream is flushed by the next workspace user on any stream of that device.
-_PENDING = {}  # device -> GemmArgs of a weight gradient whose split-K finalize is deferred
+_PENDING = {}  # device -> (GemmArgs, producing stream) of a weight gradient whose split-K finalize is deferred
 _HALF = {}     # device -> workspace half used by the last paired launch
 
 
+def _take_pending(key):
+    """The deferred weight-gradient finalize of this device, ordered after its producer: when the
+    GEMM that left it ran on another stream, the current stream waits for that stream first (the
+    finalize reads its slabs)."""
+    ent = _PENDING.pop(key, None)
+    if ent is None:
+        return None
+    args, producer = ent
+    cur = torch.cuda.current_stream()
+    if producer != cur:
+        cur.wait_stream(producer)
+    return args
+
+
 def flush():
-    """Run the deferred weight-gradient finalize of the current stream, if any (the end of a
-    backward, or before a GEMM that needs the workspace)."""
-    key = torch.cuda.current_device()
-    pend = _PENDING.pop(key, None)
+    """Run the deferred weight-gradient finalize of this device, if any (the end of a backward, or
+    before a GEMM that needs the workspace)."""
+    pend = _take_pending(torch.cuda.current_device())
     if pend is not None:
         check(lib.encdiff_gemm_finalize(C.byref(pend), _s()), "encdiff_gemm_finalize")
 
@@ -524,12 +537,12 @@ def gemm_pair(wgrad_fn, dgrad_fn, defer_dx=False):
     if h:
         w = wgrad_fn(h * WS_HALF)
     d = dgrad_fn(h * WS_HALF + nw)
-    prev = _PENDING.pop(key, None)
+    prev = _take_pending(key)
     dd = C.c_int(0)
     check(lib.encdiff_gemm_pair_dx(C.byref(w), C.byref(d), C.byref(prev) if prev is not None else None, 1,
                                    int(defer_dx), C.byref(dd), _s()), "encdiff_gemm_pair_dx")
     if nw:
-        _PENDING[key] = w
+        _PENDING[key] = (w, torch.cuda.current_stream())
     _HALF[key] = h
     return d if dd.value else None
 
@@ -854,15 +867,48 @@ def attention_bwd(q, k, v, o, lse, d_o, dq, dk, dv, batch, heads, sq, sk, dh, fp
 
 
 ST_TAIL_STATS_ADD = os.environ.get("ENCDIFF_ST_TAIL_STATS_ADD", "1") != "0"
-# producer-statistics slots the tails add into: seen (ADD_REGIONS, ptr -> view) and those a training
-# step's prologue zeroes (PREZEROED) while PROLOGUE_STEP is set (trainer.HipTrainer)
-ADD_REGIONS: dict = {}
-PREZEROED: set = set()
-PROLOGUE_STEP = False
+
+
+class StatSlots:
+    """The producer-statistics slots an executor's transformer tails ADD into (two 32-row tiles
+    per 64-row segment at 8x8): each must be zero before its one producer launch.  Outside a
+    training step the fill runs right before the launch; a HipTrainer registers the slots seen
+    (`register`) with its step prologue -- one zeroing launch per step -- and while a prologue step
+    is active (`begin_step(True)`) the fills of exactly those views are skipped, each at most once
+    per step (a second producer of one slot would add into a non-zero slot: asserted).  Keyed by
+    (data pointer, shape, strides), so another view at the same address is never taken for one."""
+
+    def __init__(self):
+        self.seen = {}          # key -> view (every slot prepared since creation)
+        self.prezeroed = set()  # keys the owner's step prologue zeroes
+        self.prologue = False
+        self._used = set()
+
+    @staticmethod
+    def key(v):
+        return v.data_ptr(), tuple(v.shape), tuple(v.stride())
+
+    def begin_step(self, prologue: bool):
+        self.prologue = prologue
+        self._used.clear()
+
+    def prepare(self, view):
+        k = self.key(view)
+        if self.prologue and k in self.prezeroed:
+            assert k not in self._used, "statistics slot produced twice in one prologue step"
+            self._used.add(k)
+            return
+        view.zero_()
+        self.seen[k] = view
+
+    def register(self):
+        """The views to zero in the step prologue (from now on their fills are skipped in steps)."""
+        self.prezeroed.update(self.seen)
+        return list(self.seen.values())
 
 
 def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps, save=None,
-                gn_stats=None) -> bool:
+                gn_stats=None, slots: Optional[StatSlots] = None) -> bool:
     """The row-local tail of a SpatialTransformer (attn1.to_out ... proj_out, attention.py:211-215,
     250-261) as one kernel.  w: dict of the bf16 GEMM weights / fp32 biases and LayerNorm affines
     (keys out1, b_out1, g2, be2, q2, out2, b_out2, g3, be3, ff1, b_ff1, ff2, b_ff2, po, b_po).
@@ -888,11 +934,12 @@ def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps
         if c == 128 and rows // 64 < 256 and ST_TAIL_STATS_ADD:
             # two 32-row tiles per 64-row segment add into the zeroed slots (twice the workgroups);
             # only this tensor's columns (the view may span a concat's other producer).  Inside a
-            # training step whose prologue zeroes the registered slots (StepPrologue) no fill runs.
+            # training step whose prologue zeroes the registered slots (StatSlots) no fill runs.
             view = gn_stats[:, :c]
-            if not (PROLOGUE_STEP and view.data_ptr() in PREZEROED):
+            if slots is not None:
+                slots.prepare(view)
+            else:
                 view.zero_()
-                ADD_REGIONS[view.data_ptr()] = view
             a.gn_stats_add = 1
     rc = lib.encdiff_st_tail_fwd(C.byref(a), _s())
     if rc in (-2, -3):

@@ -109,15 +109,19 @@ class HipTrainer:
         self._pro.set_jobs([self.arena.grad])
         self._pro_final = False  # statistics slots registered after the first step
 
+    def _slots(self):
+        """The UNet executor's statistics-slot registry (None before the executor exists)."""
+        ex = getattr(self.unet, "_ex", None)
+        return ex.stat_slots if ex is not None else None
+
     def _prologue_regions(self):
         """After the first step: the prologue also zeroes every producer-statistics slot the
         step's kernels added into (seen by ops.st_tail_fwd), so no fill runs inside the step."""
         from . import ops
         if self._pro_final:
             return
-        regions = list(ops.ADD_REGIONS.values())
+        regions = self._slots().register() if self._slots() is not None else []
         self._pro.set_jobs([self.arena.grad] + regions)
-        ops.PREZEROED.update(r.data_ptr() for r in regions)
         self._pro_final = True
 
     # ---------------------------------------------------------------- test hook
@@ -160,7 +164,7 @@ class HipTrainer:
         else:
             t, noise = self._t, self._noise
             self._pro(t, noise, timesteps=ldm.num_timesteps, data_step=self.data.step)
-        ops.PROLOGUE_STEP = self._pro_final
+        self.unet.executor().stat_slots.begin_step(self._pro_final)  # (the executor exists from here on)
         with torch.no_grad():
             z = ldm.encode_first_stage(self.img)  # frozen VQ (HIP); scale_factor applied in q_sample
         c = ldm.get_learned_conditioning(self.img)
@@ -346,7 +350,7 @@ class HipTrainer:
                     with torch.cuda.graph(self._g_opt, stream=s, pool=pool, capture_error_mode="thread_local"):
                         self.opt.launch()
             finally:
-                ops.PROLOGUE_STEP = False
+                self._slots() is not None and self._slots().begin_step(False)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
 
@@ -360,7 +364,7 @@ class HipTrainer:
             if self.dp:
                 self._exchange(self._cond_bwd, self._unet_rest if self._split_lo is not None else None)
         finally:
-            ops.PROLOGUE_STEP = False
+            self._slots() is not None and self._slots().begin_step(False)
         if not self._opt_in_fb:
             self.opt.launch()
         self._post()
@@ -396,14 +400,20 @@ class HipTrainer:
         return ex.eps
 
 
-def time_steps(trainer: HipTrainer, steps: int) -> float:
-    """Barrier + sync on both sides; returns the wall time of exactly `steps` steps."""
+def time_steps(trainer: HipTrainer, steps: int, events=None) -> float:
+    """Barrier + sync on both sides; returns the wall time of exactly `steps` steps.  events: an
+    optional (start, end) pair of timing events recorded around the steps on this rank's stream
+    (this rank's own GPU time, without the waits of the closing barrier)."""
     if trainer.world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if events is not None:
+        events[0].record()
     for _ in range(steps):
         trainer.step()
+    if events is not None:
+        events[1].record()
     torch.cuda.synchronize()
     if trainer.world > 1:
         dist.barrier()

@@ -304,6 +304,7 @@ class UNetExecutor:
         self.samp_i: Optional[int] = None
         self._samp_tabs: Dict[tuple, dict] = {}  # (S, B) -> buffers; graphs hold their addresses
         self._wgg = ops.WgradGroup()  # the backward's grouped weight gradients (planned per batch size)
+        self.stat_slots = ops.StatSlots()  # producer-statistics slots the transformer tails add into
         self._base_names = set(self.__dict__) | {"_base_names"}
         self.pack.repack()
 
@@ -718,7 +719,8 @@ class UNetExecutor:
             if save is not None:
                 save["lse2"] = S["lse2"]
             if ops.st_tail_fwd(S["o1"], S["t0"], x, k2, v2, self._tail_weights(s), S["out"], B * ntok, c, ntok,
-                               s.heads, self.lu, LN_EPS, save=save, gn_stats=self._gst(S["out"])):
+                               s.heads, self.lu, LN_EPS, save=save, gn_stats=self._gst(S["out"]),
+                               slots=self.stat_slots):
                 return S["out"]
         # cross-attention to the concept tokens (norm2 in the to_out epilogue, or at inference for
         # wide blocks in to_q's A staging)

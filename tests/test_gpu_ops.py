@@ -505,6 +505,47 @@ def test_linear_wgrad_wgl(O, T, cout, cin, monkeypatch):
         assert rel(dxs[i], dy.float() @ w.float()) < 1e-2
 
 
+def test_table_wg_tile33_pair(O, monkeypatch):
+    """with ENCDIFF_TABLE_WG on (the default), a tuned table entry naming the 8-wave WG3
+    kernel (tile 33) with its split overrides the heuristic; the paired backward then launches the
+    riding finalize of the previous layer as a launch of its own.  Two paired layers in a row vs
+    torch fp32; and a table entry that is invalid for the problem (a split that does not divide the
+    batch into whole stages) falls back to a valid plan instead of raising."""
+    from encdiff_amd.ops import Geom
+    torch.manual_seed(23)
+    B, H, cin, cout = 32, 16, 64, 64
+    g = Geom(B, H, H)
+    x, dy = bf(g.pixels, cin), bf(g.pixels, cout)
+    key = O.plan_key(cout, 9 * cin, g.pixels, O.L.OPA_ROWM, O.L.OPB_IM2COL, O.L.OUT_F32_ACCUM, 0, H)
+    table = dict(O._tile_table())
+    table[key] = [33, 4, 0.0]
+    monkeypatch.setattr(O, "_TILES", table)
+    monkeypatch.setattr(O, "TABLE_WG", 1)
+    a = O.conv3x3_wgrad_cl_args(dy, x, g, cin, torch.zeros(cout, 9 * cin, device=dev))
+    assert (a.tile, a.split_k) == (33, 4)
+    w0 = torch.zeros(cout, cin, 3, 3, device=dev, requires_grad=True)
+    F.conv2d(nhwc(x, g), w0, padding=1).backward(nhwc(dy, g))
+    ref = w0.grad.permute(0, 2, 3, 1).reshape(cout, 9 * cin)
+    wf = bf(cout, 9 * cin, scale=(9 * cin) ** -0.5)
+    dws = [torch.zeros(cout, 9 * cin, device=dev) for _ in range(2)]
+    dxs = [torch.empty(g.pixels, cin, device=dev, dtype=torch.bfloat16) for _ in range(2)]
+    for i in range(2):
+        O.conv3x3_bwd_cl(dy, g, wf, x, cin, dws[i], dxs[i])
+    O.flush()
+    torch.cuda.synchronize()
+    for i in range(2):
+        assert rel(dws[i], ref) < 2e-3, rel(dws[i], ref)
+    # an entry whose split does not divide this batch into whole 8-wave stage sets: not taken
+    table[key] = [33, 64, 0.0]
+    a = O.conv3x3_wgrad_cl_args(dy, x, g, cin, torch.zeros(cout, 9 * cin, device=dev))
+    assert (a.tile, a.split_k) != (33, 64)
+    dw = torch.zeros(cout, 9 * cin, device=dev)
+    O.conv3x3_wgrad_cl(dy, x, g, cin, dw)
+    O.flush()
+    torch.cuda.synchronize()
+    assert rel(dw, ref) < 2e-3
+
+
 def test_wgrad_group(O):
     """Grouped weight gradients (encdiff_wgrad_group_*): one grid over every body the group has --
     WG3 at 16 / 8 / 4 (resample none and nearest-up), WGL, the generic 64x64 tile for 2x2 convs and
