@@ -77,7 +77,8 @@ class GraphStepCheck:
     ``check()`` runs one replay + one oracle step and returns the error dict; the oracle
     then adopts the device parameters so that the next check starts from identical state."""
 
-    def __init__(self, B=128, config="shapes3d", lr=1e-4, seed=2024, warmup=2, threads=16, unet_params=None):
+    def __init__(self, B=128, config="shapes3d", lr=1e-4, seed=2024, warmup=2, threads=16, unet_params=None,
+                 oracle_scale=True):
         from encdiff_amd.trainer import HipTrainer
         torch.set_num_threads(max(1, min(threads, torch.get_num_threads())))
         self.B, self.config = B, config
@@ -115,8 +116,11 @@ class GraphStepCheck:
                        tr.opt.step_count, {n: v(a.ema, n) for n in self.unet_names},
                        int(ldm.model_ema.num_updates))
         # scale_by_std (ddpm_enc.py:586-608) on the oracle's own fp32 latents of the first batch
+        # (oracle_scale=False: adopt the device's -- a whole-batch statistic, and the VQ encode of a
+        # large batch of 128x128 images is what a CPU oracle cannot afford; check_rows)
         with torch.no_grad():
-            orc.scale_factor = float(1.0 / O.vq_encode(orc.V, img).flatten().std())
+            orc.scale_factor = (float(1.0 / O.vq_encode(orc.V, img).flatten().std()) if oracle_scale
+                                else self.sf_hip)
 
     def _view(self, buf, n):
         return self.tr.arena.view_in(buf, n).detach().cpu().clone()
@@ -183,6 +187,40 @@ class GraphStepCheck:
             for n in names:
                 orc.ema[n].copy_(a.view_in(a.ema, n).detach().cpu())
         return r
+
+
+    def check_rows(self, rows):
+        """The benchmarked step at a batch a full CPU oracle step cannot finish in test time: one
+        graph replay, then the oracle FORWARD of the listed rows only -- the VQ encode, q_sample and
+        the UNet are per image; Encoder4's training-mode BatchNorm couples the batch, so it runs on
+        all B images and the rows' concept tokens are taken from it -- vs the device eps of those
+        rows (eps tolerances).  Batch-level properties beside it: the device loss is the L1 of the
+        device eps of all B images, and every UNet / Encoder4 gradient and parameter update is
+        finite and non-zero."""
+        tr, orc, a = self.tr, self.orc, self.tr.arena
+        img, t, noise = self.inputs()
+        self._put(img, t, noise)
+        before = a.master.detach().clone()
+        tr.step()
+        torch.cuda.synchronize()
+        eps = tr.eps().detach().cpu().clone()
+        loss = tr.loss()
+        idx = torch.as_tensor(rows, dtype=torch.long)
+        with torch.no_grad():
+            c = O.encoder4_forward(orc.E, img, latent_unit=orc.lu)
+            x0 = orc.scale_factor * O.vq_encode(orc.V, img[idx])
+            xn = O.q_sample(orc.sched, x0, t[idx], noise[idx])
+            oeps = O.unet_forward(orc.P, orc.plan, xn, t[idx], [c[idx]])
+        host = (eps.double() - noise.double()).abs().mean().item()
+        g = a.grad.detach()
+        upd = (a.master.detach() - before)
+        unet_n = a.ema_numel
+        return dict(B=self.B, config=self.config, rows=list(rows), eps_rel=rel(eps[idx], oeps),
+                    eps_max=(eps[idx] - oeps).abs().max().item(), loss=loss,
+                    loss_vs_device_eps=abs(loss - host) / host,
+                    grads_finite=bool(torch.isfinite(g).all()),
+                    unet_grad_norm=float(g[:unet_n].norm()), cond_grad_norm=float(g[unet_n:].norm()),
+                    update_finite=bool(torch.isfinite(upd).all()), update_norm=float(upd.norm()))
 
 
 def failures(r, tol=TOL, every_param=False):

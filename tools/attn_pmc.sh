@@ -3,9 +3,10 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 DH=${1:-8}
+SHAPE=${SHAPE:+--shape $SHAPE}
 cd /tmp && export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --output-format csv -d $R/gpurun_out/apmc1 -o run -- python3 $R/tools/attn_bench.py --eager --only $DH --reps 5 > $R/gpurun_out/apmc1.log 2>&1 || exit 1
-timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVES SQ_INST_LEVEL_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VALU_TRANS_F32 --output-format csv -d $R/gpurun_out/apmc2 -o run -- python3 $R/tools/attn_bench.py --eager --only $DH --reps 5 > $R/gpurun_out/apmc2.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --output-format csv -d $R/gpurun_out/apmc1 -o run -- python3 $R/tools/attn_bench.py --eager --only $DH $SHAPE --reps 5 > $R/gpurun_out/apmc1.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_BUSY_CYCLES SQ_WAVES SQ_INST_LEVEL_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VALU_TRANS_F32 --output-format csv -d $R/gpurun_out/apmc2 -o run -- python3 $R/tools/attn_bench.py --eager --only $DH $SHAPE --reps 5 > $R/gpurun_out/apmc2.log 2>&1 || exit 1
 cd $R && python3 - <<'PY'
 import csv, glob, collections
 for d in ("apmc1", "apmc2"):
