@@ -73,11 +73,14 @@ ED_DEV void bn_block_partial(const float (&q)[NQ][8], const BnLayout& L, int c, 
       for (int i = 0; i < 8; ++i) red[(k * L.lanes + L.pl) * c + L.v * 8 + i] = q[k][i];
   }
   __syncthreads();
+  // write-through (sc1) stores: the partials reach memory without an agent release (which would
+  // write back every dirty line of the XCD's L2 in every workgroup) -- bn_last_block
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)part_out, 0, 0x7FFFFFF0, 0x00020000);
   for (int e = threadIdx.x; e < NQ * c; e += BN_T) {
     const int k = e / c, ch = e - k * c;
     float a = 0.f;
     for (int r = 0; r < L.lanes; ++r) a += red[(k * L.lanes + r) * c + ch];
-    part_out[(long)k * c + ch] = a;
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, a), rs, (int)(((long)k * c + ch) * 4), 0, 16);
   }
 }
 
@@ -107,15 +110,13 @@ ED_DEV void bn_fold(const float* part, int nblk, int c, double* out) {
 }
 
 // true in exactly one workgroup: the last to arrive, after every workgroup's partials are
-// visible to it (cdna_hip_programming.md in-launch reduction recipe: stores drained, one
-// agent-scope release by lane 0 before the ticket, one acquire in the last arriver)
+// visible to it (the guide's write-through hand-off: every wave's sc1 partial stores drained,
+// a barrier, one lane's agent-scope ticket; the last arriver acquires before reading them)
 ED_DEV bool bn_last_block(unsigned int* counter) {
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = t == gridDim.x - 1;
     if (last) {

@@ -372,7 +372,7 @@ __global__ void qsample_kernel(const float* x0, const float* eps, const long lon
 }
 
 // L1 loss: block b writes loss_simple[b] to partials; the LAST block to arrive (device-scope
-// ticket, agent release / acquire as in bn.hip) folds the batch in a fixed order and resets the
+// ticket after write-through partial stores, acquire in the last block, as in bn.hip) folds the batch in a fixed order and resets the
 // ticket.  No memset and no float atomics: graph-replay safe and bitwise reproducible.
 __global__ __launch_bounds__(256) void l1_kernel(const float* pred, const float* eps, const long long* t,
                                                  const float* lvlb, int batch, int per, float lsw, float* out2,
@@ -392,9 +392,11 @@ __global__ __launch_bounds__(256) void l1_kernel(const float* pred, const float*
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) {
-    partials[b] = (red[0] + red[1] + red[2] + red[3]) / (float)per;  // loss_simple[b]
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // loss_simple[b], stored write-through (sc1): visible to the last arriver (which acquires)
+    // without an agent release writing back the L2 (the gradient seed just written by every wave)
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)partials, 0, 0x7FFFFFF0, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, (red[0] + red[1] + red[2] + red[3]) / (float)per),
+                                          rs, b * 4, 0, 16);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned tk = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = tk == (unsigned)batch - 1;
