@@ -58,7 +58,8 @@ class GroupNormArgs(C.Structure):
                 ("accumulate_dx", C.c_int), ("dtype", C.c_int),
                 ("dgamma_part", vp), ("dbeta_part", vp), ("ld_part", C.c_long), ("dfilm", vp),
                 ("ld_dfilm", C.c_long), ("resid", vp), ("ld_resid", C.c_long), ("in_stats", vp),
-                ("ld_in_stats", C.c_long), ("x_from", vp)]
+                ("ld_in_stats", C.c_long), ("x_from", vp), ("dy_resample", C.c_int), ("resid_resample", C.c_int),
+                ("w", C.c_int), ("pad_rs_", C.c_int)]
 
 
 class LayerNormArgs(C.Structure):

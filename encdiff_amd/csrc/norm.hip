@@ -502,7 +502,37 @@ __device__ unsigned long long gn_stamps[16384][8];
 #define GN_STAMP_RT(i) do {} while (0)
 #endif
 
-template <bool SLAB>
+// dy / resid given at the resolution of a resample that follows this GroupNorm (its output feeds a
+// 2x avg-pool or nearest-up, EncdiffGroupNormArgs.dy_resample / resid_resample): the adjoint of
+// that resample read on the fly -- DOWN2: 0.25 * the parent pixel; UP2: the sum of the 4 children
+// (in the order of the elementwise adjoint kernel, so the result is bitwise its output)
+ED_DEV void gn_resample_adj(const bf16_t* base, long ld, int mode, int W, int px, float (&v)[8]) {
+  const int y = px / W, x = px - y * W;
+  if (mode == ENCDIFF_RESAMPLE_DOWN2) {
+    unpack8(*(const uint4*)(base + (long)((y >> 1) * (W >> 1) + (x >> 1)) * ld), v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] *= 0.25f;
+  } else {
+    const long r0 = (long)(2 * y) * (2 * W) + 2 * x;
+    float t[8];
+    unpack8(*(const uint4*)(base + r0 * ld), v);
+    unpack8(*(const uint4*)(base + (r0 + 1) * ld), t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] += t[i];
+    unpack8(*(const uint4*)(base + (r0 + 2 * W) * ld), t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] += t[i];
+    unpack8(*(const uint4*)(base + (r0 + 2 * W + 1) * ld), t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] += t[i];
+  }
+}
+// pixels per image of a tensor at the other side of resample `mode` from hw
+ED_DEV int gn_rs_hw(int mode, int hw) { return mode == ENCDIFF_RESAMPLE_DOWN2 ? hw >> 2 : (mode ? hw << 2 : hw); }
+
+// RS: the resampled-operand variant (dy and / or resid through gn_resample_adj); separate so the
+// common instantiations keep their registers
+template <bool SLAB, bool RS = false>
 __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNormArgs p, int cs, const GnSlabs sl) {
   __shared__ uint4 tx[GN_TILE], td[GN_TILE];
   __shared__ float red[4 * 2048], chs[4 * 512], gam_sh[512];
@@ -514,7 +544,22 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   const float inv_n = 1.f / ((float)HW * L.cpg);
   const long off = (long)L.b * HW;
   const bf16_t* X = (const bf16_t*)p.x + off * p.ldx + L.cb;
-  const bf16_t* DY = (const bf16_t*)p.dy + off * p.lddy + L.cb;
+  const int dyrs = RS ? p.dy_resample : 0, rsrs = RS ? p.resid_resample : 0;
+  const bf16_t* DY = (const bf16_t*)p.dy + (long)L.b * gn_rs_hw(dyrs, HW) * p.lddy + L.cb;
+  // dy row px (the adjoint of the following resample, re-rounded to bf16 as the adjoint kernel
+  // stores it)
+  auto dy_row = [&](int px) -> uint4 {
+    if constexpr (RS) {
+      if (dyrs) {
+        float v[8];
+        gn_resample_adj(DY, p.lddy, dyrs, p.w, px, v);
+        return pack8(v);
+      }
+    }
+    return *(const uint4*)(DY + (long)px * p.lddy);
+  };
+  const bf16_t* RSA = RS && rsrs ? (const bf16_t*)p.resid + (long)L.b * gn_rs_hw(rsrs, HW) * p.ld_resid + L.cb
+                                 : nullptr;
   // per-channel constants
   float xm[8], xr[8], ga[8], be[8], sc1[8], sf[8];
   load8f(p.gamma + L.cb, ga);
@@ -542,7 +587,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   GN_STAMP(2);
   bf16_t* DX = (bf16_t*)p.dx + off * p.lddx + L.cb;
   const bool accum = p.accumulate_dx;
-  const bf16_t* RS = p.resid ? (const bf16_t*)p.resid + off * p.ld_resid + L.cb : nullptr;
+  const bf16_t* RES = p.resid && !RSA ? (const bf16_t*)p.resid + off * p.ld_resid + L.cb : nullptr;
   // rows per batch: every load of a batch issued before the first use (a slab row already has up
   // to 8 loads in flight)
   constexpr int U1 = SLAB ? ED_GN_SLAB_U : ED_GN_BWD_U;
@@ -586,8 +631,8 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
         bx[u] = bd[u] = gr0[u] = (uint4){0u, 0u, 0u, 0u};
         if (px < HW) {
           bx[u] = *(const uint4*)(X + (long)px * p.ldx);
-          bd[u] = *(const uint4*)(DY + (long)px * p.lddy);
-          if (RS) gr0[u] = *(const uint4*)(RS + (long)px * p.ld_resid);
+          bd[u] = dy_row(px);
+          if (RES) gr0[u] = *(const uint4*)(RES + (long)px * p.ld_resid);
           else if (accum) gr0[u] = *(const uint4*)(DX + (long)px * p.lddx);
         }
       }
@@ -608,7 +653,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
               bd[u] = gn_slab_row(sl, off + px, p.c, L.cb);
               *(uint4*)(const_cast<bf16_t*>(DY) + (long)px * p.lddy) = bd[u];
             } else {
-              bd[u] = *(const uint4*)(DY + (long)px * p.lddy);
+              bd[u] = dy_row(px);
             }
           }
         }
@@ -670,19 +715,29 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   GN_STAMP(5);
   auto out_row = [&](const int px, const uint4 g, const float (&dn)[8], const float (&xh)[8]) {
     float o[8];
-    if (RS && accum) {  // both: dx (in place) + resid
+    if (RES && accum) {  // both: dx (in place) + resid
       float rr[8];
       unpack8(*(const uint4*)(DX + (long)px * p.lddx), o);
       unpack8(g, rr);
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] += rr[i];
-    } else if (RS || accum) {
+    } else if (RES || accum) {
       unpack8(g, o);  // residual-branch gradient (skip connection) or the dx being accumulated
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float r = xr[i] * (dn[i] * ga[i] - m1[i] - xh[i] * m2[i]);
-      o[i] = (accum || RS) ? o[i] + r : r;
+      o[i] = (accum || RES) ? o[i] + r : r;
+    }
+    if constexpr (RS) {
+      if (RSA) {  // + the adjoint of the skip branch's resample, after dx's own rounding (as the
+                  // separate accumulate pass it replaces added it)
+        float a[8];
+        gn_resample_adj(RSA, p.ld_resid, rsrs, p.w, px, a);
+        unpack8(pack8(o), o);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] += a[i];
+      }
     }
     *(uint4*)(DX + (long)px * p.lddx) = pack8(o);
   };
@@ -703,7 +758,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
         const int px = px0 + u * L.np;
         gr[u] = (uint4){0u, 0u, 0u, 0u};
         if (px < HW) {
-          if (RS) gr[u] = *(const uint4*)(RS + (long)px * p.ld_resid);
+          if (RES) gr[u] = *(const uint4*)(RES + (long)px * p.ld_resid);
           else if (accum) gr[u] = *(const uint4*)(DX + (long)px * p.lddx);
         }
       }
@@ -713,7 +768,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
         if (px >= HW) break;
         float v[8], d[8], dn[8], xh[8];
         unpack8(gn_row(L, tx, X, p.ldx, px), v);
-        unpack8(gn_row(L, td, DY, p.lddy, px), d);
+        unpack8(RS && dyrs && !L.tiled ? dy_row(px) : gn_row(L, td, DY, p.lddy, px), d);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           xh[i] = (v[i] - xm[i]) * xr[i];
@@ -930,7 +985,8 @@ extern "C" int encdiff_debug_gn_stamps(void* dst, int nblocks) {
 #endif
 
 extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream) {
-  if (a && a->dtype == ENCDIFF_DT_F32) return ed_groupnorm_bwd_f32(a, (hipStream_t)stream);
+  if (a && a->dtype == ENCDIFF_DT_F32)
+    return (a->dy_resample || a->resid_resample) ? ENCDIFF_ERR_UNSUPPORTED : ed_groupnorm_bwd_f32(a, (hipStream_t)stream);
   if (a && a->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_UNSUPPORTED;
   if (!a || !a->x || !a->dy || !a->dx || !a->stats || !a->dgamma_part || !a->dbeta_part) return ENCDIFF_ERR_ARG;
   if (a->film && !a->dfilm) return ENCDIFF_ERR_ARG;
@@ -941,12 +997,24 @@ extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream
     const int rc = gn_slabs_of(*a->x_from, a->dy, a->lddy, a, sl);
     if (rc != ENCDIFF_OK) return rc;
   }
-  if (sl.ws)
+  const bool rs = a->dy_resample || a->resid_resample;
+  if (rs) {  // operands at a following resample's resolution (read through its adjoint)
+    auto ok_mode = [](int m) { return m == 0 || m == ENCDIFF_RESAMPLE_DOWN2 || m == ENCDIFF_RESAMPLE_UP2; };
+    if (!ok_mode(a->dy_resample) || !ok_mode(a->resid_resample) || sl.ws || a->w <= 0 || a->hw % a->w ||
+        (a->resid_resample && !a->resid))
+      return ENCDIFF_ERR_ARG;
+    const int h = a->hw / a->w;
+    if ((a->dy_resample == ENCDIFF_RESAMPLE_DOWN2 || a->resid_resample == ENCDIFF_RESAMPLE_DOWN2) && ((h | a->w) & 1))
+      return ENCDIFF_ERR_SHAPE;
+    hipLaunchKernelGGL((gn_bwd_kernel<false, true>), dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0,
+                       (hipStream_t)stream, *a, cs, sl);
+  } else if (sl.ws) {
     hipLaunchKernelGGL(gn_bwd_kernel<true>, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream,
                        *a, cs, sl);
-  else
+  } else {
     hipLaunchKernelGGL(gn_bwd_kernel<false>, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream,
                        *a, cs, sl);
+  }
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }

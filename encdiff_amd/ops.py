@@ -806,9 +806,11 @@ def groupnorm_fwd(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_fi
 
 def groupnorm_bwd(x, g: Geom, gamma, beta, stats, eps, silu, dy, dx, dgamma_part, dbeta_part, film=None,
                   ld_film=0, dfilm=None, ld_dfilm=0, accumulate=False, groups=32, ld_part=None, resid=None,
-                  dy_from=None):
+                  dy_from=None, dy_resample=0, resid_resample=0):
     """dx (+)= GN_bwd(dy) (+ resid: the block's skip-branch gradient, added in the same pass).
-    dy_from: the GemmArgs of dy's producer whose finalize gemm_pair deferred (dy written here)."""
+    dy_from: the GemmArgs of dy's producer whose finalize gemm_pair deferred (dy written here).
+    dy_resample / resid_resample: dy / resid are at the resolution of that 2x resample following
+    the GroupNorm (L.RESAMPLE_DOWN2 / UP2); their adjoint is applied on the fly."""
     c = x.shape[1]
     a = L.GroupNormArgs(batch=g.batch, hw=g.h * g.w, c=c, groups=groups, eps=eps, silu=int(silu),
                         x=_p(x), ldx=_ld(x), gamma=_p(gamma), beta=_p(beta), film=_p(film), ld_film=ld_film,
@@ -816,7 +818,8 @@ def groupnorm_bwd(x, g: Geom, gamma, beta, stats, eps, silu, dy, dx, dgamma_part
                         accumulate_dx=int(accumulate), dgamma_part=_p(dgamma_part), dbeta_part=_p(dbeta_part),
                         ld_part=c if ld_part is None else ld_part, dfilm=_p(dfilm), ld_dfilm=ld_dfilm,
                         resid=_p(resid), ld_resid=_ld(resid) if resid is not None else 0,
-                        x_from=None if dy_from is None else C.addressof(dy_from))
+                        x_from=None if dy_from is None else C.addressof(dy_from), dy_resample=dy_resample,
+                        resid_resample=resid_resample, w=g.w)
     check(lib.encdiff_groupnorm_bwd(C.byref(a), _s()), "encdiff_groupnorm_bwd")
 
 

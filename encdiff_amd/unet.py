@@ -43,6 +43,10 @@ GN_FROM_PRODUCER = os.environ.get("ENCDIFF_GN_FROM_PRODUCER", "1") != "0"
 # -> GN2 / GN1 backward, transformer linears -> the LayerNorm / GroupNorm backward reading their
 # input gradient.  One launch instead of two (0: separate finalize launches, A/B runs)
 GN_FIN = os.environ.get("ENCDIFF_GN_FIN", "1") != "0"
+# resampling ResBlocks (cin == cout): the adjoints of conv1's input resample and of the skip branch's
+# resample read by the GN1 backward (EncdiffGroupNormArgs.dy_resample / resid_resample) instead of two
+# elementwise launches (0: separate launches, A/B)
+RS_FUSED = os.environ.get("ENCDIFF_RS_FUSED", "1") != "0"
 # grouped weight gradients (ops.WgradGroup): one grid per WG_WINDOW UNet blocks of the backward
 # (0: one grid per DP bucket region)
 WG_WINDOW = int(os.environ.get("ENCDIFF_WG_WINDOW", "1"))
@@ -1001,19 +1005,22 @@ class UNetExecutor:
         d_a1 = S["d_a1"]
         f1 = self.conv_bwd(S["d_h1"], go, r.cin, pre + "in_layers.2.weight", a1, S["d_a1r"] if r.updown else d_a1,
                            self.G(pre + "in_layers.2.bias"), resample=rs, defer_dx=GN_FIN and not r.updown)
-        if r.updown:
+        fuse = RS_FUSED and r.updown and r.cin == r.cout
+        if r.updown and not fuse:
             ops.resample_bwd(S["d_a1r"], d_a1, gi, r.updown)
         identity = r.cin == r.cout and not r.updown
-        # identity skip: its gradient (dout) rides in the GN1 backward pass
+        # identity skip: its gradient (dout) rides in the GN1 backward pass; so do, for a resampling
+        # block, the resample adjoints of conv1's input gradient and of the skip branch
         ops.groupnorm_bwd(x, gi, self.P(pre + "in_layers.0.weight"), self.P(pre + "in_layers.0.bias"), S["st1"],
-                          GN_EPS, True, d_a1, dx, dg, db, accumulate=acc, ld_part=self.gn.ld,
-                          resid=dout if identity else None, dy_from=f1)
+                          GN_EPS, True, S["d_a1r"] if fuse else d_a1, dx, dg, db, accumulate=acc, ld_part=self.gn.ld,
+                          resid=dout if (identity or fuse) else None, dy_from=f1,
+                          dy_resample=r.updown if fuse else 0, resid_resample=r.updown if fuse else 0)
         # skip path
         if r.cin != r.cout:
             ops.linear_bwd(dout, self.W(pre + "skip_connection.weight"), x, dx,
                            self.G(pre + "skip_connection.weight").view(r.cout, r.cin),
                            self.G(pre + "skip_connection.bias"), resid=dx)
-        elif r.updown:
+        elif r.updown and not fuse:
             ops.resample_bwd(dout, dx, gi, r.updown, accumulate=True)
 
     def _st_bwd(self, s: STSpec, dout, dx, acc):

@@ -279,6 +279,15 @@ typedef struct EncdiffGroupNormArgs {
                                 (C == dy, ldc == lddy; e.g. the input gradient of the conv that read
                                 this GroupNorm's output, its finalize deferred by
                                 encdiff_gemm_pair_dx) */
+  /* backward, optional (bf16, no x_from): dy / resid are given at the resolution of a 2x resample
+     (ENCDIFF_RESAMPLE_DOWN2 avg-pool / UP2 nearest) that follows this GroupNorm -- its output feeds
+     the downsampling / upsampling conv of a ResBlock, or the ResBlock's skip branch resamples x
+     (openaimodel_enc.py:248-253, 264-265) -- and the kernel reads them through that resample's
+     adjoint (dy: rounded to bf16 as the adjoint pass would store it; resid: added after dx's own
+     rounding, as an accumulating adjoint pass would): two elementwise launches fewer per ResBlock.
+     w: the image width at this GroupNorm's resolution (hw = h * w), needed with either mode. */
+  int dy_resample, resid_resample;
+  int w, pad_rs_;
 } EncdiffGroupNormArgs;
 
 int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* args, void* stream);

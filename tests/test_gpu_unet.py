@@ -262,6 +262,47 @@ def test_unet_gn_fin_bitwise(unet, B, train):
         assert torch.equal(u, v)
 
 
+@pytest.mark.parametrize("B", [16, 64])
+def test_unet_resample_adjoint_fused_bitwise(unet, B):
+    """Resampling ResBlocks: the GN1 backward reads conv1's input gradient and the skip branch's
+    gradient through the resample adjoints (EncdiffGroupNormArgs.dy_resample / resid_resample)
+    instead of two elementwise adjoint launches -- the gradients and d(context) bitwise equal to
+    the separate launches, and the fused form actually runs (6 ResBlocks)."""
+    from encdiff_amd import ops, unet as U
+    torch.manual_seed(31)
+    x = torch.randn(B, 3, 16, 16, device="cuda")
+    t = torch.randint(0, 1000, (B,), device="cuda")
+    c = torch.randn(B, 320, device="cuda")
+    gout = torch.randn(B, 3, 16, 16, device="cuda")
+    seen = []
+    orig = ops.groupnorm_bwd
+
+    def counted(*a, **k):
+        seen.append(bool(k.get("dy_resample")))
+        return orig(*a, **k)
+    ops.groupnorm_bwd = counted
+
+    def run(on):
+        U.RS_FUSED = on
+        seen.clear()
+        unet.executor()
+        unet._arena.zero_grad()
+        cc = c.clone().requires_grad_(True)
+        eps = unet(x, t, context=[cc])
+        eps.backward(gout)
+        torch.cuda.synchronize()
+        return (unet._arena.grad.clone(), cc.grad.clone()), sum(seen)
+    try:
+        a, n_on = run(True)
+        b, n_off = run(False)
+    finally:
+        U.RS_FUSED = True
+        ops.groupnorm_bwd = orig
+    assert n_on == 6 and n_off == 0, (n_on, n_off)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v), (u - v).abs().max()
+
+
 @pytest.mark.parametrize("res", [True, False], ids=["resblocks", "st_heads"])
 @pytest.mark.parametrize("B", [2, 8, 32])
 def test_unet_agn_inference(unet, B, res):
