@@ -129,6 +129,16 @@ class StHeadArgs(C.Structure):
                 ("n1", vp), ("ld_n1", C.c_long), ("s1", vp), ("qkv", vp), ("ld_qkv", C.c_long)]
 
 
+class ResConvArgs(C.Structure):
+    _fields_ = [("batch", C.c_int), ("h", C.c_int), ("cin", C.c_int), ("cout", C.c_int), ("resample", C.c_int),
+                ("groups", C.c_int), ("silu", C.c_int), ("eps", C.c_float), ("x", vp), ("ld_x", C.c_long),
+                ("gamma", vp), ("beta", vp), ("film", vp), ("ld_film", C.c_long), ("w", vp), ("ld_w", C.c_long),
+                ("bias", vp), ("resid", vp), ("ld_resid", C.c_long), ("resid_resample", C.c_int), ("cskip", C.c_int),
+                ("xskip", vp), ("ld_xskip", C.c_long), ("wskip", vp), ("ld_wskip", C.c_long), ("bskip", vp),
+                ("y", vp), ("ld_y", C.c_long), ("tile_m", C.c_int), ("tile_n", C.c_int),
+                ("skip_stages", C.c_int), ("pad_", C.c_int)]
+
+
 class ZeroJob(C.Structure):
     _fields_ = [("ptr", vp), ("rows", C.c_longlong), ("row_bytes", C.c_longlong), ("ld_bytes", C.c_longlong)]
 
@@ -194,6 +204,8 @@ _PROTOS = {
     "encdiff_nchw_to_rows_split3": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_long, vp],
     "encdiff_st_tail_fwd": [C.POINTER(StTailArgs), vp],
     "encdiff_st_head_fwd": [C.POINTER(StHeadArgs), vp],
+    "encdiff_resconv_fwd": [C.POINTER(ResConvArgs), vp],
+    "encdiff_resconv_query": [C.POINTER(ResConvArgs), C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "encdiff_step_prologue": [C.POINTER(StepPrologueArgs), vp],
     "encdiff_version": [],
 }

@@ -977,6 +977,57 @@ def st_head_fwd(x, gn, w_in, b_in, g1, be1, w_qkv, t0, qkv, rows, c, tokens, gn_
     return True
 
 
+RC_TILE_M = int(os.environ.get("ENCDIFF_RC_TILE_M", "0"))  # plan overrides for tuning (0: heuristic)
+RC_TILE_N = int(os.environ.get("ENCDIFF_RC_TILE_N", "0"))
+
+
+def resconv_supported(x, g: Geom, w, resample=L.RESAMPLE_NONE, film=None, ld_film=0, cskip=0, groups=32) -> bool:
+    """Whether encdiff_resconv_fwd plans this conv (encdiff_resconv_query: shapes, LDS fit, FiLM
+    row alignment), so a caller can choose the fused pair before launching either of its convs."""
+    if g.h != g.w:
+        return False
+    fp = _p(film) or 0
+    key = (g.batch, g.h, w.shape[1] // 9, w.shape[0], resample, groups, _ld(x), _ld(w), RC_TILE_M, RC_TILE_N,
+           fp % 16 if film is not None else -1, ld_film % 4, cskip)
+    hit = _RC_OK.get(key)
+    if hit is None:
+        a = L.ResConvArgs(batch=g.batch, h=g.h, cin=w.shape[1] // 9, cout=w.shape[0], resample=resample,
+                          groups=groups, x=_p(x), ld_x=_ld(x), gamma=_p(x), beta=_p(x), film=fp or None,
+                          ld_film=ld_film, w=_p(w), ld_w=_ld(w), y=_p(x), ld_y=w.shape[0], cskip=cskip,
+                          xskip=_p(x) if cskip else None, ld_xskip=cskip, wskip=_p(w) if cskip else None,
+                          ld_wskip=cskip, tile_m=RC_TILE_M, tile_n=RC_TILE_N)
+        hit = _RC_OK[key] = lib.encdiff_resconv_query(C.byref(a), None, None) == 0
+    return hit
+
+
+_RC_OK = {}
+
+
+def resconv_fwd(x, g: Geom, w, y, gamma, beta, eps, silu=True, film=None, ld_film=0, bias=None,
+                resample=L.RESAMPLE_NONE, resid=None, resid_resample=L.RESAMPLE_NONE, xskip=None, wskip=None,
+                bskip=None, groups=32) -> bool:
+    """An inference ResBlock conv with the GroupNorm in front of it, one launch
+    (openaimodel_enc.py:255-275): y = conv3x3(resample(SiLU(GN(x)(1 + scale) + shift))) + bias
+    + resid (read through resid_resample) or bf16(xskip wskip^T + bskip).  x: [B*h*h][cin] at the
+    geometry g, w: packed [cout][9*cin].  Returns False outside the kernel's support (the caller
+    issues the unfused launches)."""
+    cin = w.shape[1] // 9
+    a = L.ResConvArgs(batch=g.batch, h=g.h, cin=cin, cout=w.shape[0], resample=resample, groups=groups,
+                      silu=int(silu), eps=eps, x=_p(x), ld_x=_ld(x), gamma=_p(gamma), beta=_p(beta),
+                      film=_p(film), ld_film=ld_film, w=_p(w), ld_w=_ld(w), bias=_p(bias), y=_p(y), ld_y=_ld(y),
+                      tile_m=RC_TILE_M, tile_n=RC_TILE_N)
+    if resid is not None:
+        a.resid, a.ld_resid, a.resid_resample = _p(resid), _ld(resid), resid_resample
+    if xskip is not None:
+        a.cskip, a.xskip, a.ld_xskip = xskip.shape[1], _p(xskip), _ld(xskip)
+        a.wskip, a.ld_wskip, a.bskip = _p(wskip), _ld(wskip), _p(bskip)
+    rc = lib.encdiff_resconv_fwd(C.byref(a), _s())
+    if rc in (-2, -3):
+        return False
+    check(rc, "encdiff_resconv_fwd")
+    return True
+
+
 # ------------------------------------------------------------------ elementwise
 def ew(op, x, y, x2=None, rows=None, cols=None, accumulate=False, resample=0, g: Optional[Geom] = None):
     rows = rows if rows is not None else y.shape[0]

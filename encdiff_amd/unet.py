@@ -67,6 +67,10 @@ AGN_MAX_B = int(os.environ.get("ENCDIFF_AGN_MAX_B", "32"))
 # with it vs 595 without (the per-workgroup statistics prologue costs more than the launches it saves)
 AGN_RES = os.environ.get("ENCDIFF_AGN_RES", "0") != "0"
 AGN_FOLD = os.environ.get("ENCDIFF_AGN_FOLD", "1") != "0"  # split-K combined in the kernel (else a finalize pass)
+# inference at sampling batches: each ResBlock as two launches (ops.resconv_fwd: GroupNorm in LDS
+# over whole staged images + conv + skip) instead of four to six (0: the unfused launches, A/B)
+RC = os.environ.get("ENCDIFF_RC", "1") != "0"
+RC_MAX_B = int(os.environ.get("ENCDIFF_RC_MAX_B", "32"))
 # widest level that uses it: at c = 256 one workgroup streams 2.6 MB of weights through one CU
 # (74 us at B = 8 against ~35 us for the separate launches, tools/st_tail_bench.py)
 ST_TAIL_MAXC = int(os.environ.get("ENCDIFF_ST_TAIL_MAXC", "128"))
@@ -597,6 +601,8 @@ class UNetExecutor:
         S = self.state[r.prefix]
         S["x"] = x
         gi, go = Geom(B, r.hin, r.hin), Geom(B, r.hout, r.hout)
+        if self.infer and RC and B <= RC_MAX_B and self._res_fwd_rc(r, S, x, gi, go):
+            return S["out"]
         if self.infer and AGN and AGN_RES and B <= AGN_MAX_B:
             return self._res_fwd_agn(r, S, x, gi, go)
         ops.groupnorm_fwd(x, gi, self.P(r.prefix + "in_layers.0.weight"), self.P(r.prefix + "in_layers.0.bias"),
@@ -626,6 +632,35 @@ class UNetExecutor:
                                      bias=self.P(r.prefix + "out_layers.3.bias"), resid=resid, gn_stats=self._gst(out),
                                      defer=GN_FIN and self._gst(out) is None)
         return out
+
+    def _res_fwd_rc(self, r: ResSpec, S, x, gi: Geom, go: Geom) -> bool:
+        """Inference ResBlock as two ops.resconv_fwd launches: h1 = conv1(resample(SiLU(GN1(x)))) + b1,
+        out = conv2(SiLU(GN2(h1)(1 + scale) + shift)) + b2 + skip(x) -- each conv stages the whole
+        images it reads in LDS and normalises them there, so no GroupNorm launch, no normalised
+        activation in memory and no skip / resample launch.  x complete first (a producer that
+        deferred its finalize finalizes now).  False (nothing launched) outside the kernel's
+        support: the caller runs the unfused launches."""
+        pre = r.prefix
+        w1, w2 = self.W(pre + "in_layers.2.weight"), self.W(pre + "out_layers.3.weight")
+        film = self._E_use[:, r.film_off:]
+        cskip = r.cin if r.cin != r.cout else 0
+        if not (ops.resconv_supported(x, gi, w1, r.updown)
+                and ops.resconv_supported(S["h1"], go, w2, film=film, ld_film=self._E_ld, cskip=cskip)):
+            return False
+        p = self._pend
+        self._pend = None
+        ops.finalize(p)
+        ok = ops.resconv_fwd(x, gi, w1, S["h1"], self.P(pre + "in_layers.0.weight"), self.P(pre + "in_layers.0.bias"),
+                             GN_EPS, bias=self.P(pre + "in_layers.2.bias"), resample=r.updown)
+        if cskip:
+            skip = dict(xskip=x, wskip=self.W(pre + "skip_connection.weight"), bskip=self.P(pre + "skip_connection.bias"))
+        else:
+            skip = dict(resid=x, resid_resample=r.updown)
+        ok = ok and ops.resconv_fwd(S["h1"], go, w2, S["out"], self.P(pre + "out_layers.0.weight"),
+                                    self.P(pre + "out_layers.0.bias"), GN_EPS, film=film, ld_film=self._E_ld,
+                                    bias=self.P(pre + "out_layers.3.bias"), **skip)
+        assert ok, "encdiff_resconv_fwd declined a conv its query accepted"
+        return True
 
     def _res_fwd_agn(self, r: ResSpec, S, x, gi: Geom, go: Geom):
         """Inference ResBlock with its GroupNorms in the convs' A staging (EncdiffGemmArgs.agn_*):

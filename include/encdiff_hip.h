@@ -670,6 +670,51 @@ int encdiff_st_head_fwd(const EncdiffStHeadArgs* args, void* stream);
  *     encdiff_gather_images_u8 earlier in the step) by the last workgroup to finish (ticket
  *     `done`, zero on entry, left zero), so a captured step advances both by itself.
  * t or noise may be NULL (a test feeding its own). */
+/* One convolution of an inference ResBlock with the GroupNorm in front of it, as ONE launch
+ * (openaimodel_enc.py:255-275 with use_scale_shift_norm, replacing the GroupNorm launch, the conv
+ * launch and -- for conv2 -- the skip / resample launch of the unfused path):
+ *   y = conv3x3(resample(SiLU(GN(x) (1 + scale) + shift))) + bias + skip
+ * A workgroup stages the whole images its output rows read into LDS, reduces their GroupNorm
+ * statistics, normalises them in place (bf16, as the GroupNorm launch would store them), applies
+ * the 2x resample (DOWN2: avg-pool of the normalised rows, rounded to bf16 as the resample pass
+ * stores it; UP2: nearest, read through the gather), and runs the implicit-im2col GEMM of its
+ * 16-row tiles x 16-column slice on MFMA with the weights streamed from L2.  skip: resid (bf16 rows
+ * at the output resolution, or read through resid_resample from the ResBlock input) or a 1x1
+ * skip conv (out += bf16(xskip Wskip^T + bskip), as the skip launch would store it).
+ * Constraints: cin % 32 == 0, cout % 16 == 0, square images, the staged images fit in LDS
+ * (ENCDIFF_ERR_UNSUPPORTED otherwise: the caller issues the unfused launches). */
+typedef struct EncdiffResConvArgs {
+  int batch, h, cin, cout;       /* x: batch images of h x h pixels, cin channels             */
+  int resample;                  /* ENCDIFF_RESAMPLE_*: after the GroupNorm (conv at 2h / h/2) */
+  int groups, silu;
+  float eps;
+  const void* x; long ld_x;      /* bf16 rows [batch*h*h][cin]                                 */
+  const float* gamma; const float* beta;
+  const float* film; long ld_film;  /* optional fp32 [batch][ld_film]: scale at [c], shift at
+                                       [cin + c]; ld_film 0: one row for every image          */
+  const void* w; long ld_w;      /* bf16 [cout][9*cin] (tap-major, channels-last)              */
+  const float* bias;             /* optional fp32 [cout]                                       */
+  const void* resid; long ld_resid;  /* optional bf16 rows added to the output               */
+  int resid_resample;            /* resid at the output resolution (NONE), its half (UP2: nearest)
+                                    or its double (DOWN2: 2x2 average rounded to bf16)        */
+  int cskip;                     /* 1x1 skip conv input channels (0: none)                     */
+  const void* xskip; long ld_xskip;  /* bf16 rows [batch*ho*ho][cskip]                        */
+  const void* wskip; long ld_wskip;  /* bf16 [cout][cskip]                                    */
+  const float* bskip;            /* optional fp32 [cout]                                       */
+  void* y; long ld_y;            /* bf16 rows [batch*ho*ho][cout]                              */
+  int tile_m, tile_n;            /* plan overrides (0: heuristic): 16-row tiles per workgroup
+                                    (1, 2, 4), 16-column tiles per workgroup (1, 2)           */
+  int skip_stages;               /* 0; timing experiments only (tools/rc_bench.py): 1 no staging
+                                    loads, 2 no normalisation, 4 no GEMM (nor its B staging), 8 no
+                                    stores, 16 no B staging, 32 no GEMM arithmetic */
+  int pad_;
+} EncdiffResConvArgs;
+
+int encdiff_resconv_fwd(const EncdiffResConvArgs* args, void* stream);
+/* The plan of encdiff_resconv_fwd for these arguments without launching (pointers are not read):
+ * ENCDIFF_OK and the LDS bytes / workgroups per launch, or the error the launch would return. */
+int encdiff_resconv_query(const EncdiffResConvArgs* args, int* lds_bytes, int* grid);
+
 typedef struct EncdiffZeroJob {
   void* ptr;
   long long rows, row_bytes, ld_bytes;

@@ -33,7 +33,7 @@ STRUCTS = {
     "EncdiffLayerNormArgs": "LayerNormArgs", "EncdiffAttnArgs": "AttnArgs", "EncdiffEwArgs": "EwArgs",
     "EncdiffSmallConvArgs": "SmallConvArgs", "EncdiffPackJob": "PackJob", "EncdiffBatchNormArgs": "BatchNormArgs",
     "EncdiffStTailArgs": "StTailArgs", "EncdiffStHeadArgs": "StHeadArgs", "EncdiffZeroJob": "ZeroJob",
-    "EncdiffStepPrologueArgs": "StepPrologueArgs",
+    "EncdiffStepPrologueArgs": "StepPrologueArgs", "EncdiffResConvArgs": "ResConvArgs",
 }
 
 

@@ -1,0 +1,187 @@
+"""The inference ResBlock conv with its GroupNorm in LDS (encdiff_resconv_fwd, ops.resconv_fwd;
+openaimodel_enc.py:255-275): per op against a torch fp32 restatement of GroupNorm32 (+FiLM) + SiLU
+-> resample -> conv3x3 + bias + skip at the UNet's sampling shapes, and the UNet's two-launch
+ResBlocks (unet.RC) against the CPU oracle and the unfused launches.
+
+Tolerance: the kernel rounds the normalised activation to bf16 (as the unfused GroupNorm launch
+stores it) and accumulates in fp32; the fp32 restatement rounds at the same points, so the
+difference is the statistics' summation order (one-pass E[x^2] - mean^2 as encdiff_groupnorm_fwd)
+flipping a few bf16 roundings: rel-L2 <= 1e-2 and max-abs <= 3e-2 of the output's RMS scale."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+R_DOWN, R_UP = 1, 2
+
+
+def bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).double().cpu(); b = torch.as_tensor(b).double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def pack(w):  # [cout][cin][3][3] -> [cout][9*cin] tap-major channels-last (ops.conv3x3_fwd's layout)
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).contiguous()
+
+
+def restated(x, B, h, cin, gamma, beta, film, w, bias, resample, resid, resid_rs, xs, ws, bs, eps=1e-5):
+    xf = x.float().view(B, h, h, cin).permute(0, 3, 1, 2)
+    n = F.group_norm(xf, 32, gamma, beta, eps)
+    if film is not None:
+        n = n * (1 + film[:, :cin, None, None]) + film[:, cin:2 * cin, None, None]
+    a = bf(F.silu(n))
+    if resample == R_DOWN:
+        a = bf(F.avg_pool2d(a, 2))
+    elif resample == R_UP:
+        a = F.interpolate(a, scale_factor=2, mode="nearest")
+    y = F.conv2d(a, w, bias, padding=1)
+    ho = y.shape[-1]
+    if xs is not None:
+        y = y + bf(F.conv2d(xs.float().view(B, ho, ho, -1).permute(0, 3, 1, 2), ws[:, :, None, None], bs))
+    if resid is not None:
+        hr = ho // 2 if resid_rs == R_UP else (ho * 2 if resid_rs == R_DOWN else ho)
+        r = resid.float().view(B, hr, hr, -1).permute(0, 3, 1, 2)
+        if resid_rs == R_DOWN:
+            r = bf(F.avg_pool2d(r, 2))
+        elif resid_rs == R_UP:
+            r = F.interpolate(r, scale_factor=2, mode="nearest")
+        y = y + r
+    return y.permute(0, 2, 3, 1).reshape(-1, y.shape[1])
+
+
+CASES = [  # (B, h, cin, cout, resample, skip, film)  -- the UNet's ResBlock convs at sampling batches
+    (8, 16, 64, 64, 0, "resid", True),      # 16x16 level
+    (8, 16, 192, 64, 0, "conv", True),      # 16x16 output block (concat input)
+    (8, 16, 64, 64, R_DOWN, "resid_down", False),  # down block conv1 (+ its conv2's pooled skip)
+    (8, 8, 384, 128, 0, "conv", True),      # 8x8 output block
+    (8, 8, 128, 128, R_UP, "resid_up", False),     # up block 8 -> 16
+    (8, 4, 256, 256, R_DOWN, None, False),  # 4x4 -> 2x2 (four images per 16-row tile)
+    (8, 2, 512, 256, 0, "conv", True),      # 2x2 output block
+    (4, 2, 256, 256, R_UP, "resid_up", True),      # 2x2 -> 4x4 up block
+    (32, 4, 256, 256, 0, "resid", True),    # a larger sampling batch
+]
+
+
+@pytest.mark.parametrize("B,h,cin,cout,rs,skip,film", CASES)
+@pytest.mark.parametrize("tiles", [(0, 0), (1, 2)], ids=["heuristic", "m1n2"])
+def test_resconv_matches_restatement(B, h, cin, cout, rs, skip, film, tiles):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from encdiff_amd import ops
+    from encdiff_amd.ops import Geom
+    g = torch.Generator().manual_seed(B * 1000 + h * 10 + cin + rs)
+    ho = 2 * h if rs == R_UP else (h // 2 if rs == R_DOWN else h)
+    x = bf(torch.randn(B * h * h, cin, generator=g) * 1.5 + 0.3)
+    gamma = 1 + 0.2 * torch.randn(cin, generator=g)
+    beta = 0.2 * torch.randn(cin, generator=g)
+    filmt = 0.3 * torch.randn(B, 2 * cin, generator=g) if film else None
+    w = bf(torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5))
+    bias = 0.1 * torch.randn(cout, generator=g)
+    resid = xs = ws = bs = None
+    resid_rs = 0
+    if skip == "conv":
+        xs = bf(torch.randn(B * ho * ho, cin // 2 if cin > cout else cout // 2 * 2, generator=g))
+        ws = bf(torch.randn(cout, xs.shape[1], generator=g) / xs.shape[1] ** 0.5)
+        bs = 0.1 * torch.randn(cout, generator=g)
+    elif skip is not None:
+        resid_rs = {"resid": 0, "resid_down": R_DOWN, "resid_up": R_UP}[skip]
+        hr = ho // 2 if resid_rs == R_UP else (ho * 2 if resid_rs == R_DOWN else ho)
+        resid = bf(torch.randn(B * hr * hr, cout, generator=g))
+    ref = restated(x, B, h, cin, gamma, beta, filmt, w, bias, rs, resid, resid_rs, xs, ws, bs)
+    cu = lambda t: None if t is None else t.cuda()  # noqa: E731
+    y = torch.full((B * ho * ho, cout), float("nan"), device="cuda", dtype=torch.bfloat16)
+    old = ops.RC_TILE_M, ops.RC_TILE_N
+    ops.RC_TILE_M, ops.RC_TILE_N = tiles
+    try:
+        ok = ops.resconv_fwd(x.cuda().bfloat16(), Geom(B, h, h), pack(w).cuda().bfloat16(), y, gamma.cuda(),
+                             beta.cuda(), 1e-5, film=cu(filmt), ld_film=2 * cin if film else 0, bias=bias.cuda(),
+                             resample=rs, resid=None if resid is None else resid.cuda().bfloat16(),
+                             resid_resample=resid_rs, xskip=None if xs is None else xs.cuda().bfloat16(),
+                             wskip=None if ws is None else ws.cuda().bfloat16(), bskip=cu(bs))
+    finally:
+        ops.RC_TILE_M, ops.RC_TILE_N = old
+    assert ok
+    assert ops.resconv_supported(x, Geom(B, h, h), pack(w), rs)
+    out = y.float().cpu()
+    scale = ref.pow(2).mean().sqrt().item()
+    r, m = rel(out, ref), (out - ref).abs().max().item() / scale
+    print(f"B={B} h={h} cin={cin} cout={cout} rs={rs} skip={skip} film={film} tiles={tiles}: "
+          f"rel-L2 {r:.2e} max-abs/rms {m:.2e}")
+    assert torch.isfinite(out).all()
+    assert r < 1e-2 and m < 3e-2
+
+
+def test_resconv_rejects_unsupported():
+    """Outside the kernel's support the op declines (the caller issues the unfused launches): a
+    2x2 batch that is not a multiple of four images, cin not a multiple of 32."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from encdiff_amd import ops
+    from encdiff_amd.ops import Geom
+    d = dict(device="cuda", dtype=torch.bfloat16)
+    f = dict(device="cuda", dtype=torch.float32)
+    x = torch.zeros(2 * 4, 256, **d)
+    w = torch.zeros(256, 9 * 256, **d)
+    y = torch.zeros(2 * 4, 256, **d)
+    gm, bt = torch.ones(256, **f), torch.zeros(256, **f)
+    assert not ops.resconv_supported(x, Geom(2, 2, 2), w)
+    assert not ops.resconv_fwd(x, Geom(2, 2, 2), w, y, gm, bt, 1e-5)
+    x2 = torch.zeros(8 * 16, 48, **d)
+    w2 = torch.zeros(64, 9 * 48, **d)
+    assert not ops.resconv_supported(x2, Geom(8, 4, 4), w2)
+
+
+@pytest.mark.parametrize("B", [2, 8, 32])
+def test_unet_rc_inference(B):
+    """No-grad forwards at sampling batches run every ResBlock as two encdiff_resconv_fwd launches
+    (unet.RC): eps vs the CPU oracle within the bf16 bound (rel-L2 <= 3e-2, max-abs <= 6e-2) and vs
+    the unfused launches within the same rel-L2 bound (the same bf16 rounding points, different
+    summation orders: a flipped rounding grows through 28 blocks as any bf16 difference does); 56
+    fused convs (28 ResBlocks) at B = 8 / 32, and at B = 2 the
+    2x2 blocks (a 16-row tile would need four images) fall back to the unfused launches."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import encdiff_amd  # noqa: F401
+    from encdiff_amd import ops, unet as U
+    from encdiff_amd.ldm.modules.diffusionmodules.openaimodel_enc import UNetModel
+    from oracle import encdiff_oracle as O
+    m = UNetModel(**O.SHAPES3D_UNET)
+    P = O.recipe_params(O.param_shapes(O.build_plan()))
+    m.load_state_dict(P, strict=True)
+    m = m.cuda()
+    g = torch.Generator().manual_seed(100 + B)
+    x = torch.randn(B, 3, 16, 16, generator=g)
+    t = torch.randint(0, 1000, (B,), generator=g)
+    c = torch.randn(B, 320, generator=g) * 0.5
+    calls = []
+    orig = ops.resconv_fwd
+
+    def counted(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+    ops.resconv_fwd = counted
+    try:
+        with torch.no_grad():
+            U.RC = True
+            e_f = m(x.cuda(), t.cuda(), context=[c.cuda()]).cpu()
+            n_f = len(calls)
+            calls.clear()
+            U.RC = False
+            e_u = m(x.cuda(), t.cuda(), context=[c.cuda()]).cpu()
+            n_u = len(calls)
+    finally:
+        U.RC = True
+        ops.resconv_fwd = orig
+    ref = O.unet_forward(P, O.build_plan(), x, t, [c])
+    r_ref, r_unf, mab = rel(e_f, ref), rel(e_f, e_u), (e_f - ref).abs().max().item()
+    print(f"B={B}: fused ResBlocks eps rel-L2 vs oracle {r_ref:.3e} (max-abs {mab:.3e}; unfused vs oracle "
+          f"{rel(e_u, ref):.3e}), vs unfused {r_unf:.3e}; resconv launches {n_f}")
+    assert r_ref < 3e-2 and mab < 6e-2 and r_unf < 3e-2
+    # B = 2: the eight ResBlocks with a conv at 2x2 (the 4x4 -> 2x2 down block, two input, two
+    # middle and three output blocks) run unfused; the 2x2 -> 4x4 up block's convs are at 4x4
+    assert n_f == (56 if B % 4 == 0 else 56 - 16) and n_u == 0, n_f

@@ -228,8 +228,9 @@ def test_unet_gn_fin_bitwise(unet, B, train):
     ops.groupnorm_bwd = counted_b
     ops.layernorm_bwd = counted_l
 
-    agn = U.AGN
+    agn, rc = U.AGN, U.RC
     U.AGN = False  # inference at B = 8 would fold these GroupNorms into the convs (test_unet_agn_inference)
+    U.RC = False   # ... or run the ResBlocks as two fused launches (test_gpu_resconv.py)
 
     def run(on):
         U.GN_FIN = on
@@ -251,7 +252,7 @@ def test_unet_gn_fin_bitwise(unet, B, train):
         b, n_off = run(False)
     finally:
         U.GN_FIN = True
-        U.AGN = agn
+        U.AGN, U.RC = agn, rc
         ops.groupnorm_fwd, ops.groupnorm_bwd, ops.layernorm_bwd = orig, orig_b, orig_l
     print(f"B={B}: {n_on % 1000} GroupNorm forwards / {n_on // 1000} Group/LayerNorm backwards combined their "
           f"producer's slabs")
@@ -328,8 +329,9 @@ def test_unet_agn_inference(unet, B, res):
         calls.append(1)
         return orig(*a, **k)
     ops.groupnorm_fwd = counted
-    agn_res = U.AGN_RES
+    agn_res, rc = U.AGN_RES, U.RC
     U.AGN_RES = res
+    U.RC = False  # the two-launch ResBlocks would replace these convs (test_gpu_resconv.py)
     try:
         with torch.no_grad():
             U.AGN = True
@@ -341,7 +343,7 @@ def test_unet_agn_inference(unet, B, res):
             n_u = len(calls)
     finally:
         U.AGN = True
-        U.AGN_RES = agn_res
+        U.AGN_RES, U.RC = agn_res, rc
         ops.groupnorm_fwd = orig
     P = O.recipe_params(O.param_shapes(O.build_plan()))
     ref = O.unet_forward(P, O.build_plan(), x, t, [c])
