@@ -23,7 +23,11 @@
 
 namespace {
 
-constexpr int RC_THREADS = 256;
+#ifndef RC_NT
+#define RC_NT 512  // threads per workgroup (256: 648 us per UNet forward of fused convs at B = 8, 512: 617, 1024: spills)
+#endif
+constexpr int RC_THREADS = RC_NT;
+constexpr int RC_NW = RC_NT / 64;  // waves per workgroup
 constexpr int RC_PAD = 8;   // LDS row padding (bf16 elements)
 constexpr int RC_D = 8;     // k-steps per B prefetch batch
 constexpr int RC_LDS_MAX = 160 * 1024;
@@ -59,7 +63,7 @@ __device__ unsigned long long rc_stamps[4096][10];
 
 struct RcPlan {
   int ho, hwo, ipw;         // conv (output) resolution, its pixels per image, images per group
-  int mc, wk;               // 16-row tiles per workgroup (= waves along M), k-split (mc * wk == 4)
+  int mc, wk;               // 16-row tiles per workgroup (= waves along M), k-split (mc * wk == RC_NW)
   int nchunk, ngroup;       // tile chunks per group, image groups
   int ldx;                  // LDS row stride (elements)
   int nsr, ncr;             // max staged rows per image (resolution h), max conv-input rows (DOWN2)
@@ -83,7 +87,9 @@ __global__ __launch_bounds__(RC_THREADS) void resconv_kernel(const EncdiffResCon
   bf16_t* sk = (bf16_t*)(smem + q.sk_off);    // skip conv: [mc][cskip/32] A, then [TN][cskip/32] B fragments
   RC_ST_RT(0);
   RC_ST(1);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the wave index as a scalar: everything derived from it (k ranges, taps, tile rows) stays in
+  // SGPRs with scalar branches instead of exec-masked vector ones
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l16 = lane & 15, g4 = lane >> 4;
   const int G = gridDim.x, bid = blockIdx.x;
   // XCD-aware order: consecutive logical indices run on one XCD (workgroup i -> XCD i % 8), and
@@ -100,7 +106,7 @@ __global__ __launch_bounds__(RC_THREADS) void resconv_kernel(const EncdiffResCon
   const int KS2 = p.cskip >> 5;
   const int grow0 = b0 * hwo;  // first output row of the group
   const bool up = p.resample == ENCDIFF_RESAMPLE_UP2, down = p.resample == ENCDIFF_RESAMPLE_DOWN2;
-  const int wm_i = wave % q.mc, wk_i = wave / q.mc;
+  const int wm_i = wave % q.mc, wk_i = wave / q.mc;  // (wk_i < q.wk: mc * wk == RC_NW)
   const int mt = chunk * q.mc + wm_i;
   const int np = RC_THREADS / nv, tv = tid % nv, tp = tid / nv;
   const int cpg = cin / p.groups;
@@ -110,14 +116,14 @@ __global__ __launch_bounds__(RC_THREADS) void resconv_kernel(const EncdiffResCon
   // lane-linear), the affine parameters of this thread's channels and the epilogue's bias /
   // residual values into registers; the staging loads follow ----
   if (!(p.skip_stages & 20)) {
-    for (int f = wave; f < q.kl * TN; f += 4) {
+    for (int f = wave; f < q.kl * TN; f += RC_NW) {
       const int ks = f / TN, t = f - ks * TN;
       const bf16_t* src = (const bf16_t*)p.w + (long)(n0 + t * 16 + l16) * p.ld_w + ks * 32 + g4 * 8;
       __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(bs + f * 512), 16, 0, 0);
     }
   }
   if (KS2) {
-    for (int f = wave; f < (q.mc + TN) * KS2; f += 4) {
+    for (int f = wave; f < (q.mc + TN) * KS2; f += RC_NW) {
       const int u = f / KS2, ks = f - u * KS2;
       const bf16_t* src = u < q.mc
           ? (const bf16_t*)p.xskip + (long)(grow0 + (chunk * q.mc + u) * 16 + l16) * p.ld_xskip + ks * 32 + g4 * 8
@@ -275,20 +281,33 @@ __global__ __launch_bounds__(RC_THREADS) void resconv_kernel(const EncdiffResCon
       const float var = fmaxf(b * inv_n - mean * mean, 0.f);
       gst[e] = make_float2(mean, rsqrtf(var + p.eps));
     }
-  } else {
-    if (tp < lpi * ipw) {
+  } else {  // (host: one image per group) lanes l, l + nv, l + 2 nv of a wave share a channel vector
+    float* rs = red + wave * cin;
+    float* rq = red + (RC_NW + wave) * cin;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float a = s[i], b = ss[i];
+      for (int k = 1; k * nv < 64; ++k) {
+        const int src = lane + k * nv;
+        const float ta = __shfl(s[i], src < 64 ? src : lane, 64), tb = __shfl(ss[i], src < 64 ? src : lane, 64);
+        if (src < 64) { a += ta; b += tb; }
+      }
+      s[i] = a;
+      ss[i] = b;
+    }
+    if (lane < nv) {  // the wave's first nv lanes cover every channel vector once (zeros past np)
+      const int c0 = ((wave * 64 + lane) % nv) * 8;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        red[tp * cin + tv * 8 + i] = s[i];
-        red[(ipw * lpi + tp) * cin + tv * 8 + i] = ss[i];
+        rs[c0 + i] = s[i];
+        rq[c0 + i] = ss[i];
       }
     }
     __syncthreads();
-    for (int e = tid; e < ipw * cin; e += RC_THREADS) {  // (image, channel): its lanes in order
-      const int jj = e / cin, c = e - jj * cin;
+    for (int e = tid; e < cin; e += RC_THREADS) {  // channel: the waves' rows in order
       float a = 0.f, b = 0.f;
 #pragma unroll 4
-      for (int r = jj * lpi; r < (jj + 1) * lpi; ++r) { a += red[r * cin + c]; b += red[(ipw * lpi + r) * cin + c]; }
+      for (int r = 0; r < RC_NW; ++r) { a += red[r * cin + e]; b += red[(RC_NW + r) * cin + e]; }
       chs[e] = make_float2(a, b);
     }
     __syncthreads();
@@ -311,39 +330,37 @@ __global__ __launch_bounds__(RC_THREADS) void resconv_kernel(const EncdiffResCon
   const int ncr = cy1 - cy0 + 1, pis = q.ncr * ho * q.ldx;
   if (!(p.skip_stages & 2)) {
     const bool silu = p.silu;
-    if (tp < np) {
-      for (int jj = 0; jj < ipw; ++jj) {
-        float mul[8], add[8];
+    if (tp < lpi * ipw) {  // thread = (image j, channel vector tv, pixel lane l), as in the staging
+      float mul[8], add[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {  // y = ((x - m) r ga + be)(1 + sc) + sh
-          const float2 st = gst[jj * p.groups + (tv * 8 + i) / cpg];
-          float a = st.y * ng[i], bb = nb[i] - st.x * a;
-          if (p.film) {
-            const float sc = fl[jj * 2 * cin + tv * 8 + i], sf = fl[jj * 2 * cin + cin + tv * 8 + i];
-            a *= (1.f + sc);
-            bb = bb * (1.f + sc) + sf;
-          }
-          mul[i] = a;
-          add[i] = bb;
+      for (int i = 0; i < 8; ++i) {  // y = ((x - m) r ga + be)(1 + sc) + sh
+        const float2 st = gst[j * p.groups + (tv * 8 + i) / cpg];
+        float a = st.y * ng[i], bb = nb[i] - st.x * a;
+        if (p.film) {
+          const float sc = fl[j * 2 * cin + tv * 8 + i], sf = fl[j * 2 * cin + cin + tv * 8 + i];
+          a *= (1.f + sc);
+          bb = bb * (1.f + sc) + sf;
         }
-        bf16_t* base = xs + jj * xis + tv * 8;
-        for (int pl = tp; pl < npx; pl += 4 * np) {  // four rows' reads issued before any math
-          uint4 u[4];
+        mul[i] = a;
+        add[i] = bb;
+      }
+      bf16_t* base = xs + j * xis + tv * 8;
+      for (int pl = l; pl < npx; pl += 4 * lpi) {  // four rows' reads issued before any math
+        uint4 u[4];
 #pragma unroll
-          for (int d = 0; d < 4; ++d)
-            if (pl + d * np < npx) u[d] = *(const uint4*)(base + (pl + d * np) * q.ldx);
+        for (int d = 0; d < 4; ++d)
+          if (pl + d * lpi < npx) u[d] = *(const uint4*)(base + (pl + d * lpi) * q.ldx);
 #pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            if (pl + d * np < npx) {
-              float v[8];
-              unpack8(u[d], v);
+        for (int d = 0; d < 4; ++d) {
+          if (pl + d * lpi < npx) {
+            float v[8];
+            unpack8(u[d], v);
 #pragma unroll
-              for (int i = 0; i < 8; ++i) {
-                const float z = v[i] * mul[i] + add[i];
-                v[i] = silu ? silu_f(z) : z;
-              }
-              *(uint4*)(base + (pl + d * np) * q.ldx) = pack8(v);
+            for (int i = 0; i < 8; ++i) {
+              const float z = v[i] * mul[i] + add[i];
+              v[i] = silu ? silu_f(z) : z;
             }
+            *(uint4*)(base + (pl + d * lpi) * q.ldx) = pack8(v);
           }
         }
       }
@@ -533,6 +550,7 @@ int rc_plan(const EncdiffResConvArgs& a, RcPlan& q, int& tn) {
   if (a.batch % q.ipw) return ENCDIFF_ERR_UNSUPPORTED;
   const int nv = a.cin / 8, np = RC_THREADS / nv;
   if (np < q.ipw || q.ipw * a.cin > RC_CE * RC_THREADS) return ENCDIFF_ERR_UNSUPPORTED;
+  if ((nv & (nv - 1)) && q.ipw != 1) return ENCDIFF_ERR_UNSUPPORTED;  // non-power-of-two statistics path
   tn = a.tile_n ? a.tile_n : 1;
   if ((tn != 1 && tn != 2) || a.cout % (16 * tn)) return ENCDIFF_ERR_ARG;
   const int mtg = q.ipw * q.hwo / 16, nslice = a.cout / (16 * tn);
@@ -544,7 +562,7 @@ int rc_plan(const EncdiffResConvArgs& a, RcPlan& q, int& tn) {
     q.mc = mtg >= 4 ? 4 : mtg >= 2 ? 2 : 1;
     while (q.mc > 1 && q.ngroup * (mtg / q.mc) * nslice < 128) q.mc >>= 1;
   }
-  q.wk = 4 / q.mc;
+  q.wk = RC_NW / q.mc;
   q.nchunk = mtg / q.mc;
   q.ldx = a.cin + RC_PAD;
   // the largest row window of any chunk (kernel: cy0 / cy1 / sy0 / sy1)
@@ -565,7 +583,7 @@ int rc_plan(const EncdiffResConvArgs& a, RcPlan& q, int& tn) {
   auto take = [&](long bytes) { const int o = off; off += (int)((bytes + 15) & ~15L); return o; };
   q.xs_off = take((long)q.ipw * q.nsr * a.h * q.ldx * 2);
   q.ps_off = a.resample == ENCDIFF_RESAMPLE_DOWN2 ? take((long)q.ipw * q.ncr * q.ho * q.ldx * 2) : q.xs_off;
-  const long red_f = 2L * np * a.cin, kred_f = 3L * 2 * tn * 256;
+  const long red_f = (nv & (nv - 1)) ? 2L * RC_NW * a.cin : 2L * 16 * 64, kred_f = (q.wk - 1L) * q.mc * 2 * tn * 256;
   q.red_off = take(4 * (red_f > kred_f ? red_f : kred_f));
   q.chs_off = take((nv & (nv - 1)) ? 8L * q.ipw * a.cin : 0);
   q.gst_off = take(8L * q.ipw * a.groups);
@@ -575,6 +593,7 @@ int rc_plan(const EncdiffResConvArgs& a, RcPlan& q, int& tn) {
   q.bs_off = off;
   const int ks = 9 * a.cin / 32, room = (RC_LDS_MAX - off) / (1024 * tn);
   q.kl = room < 0 ? 0 : (room < ks ? room & ~1 : ks);
+  if (a.skip_stages & 64) q.kl = 0;  // timing experiments: every B fragment streamed from L2
   q.lds = off + q.kl * tn * 1024;
   if (q.lds > RC_LDS_MAX) return ENCDIFF_ERR_UNSUPPORTED;
   return ENCDIFF_OK;
