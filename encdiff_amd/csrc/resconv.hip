@@ -558,9 +558,10 @@ int rc_plan(const EncdiffResConvArgs& a, RcPlan& q, int& tn) {
   if (a.tile_m) {
     if ((a.tile_m != 1 && a.tile_m != 2 && a.tile_m != 4) || mtg % a.tile_m) return ENCDIFF_ERR_ARG;
     q.mc = a.tile_m;
-  } else {  // up to 4 tiles per workgroup (one per wave), fewer while that leaves < 128 workgroups
+  } else {  // up to 4 tiles per workgroup, fewer while that leaves < 256 workgroups (tools/rc_bench.py
+            // --tiles at B = 8: 16x16 x 64 channels 11.6 -> 10.8 us with 2 tiles / 256 workgroups)
     q.mc = mtg >= 4 ? 4 : mtg >= 2 ? 2 : 1;
-    while (q.mc > 1 && q.ngroup * (mtg / q.mc) * nslice < 128) q.mc >>= 1;
+    while (q.mc > 1 && q.ngroup * (mtg / q.mc) * nslice < 256) q.mc >>= 1;
   }
   q.wk = RC_NW / q.mc;
   q.nchunk = mtg / q.mc;
