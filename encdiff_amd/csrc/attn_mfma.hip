@@ -458,6 +458,16 @@ __device__ __host__ inline int attn_qsplit(int ktiles, int hpb) {
 // dS^T row pitch in LDS: +16 elements (32 B) per row so the transposed reads of 8 consecutive
 // rows fall on different banks
 __device__ __host__ inline int ds_pitch(int sqp) { return sqp + 16; }
+// The chunked dS^T (dsl > 1, S = 256) is instead unpadded with its 8-byte chunks XOR-swizzled per
+// row: chunk c of row r sits at c ^ dsw(r & 15).  dsw was searched so that both the b64 stores (16
+// rows x 2 chunks per half-wave) and the transposed b64 reads (4 rows x 4 chunks x 2 lane groups)
+// hit 32 distinct bank pairs (the padded pitch left 2-way conflicts on the stores)
+ED_DEV int dsw(int r) { return ((4 * r) ^ (2 * (r >> 3))) & 63; }
+ED_DEV s4 ldtr_sw(const bf16_t* t, int ld, int r0, int c0, int l16, int g) {
+  const int r = r0 + 4 * g + (l16 >> 2);
+  const int c = ((c0 >> 2) + (l16 & 3)) ^ dsw(r & 15);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(t + r * ld + 4 * c));
+}
 
 // split: phase A (dK, dV) and phase B (dQ, scores recomputed) run in two workgroups of their own
 // (twice the workgroups per CU to hide each wave's LDS -> MFMA -> exp chains); both stage the
@@ -496,7 +506,8 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
   const int oG = QE, oK = 2 * QE, oV = oK + KE;
   const int per_head = oV + KE;
   float* fls = (float*)(sm + hpb * per_head);
-  const int DSP = ds_pitch(SQP);
+  const bool swz = dsl > 1 && (SQP & 255) == 0;  // swizzled chunked dS^T (dsw)
+  const int DSP = swz ? SQP : ds_pitch(SQP);
   bf16_t* dS = (bf16_t*)(fls + hpb * 2 * SQP);  // [hpb][SKP][DSP] when dsl
   const int qtiles = SQP >> 4, ktiles = SKP >> 4;
   const int QS = attn_qsplit(ktiles, hpb);
@@ -631,7 +642,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
           }
           const s4 pf = pack4(pv[0], pv[1], pv[2], pv[3]);
           const s4 df = pack4(ds[0], ds[1], ds[2], ds[3]);
-          *(s4*)(dS + (t * 16 + l16) * DSP + qt * 16 + 4 * g) = df;
+          *(s4*)(dS + (t * 16 + l16) * DSP + 4 * (swz ? (qt * 4 + g) ^ dsw(l16) : qt * 4 + g)) = df;
 #pragma unroll
           for (int dt = 0; dt < KC; ++dt) {
             dv[u][dt] = mma(ldtr(Gs, RP, qt * 16, dt * 16, l16, g), pf, dv[u][dt]);
@@ -670,7 +681,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const EncdiffAttnArgs p, in
         const int qt = wave + 4 * j;
         if (qt < qtiles) {
           for (int t = 0; t < nkt; ++t) {
-            const s4 df = ldtr(dS, DSP, t * 16, qt * 16, l16, g);
+            const s4 df = swz ? ldtr_sw(dS, DSP, t * 16, qt * 16, l16, g) : ldtr(dS, DSP, t * 16, qt * 16, l16, g);
 #pragma unroll
             for (int dt = 0; dt < KC; ++dt) dq[j][dt] = mma(ldtr(Ks, RP, c0 + t * 16, dt * 16, l16, g), df, dq[j][dt]);
           }
