@@ -306,7 +306,13 @@ def test_conv_halo_split_k(O, tile, split, B, H, cin, cout, mode):
     bias = torch.randn(cout, device=dev)
     cg = L.ConvGeom(batch=B, h=H, w=H, cin=cin, resample=mode, ld_src=cin)
     if not O.halo_fits(tile, B, H, H, cin, mode, split):
-        pytest.skip("window does not fit")
+        # the host mirror declines: the library must decline too (an error, no launch) -- the
+        # planner relies on the two agreeing
+        out = torch.empty(g.pixels, cout, device=dev)
+        with pytest.raises(L.HipError):
+            O.gemm(g.pixels, cout, 9 * cin, x, cin, wf, 9 * cin, out, cout, a_mode=L.OPA_IM2COL, c_mode=L.OUT_F32,
+                   conv=cg, split_k=split, tile=tile)
+        return
     xin = nhwc(x, gs)
     if mode == 2:
         xin = F.interpolate(xin, scale_factor=2, mode="nearest")
@@ -1396,11 +1402,15 @@ def test_groupnorm_x_from_rejects_mismatch(O):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("M,C,resid", [(4096, 64, True), (1024, 128, False), (8192, 128, True)])
+@pytest.mark.parametrize("M,C,resid", [(4096, 64, True), (1024, 128, False), (8192, 128, True), (128, 256, True),
+                                        (32, 256, False), (2048, 256, True)])
 def test_linear_layernorm_fused(O, M, C, resid):
     """LayerNorm in the producing GEMM's epilogue (attention.py norm1/2/3 after proj_in /
     to_out) vs the separate LayerNorm kernel: same GEMM output bitwise, normalised rows and
-    (mean, rstd) within fp32 summation-order noise, and torch fp32 within bf16 tolerance."""
+    (mean, rstd) within fp32 summation-order noise, and torch fp32 within bf16 tolerance.
+    C = 256 takes the separate LayerNorm launch in both arms (a 64x256 tile spanning the row measured
+    slower: DDIM B=8 703 -> 653 steps/s), so its GEMM output is held to the torch fp32
+    product within bf16 rounding."""
     torch.manual_seed(13)
     x = bf(M, C)
     w = bf(C, C, scale=C ** -0.5)
@@ -1419,9 +1429,15 @@ def test_linear_layernorm_fused(O, M, C, resid):
         finally:
             O.LN_FUSED = True
         res.append((out, y, st))
-    assert torch.equal(res[0][0], res[1][0])
-    assert rel(res[0][2], res[1][2]) < 1e-5
-    assert (res[0][1].float() - res[1][1].float()).abs().max().item() < 0.05
+    if C <= 128:
+        assert torch.equal(res[0][0], res[1][0])
+        assert rel(res[0][2], res[1][2]) < 1e-5
+        assert (res[0][1].float() - res[1][1].float()).abs().max().item() < 0.05
+    else:
+        prod = x.float() @ w.float().t() + b + (r.float() if r is not None else 0.)
+        assert rel(res[0][0], prod) < 1e-2 and rel(res[1][0], prod) < 1e-2
+        st_ref = torch.stack([res[0][0].float().mean(1), 1 / (res[0][0].float().var(1, unbiased=False) + 1e-5).sqrt()], 1)
+        assert rel(res[0][2], st_ref) < 1e-4
     ref = F.layer_norm(res[0][0].float(), (C,), gam, bet, 1e-5)
     assert rel(res[0][1], ref) < 1e-2
 
