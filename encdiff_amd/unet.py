@@ -71,6 +71,10 @@ AGN_FOLD = os.environ.get("ENCDIFF_AGN_FOLD", "1") != "0"  # split-K combined in
 # over whole staged images + conv + skip) instead of four to six (0: the unfused launches, A/B)
 RC = os.environ.get("ENCDIFF_RC", "1") != "0"
 RC_MAX_B = int(os.environ.get("ENCDIFF_RC_MAX_B", "32"))
+# ... for images of at most this many elements (pixels x channels): every workgroup re-reduces its
+# whole images' statistics, which at configs[4]'s 32x32 x 128+ level (1024 workgroups each reading a
+# 256 KB image) made DDIM slower than the separate GroupNorm launches (270 -> 227 steps/s)
+RC_MAX_IMG = int(os.environ.get("ENCDIFF_RC_MAX_IMG", "65536"))
 # widest level that uses it: at c = 256 one workgroup streams 2.6 MB of weights through one CU
 # (74 us at B = 8 against ~35 us for the separate launches, tools/st_tail_bench.py)
 ST_TAIL_MAXC = int(os.environ.get("ENCDIFF_ST_TAIL_MAXC", "128"))
@@ -644,6 +648,8 @@ class UNetExecutor:
         w1, w2 = self.W(pre + "in_layers.2.weight"), self.W(pre + "out_layers.3.weight")
         film = self._E_use[:, r.film_off:]
         cskip = r.cin if r.cin != r.cout else 0
+        if r.hin * r.hin * r.cin > RC_MAX_IMG or r.hout * r.hout * r.cout > RC_MAX_IMG:
+            return False
         if not (ops.resconv_supported(x, gi, w1, r.updown)
                 and ops.resconv_supported(S["h1"], go, w2, film=film, ld_film=self._E_ld, cskip=cskip)):
             return False
