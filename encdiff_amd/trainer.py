@@ -108,6 +108,8 @@ class HipTrainer:
         self._pro = ops.StepPrologue(self.dev, seed=rank_seed(seed, self.rank))
         self._pro.set_jobs([self.arena.grad])
         self._pro_final = False  # statistics slots registered after the first step
+        self._melk = False       # SIGUSR1 (install_signal_handlers): checkpoint at the step boundary
+        self._ckptdir = "."
 
     def _slots(self):
         """The UNet executor's statistics-slot registry (None before the executor exists)."""
@@ -388,6 +390,33 @@ class HipTrainer:
         if self.sched is not None:
             self.sched.step()
         self.ldm.global_step += 1
+        if self._melk:  # SIGUSR1 arrived during the step: the checkpoint at its boundary
+            self._melk = False
+            if self.rank == 0:
+                print("Summoning checkpoint.", flush=True)
+                self.save_checkpoint(os.path.join(self._ckptdir, "last.ckpt"))
+
+    def save_checkpoint(self, path: str, epoch: int = 0):
+        """The trained state as a Lightning-layout .ckpt -- {'state_dict', 'epoch', 'global_step'},
+        what ``trainer.save_checkpoint`` writes (main_val.py:845-851) and ``init_from_ckpt``
+        reads.  The module parameters and LitEma buffers are views of the parameter / EMA arenas
+        the graph-replayed optimizer updates, so this is the state after the last step."""
+        torch.cuda.synchronize()
+        sd = {k: v.detach().to("cpu", copy=True).contiguous() for k, v in self.ldm.state_dict().items()}
+        torch.save({"state_dict": sd, "epoch": int(epoch), "global_step": int(self.ldm.global_step)}, path)
+
+    def install_signal_handlers(self, ckptdir: str):
+        """main_val.py:845-862: SIGUSR1 summons a checkpoint -- rank 0 writes ``ckptdir/last.ckpt``.
+        The handler only raises a flag (the signal may land inside a graph replay); the step in
+        progress finishes and its boundary saves.  (The reference's SIGUSR2 starts a pudb session
+        on rank 0: an interactive debugger, not reproduced.)"""
+        import signal
+        self._ckptdir = ckptdir
+        os.makedirs(ckptdir, exist_ok=True)
+
+        def melk(*_):
+            self._melk = True
+        signal.signal(signal.SIGUSR1, melk)
 
     def loss(self):
         return float(self.loss_buf[0])
