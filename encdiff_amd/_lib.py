@@ -117,7 +117,8 @@ class StTailArgs(C.Structure):
                 ("save_t1", vp), ("save_n2", vp), ("save_q2", vp), ("save_o2", vp), ("save_t2", vp),
                 ("save_n3", vp), ("save_f", vp), ("save_a", vp), ("save_t3", vp), ("ld_save", C.c_long),
                 ("save_s2", vp), ("save_s3", vp), ("save_lse2", vp), ("gn_stats", vp), ("ld_gn_stats", C.c_long),
-                ("gn_stats_add", C.c_int), ("pad2_", C.c_int)]
+                ("gn_stats_add", C.c_int), ("pad2_", C.c_int), ("head_t2", vp), ("head_n3", vp),
+                ("ld_head", C.c_long)]
 
 
 class StHeadArgs(C.Structure):

@@ -333,11 +333,17 @@ __global__ __launch_bounds__(64 * NWV) void st_tail_kernel(const EncdiffStTailAr
   mma(acc, Xa, LDX, wo2, lane);
   acc_add_tr(acc, Tr, LDT, p.b_out2, n0, lane);
   __syncthreads();
-  // ---- n3 = LN3(t2)
+  // ---- n3 = LN3(t2)  (head mode: t2 / n3 to the caller's buffers, the feed-forward is theirs)
+  const bool head = p.head_n3 != nullptr;
   if (!(dbg & 4))
   ln_rows<C, R, NTH>(Tr, LDT, Xa, LDX, p.g3, p.be3, p.ln_eps, tid,
-                save ? (bf16_t*)p.save_n3 + (long)row0 * p.ld_save : nullptr, p.ld_save,
-                save ? (bf16_t*)p.save_t2 + (long)row0 * p.ld_save : nullptr, save ? p.save_s3 + 2L * row0 : nullptr);
+                save ? (bf16_t*)p.save_n3 + (long)row0 * p.ld_save
+                     : (head ? (bf16_t*)p.head_n3 + (long)row0 * p.ld_head : nullptr),
+                save ? p.ld_save : p.ld_head,
+                save ? (bf16_t*)p.save_t2 + (long)row0 * p.ld_save
+                     : (head ? (bf16_t*)p.head_t2 + (long)row0 * p.ld_head : nullptr),
+                save ? p.save_s3 + 2L * row0 : nullptr);
+  if (head) return;
   // ---- GEGLU feed-forward in 64-column chunks of the hidden a; t3 accumulates in registers
   if constexpr (!PRE) {
     load_b(wv[0], W1, p.ld_ff1, nc16, 0, lane);
@@ -469,6 +475,7 @@ __global__ __launch_bounds__(64 * NWV) void st_tail_kernel(const EncdiffStTailAr
 template <int C, int RR, int NWV>
 int launch_tail_w(const EncdiffStTailArgs& p, hipStream_t s) {
   using T = Tail<C, RR>;
+  if (p.head_n3 && (!p.head_t2 || p.save_t1 || p.gn_stats || p.ld_head % 8)) return ENCDIFF_ERR_ARG;
   if (p.rows % T::R || (T::R % p.tokens && p.tokens % T::R)) return ENCDIFF_ERR_SHAPE;
   const int nimg = T::R > p.tokens ? T::R / p.tokens : 1;
   const size_t lds = T::lds_bytes(nimg, p.n_ctx);

@@ -911,13 +911,15 @@ class StatSlots:
 
 
 def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps, save=None,
-                gn_stats=None, slots: Optional[StatSlots] = None) -> bool:
+                gn_stats=None, slots: Optional[StatSlots] = None, head=None) -> bool:
     """The row-local tail of a SpatialTransformer (attn1.to_out ... proj_out, attention.py:211-215,
     250-261) as one kernel.  w: dict of the bf16 GEMM weights / fp32 biases and LayerNorm affines
     (keys out1, b_out1, g2, be2, q2, out2, b_out2, g3, be3, ff1, b_ff1, ff2, b_ff2, po, b_po).
     save: None (inference) or a dict of the training activations (t1 n2 q2 o2 t2 n3 f a t3 s2 s3
-    lse2).  Returns False when the shape is outside the fused kernel's support (the caller issues
-    the separate launches); any other error raises."""
+    lse2).  head: None or (t2, n3) -- inference only: the kernel stops after norm3 and writes t2
+    and n3 = LN3(t2) there (bf16 rows), the feed-forward and proj_out being the caller's launches.
+    Returns False when the shape is outside the fused kernel's support (the caller issues the
+    separate launches); any other error raises."""
     a = L.StTailArgs(rows=rows, c=c, tokens=tokens, heads=heads, n_ctx=n_ctx, ln_eps=ln_eps,
                      scale=(c // heads) ** -0.5,
                      o1=_p(o1), ld_o1=_ld(o1), t0=_p(t0), ld_t0=_ld(t0), x=_p(x), ld_x=_ld(x),
@@ -932,6 +934,10 @@ def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps
         for k in ("t1", "n2", "q2", "o2", "t2", "n3", "f", "a", "t3", "s2", "s3", "lse2"):
             setattr(a, "save_" + k, _p(save[k]))
         a.ld_save = _ld(save["t1"])
+    if head is not None:
+        assert save is None and gn_stats is None
+        a.head_t2, a.head_n3, a.ld_head = _p(head[0]), _p(head[1]), _ld(head[1])
+        assert _ld(head[0]) == a.ld_head
     if gn_stats is not None:  # the next GroupNorm's producer statistics of out
         a.gn_stats, a.ld_gn_stats = _p(gn_stats), _ld(gn_stats)
         if c == 128 and rows // 64 < 256 and ST_TAIL_STATS_ADD:

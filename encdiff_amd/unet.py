@@ -80,6 +80,12 @@ RC_MAX_IMG = int(os.environ.get("ENCDIFF_RC_MAX_IMG", "65536"))
 ST_TAIL_MAXC = int(os.environ.get("ENCDIFF_ST_TAIL_MAXC", "128"))
 # ... also in the training forward, writing the activations the backward reads
 ST_TAIL_TRAIN = os.environ.get("ENCDIFF_ST_TAIL_TRAIN", "1") != "0"
+# inference, wider blocks (ST_TAIL_MAXC < c <= ST_TAIL_HEAD_MAXC) at sampling batches: the fused
+# tail up to norm3 (t2, n3 written), the feed-forward and proj_out as GEMM launches -- one workgroup
+# per row tile streaming the 1.5 MB feed-forward weights is what makes the whole tail slow there
+ST_TAIL_HEAD = os.environ.get("ENCDIFF_ST_TAIL_HEAD", "1") != "0"
+ST_TAIL_HEAD_MAXC = int(os.environ.get("ENCDIFF_ST_TAIL_HEAD_MAXC", "256"))
+ST_TAIL_HEAD_MAX_B = int(os.environ.get("ENCDIFF_ST_TAIL_HEAD_MAX_B", "32"))
 
 
 # --------------------------------------------------------------------------- spec
@@ -767,6 +773,11 @@ class UNetExecutor:
                                s.heads, self.lu, LN_EPS, save=save, gn_stats=self._gst(S["out"]),
                                slots=self.stat_slots):
                 return S["out"]
+        if (ST_TAIL_FUSED and ST_TAIL_HEAD and self.infer and ST_TAIL_MAXC < c <= ST_TAIL_HEAD_MAXC
+                and B <= ST_TAIL_HEAD_MAX_B
+                and ops.st_tail_fwd(S["o1"], S["t0"], x, k2, v2, self._tail_weights(s), S["out"], B * ntok, c,
+                                    ntok, s.heads, self.lu, LN_EPS, head=(S["t2"], S["n3"]))):
+            return self._st_ff(s, x, S)
         # cross-attention to the concept tokens (norm2 in the to_out epilogue, or at inference for
         # wide blocks in to_q's A staging)
         if lna:
@@ -784,6 +795,11 @@ class UNetExecutor:
         ops.linear_fwd_ln(S["o2"], self.W(tb + "attn2.to_out.0.weight"), S["t2"], self.P(tb + "norm3.weight"),
                           self.P(tb + "norm3.bias"), S["n3"], S["s3"], LN_EPS,
                           bias=self.P(tb + "attn2.to_out.0.bias"), resid=S["t1"])
+        return self._st_ff(s, x, S)
+
+    def _st_ff(self, s: STSpec, x, S):
+        """attention.py:215 + :260-261: the GEGLU feed-forward from n3 (residual t2), proj_out."""
+        tb = s.prefix + "transformer_blocks.0."
         ops.linear_fwd_geglu(S["n3"], self.W(tb + "ff.net.0.proj.weight"), S["f"], S["a"],
                              bias=self.P(tb + "ff.net.0.proj.bias"))
         ops.linear_fwd(S["a"], self.W(tb + "ff.net.2.weight"), S["t3"], bias=self.P(tb + "ff.net.2.bias"),

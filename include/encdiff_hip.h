@@ -628,6 +628,11 @@ typedef struct EncdiffStTailArgs {
                                          same bits in either order) -- twice the workgroups when a
                                          64-row tile would leave CUs idle; 0: written by one tile */
   int pad2_;
+  void* head_t2; void* head_n3; long ld_head;  /* optional (inference, no saves): stop after norm3 --
+                                         t2 and n3 = LN3(t2) written here (bf16 rows); the
+                                         feed-forward and proj_out are the caller's launches (c = 256
+                                         at sampling batches, where one workgroup streaming the
+                                         feed-forward's 1.5 MB of weights is the slow part) */
 } EncdiffStTailArgs;
 
 int encdiff_st_tail_fwd(const EncdiffStTailArgs* args, void* stream);

@@ -415,3 +415,48 @@ def test_st_tail_fused_inference(unet, golden_dir):
         ops.st_head_fwd = orig_head
         U.ST_TAIL_FUSED = True
         U.ST_TAIL_MAXC = maxc
+
+
+@pytest.mark.parametrize("B", [4, 8])
+def test_st_tail_head_mode_inference(unet, golden_dir, B):
+    """Inference at sampling batches runs the c = 256 SpatialTransformers' tail up to norm3 as one
+    kernel (encdiff_st_tail_fwd with head = (t2, n3)) and the feed-forward / proj_out as GEMM
+    launches.  Every c = 256 block must take that path, and the output must match the reference
+    (fixture at B=4, oracle at B=8) and the all-separate-launch path within the fused tail's bound."""
+    from encdiff_amd import ops, unet as U
+    from oracle import encdiff_oracle as O
+    fx = np.load(os.path.join(golden_dir, "unet_b4.npz"))
+    modes = []
+    orig = ops.st_tail_fwd
+
+    def counted(*a, **k):
+        ok = orig(*a, **k)
+        modes.append((a[8], k.get("head") is not None, ok))
+        return ok
+    ops.st_tail_fwd = counted
+    try:
+        if B == 4:
+            x, t, ctx = (torch.tensor(fx[k]).cuda() for k in ("x", "t", "ctx"))
+        else:
+            g = torch.Generator().manual_seed(7)
+            x = torch.randn(B, 3, 16, 16, generator=g).cuda()
+            t = torch.randint(0, 1000, (B,), generator=g).cuda()
+            ctx = (torch.randn(B, 320, generator=g) * 0.5).cuda()
+        with torch.no_grad():
+            U.ST_TAIL_HEAD = True
+            e_h = unet(x, t, context=[ctx]).float().cpu()
+            got = list(modes)
+            U.ST_TAIL_HEAD = False
+            e_u = unet(x, t, context=[ctx]).float().cpu()
+        head = [m for m in got if m[1]]
+        assert len(head) == 6 and all(m[0] == 256 and m[2] for m in head), got
+        ref = torch.tensor(fx["eps"]) if B == 4 else O.unet_forward(
+            O.recipe_params(O.param_shapes(O.build_plan())), O.build_plan(), x.cpu(), t.cpu(), [ctx.cpu()])
+        r_ref, r_unf = rel(e_h, ref), rel(e_h, e_u)
+        mab = (e_h - ref).abs().max().item()
+        print(f"B={B}: head-mode tail eps rel-L2 vs reference {r_ref:.3e} (max-abs {mab:.3e}), vs separate {r_unf:.3e}")
+        assert r_ref < EPS_TOL and mab < 6e-2
+        assert r_unf < EPS_TOL
+    finally:
+        ops.st_tail_fwd = orig
+        U.ST_TAIL_HEAD = True

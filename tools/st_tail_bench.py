@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--eager", action="store_true", help="5 eager launches per case (PMC runs), no timing")
     ap.add_argument("--only", type=int, default=0, help="only this channel count")
+    ap.add_argument("--head", action="store_true", help="head mode: stop after norm3 (t2, n3 written)")
     a = ap.parse_args()
     from encdiff_amd import _lib as L
     from encdiff_amd import ops
@@ -37,6 +38,7 @@ def main():
             w[k] = torch.zeros(8 * c if k == "b_ff1" else c, device=dev)
         w["g2"] = torch.ones(c, device=dev)
         w["g3"] = torch.ones(c, device=dev)
+        head = (torch.empty(rows, c, device=dev, dtype=bf), torch.empty(rows, c, device=dev, dtype=bf)) if a.head else None
         for dbg in ((0,) if a.eager else (0, 1, 2, 4, 7, 8, 15)):
             orig = L.lib.encdiff_st_tail_fwd
 
@@ -45,7 +47,8 @@ def main():
                 return orig(argp, s)
             L.lib.encdiff_st_tail_fwd = f
             try:
-                run = lambda: ops.st_tail_fwd(o1, t0, x, kv[:, :c], kv[:, c:], w, out, rows, c, hw, 8, 20, 1e-5)  # noqa
+                run = lambda: ops.st_tail_fwd(o1, t0, x, kv[:, :c], kv[:, c:], w, out, rows, c, hw, 8, 20, 1e-5,  # noqa
+                                                 head=head)
                 run()
                 if a.eager:
                     for _ in range(5):
