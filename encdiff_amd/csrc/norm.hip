@@ -569,12 +569,19 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
     load8f(p.film + (long)L.b * p.ld_film + p.c + L.cb, sf);
   }
   const float* st = p.stats + ((long)L.b * p.groups) * 2;
+  // z = xhat * zg + zb (gamma and the FiLM scale folded), xhat = x * xr + xo; pass 2's dn * gamma =
+  // dz * sg
+  float zg[8], zb[8], xo[8], sg[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int g = (L.cb + i) / L.cpg;
     xm[i] = st[2 * g]; xr[i] = st[2 * g + 1];
     sc1[i] = film ? 1.f + sc1[i] : 1.f;
     sf[i] = film ? sf[i] : 0.f;
+    zg[i] = ga[i] * sc1[i];
+    zb[i] = be[i] * sc1[i] + sf[i];
+    xo[i] = -xm[i] * xr[i];
+    sg[i] = sc1[i] * ga[i];
   }
   // the slice's gamma for the group terms: loaded now into registers, stored to LDS after pass 1
   // (a store here would wait for the load before pass 1 issues its own)
@@ -598,12 +605,16 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   // the SiLU gradient.  (Issuing these loads ahead of the per-channel constants measured no gain.)
   constexpr bool CACHE = !SLAB;
   const bool one = CACHE && HW <= U1 * L.np;
-  float cdn[U1][8], cxh[U1][8];
+  float cdz[U1][8], cxh[U1][8];
   uint4 gr0[U1];
-  // pass 1: per-channel sums of dn, dn*xhat, dz, dz*n
-  float acc[4][8];
+  // pass 1: per-channel sums of dz and dz*xhat -- the four the backward needs follow from them per
+  // channel (dn = dz * s with s = 1 + FiLM scale constant over the image, n = xhat * gamma + beta):
+  // sum dn = s sum dz, sum dn*xhat = s sum dz*xhat, sum dz*n = gamma sum dz*xhat + beta sum dz.
+  // (Four accumulators cost pass 1 three more VALU ops per element and the reduction twice the
+  // shuffles / LDS rows; pass 1 is VALU-bound.)
+  float acc[2][8];
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
+  for (int k = 0; k < 2; ++k)
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[k][i] = 0.f;
   auto row1 = [&](const uint4 ux, const uint4 ud, const int u, const bool keep) {
@@ -612,14 +623,11 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
     unpack8(ud, d);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float xh = (v[i] - xm[i]) * xr[i];
-      const float n = xh * ga[i] + be[i];
-      const float z = n * sc1[i] + sf[i];
+      const float xh = v[i] * xr[i] + xo[i];
+      const float z = xh * zg[i] + zb[i];
       const float dz = silu ? d[i] * silu_grad(z) : d[i];
-      const float dn = dz * sc1[i];
-      acc[0][i] += dn; acc[1][i] += dn * xh;
-      acc[2][i] += dz; acc[3][i] += dz * n;
-      if (keep) { cdn[u][i] = dn; cxh[u][i] = xh; }
+      acc[0][i] += dz; acc[1][i] += dz * xh;
+      if (keep) { cdz[u][i] = dz; cxh[u][i] = xh; }
     }
   };
   if (L.active) {
@@ -673,7 +681,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
     if (cl < L.cs) gam_sh[cl] = gam_r[j];
   }
   GN_STAMP(3);
-  slice_reduce<4>(acc, L, red, chs);
+  slice_reduce<2>(acc, L, red, chs);
   GN_STAMP(4);
   // per-channel outputs + gamma-weighted sums for the group terms.  (Threads owning a whole group
   // -- channel totals, partials and group terms behind ONE barrier -- measured slower: +0.3 us at
@@ -682,14 +690,17 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   for (int cl = threadIdx.x; cl < L.cs; cl += GN_THREADS) {
     const int c = L.c0 + cl;
     const float gam = gam_sh[cl];
-    p.dbeta_part[(long)L.b * p.ld_part + c] = chs[cl];
-    p.dgamma_part[(long)L.b * p.ld_part + c] = chs[L.cs + cl];
+    const float sdz = chs[cl], sdzx = chs[L.cs + cl];
+    const float s = film ? 1.f + p.film[(long)L.b * p.ld_film + c] : 1.f;
+    const float sdn = s * sdz, sdnx = s * sdzx;
+    p.dbeta_part[(long)L.b * p.ld_part + c] = sdn;
+    p.dgamma_part[(long)L.b * p.ld_part + c] = sdnx;
     if (film) {
-      p.dfilm[(long)L.b * p.ld_dfilm + c] = chs[3 * L.cs + cl];         // d scale = sum dz * n
-      p.dfilm[(long)L.b * p.ld_dfilm + p.c + c] = chs[2 * L.cs + cl];   // d shift = sum dz
+      p.dfilm[(long)L.b * p.ld_dfilm + c] = gam * sdzx + p.beta[c] * sdz;  // d scale = sum dz * n
+      p.dfilm[(long)L.b * p.ld_dfilm + p.c + c] = sdz;                    // d shift = sum dz
     }
-    gch[cl] = gam * chs[cl];
-    gch[L.cs + cl] = gam * chs[L.cs + cl];
+    gch[cl] = gam * sdn;
+    gch[L.cs + cl] = gam * sdnx;
   }
   __syncthreads();
   // group sums by one thread per group (a per-thread sum over the group's channels instead, with no
@@ -713,7 +724,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
     m1[i] = gsh[g]; m2[i] = gsh[64 + g];
   }
   GN_STAMP(5);
-  auto out_row = [&](const int px, const uint4 g, const float (&dn)[8], const float (&xh)[8]) {
+  auto out_row = [&](const int px, const uint4 g, const float (&dz)[8], const float (&xh)[8]) {
     float o[8];
     if (RES && accum) {  // both: dx (in place) + resid
       float rr[8];
@@ -726,7 +737,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float r = xr[i] * (dn[i] * ga[i] - m1[i] - xh[i] * m2[i]);
+      const float r = xr[i] * (dz[i] * sg[i] - m1[i] - xh[i] * m2[i]);
       o[i] = (accum || RES) ? o[i] + r : r;
     }
     if constexpr (RS) {
@@ -745,7 +756,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
 #pragma unroll
     for (int u = 0; u < U1; ++u) {
       const int px = L.tp + u * L.np;
-      if (px < HW) out_row(px, gr0[u], cdn[u], cxh[u]);
+      if (px < HW) out_row(px, gr0[u], cdz[u], cxh[u]);
     }
   } else {
     // U rows per thread: the global (resid / accumulate) reads of all U are issued before the
@@ -766,18 +777,16 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
       for (int u = 0; u < U; ++u) {
         const int px = px0 + u * L.np;
         if (px >= HW) break;
-        float v[8], d[8], dn[8], xh[8];
+        float v[8], d[8], dz[8], xh[8];
         unpack8(gn_row(L, tx, X, p.ldx, px), v);
         unpack8(RS && dyrs && !L.tiled ? dy_row(px) : gn_row(L, td, DY, p.lddy, px), d);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          xh[i] = (v[i] - xm[i]) * xr[i];
-          const float n = xh[i] * ga[i] + be[i];
-          const float z = n * sc1[i] + sf[i];
-          const float dz = silu ? d[i] * silu_grad(z) : d[i];
-          dn[i] = dz * sc1[i];
+          xh[i] = v[i] * xr[i] + xo[i];
+          const float z = xh[i] * zg[i] + zb[i];
+          dz[i] = silu ? d[i] * silu_grad(z) : d[i];
         }
-        out_row(px, gr[u], dn, xh);
+        out_row(px, gr[u], dz, xh);
       }
     }
   }
