@@ -19,6 +19,9 @@ namespace {
 #ifndef ED_GN_SLAB_U
 #define ED_GN_SLAB_U 1  // backward, dy from slabs: rows per load batch
 #endif
+#ifndef ED_LN_BWD_U
+#define ED_LN_BWD_U 2  // LayerNorm backward rows per thread in flight (4 measured slower: 9.09 -> 9.11 ms/step)
+#endif
 #ifndef ED_GN_BWD_U
 #define ED_GN_BWD_U 4  // backward rows per load batch (code size vs loads in flight)
 #endif
@@ -837,9 +840,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const EncdiffLayerNormArgs 
   float ga[8], dga[8], dbe[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) { ga[i] = p.gamma[lr * 8 + i]; dga[i] = 0.f; dbe[i] = 0.f; }
-  // two rows per thread in flight: every load of both is issued before either's store (the
-  // stores to dx may alias the loaded tensors, so the compiler would not hoist them itself)
-  constexpr int U = 2;
+  // U rows per thread in flight: every load of all U is issued before any store (the stores to
+  // dx may alias the loaded tensors, so the compiler would not hoist them itself).  (4 -- one load
+  // round trip for the step's c = 64 calls instead of two -- measured slower: 256+ VGPRs)
+  constexpr int U = ED_LN_BWD_U;
   const int stride = gridDim.x * RPB;
   for (int row0 = blockIdx.x * RPB + rr; row0 < p.rows; row0 += U * stride) {
     float v[U][8], d[U][8], o8[U][8], mean[U], rstd[U];
