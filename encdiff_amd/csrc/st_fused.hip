@@ -495,6 +495,11 @@ int launch_tail(const EncdiffStTailArgs& p, hipStream_t s) {
   if constexpr (C == 128) {
     if (p.rows / RR < 256) return launch_tail_w<C, RR, 8>(p, s);
   }
+  // head mode at c = 256, sampling batches (8 - 128 rows): 8 waves stream the three projections'
+  // weights (tools/st_tail_bench.py --head, B=8 4x4: 20.1 -> 18.7 us)
+  if constexpr (C == 256 && RR == 16) {
+    if (p.head_n3 && p.rows / RR < 256) return launch_tail_w<C, RR, 8>(p, s);
+  }
   return launch_tail_w<C, RR, 4>(p, s);
 }
 
@@ -502,9 +507,14 @@ int launch_tail(const EncdiffStTailArgs& p, hipStream_t s) {
 // ---------------------------------------------------------------------------------------------
 // The head: gn = GroupNorm(x) (from producer segment sums) or read, t0 = proj_in(gn) + b,
 // n1 = LN1(t0), qkv = n1 Wqkv^T -- row-local once the GroupNorm statistics are known.
-template <int C, int RR>
-__global__ __launch_bounds__(256) void st_head_kernel(const EncdiffStHeadArgs p) {
-  constexpr int R = RR, TM = R / 16, NT = C / 64, NT3 = 3 * C / 64, LDT = C + 4, LDX = C + 8, LDQ = 3 * C + 8;
+// NWV waves, each owning C / NWV columns of proj_in and of each of the q / k / v column blocks.
+// c <= 128 (4 waves): every weight fragment is loaded up front (registers); c = 256 (8 waves,
+// sampling tiles of 16 rows): the q / k / v blocks' fragments stream one block ahead.
+template <int C, int RR, int NWV>
+__global__ __launch_bounds__(64 * NWV) void st_head_kernel(const EncdiffStHeadArgs p) {
+  constexpr int NTH = 64 * NWV;
+  constexpr int R = RR, TM = R / 16, NT = C / (16 * NWV), LDT = C + 4, LDX = C + 8, LDQ = 3 * C + 8;
+  constexpr bool PRE = C <= 128;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   float* Tr = (float*)smem_raw;
   bf16_t* Xa = (bf16_t*)(Tr + R * LDT);
@@ -514,17 +524,20 @@ __global__ __launch_bounds__(256) void st_head_kernel(const EncdiffStHeadArgs p)
   const int row0 = blockIdx.x * R;
   const int img0 = row0 / p.tokens;
   const int nimg = R > p.tokens ? R / p.tokens : 1;
-  const int n0 = wave * (C / 4), n03 = wave * (3 * C / 4);
+  const int n0 = wave * (C / NWV);
   BFrags<NT, C> win;
-  BFrags<NT3, C> wq;
+  BFrags<NT, C> wq[PRE ? 3 : 2];
   load_b(win, (const bf16_t*)p.w_in, p.ld_in, n0, 0, lane);
-  load_b(wq, (const bf16_t*)p.w_qkv, p.ld_w_qkv, n03, 0, lane);
+  if constexpr (PRE) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) load_b(wq[j], (const bf16_t*)p.w_qkv, p.ld_w_qkv, j * C + n0, 0, lane);
+  }
   constexpr int CH = C / 8;
   if (!p.gn_in_stats && !p.gn) {
     // inference: the statistics of the tile's images from x itself (per channel sum / sum of
     // squares over the image's tokens, thread = (8-channel vector, token lane), lanes and the
     // group's channels added in order), then the same apply as below
-    constexpr int cpg = C / 32, NP = 256 / CH;
+    constexpr int cpg = C / 32, NP = NTH / CH;
     float* red = gms + nimg * 64;  // [2][NP][C] scratch behind the statistics (launch_head sizes it)
     const int tv = tid % CH, tp = tid / CH;
     for (int i = 0; i < nimg; ++i) {
@@ -594,7 +607,7 @@ __global__ __launch_bounds__(256) void st_head_kernel(const EncdiffStHeadArgs p)
     constexpr int cpg = C / 32;
     const bf16_t* xg = (const bf16_t*)p.x + (long)row0 * p.ld_x;
     bf16_t* gg = p.gn ? (bf16_t*)p.gn + (long)row0 * p.ld_gn : nullptr;
-    for (int e = tid; e < R * CH; e += 256) {
+    for (int e = tid; e < R * CH; e += NTH) {
       const int r = e / CH, c8 = (e - r * CH) * 8, i = (row0 + r) / p.tokens - img0;
       float v[8];
       unpack8(*(const uint4*)(xg + (long)r * p.ld_x + c8), v);
@@ -609,13 +622,14 @@ __global__ __launch_bounds__(256) void st_head_kernel(const EncdiffStHeadArgs p)
       if (gg) *(uint4*)(gg + (long)r * p.ld_gn + c8) = y;
     }
   } else {
-    rows_to_lds<C, R>(Xa, LDX, (const bf16_t*)p.gn + (long)row0 * p.ld_gn, p.ld_gn, tid);
+    rows_to_lds<C, R, NTH>(Xa, LDX, (const bf16_t*)p.gn + (long)row0 * p.ld_gn, p.ld_gn, tid);
   }
   __syncthreads();
   // ---- t0 = gn Win^T + b  (fp32 stream in Tr, bf16 t0 out)
   v4f acc[TM][NT];
   zero(acc);
   mma(acc, Xa, LDX, win, lane);
+  if constexpr (!PRE) load_b(wq[0], (const bf16_t*)p.w_qkv, p.ld_w_qkv, n0, 0, lane);  // q block in flight
   {
     const int l16 = lane & 15, g4 = lane >> 4;
 #pragma unroll
@@ -630,11 +644,12 @@ __global__ __launch_bounds__(256) void st_head_kernel(const EncdiffStHeadArgs p)
   }
   __syncthreads();
   // ---- n1 = LN1(t0) -> Xa (t0 saved as its bf16 rounding, which the LayerNorm reads)
-  ln_rows<C, R>(Tr, LDT, Xa, LDX, p.g1, p.be1, p.ln_eps, tid, p.n1 ? (bf16_t*)p.n1 + (long)row0 * p.ld_n1 : nullptr,
-                p.ld_n1, p.n1 ? (bf16_t*)p.t0 + (long)row0 * p.ld_t0 : nullptr, p.s1 ? p.s1 + 2L * row0 : nullptr);
+  ln_rows<C, R, NTH>(Tr, LDT, Xa, LDX, p.g1, p.be1, p.ln_eps, tid,
+                     p.n1 ? (bf16_t*)p.n1 + (long)row0 * p.ld_n1 : nullptr, p.ld_n1,
+                     p.n1 ? (bf16_t*)p.t0 + (long)row0 * p.ld_t0 : nullptr, p.s1 ? p.s1 + 2L * row0 : nullptr);
   if (!p.n1) {  // inference: t0 is still the tail's residual input
     bf16_t* tg = (bf16_t*)p.t0 + (long)row0 * p.ld_t0;
-    for (int e = tid; e < R * CH; e += 256) {
+    for (int e = tid; e < R * CH; e += NTH) {
       const int r = e / CH, c8 = (e - r * CH) * 8;
       float f[8];
 #pragma unroll
@@ -643,28 +658,34 @@ __global__ __launch_bounds__(256) void st_head_kernel(const EncdiffStHeadArgs p)
     }
   }
   __syncthreads();
-  // ---- qkv = n1 Wqkv^T  (staged through LDS for 16-byte stores)
-  v4f aq[TM][NT3];
-  zero(aq);
-  mma(aq, Xa, LDX, wq, lane);
-  acc_store_bf(aq, Xq, LDQ, n03, lane);
+  // ---- qkv = n1 Wqkv^T, one C-column block at a time (staged through LDS for 16-byte stores)
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if constexpr (!PRE) {
+      if (j + 1 < 3) load_b(wq[(j + 1) & 1], (const bf16_t*)p.w_qkv, p.ld_w_qkv, (j + 1) * C + n0, 0, lane);
+    }
+    v4f aq[TM][NT];
+    zero(aq);
+    mma(aq, Xa, LDX, wq[PRE ? j : (j & 1)], lane);
+    acc_store_bf(aq, Xq, LDQ, j * C + n0, lane);
+  }
   __syncthreads();
-  rows_to_global<3 * C, R>((bf16_t*)p.qkv + (long)row0 * p.ld_qkv, p.ld_qkv, Xq, LDQ, tid);
+  rows_to_global<3 * C, R, NTH>((bf16_t*)p.qkv + (long)row0 * p.ld_qkv, p.ld_qkv, Xq, LDQ, tid);
 }
 
-template <int C, int RR>
+template <int C, int RR, int NWV = 4>
 int launch_head(const EncdiffStHeadArgs& p, hipStream_t s) {
   constexpr int R = RR;
   if (p.rows % R || (R % p.tokens && p.tokens % R)) return ENCDIFF_ERR_SHAPE;
   const int nimg = R > p.tokens ? R / p.tokens : 1;
-  const bool self_stats = !p.gn_in_stats && !p.gn;  // + the statistics scratch [2][256 / (C / 8)][C] floats
+  const bool self_stats = !p.gn_in_stats && !p.gn;  // + the statistics scratch [2][NTH / (C / 8)][C] floats
   const size_t lds = (size_t)R * (C + 4) * 4 + (size_t)R * (C + 8) * 2 + (size_t)R * (3 * C + 8) * 2 + nimg * 64 * 4 +
-                     (self_stats ? 2 * 2048 * 4 : 0);
+                     (self_stats ? (size_t)64 * 64 * NWV : 0);
   if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
-  static const hipError_t attr_ok = hipFuncSetAttribute((const void*)st_head_kernel<C, RR>,
+  static const hipError_t attr_ok = hipFuncSetAttribute((const void*)st_head_kernel<C, RR, NWV>,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr_ok != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)attr_ok;
-  hipLaunchKernelGGL((st_head_kernel<C, RR>), dim3((unsigned)(p.rows / R)), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((st_head_kernel<C, RR, NWV>), dim3((unsigned)(p.rows / R)), dim3(64 * NWV), lds, s, p);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
 }
@@ -720,8 +741,11 @@ extern "C" int encdiff_st_tail_fwd(const EncdiffStTailArgs* a, void* stream) {
 extern "C" int encdiff_st_head_fwd(const EncdiffStHeadArgs* a, void* stream) {
   if (!a) return ENCDIFF_ERR_ARG;
   const EncdiffStHeadArgs& p = *a;
-  if (p.c != 64 && p.c != 128) return ENCDIFF_ERR_UNSUPPORTED;
+  if (p.c != 64 && p.c != 128 && p.c != 256) return ENCDIFF_ERR_UNSUPPORTED;
   if (p.tokens < 1 || p.rows < 1 || p.rows % p.tokens) return ENCDIFF_ERR_SHAPE;
+  // c = 256: sampling tiles only (16 rows, 8 waves streaming the weights; a 64-row tile's LDS and
+  // the training saves are not provided)
+  if (p.c == 256 && (p.rows / 16 >= 256 || p.n1)) return ENCDIFF_ERR_SHAPE;
   if (p.gn_in_stats && (p.tokens % 64 || p.ld_gn_in_stats < p.c || !p.x || !al16(p.x) || p.ld_x % 8))
     return ENCDIFF_ERR_SHAPE;
   const bool self_stats = !p.gn_in_stats && !p.gn;  // statistics from x in the kernel (no gn output)
@@ -740,5 +764,6 @@ extern "C" int encdiff_st_head_fwd(const EncdiffStHeadArgs* a, void* stream) {
   const bool big = p.rows / 64 >= 256;
   int rc = big ? (p.c == 64 ? launch_head<64, 64>(p, s) : launch_head<128, 64>(p, s)) : ENCDIFF_ERR_SHAPE;
   if (rc != ENCDIFF_ERR_SHAPE) return rc;
+  if (p.c == 256) return launch_head<256, 16, 8>(p, s);
   return p.c == 64 ? launch_head<64, 16>(p, s) : launch_head<128, 16>(p, s);
 }

@@ -86,6 +86,10 @@ ST_TAIL_TRAIN = os.environ.get("ENCDIFF_ST_TAIL_TRAIN", "1") != "0"
 ST_TAIL_HEAD = os.environ.get("ENCDIFF_ST_TAIL_HEAD", "1") != "0"
 ST_TAIL_HEAD_MAXC = int(os.environ.get("ENCDIFF_ST_TAIL_HEAD_MAXC", "256"))
 ST_TAIL_HEAD_MAX_B = int(os.environ.get("ENCDIFF_ST_TAIL_HEAD_MAX_B", "32"))
+# ... and their head (GroupNorm statistics from x, proj_in, norm1, q/k/v) as one kernel too: off by
+# default -- DDIM B=8 716 -> 705 steps/s with it (8 workgroups at the 4x4 level each stream the
+# 512 KB of proj_in + q/k/v weights; the GroupNorm + GEMM + LayerNorm + GEMM launches spread them)
+ST_HEAD_256 = os.environ.get("ENCDIFF_ST_HEAD_256", "0") != "0"
 
 
 # --------------------------------------------------------------------------- spec
@@ -730,23 +734,25 @@ class UNetExecutor:
         tb = s.prefix + "transformer_blocks.0."
         ntok = s.h * s.h
         fused = ST_TAIL_FUSED and c <= ST_TAIL_MAXC and (self.infer or ST_TAIL_TRAIN)
+        # the fused head: with the fused tail, or alone at inference for c = 256 sampling blocks
+        hfused = fused or (ST_TAIL_FUSED and ST_HEAD_256 and self.infer and c == 256 and B <= ST_TAIL_HEAD_MAX_B)
         # inference, blocks whose LayerNorms would be launches of their own (c > 128: the GEMM
         # epilogue form needs the tile to span the row): norm1 / norm2 in the consumer's A staging
         lna = self.infer and LNA_IN and 128 < c <= 1024
         in_st = self._gst(x)
         # inference at sampling batches: the fused head computes the GroupNorm statistics itself
-        self_st = fused and in_st is None and self.infer and AGN and B <= AGN_MAX_B
-        if fused and in_st is None and not self_st:  # no producer statistics: the GroupNorm kernel reduces them
+        self_st = hfused and in_st is None and self.infer and AGN and B <= AGN_MAX_B
+        if hfused and in_st is None and not self_st:  # no producer statistics: the GroupNorm kernel reduces them
             ops.groupnorm_fwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["gn"],
                               S["stg"], ST_GN_EPS, False)
         # GroupNorm (from producer statistics) + proj_in + norm1 + q/k/v as one kernel
-        if not (fused and ops.st_head_fwd(
+        if not (hfused and ops.st_head_fwd(
                 x, S["gn"], self.W(s.prefix + "proj_in.weight"), self.P(s.prefix + "proj_in.bias"),
                 self.P(tb + "norm1.weight"), self.P(tb + "norm1.bias"), self.W(s.prefix + "qkv"), S["t0"], S["qkv"],
                 B * ntok, c, ntok, ST_GN_EPS, LN_EPS, in_stats=in_st, gn_gamma=self.P(s.prefix + "norm.weight"),
                 gn_beta=self.P(s.prefix + "norm.bias"), gn_stats=None if self_st else S["stg"],
                 n1=None if self.infer else S["n1"], s1=None if self.infer else S["s1"], self_stats=self_st)):
-            if not fused or in_st is not None or self_st:
+            if not hfused or in_st is not None or self_st:
                 ops.groupnorm_fwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["gn"],
                                   S["stg"], ST_GN_EPS, False, in_stats=in_st)
             if lna:  # norm1 applied in q/k/v's A staging (no LayerNorm launch)

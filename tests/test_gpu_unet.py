@@ -312,10 +312,10 @@ def test_unet_agn_inference(unet, B, res):
     x itself, the tile normalised in LDS): eps vs the CPU oracle within the bf16 bound, vs the
     separate GroupNorm launches within the same bound (two bf16 paths with different rounding
     points), and only the three down blocks' GN1 (their conv reads the pooled output), the six c = 256
-    transformer GroupNorms
-    (the fused c <= 128 heads compute theirs in the kernel) and the output GroupNorm still launch
+    transformer GroupNorms (the fused heads compute theirs in the kernel) and the output GroupNorm
+    still launch
     encdiff_groupnorm_fwd.  res=False (the default, U.AGN_RES: measured faster for DDIM at B = 8) keeps
-    the ResBlock GroupNorm launches and folds only the ten fused transformer heads' statistics."""
+    the ResBlock GroupNorm launches and folds only the fused transformer heads' statistics."""
     from encdiff_amd import ops, unet as U
     from oracle import encdiff_oracle as O
     g = torch.Generator().manual_seed(B)
@@ -351,7 +351,10 @@ def test_unet_agn_inference(unet, B, res):
     print(f"B={B}: agn eps rel-L2 vs oracle {r_ref:.3e} (max-abs {mab:.3e}), vs GroupNorm launches {r_unf:.3e}; "
           f"groupnorm_fwd launches {n_f} (without: {n_u})")
     assert r_ref < EPS_TOL and mab < MAXABS_TOL and r_unf < EPS_TOL
-    assert n_f == (3 + 6 + 1 if res else 28 * 2 + 6 + 1) and n_u == 28 * 2 + 16 + 1
+    # the six c = 256 heads launch their GroupNorm, unless their fused 8-wave form is switched on
+    # (U.ST_HEAD_256): then only the 2x2 middle block's when its B * 4 rows do not fill 16-row tiles
+    n256 = (1 if (B * 4) % 16 else 0) if U.ST_HEAD_256 else 6
+    assert n_f == (3 + n256 + 1 if res else 28 * 2 + n256 + 1) and n_u == 28 * 2 + 16 + 1
 
 
 def test_st_tail_fused_inference(unet, golden_dir):
@@ -400,7 +403,7 @@ def test_st_tail_fused_inference(unet, golden_dir):
                 U.ST_TAIL_FUSED = False
                 e_u = unet(x, t, context=[ctx]).float().cpu()
             assert n_st == 16 and all(calls[:n_st]), calls
-            assert sum(heads) == 10, heads  # the fused head runs at c in {64, 128}
+            assert sum(heads) == 16, heads  # the fused head runs at every width (c = 256: 8-wave sampling form)
             ref = torch.tensor(fx["eps"]) if B == 4 else O.unet_forward(
                 O.recipe_params(O.param_shapes(O.build_plan())), O.build_plan(), x.cpu(), t.cpu(), [ctx.cpu()])
             r_ref, r_unf = rel(e_f, ref), rel(e_f, e_u)
@@ -419,21 +422,27 @@ def test_st_tail_fused_inference(unet, golden_dir):
 
 @pytest.mark.parametrize("B", [4, 8])
 def test_st_tail_head_mode_inference(unet, golden_dir, B):
-    """Inference at sampling batches runs the c = 256 SpatialTransformers' tail up to norm3 as one
-    kernel (encdiff_st_tail_fwd with head = (t2, n3)) and the feed-forward / proj_out as GEMM
-    launches.  Every c = 256 block must take that path, and the output must match the reference
+    """Inference at sampling batches runs the c = 256 SpatialTransformers' head (GroupNorm from x,
+    proj_in, norm1, q/k/v: encdiff_st_head_fwd, 8-wave form) and tail up to norm3 as one kernel each
+    (encdiff_st_tail_fwd with head = (t2, n3)), the feed-forward / proj_out as GEMM launches.  Every c = 256 block must take that path, and the output must match the reference
     (fixture at B=4, oracle at B=8) and the all-separate-launch path within the fused tail's bound."""
     from encdiff_amd import ops, unet as U
     from oracle import encdiff_oracle as O
     fx = np.load(os.path.join(golden_dir, "unet_b4.npz"))
-    modes = []
-    orig = ops.st_tail_fwd
+    modes, heads = [], []
+    orig, orig_head = ops.st_tail_fwd, ops.st_head_fwd
 
     def counted(*a, **k):
         ok = orig(*a, **k)
         modes.append((a[8], k.get("head") is not None, ok))
         return ok
+
+    def counted_head(*a, **k):
+        ok = orig_head(*a, **k)
+        heads.append((a[10], ok))
+        return ok
     ops.st_tail_fwd = counted
+    ops.st_head_fwd = counted_head
     try:
         if B == 4:
             x, t, ctx = (torch.tensor(fx[k]).cuda() for k in ("x", "t", "ctx"))
@@ -443,13 +452,15 @@ def test_st_tail_head_mode_inference(unet, golden_dir, B):
             t = torch.randint(0, 1000, (B,), generator=g).cuda()
             ctx = (torch.randn(B, 320, generator=g) * 0.5).cuda()
         with torch.no_grad():
-            U.ST_TAIL_HEAD = True
+            U.ST_TAIL_HEAD = U.ST_HEAD_256 = True
             e_h = unet(x, t, context=[ctx]).float().cpu()
-            got = list(modes)
-            U.ST_TAIL_HEAD = False
+            got, got_heads = list(modes), list(heads)
+            U.ST_TAIL_HEAD = U.ST_HEAD_256 = False
             e_u = unet(x, t, context=[ctx]).float().cpu()
         head = [m for m in got if m[1]]
         assert len(head) == 6 and all(m[0] == 256 and m[2] for m in head), got
+        # the c = 256 blocks' heads (GroupNorm statistics, proj_in, norm1, q/k/v) fused as well
+        assert sum(ok for c_, ok in got_heads if c_ == 256) == 6, got_heads
         ref = torch.tensor(fx["eps"]) if B == 4 else O.unet_forward(
             O.recipe_params(O.param_shapes(O.build_plan())), O.build_plan(), x.cpu(), t.cpu(), [ctx.cpu()])
         r_ref, r_unf = rel(e_h, ref), rel(e_h, e_u)
@@ -458,5 +469,5 @@ def test_st_tail_head_mode_inference(unet, golden_dir, B):
         assert r_ref < EPS_TOL and mab < 6e-2
         assert r_unf < EPS_TOL
     finally:
-        ops.st_tail_fwd = orig
-        U.ST_TAIL_HEAD = True
+        ops.st_tail_fwd, ops.st_head_fwd = orig, orig_head
+        U.ST_TAIL_HEAD = U.ST_HEAD_256 = True
