@@ -18,6 +18,10 @@
 // writes the activations its backward reads (save_*).
 #include "common.h"
 
+#ifndef ED_HEAD128_NWV
+#define ED_HEAD128_NWV 4  // waves of the c = 128 head at sampling tiles (8: DDIM 717.8 vs 716.9, no change)
+#endif
+
 namespace {
 
 template <int C, int RR>
@@ -765,5 +769,5 @@ extern "C" int encdiff_st_head_fwd(const EncdiffStHeadArgs* a, void* stream) {
   int rc = big ? (p.c == 64 ? launch_head<64, 64>(p, s) : launch_head<128, 64>(p, s)) : ENCDIFF_ERR_SHAPE;
   if (rc != ENCDIFF_ERR_SHAPE) return rc;
   if (p.c == 256) return launch_head<256, 16, 8>(p, s);
-  return p.c == 64 ? launch_head<64, 16>(p, s) : launch_head<128, 16>(p, s);
+  return p.c == 64 ? launch_head<64, 16>(p, s) : launch_head<128, 16, ED_HEAD128_NWV>(p, s);
 }
