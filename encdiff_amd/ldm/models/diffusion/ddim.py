@@ -273,11 +273,23 @@ class DDIMSampler(object):
         ex = self._hip_executor() if HOIST else None
         if ex is not None:
             ex.samp_ts, ex.samp_i = st["ts_col"], None
+        um = self._borrow(True)
         try:
             self._loop_steps(st, total, x, xn, logs, noise_n, ex)
         finally:
             if ex is not None:
                 ex.samp_ts = ex.samp_i = None
+            if um is not None:
+                um.borrow_eps = False
+
+    def _borrow(self, on):
+        """Let the HIP UNet hand its eps buffer over without a copy: each loop step consumes e_t
+        (ddim_step) before the next forward overwrites it.  Returns the UNet (None: another backbone)."""
+        um = getattr(getattr(self.model, "model", None), "diffusion_model", None)
+        if um is None or not hasattr(um, "executor"):
+            return None
+        um.borrow_eps = on
+        return um
 
     def _loop_steps(self, st, total, x, xn, logs, noise_n, ex):
         for i in range(total):
@@ -334,7 +346,12 @@ class DDIMSampler(object):
     def _step_body(self, st):
         idx = st["idx"]
         st["t"].copy_(self._ts.index_select(0, idx.long()).expand(st["t"].shape[0]))
-        e_t = self.model.apply_model(st["x"], st["t"], st["cond"])
+        um = self._borrow(True)
+        try:
+            e_t = self.model.apply_model(st["x"], st["t"], st["cond"])
+        finally:
+            if um is not None:
+                um.borrow_eps = False
         if st["noise"].shape[0] > 1:  # noise row of loop step i (device counter)
             st["zrow"].copy_(st["noise"].index_select(0, st["i"]).view_as(st["zrow"]))
             st["i"].add_(1)

@@ -222,6 +222,10 @@ class UNetModel(nn.Module):
             self._arena.attach_grads()
             return _UNetF32Fn.apply(x.float(), timesteps.long(), c, self._f32)
         ex.infer = not torch.is_grad_enabled()  # inference-only fusions (no saved activations)
+        if ex.infer and getattr(self, "borrow_eps", False):
+            # a sampler loop that consumes eps before its next call (DDIMSampler's captured loops):
+            # the executor's output buffer itself, without the copy a returned tensor needs
+            return ex.forward(x.float(), timesteps.long(), c)
         if torch.is_grad_enabled():
             self._arena.attach_grads()
         return _UNetFn.apply(x.float(), timesteps.long(), c, ex)
