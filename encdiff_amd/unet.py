@@ -327,8 +327,14 @@ class UNetExecutor:
         self._samp_tabs: Dict[tuple, dict] = {}  # (S, B) -> buffers; graphs hold their addresses
         self._wgg = ops.WgradGroup()  # the backward's grouped weight gradients (planned per batch size)
         self.stat_slots = ops.StatSlots()  # producer-statistics slots the transformer tails add into
-        self._base_names = set(self.__dict__) | {"_base_names"}
+        # names shared by every batch size; everything bind() (re)creates is per batch size and is
+        # kept in / restored from self._sets -- the GroupNorm partials (rows = B) included: excluded
+        # from the shared names although declared above, else a switch back to a larger batch kept
+        # the smaller batch's partial rows and its GroupNorm backwards wrote past them
+        self._base_names = (set(self.__dict__) - self._PER_BATCH) | {"_base_names"}
         self.pack.repack()
+
+    _PER_BATCH = frozenset({"gn"})  # declared in __init__, rebound per batch size by bind()
 
     # ---------------------------------------------------------------- helpers
     def W(self, key):

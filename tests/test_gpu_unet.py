@@ -471,3 +471,32 @@ def test_st_tail_head_mode_inference(unet, golden_dir, B):
     finally:
         ops.st_tail_fwd, ops.st_head_fwd = orig, orig_head
         U.ST_TAIL_HEAD = U.ST_HEAD_256 = True
+
+
+def test_unet_batch_switch_keeps_per_batch_state(unet):
+    """The executor keeps one buffer set per batch size (UNetExecutor.bind).  A detour through a
+    smaller batch must leave the larger batch's state intact -- its GroupNorm partial rows
+    included (they were shared once: the B=64 GroupNorm backwards after a B=16 step wrote 48 rows
+    past the 16-row buffer).  Gradients of a B=64 step before and after a B=16 step: bitwise equal."""
+    from encdiff_amd import unet as U  # noqa: F401
+    g = torch.Generator().manual_seed(41)
+
+    def inputs(B):
+        return (torch.randn(B, 3, 16, 16, generator=g).cuda(), torch.randint(0, 1000, (B,), generator=g).cuda(),
+                torch.randn(B, 320, generator=g).cuda(), torch.randn(B, 3, 16, 16, generator=g).cuda())
+
+    def step(x, t, c, gout):
+        unet.executor()
+        unet._arena.zero_grad()
+        cc = c.clone().requires_grad_(True)
+        unet(x, t, context=[cc]).backward(gout)
+        torch.cuda.synchronize()
+        assert unet.executor().gn.rows == x.shape[0]
+        return unet._arena.grad.clone(), cc.grad.clone()
+
+    big, small = inputs(64), inputs(16)
+    a = step(*big)
+    step(*small)
+    b = step(*big)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v), (u - v).abs().max()
