@@ -728,6 +728,7 @@ extern "C" int encdiff_st_tail_fwd(const EncdiffStTailArgs* a, void* stream) {
   // debug mask bit 3: force the 16-row tile; producer statistics need one 64-row tile per segment
   if (p.gn_stats && p.gn_stats_add && p.c == 128 && p.rows / 64 < 256)
     return launch_tail<128, 32>(p, s);  // 8x8 level at B = 128: 256 workgroups instead of 128
+  if (p.gn_stats && p.gn_stats_add && p.c == 64) return launch_tail<64, 32>(p, s);  // (ENCDIFF_ST_TAIL_R32_C64)
   if (p.gn_stats || (!(p.pad_ & 8) && p.rows / rdef >= 256))
   switch (p.c) {
     case 64: rc = launch_tail<64, 64>(p, s); break;

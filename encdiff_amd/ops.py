@@ -870,6 +870,9 @@ def attention_bwd(q, k, v, o, lse, d_o, dq, dk, dv, batch, heads, sq, sk, dh, fp
 
 
 ST_TAIL_STATS_ADD = os.environ.get("ENCDIFF_ST_TAIL_STATS_ADD", "1") != "0"
+# c = 64 tails on 32-row tiles too (the 16x16 level at B = 128: 1024 workgroups instead of 512):
+# off -- 9.09 -> 9.13 ms/step (parity unchanged: test_graph_step_b128_matches_oracle with it on)
+ST_TAIL_R32_C64 = os.environ.get("ENCDIFF_ST_TAIL_R32_C64", "0") != "0"
 
 
 class StatSlots:
@@ -940,7 +943,7 @@ def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps
         assert _ld(head[0]) == a.ld_head
     if gn_stats is not None:  # the next GroupNorm's producer statistics of out
         a.gn_stats, a.ld_gn_stats = _p(gn_stats), _ld(gn_stats)
-        if c == 128 and rows // 64 < 256 and ST_TAIL_STATS_ADD:
+        if ((c == 128 and rows // 64 < 256) or (c == 64 and ST_TAIL_R32_C64)) and ST_TAIL_STATS_ADD:
             # two 32-row tiles per 64-row segment add into the zeroed slots (twice the workgroups);
             # only this tensor's columns (the view may span a concat's other producer).  Inside a
             # training step whose prologue zeroes the registered slots (StatSlots) no fill runs.
