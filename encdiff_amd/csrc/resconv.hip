@@ -87,6 +87,7 @@ __global__ __launch_bounds__(RC_THREADS) void resconv_kernel(const EncdiffResCon
   bf16_t* sk = (bf16_t*)(smem + q.sk_off);    // skip conv: [mc][cskip/32] A, then [TN][cskip/32] B fragments
   RC_ST_RT(0);
   RC_ST(1);
+  if (p.skip_stages & 128) return;  // timing experiments: the launch of this grid alone
   // the wave index as a scalar: everything derived from it (k ranges, taps, tile rows) stays in
   // SGPRs with scalar branches instead of exec-masked vector ones
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -230,6 +231,7 @@ __global__ __launch_bounds__(RC_THREADS) void resconv_kernel(const EncdiffResCon
   // the last); the barrier below publishes all waves' LDS-DMA with the staged rows
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   RC_ST(3);
+  if (p.skip_stages & 256) return;  // timing experiments: launch + the prologue's memory round trip
 
   // ---- statistics.  Power-of-two nv: xor-shuffles over the lanes of one image inside a wave
   // (lane offsets nv, 2 nv, ...), the owner lane folds its 8 channels into group partials (or

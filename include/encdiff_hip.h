@@ -711,7 +711,8 @@ typedef struct EncdiffResConvArgs {
                                     (1, 2, 4), 16-column tiles per workgroup (1, 2)           */
   int skip_stages;               /* 0; timing experiments only (tools/rc_bench.py): 1 no staging
                                     loads, 2 no normalisation, 4 no GEMM (nor its B staging), 8 no
-                                    stores, 16 no B staging, 32 no GEMM arithmetic */
+                                    stores, 16 no B staging, 32 no GEMM arithmetic, 64 kl = 0,
+                                    128 return at entry, 256 return once every operand landed */
   int pad_;
 } EncdiffResConvArgs;
 
