@@ -25,6 +25,7 @@ sys.path.insert(0, os.path.join(REPO, "tools"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--mask", type=int, default=0, help="EncdiffResConvArgs.skip_stages (stage ablation)")
     a = ap.parse_args()
     from rc_bench import shapes
     from encdiff_amd import _lib as L
@@ -32,6 +33,13 @@ def main():
     from encdiff_amd.ops import Geom
     lib = ops.lib
     lib.encdiff_debug_rc_stamps.argtypes = [C.c_void_p, C.c_int]
+    if a.mask:
+        fwd = L.lib.encdiff_resconv_fwd
+
+        def masked(argp, s, _f=fwd):
+            argp._obj.skip_stages = a.mask
+            return _f(argp, s)
+        L.lib.encdiff_resconv_fwd = masked
     dev, bf, B = "cuda", torch.bfloat16, a.batch
     names = ["issue", "stage", "stats", "norm+B", "gemm", "kred", "epi"]
     print(f"B={B}: cycles per phase (mean over workgroups): " + " ".join(names))
