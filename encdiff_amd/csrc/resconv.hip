@@ -48,6 +48,13 @@ ED_DEV void load8f_(const float* p, float* v) {  // (no alignment assumed: param
 // staged / statistics / window normalised (B landed) / GEMM done / k-split combined / exit,
 // [9] realtime at exit
 __device__ unsigned long long rc_stamps[4096][10];
+// per wave (lane 0): [w][0] entry, [w][1] operands issued, [w][2] staged (own loads landed),
+// [w][3] arrival at the statistics barrier
+__device__ unsigned long long rc_wstamps[4096][16][4];
+#define RC_WST(i)                                                                                    \
+  do {                                                                                               \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) rc_wstamps[blockIdx.x][threadIdx.x >> 6][i] = __builtin_readcyclecounter(); \
+  } while (0)
 #define RC_ST(i)                                                                                     \
   do {                                                                                               \
     if (threadIdx.x == 0 && blockIdx.x < 4096) rc_stamps[blockIdx.x][i] = __builtin_readcyclecounter(); \
@@ -59,6 +66,7 @@ __device__ unsigned long long rc_stamps[4096][10];
 #else
 #define RC_ST(i) do {} while (0)
 #define RC_ST_RT(i) do {} while (0)
+#define RC_WST(i) do {} while (0)
 #endif
 
 struct RcPlan {
@@ -87,6 +95,7 @@ __global__ __launch_bounds__(RC_THREADS) void resconv_kernel(const EncdiffResCon
   bf16_t* sk = (bf16_t*)(smem + q.sk_off);    // skip conv: [mc][cskip/32] A, then [TN][cskip/32] B fragments
   RC_ST_RT(0);
   RC_ST(1);
+  RC_WST(0);
   if (p.skip_stages & 128) return;  // timing experiments: the launch of this grid alone
   // the wave index as a scalar: everything derived from it (k ranges, taps, tile rows) stays in
   // SGPRs with scalar branches instead of exec-masked vector ones
@@ -183,6 +192,7 @@ __global__ __launch_bounds__(RC_THREADS) void resconv_kernel(const EncdiffResCon
   }
   for (int i = tid; i < nv; i += RC_THREADS) *(uint4*)(zr + i * 8) = make_uint4(0u, 0u, 0u, 0u);
   RC_ST(2);
+  RC_WST(1);
 
   // rows the workgroup's tiles read: conv-input rows [cy0, cy1] (resolution ho), staged rows
   // [sy0, sy1] (resolution h); whole images when a tile holds several
@@ -231,6 +241,7 @@ __global__ __launch_bounds__(RC_THREADS) void resconv_kernel(const EncdiffResCon
   // the last); the barrier below publishes all waves' LDS-DMA with the staged rows
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   RC_ST(3);
+  RC_WST(2);
   if (p.skip_stages & 256) return;  // timing experiments: launch + the prologue's memory round trip
 
   // ---- statistics.  Power-of-two nv: xor-shuffles over the lanes of one image inside a wave
@@ -268,6 +279,7 @@ __global__ __launch_bounds__(RC_THREADS) void resconv_kernel(const EncdiffResCon
         row[tv] = make_float2(a, b);
       }
     }
+    RC_WST(3);
     __syncthreads();
     for (int e = tid; e < ipw * p.groups; e += RC_THREADS) {  // (image, group): rows, then vectors in order
       const int jj = e / p.groups, g = e - jj * p.groups;
@@ -608,6 +620,10 @@ int rc_plan(const EncdiffResConvArgs& a, RcPlan& q, int& tn) {
 extern "C" int encdiff_debug_rc_stamps(void* dst, int nblocks) {
   return hipMemcpyFromSymbol(dst, HIP_SYMBOL(rc_stamps), (size_t)nblocks * 10 * sizeof(unsigned long long)) == hipSuccess
              ? 0 : -1;
+}
+extern "C" int encdiff_debug_rc_wstamps(void* dst, int nblocks) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(rc_wstamps), (size_t)nblocks * 64 * sizeof(unsigned long long)) ==
+                 hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -26,6 +26,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--mask", type=int, default=0, help="EncdiffResConvArgs.skip_stages (stage ablation)")
+    ap.add_argument("--waves", action="store_true", help="per-wave stamps (entry, issued, landed, at barrier)")
     a = ap.parse_args()
     from rc_bench import shapes
     from encdiff_amd import _lib as L
@@ -75,6 +76,16 @@ def main():
         d = np.diff(b[:, 1:9], axis=1).mean(axis=0)
         print(f"h{h:<3} cin{cin:<4} cout{cout:<4} rs{rs} {skip:7s} grid {nb:4d} lds {lds.value // 1024:3d}K span {span:6.2f} us "
               f"skew {skew.max():5.2f} us | " + " ".join(f"{v:6.0f}" for v in d) + f" | total {d.sum():6.0f}", flush=True)
+        if a.waves:  # per wave, relative to the workgroup's earliest wave entry: entry / issued / landed / at barrier
+            fn = lib.encdiff_debug_rc_wstamps
+            fn.argtypes = [C.c_void_p, C.c_int]
+            wb = np.zeros((4096, 16, 4), dtype=np.uint64)
+            assert fn(wb.ctypes.data_as(C.c_void_p), 4096) == 0
+            w = wb[:nb, :8].astype(np.int64)
+            rel = w - w[:, :, 0].min(axis=1)[:, None, None]
+            m = rel.mean(axis=0)
+            print("    per wave (entry, issued, landed, at barrier): " +
+                  "  ".join(f"w{i}:{m[i, 0]:.0f}/{m[i, 1]:.0f}/{m[i, 2]:.0f}/{m[i, 3]:.0f}" for i in range(8)), flush=True)
 
 
 if __name__ == "__main__":
