@@ -43,6 +43,16 @@ ED_DEV void load8f_(const float* p, float* v) {  // (no alignment assumed: param
 #ifndef RC_STAMP
 #define RC_STAMP 0  // diagnostic builds: phase stamps (tools/rc_stamps.py)
 #endif
+// v + v of lane ^ 16 / ^ 32 (gfx950 permlane swaps: VALU, no LDS round trip)
+ED_DEV float rc_sum_x16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+ED_DEV float rc_sum_x32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 #if RC_STAMP
 // per workgroup, thread 0: [0] realtime at entry, [1..8] shader clock at entry / operands issued /
 // staged / statistics / window normalised (B landed) / GEMM done / k-split combined / exit,
@@ -252,14 +262,25 @@ __global__ __launch_bounds__(RC_THREADS) void resconv_kernel(const EncdiffResCon
   const float inv_n = 1.f / ((float)hw * (float)cpg);
   if (pow2) {
     const int span = min(64, lpi * nv);  // lanes of one image inside a wave
+    // lane offsets 16 / 32 by the gfx950 permlane swaps (VALU; a + b in either order: the same bits
+    // as the ds_bpermute shuffle), 4 / 8 by shuffles -- 16 serial LDS round trips per wave were
+    // ~3 000 cycles before the first barrier (per-wave stamps, tools/rc_stamps.py --waves)
 #pragma unroll
-    for (int o = 4; o < 64; o <<= 1) {
+    for (int o = 4; o < 16; o <<= 1) {
       if (o < nv || o >= span) continue;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         s[i] += __shfl_xor(s[i], o, 64);
         ss[i] += __shfl_xor(ss[i], o, 64);
       }
+    }
+    if (16 >= nv && 16 < span) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { s[i] = rc_sum_x16(s[i]); ss[i] = rc_sum_x16(ss[i]); }
+    }
+    if (32 >= nv && 32 < span) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { s[i] = rc_sum_x32(s[i]); ss[i] = rc_sum_x32(ss[i]); }
     }
     const int nr = lpi * nv >= 64 ? lpi * nv / 64 : 1;  // partial rows per image
     const int nslot = cpg <= 8 ? p.groups : nv;        // slots per row: groups, or vectors
