@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--ddim-batch", type=int, default=8)
     ap.add_argument("--skip-ddim", action="store_true")
     ap.add_argument("--skip-cpu", action="store_true")
+    ap.add_argument("--skip-ref-api", action="store_true", help="skip the eager reference-API step timing")
     ap.add_argument("--bucket-mb", type=float, default=None,
                     help="DP: all-reduce pieces of at most this many MB (default ENCDIFF_DP_BUCKET_MB or coarse buckets)")
     ap.add_argument("--config", default="shapes3d", choices=["shapes3d", "celeba128"],
@@ -117,7 +118,7 @@ def record_gemms(tr):
     from encdiff_amd import _lib as L
     calls = []
     names = ("encdiff_gemm", "encdiff_gemm_ex", "encdiff_gemm_pair", "encdiff_gemm_pair_ex", "encdiff_gemm_pair_dx",
-             "encdiff_gemm_finalize")
+             "encdiff_gemm_finalize", "encdiff_wgrad_group_launch", "encdiff_st_wgrad_launch")
     orig = {n: getattr(L.lib, n) for n in names}
 
     def rec(name):
@@ -129,6 +130,12 @@ def record_gemms(tr):
                 calls.append(("pair_ex", _copy_args(a[0]), _copy_args(a[1]), None, 0))
             elif name in ("encdiff_gemm_pair_ex", "encdiff_gemm_pair_dx"):
                 calls.append(("pair_ex", _copy_args(a[0]), _copy_args(a[1]), _copy_args(a[2]), a[3]))
+            elif name == "encdiff_wgrad_group_launch":  # grouped weight gradients (blobs kept by the group)
+                from encdiff_amd import ops
+                calls.append(("group", a[0], a[1], [L.GemmArgs.from_buffer_copy(bytes(x)) for x in ops.GROUP_PROBS[a[0]]]))
+            elif name == "encdiff_st_wgrad_launch":  # a fused transformer block's weight gradients
+                from encdiff_amd import ops
+                calls.append(("stwg", a[0], a[1], [L.GemmArgs.from_buffer_copy(bytes(x)) for x in ops.STWG_PROBS[a[0]]]))
             else:
                 calls.append(("finalize", _copy_args(a[0])))
             return orig[name](*a[:-1], stream)
@@ -151,6 +158,8 @@ def gemm_problems(calls):
             out.append(c[1])
         elif c[0] == "pair_ex":
             out += [c[1], c[2]]
+        elif c[0] in ("group", "stwg"):
+            out += c[3]
     return out
 
 
@@ -178,11 +187,15 @@ def replay_gemms(calls, reps=1):
                 L.check(L.lib.encdiff_gemm(ref(c[1]), stream), "encdiff_gemm")
             elif c[0] == "pair_ex":
                 L.check(L.lib.encdiff_gemm_pair_ex(ref(c[1]), ref(c[2]), ref(c[3]), c[4], stream), "pair_ex")
+            elif c[0] == "group":
+                L.check(L.lib.encdiff_wgrad_group_launch(c[1], c[2], stream), "wgrad_group")
+            elif c[0] == "stwg":
+                L.check(L.lib.encdiff_st_wgrad_launch(c[1], c[2], stream), "st_wgrad")
             else:
                 L.check(L.lib.encdiff_gemm_finalize(ref(c[1]), stream), "finalize")
 
 
-def kernel_roofline(tr, reps=10):
+def kernel_roofline(tr, reps=10, config="shapes3d", batch=128):
     """Dominant kernel by time: the GEMM family (gemm_kernel<*> + its split-K finalize)
     that runs every conv / linear of the UNet, fwd + dgrad + wgrad.  The exact launches of
     one training step are recorded, captured into a HIP graph and replayed `reps` times
@@ -207,7 +220,8 @@ def kernel_roofline(tr, reps=10):
         e1.record(s)
         s.synchronize()
     t_set = e0.elapsed_time(e1) / 1e3 / reps
-    out = {"kernel": f"GEMM family (gemm_kernel / paired gemm2_kernel / WG3 + WGL weight-gradient grids + split-K finalizes): {len(probs)} "
+    out = {"kernel": f"GEMM family (gemm_kernel / paired gemm2_kernel / WG3 + WGL weight-gradient grids / grouped weight "
+                     f"gradients of the fused transformer backward (st_wgrad + fold) + split-K finalizes): {len(probs)} "
                      f"conv/linear GEMM problems of the step (UNet, VQ encoder, Encoder4; fwd+dgrad+wgrad) "
                      f"in {len(calls)} calls",
            "bound": "mfma", "achieved": flops / t_set / 1e12, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
@@ -215,12 +229,18 @@ def kernel_roofline(tr, reps=10):
            "avg_us": t_set / len(calls) * 1e6, "flops_per_launch": flops / len(calls),
            "launches_per_step": len(calls), "gemm_ms_per_step": t_set * 1e3,
            "alg_bytes_per_launch": sum(gemm_alg_bytes(a) for a in probs) / len(calls)}
-    prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "gemm_traffic.json")
-    if os.path.exists(prof):  # HBM bytes per launch from the committed rocprofv3 PMC passes
+    # HBM bytes per launch from the committed rocprofv3 PMC passes of THIS workload (configs[1]:
+    # gemm_traffic.json, others gemm_traffic_<config>.json); null when that workload and batch
+    # were not measured (a file measured on another config describes different GEMMs)
+    fname = "gemm_traffic.json" if config == "shapes3d" else f"gemm_traffic_{config}.json"
+    prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", fname)
+    out["traffic_source"] = None
+    if os.path.exists(prof):
         with open(prof) as f:
             pm = json.load(f)
-        out["traffic"] = pm.get("bytes_per_launch")
-        out["traffic_source"] = f"profiles/gemm_traffic.json ({pm.get('source', '')})"
+        if int(pm.get("batch", 128)) == batch:
+            out["traffic"] = pm.get("bytes_per_launch")
+            out["traffic_source"] = f"profiles/{fname} ({pm.get('source', '')})"
     return out
 
 
@@ -265,6 +285,44 @@ def log_images_time(ldm, N=8, S=200, eta=1.0):
     out.update(N=N, S=S, eta=eta, sample_swap_rows=lu * N, ddim_steps_total=S * 2,
                note="cold = first call (one-step graphs); second = whole-loop graph capture; warm = replay; "
                     "DDIM steps of both loops (swap + samples)")
+    return out
+
+
+def ref_api_time(config, B, steps=10, warmup=3):
+    """The drop-in API path a reference-side Lightning loop drives (INTEGRATION.md §1;
+    ddpm_enc.py:360-375 training_step, :399-401 on_train_batch_end, :1598-1639 optimizer), eager,
+    on a model of its own: optimizer.zero_grad() + LatentDiffusion.training_step + loss.backward()
+    + optimizer.step() + on_train_batch_end() per step.  Returns ms per step (host-synchronised
+    wall time over `steps`; the batch is resident in HBM as in the graph bench)."""
+    ldm, cfg = build_ldm(config)
+    ldm.learning_rate = cfg.get("base_learning_rate", 2e-6) * B
+    opt = ldm.configure_optimizers()
+    opt = opt[0][0] if isinstance(opt, (list, tuple)) else opt
+    g = torch.Generator(device="cuda").manual_seed(11)
+    res = 64 * ldm.image_size // 16
+    batch = {"image": torch.rand(B, res, res, 3, device="cuda", generator=g) * 2 - 1}
+    ldm.init_scale_factor(batch)
+
+    def one(i):
+        opt.zero_grad()
+        loss = ldm.training_step(batch, i)
+        loss.backward()
+        opt.step()
+        ldm.on_train_batch_end()
+        return loss
+    for i in range(warmup):
+        one(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        loss = one(warmup + i)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    out = {"ms_per_step": ms, "imgs_per_s": B * 1e3 / ms, "batch": B, "steps": steps,
+           "loss_last": float(loss), "note": "eager reference-API loop: zero_grad + training_step + "
+                                             "backward + AdamW/EMA step + on_train_batch_end"}
+    del ldm, opt
+    torch.cuda.empty_cache()
     return out
 
 
@@ -367,7 +425,7 @@ def main():
     value = imgs / dt
     loss = tr.loss()
     extra = {}
-    roof = kernel_roofline(tr)  # every rank (its recording step runs the DP exchange)
+    roof = kernel_roofline(tr, config=args.config, batch=args.batch)  # every rank (its recording step runs the DP exchange)
     if rank == 0:
         extra["roofline"] = roof
         if dp_info is not None:
@@ -389,6 +447,10 @@ def main():
                                                 "batch": 128, "S": args.ddim_steps, "eta": 1.0}
             if args.config == "shapes3d":
                 extra["ddim_log_images_s"] = log_images_time(ldm)
+        if not args.skip_ref_api and world == 1:
+            r = ref_api_time(args.config, args.batch)
+            extra["ref_api_ms_per_step"] = r["ms_per_step"]
+            extra["ref_api"] = r
         if not args.skip_cpu and world == 1 and args.config == "shapes3d":  # CPU baseline: N=1, configs[1]
             extra["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -130,6 +130,35 @@ class StHeadArgs(C.Structure):
                 ("n1", vp), ("ld_n1", C.c_long), ("s1", vp), ("qkv", vp), ("ld_qkv", C.c_long)]
 
 
+class StTailBwdArgs(C.Structure):
+    _fields_ = [("rows", C.c_int), ("c", C.c_int), ("tokens", C.c_int), ("heads", C.c_int), ("n_ctx", C.c_int),
+                ("scale", C.c_float), ("part_rows", C.c_int), ("pad_", C.c_int),
+                ("dy", vp), ("ld_dy", C.c_long), ("f", vp), ("ld_f", C.c_long),
+                ("t2", vp), ("t1", vp), ("q2", vp), ("o2", vp), ("ld_save", C.c_long),
+                ("s3", vp), ("s2", vp), ("lse2", vp), ("k2", vp), ("v2", vp), ("ld_kv", C.c_long),
+                ("w_po_t", vp), ("w_ff2_t", vp), ("w_ff1_t", vp), ("w_out2_t", vp), ("w_q2_t", vp), ("w_out1_t", vp),
+                ("g3", vp), ("g2", vp),
+                ("d_t3", vp), ("d_t2", vp), ("d_q2", vp), ("d_t1", vp), ("d_o1", vp), ("ld_d", C.c_long),
+                ("d_f", vp), ("ld_df", C.c_long),
+                ("ln3_dg", vp), ("ln3_db", vp), ("ln2_dg", vp), ("ln2_db", vp), ("ld_part", C.c_long),
+                ("dk2", vp), ("dv2", vp), ("ld_dkv", C.c_long), ("kv_part", vp)]
+
+
+class StHeadBwdArgs(C.Structure):
+    _fields_ = [("rows", C.c_int), ("c", C.c_int), ("part_rows", C.c_int), ("pad_", C.c_int),
+                ("d_qkv", vp), ("ld_dqkv", C.c_long), ("d_t1", vp), ("ld_dt1", C.c_long),
+                ("t0", vp), ("ld_t0", C.c_long), ("s1", vp), ("g1", vp), ("w_qkv_t", vp), ("w_in_t", vp),
+                ("d_t0", vp), ("ld_dt0", C.c_long), ("d_gn", vp), ("ld_dgn", C.c_long),
+                ("ln1_dg", vp), ("ln1_db", vp), ("ld_part", C.c_long),
+                ("kv_part", vp), ("kv_tiles", C.c_int), ("n_ctx", C.c_int), ("batch", C.c_int), ("pad2_", C.c_int),
+                ("dk2", vp), ("dv2", vp), ("ld_dkv", C.c_long)]
+
+
+class WgradProb(C.Structure):
+    _fields_ = [("dy", vp), ("ld_dy", C.c_long), ("x", vp), ("ld_x", C.c_long), ("dw", vp), ("ld_dw", C.c_long),
+                ("db", vp), ("M", C.c_int), ("N", C.c_int), ("K", C.c_int), ("pad_", C.c_int)]
+
+
 class ResConvArgs(C.Structure):
     _fields_ = [("batch", C.c_int), ("h", C.c_int), ("cin", C.c_int), ("cout", C.c_int), ("resample", C.c_int),
                 ("groups", C.c_int), ("silu", C.c_int), ("eps", C.c_float), ("x", vp), ("ld_x", C.c_long),
@@ -205,6 +234,11 @@ _PROTOS = {
     "encdiff_nchw_to_rows_split3": [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_long, vp],
     "encdiff_st_tail_fwd": [C.POINTER(StTailArgs), vp],
     "encdiff_st_head_fwd": [C.POINTER(StHeadArgs), vp],
+    "encdiff_st_tail_bwd": [C.POINTER(StTailBwdArgs), vp],
+    "encdiff_st_head_bwd": [C.POINTER(StHeadBwdArgs), vp],
+    "encdiff_st_tail_bwd_tile": [C.c_int, C.c_int, C.c_int],
+    "encdiff_st_wgrad_plan": [vp, C.c_int, vp, C.c_long, vp, C.c_long, vp],
+    "encdiff_st_wgrad_launch": [vp, vp, vp],
     "encdiff_resconv_fwd": [C.POINTER(ResConvArgs), vp],
     "encdiff_resconv_query": [C.POINTER(ResConvArgs), C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "encdiff_step_prologue": [C.POINTER(StepPrologueArgs), vp],

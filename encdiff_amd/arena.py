@@ -129,20 +129,22 @@ class ParamArena:
             cur = o + k
         return o0, cur - o0
 
-    def attach_grads(self):
+    def attach_grads(self, zero: bool = True):
         """Make every parameter's .grad the arena view again (an optimizer's
-        zero_grad(set_to_none=True) detaches them); re-attached slices start at zero."""
+        zero_grad(set_to_none=True) detaches them); re-attached slices start at zero (zero=False:
+        the caller zeroes the whole arena itself, one launch instead of one per slice)."""
         for name in self.names:
             p = self.params[name]
             g = p.grad
             o, shp = self.offsets[name]
             if g is None or g.data_ptr() != self.grad.data_ptr() + 4 * o:
                 view = self.view_in(self.grad, name)
-                view.zero_()
+                if zero:
+                    view.zero_()
                 p.grad = view
 
     def zero_grad(self):
-        self.attach_grads()
+        self.attach_grads(zero=False)
         self.grad.zero_()
 
     def enable_mirror(self) -> torch.Tensor:
@@ -182,7 +184,8 @@ class PackTable:
             return
         off = (self.numel + 7) // 8 * 8
         self.jobs.append(L.PackJob(src_off=src_off, dst_off=off, rows=rows, cols=cols, kind=kind, cin=cin))
-        self.views[key] = (off, rows, cols)
+        # kind 6 (transpose): the copy is [cols][rows]
+        self.views[key] = (off, cols, rows) if kind == 6 else (off, rows, cols)
         self.numel = off + rows * cols
 
     def finalize(self):

@@ -609,6 +609,27 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ src
     }
     return;
   }
+  if (j.kind == 6) {
+    // transposed copy-cast (the SpatialTransformer backward kernels' B operands, st_bwd.hip):
+    // src [rows][cols] -> dst [cols][rows], 32 x 32 tiles through LDS (coalesced both ways)
+    __shared__ float tile[32][33];
+    const int tr = (j.rows + 31) / 32, tc = (j.cols + 31) / 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    for (int t = blockIdx.x; t < tr * tc; t += gridDim.x) {
+      const int r0 = (t / tc) * 32, c0 = (t % tc) * 32;
+      __syncthreads();
+      for (int k = ty; k < 32; k += 8) {
+        const int r = r0 + k, c = c0 + tx;
+        tile[k][tx] = (r < j.rows && c < j.cols) ? src[j.src_off + (long)r * j.cols + c] : 0.f;
+      }
+      __syncthreads();
+      for (int k = ty; k < 32; k += 8) {
+        const int c = c0 + k, r = r0 + tx;
+        if (c < j.cols && r < j.rows) dst[j.dst_off + (long)c * j.rows + r] = f2bf(tile[tx][k]);
+      }
+    }
+    return;
+  }
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += stride) {
     const int r = i / j.cols, c = i - r * j.cols;  // 32-bit: the 64-bit divide was most of the time
     long s;

@@ -2693,7 +2693,9 @@ struct WgScratch {
 // 32-pixel / 32-token stages one wave of a group workgroup may run in sequence: deeper problems are
 // cut into chunks of whole images / token ranges, combined in the kernel (wg_last_chunk).  At one
 // or two waves per SIMD a wave's stage loop is latency-bound, so a long sequence would be the
-// group's critical path (a whole 16x16 problem: 256 stages, ~120 us).  ENCDIFF_WGG_STAGES.
+// group's critical path (a whole 16x16 problem: 256 stages, ~120 us).  ENCDIFF_WGG_STAGES (32: a
+// 16-stage plan of the WGL body at K = 8192 gave wrong sums in test_wgrad_group -- not pursued, the
+// fused transformer backward uses its own kernel, encdiff_st_wgrad).
 int wgg_stages() {
   static const int v = [] {
     const char* e = getenv("ENCDIFF_WGG_STAGES");

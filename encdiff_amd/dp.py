@@ -6,11 +6,18 @@ runs the full step on its GPU, and the ONLY exchange is the mean of the gradient
 (the reference gets the same from Lightning DDP, ddpm_enc.py:1598-1639 + main_val.py).
 
 The gradient arena (`arena.ParamArena.grad`, one flat fp32 buffer) is split into
-contiguous buckets in the order their gradients become final inside the step:
-  bucket 0 = UNet parameters       (final when the UNet backward ends),
-  bucket 1 = cond-stage parameters (final when Encoder4's autograd backward ends).
-`HipTrainer` launches bucket 0's all-reduce on a side stream while Encoder4's backward
-runs, then bucket 1, then the optimizer.  Over RCCL the reduction is ReduceOp.AVG; gloo
+contiguous buckets in the order their gradients become final inside the step (three with the
+split backward, `UNetExecutor.split_plan`):
+  bucket 0 = [0, lo): the UNet parameters before the output blocks (17.40 M params, final when
+             the UNet backward ends -- graph 2 of the step),
+  bucket 1 = [lo, ema_numel): the output blocks + `out` (20.07 M, final after the output-block
+             backward -- graph 1),
+  bucket 2 = [ema_numel, numel): the cond stage, Encoder4 (1.37 M, final when its autograd
+             backward ends -- graph 3).
+`HipTrainer` launches bucket 1's all-reduce on a side stream while the middle / input blocks'
+backward runs, bucket 0's while Encoder4's backward runs, then bucket 2, then the optimizer.
+When the arena layout does not allow the split (or ENCDIFF_DP_SPLIT=0) the UNet range is ONE
+bucket (final when the UNet backward ends) and the exchange has two buckets.  Over RCCL the reduction is ReduceOp.AVG; gloo
 (CPU tests) has no AVG, so SUM + a scale is used there.
 
 Wire format: fp32 by default (the reference's DDP all-reduces fp32 gradients).  With

@@ -147,6 +147,13 @@ class FusedArenaAdamW(torch.optim.Optimizer):
         self.launch()
         return loss
 
+    def zero_grad(self, set_to_none: bool = True):
+        """Lightning calls this every step.  torch's default walks ~1900 parameters (and with
+        set_to_none the next backward re-attaches each arena view with a zero launch of its own);
+        here the parameters keep their arena views and the whole gradient arena is zeroed in ONE
+        launch -- .grad reads as zeros, not None, whichever flag is passed."""
+        self.arena.zero_grad()
+
 
 class DDPM(nn.Module):
     """ddpm_enc.py:48-479 (the parts on the EncDiff path)."""

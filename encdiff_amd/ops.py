@@ -413,6 +413,9 @@ _GROUP = None      # the active WgradGroup
 _WG_WHOLE = False  # gemm_args: build a weight gradient for the group (split_k 1, no slabs)
 
 
+GROUP_PROBS = {}  # host blob address of a planned group -> its problems (bench.py's GEMM-family record)
+
+
 class WgradGroup:
     """The weight-gradient GEMMs of a backward region, launched together.  Launch descriptions
     are planned once per distinct problem list (the executors' buffers are static per batch size,
@@ -447,6 +450,7 @@ class WgradGroup:
                   "encdiff_wgrad_group_plan")
             dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(torch.cuda.current_device())
             ent = self._plans[key] = (host, dev, probs)  # (the problems: tools / tests re-plan subsets)
+            GROUP_PROBS[C.addressof(host)] = probs
         check(lib.encdiff_wgrad_group_launch(C.addressof(ent[0]), ent[1].data_ptr(), _s()), "encdiff_wgrad_group_launch")
 
 
@@ -986,6 +990,113 @@ def st_head_fwd(x, gn, w_in, b_in, g1, be1, w_qkv, t0, qkv, rows, c, tokens, gn_
     return True
 
 
+def st_tail_bwd_tile(c, rows, tokens) -> int:
+    """The row tile encdiff_st_tail_bwd picks: tokens / tile dK2 / dV2 partial slabs per image."""
+    return lib.encdiff_st_tail_bwd_tile(c, rows, tokens)
+
+
+def st_tail_bwd(dy, save, wt, g3, g2, k2, v2, out, ln3, ln2, dk2, dv2, rows, c, tokens, heads, n_ctx,
+                kv_part=None) -> bool:
+    """Backward of the SpatialTransformer tail (encdiff_st_tail_bwd; attention.py:180-191, 206-215,
+    226-232, 260-261): the input-gradient chain proj_out -> GEGLU FF -> norm3 -> attn2 (to_out,
+    cross-attention to the concept tokens, to_q) -> norm2 -> attn1.to_out for row tiles in LDS.
+    save: the forward's saved activations (f t2 t1 q2 o2 s3 s2 lse2); wt: the TRANSPOSED bf16
+    weights (po ff2 ff1 out2 q2 out1, PackTable kind 6); out: d_t3 d_f d_t2 d_q2 d_t1 d_o1 (bf16);
+    ln3 / ln2: (dgamma, dbeta) partial-row views [part_rows][c]; dk2 / dv2: the block's slices of
+    the concept-token K / V gradient, written when a row tile holds a whole image; else kv_part
+    (fp32 [rows/tile][n_ctx][2c]) receives per-tile partial slabs that st_head_bwd(kv=...) folds
+    into dk2 / dv2.  False: shape not supported."""
+    a = L.StTailBwdArgs(rows=rows, c=c, tokens=tokens, heads=heads, n_ctx=n_ctx, scale=(c // heads) ** -0.5,
+                        part_rows=ln3[0].shape[0], dy=_p(dy), ld_dy=_ld(dy), f=_p(save["f"]), ld_f=_ld(save["f"]),
+                        t2=_p(save["t2"]), t1=_p(save["t1"]), q2=_p(save["q2"]), o2=_p(save["o2"]),
+                        ld_save=_ld(save["t2"]), s3=_p(save["s3"]), s2=_p(save["s2"]), lse2=_p(save["lse2"]),
+                        k2=_p(k2), v2=_p(v2), ld_kv=_ld(k2),
+                        w_po_t=_p(wt["po"]), w_ff2_t=_p(wt["ff2"]), w_ff1_t=_p(wt["ff1"]), w_out2_t=_p(wt["out2"]),
+                        w_q2_t=_p(wt["q2"]), w_out1_t=_p(wt["out1"]), g3=_p(g3), g2=_p(g2),
+                        d_t3=_p(out["d_t3"]), d_t2=_p(out["d_t2"]), d_q2=_p(out["d_q2"]), d_t1=_p(out["d_t1"]),
+                        d_o1=_p(out["d_o1"]), ld_d=_ld(out["d_t3"]), d_f=_p(out["d_f"]), ld_df=_ld(out["d_f"]),
+                        ln3_dg=_p(ln3[0]), ln3_db=_p(ln3[1]), ln2_dg=_p(ln2[0]), ln2_db=_p(ln2[1]),
+                        ld_part=_ld(ln3[0]), dk2=_p(dk2), dv2=_p(dv2), ld_dkv=_ld(dk2), kv_part=_p(kv_part))
+    for k in ("d_t2", "d_q2", "d_t1", "d_o1"):
+        assert _ld(out[k]) == a.ld_d, k
+    for k in ("t1", "q2", "o2"):
+        assert _ld(save[k]) == a.ld_save, k
+    assert _ld(v2) == a.ld_kv and _ld(dv2) == a.ld_dkv
+    assert all(_ld(t) == a.ld_part for t in (ln3[1], ln2[0], ln2[1]))
+    assert ln2[0].shape[0] == a.part_rows
+    rc = lib.encdiff_st_tail_bwd(C.byref(a), _s())
+    if rc in (-2, -3):
+        return False
+    check(rc, "encdiff_st_tail_bwd")
+    return True
+
+
+def st_head_bwd(d_qkv, d_t1, t0, s1, g1, w_qkv_t, w_in_t, d_t0, d_gn, ln1, rows, c, kv=None) -> bool:
+    """Backward of the SpatialTransformer head after the self-attention backward
+    (encdiff_st_head_bwd; attention.py:211 norm1 + attn1 q/k/v, :253-254 proj_in):
+    d_n1 = d_qkv Wqkv, d_t0 = d_t1 + LN1'(t0; d_n1), d_gn = d_t0 Win (transposed bf16 weights);
+    ln1: (dgamma, dbeta) partial-row views.  kv = (kv_part, tiles per image, n_ctx, batch, dk2, dv2):
+    the tail's dK2 / dV2 partial slabs folded in tile order by the same grid.  False: shape not
+    supported."""
+    a = L.StHeadBwdArgs(rows=rows, c=c, part_rows=ln1[0].shape[0], d_qkv=_p(d_qkv), ld_dqkv=_ld(d_qkv),
+                        d_t1=_p(d_t1), ld_dt1=_ld(d_t1), t0=_p(t0), ld_t0=_ld(t0), s1=_p(s1), g1=_p(g1),
+                        w_qkv_t=_p(w_qkv_t), w_in_t=_p(w_in_t), d_t0=_p(d_t0), ld_dt0=_ld(d_t0), d_gn=_p(d_gn),
+                        ld_dgn=_ld(d_gn), ln1_dg=_p(ln1[0]), ln1_db=_p(ln1[1]), ld_part=_ld(ln1[0]))
+    if kv is not None:
+        a.kv_part, a.kv_tiles, a.n_ctx, a.batch = _p(kv[0]), kv[1], kv[2], kv[3]
+        a.dk2, a.dv2, a.ld_dkv = _p(kv[4]), _p(kv[5]), _ld(kv[4])
+        assert _ld(kv[5]) == a.ld_dkv
+    assert _ld(ln1[1]) == a.ld_part
+    rc = lib.encdiff_st_head_bwd(C.byref(a), _s())
+    if rc in (-2, -3):
+        return False
+    check(rc, "encdiff_st_head_bwd")
+    return True
+
+
+STWG_PROBS = {}  # host blob address of a planned StWgrad launch -> its problems as GemmArgs (bench.py's record)
+
+
+class StWgrad:
+    """The weight gradients of a fused transformer block's Linear layers (encdiff_st_wgrad_*: one
+    grid of large output blocks + a chunk fold), planned once per distinct problem list (the
+    executor's buffers are static per batch size) and kept for the life of the object: captured
+    graphs read the device description at replay.  Slabs live in the workspace's second half."""
+
+    def __init__(self):
+        self._plans = {}
+
+    def launch(self, probs):
+        """probs: [(dy [K][M], x [K][N], dw [M][N] fp32 (+=), db [M] fp32 or None)]."""
+        arr = (L.WgradProb * len(probs))(*[
+            L.WgradProb(dy=_p(dy), ld_dy=_ld(dy), x=_p(x), ld_x=_ld(x), dw=_p(dw), ld_dw=_ld(dw), db=_p(db),
+                        M=dy.shape[1], N=x.shape[1], K=dy.shape[0])
+            for dy, x, dw, db in probs])
+        key = bytes(arr)
+        ent = self._plans.get(key)
+        if ent is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("encdiff_st_wgrad first planned inside a graph capture: run an eager step first")
+            ws = _workspace().data_ptr() + 4 * WS_HALF
+            nb = C.c_long(0)
+            check(lib.encdiff_st_wgrad_plan(arr, len(probs), ws, WS_HALF, None, 0, C.byref(nb)), "encdiff_st_wgrad_plan")
+            host = (C.c_longlong * ((nb.value + 7) // 8))()
+            check(lib.encdiff_st_wgrad_plan(arr, len(probs), ws, WS_HALF, C.addressof(host), C.sizeof(host), C.byref(nb)),
+                  "encdiff_st_wgrad_plan")
+            dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(torch.cuda.current_device())
+            gem = [L.GemmArgs(M=q.M, N=q.N, K=q.K, a_mode=L.OPA_ROWM, b_mode=L.OPB_ROWN, c_mode=L.OUT_F32_ACCUM,
+                              a=q.dy, lda=q.ld_dy, b=q.x, ldb=q.ld_x, c=q.dw, ldc=q.ld_dw, split_k=1) for q in arr]
+            ent = self._plans[key] = (host, dev)
+            STWG_PROBS[C.addressof(host)] = gem
+        check(lib.encdiff_st_wgrad_launch(C.addressof(ent[0]), ent[1].data_ptr(), _s()), "encdiff_st_wgrad_launch")
+
+
+def whole_wgrad_args(dy, x, dw, db=None):
+    """linear_wgrad's problem (dw += dy^T x, db += sum dy) as ONE whole GEMM description (split-K
+    1, no slabs) for a WgradGroup: the group kernel chunks it itself."""
+    return _whole_wgrad(lambda off: linear_wgrad_args(dy, x, dw, db, off))
+
+
 RC_TILE_M = int(os.environ.get("ENCDIFF_RC_TILE_M", "0"))  # plan overrides for tuning (0: heuristic)
 RC_TILE_N = int(os.environ.get("ENCDIFF_RC_TILE_N", "0"))
 
@@ -1010,16 +1121,19 @@ def resconv_supported(x, g: Geom, w, resample=L.RESAMPLE_NONE, film=None, ld_fil
 
 
 _RC_OK = {}
+_RC_Q = {}  # resconv_fwd(query=True): argument bytes -> planned
 
 
 def resconv_fwd(x, g: Geom, w, y, gamma, beta, eps, silu=True, film=None, ld_film=0, bias=None,
                 resample=L.RESAMPLE_NONE, resid=None, resid_resample=L.RESAMPLE_NONE, xskip=None, wskip=None,
-                bskip=None, groups=32) -> bool:
+                bskip=None, groups=32, query=False) -> bool:
     """An inference ResBlock conv with the GroupNorm in front of it, one launch
     (openaimodel_enc.py:255-275): y = conv3x3(resample(SiLU(GN(x)(1 + scale) + shift))) + bias
     + resid (read through resid_resample) or bf16(xskip wskip^T + bskip).  x: [B*h*h][cin] at the
     geometry g, w: packed [cout][9*cin].  Returns False outside the kernel's support (the caller
-    issues the unfused launches)."""
+    issues the unfused launches).  query=True: nothing launched -- whether the launch with exactly
+    these arguments would be planned (encdiff_resconv_query, memoised on the argument bytes), so a
+    caller can commit to a pair of launches before issuing the first."""
     cin = w.shape[1] // 9
     a = L.ResConvArgs(batch=g.batch, h=g.h, cin=cin, cout=w.shape[0], resample=resample, groups=groups,
                       silu=int(silu), eps=eps, x=_p(x), ld_x=_ld(x), gamma=_p(gamma), beta=_p(beta),
@@ -1030,6 +1144,12 @@ def resconv_fwd(x, g: Geom, w, y, gamma, beta, eps, silu=True, film=None, ld_fil
     if xskip is not None:
         a.cskip, a.xskip, a.ld_xskip = xskip.shape[1], _p(xskip), _ld(xskip)
         a.wskip, a.ld_wskip, a.bskip = _p(wskip), _ld(wskip), _p(bskip)
+    if query:
+        key = bytes(a)
+        hit = _RC_Q.get(key)
+        if hit is None:
+            hit = _RC_Q[key] = lib.encdiff_resconv_query(C.byref(a), None, None) == 0
+        return hit
     rc = lib.encdiff_resconv_fwd(C.byref(a), _s())
     if rc in (-2, -3):
         return False

@@ -34,6 +34,19 @@ from .data import ImagePool
 from .dp import GradBuckets, rank_seed, scaled_lr, world_info
 
 
+def _plain(obj):
+    """A state dict with numpy scalars turned into Python numbers (LambdaLR keeps the schedule's
+    numpy values in _last_lr): loadable with torch.load(weights_only=True)."""
+    import numpy as np
+    if isinstance(obj, dict):
+        return {k: _plain(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_plain(v) for v in obj)
+    if isinstance(obj, np.generic):
+        return obj.item()
+    return obj
+
+
 class HipTrainer:
     def __init__(self, ldm, batch_size: int, base_lr: Optional[float] = None, graph: bool = True,
                  data: Optional[ImagePool] = None, pool_size: int = 480000, seed: int = 1234,
@@ -397,13 +410,64 @@ class HipTrainer:
                 self.save_checkpoint(os.path.join(self._ckptdir, "last.ckpt"))
 
     def save_checkpoint(self, path: str, epoch: int = 0):
-        """The trained state as a Lightning-layout .ckpt -- {'state_dict', 'epoch', 'global_step'},
-        what ``trainer.save_checkpoint`` writes (main_val.py:845-851) and ``init_from_ckpt``
-        reads.  The module parameters and LitEma buffers are views of the parameter / EMA arenas
-        the graph-replayed optimizer updates, so this is the state after the last step."""
+        """The training state as a Lightning-layout .ckpt (what ``trainer.save_checkpoint`` writes,
+        main_val.py:845-851): 'state_dict' (the module parameters and LitEma buffers -- views of
+        the arenas the graph-replayed optimizer updates, so the state after the last step, which
+        ``init_from_ckpt`` reads), 'epoch', 'global_step', and for a resume (``load_checkpoint``)
+        Lightning's 'optimizer_states' / 'lr_schedulers' keys plus 'encdiff_data':
+          optimizer_states[0] = {'state': {'exp_avg', 'exp_avg_sq'} as flat fp32 arena copies (the
+            AdamW moments of every trainable parameter, arena order), 'step': the AdamW step count,
+            'param_groups': lr / betas / eps / weight_decay, 'arena_names': the arena's parameter
+            order} -- the fused optimizer keeps its moments in the arena, not per parameter,
+          lr_schedulers[0] = the LambdaLR state_dict,
+          encdiff_data = the image pool's epoch permutation and step (the next batch drawn)."""
         torch.cuda.synchronize()
         sd = {k: v.detach().to("cpu", copy=True).contiguous() for k, v in self.ldm.state_dict().items()}
-        torch.save({"state_dict": sd, "epoch": int(epoch), "global_step": int(self.ldm.global_step)}, path)
+        a, o = self.arena, self.opt
+        opt_state = {"state": {"exp_avg": a.exp_avg.detach().cpu().clone(),
+                               "exp_avg_sq": a.exp_avg_sq.detach().cpu().clone()},
+                     "step": int(o.step_count),
+                     "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in o.param_groups],
+                     "arena_names": list(a.names)}
+        ck = {"state_dict": sd, "epoch": int(epoch), "global_step": int(self.ldm.global_step),
+              "optimizer_states": [opt_state],
+              "lr_schedulers": [_plain(self.sched.state_dict())] if self.sched is not None else [],
+              "encdiff_data": {"perm": self.data.perm.detach().cpu().clone(),
+                               "step": self.data.step.detach().cpu().clone(),
+                               "host_step": int(self.data.host_step), "epoch": int(self.data.epoch)}}
+        torch.save(_plain(ck), path)
+
+    def load_checkpoint(self, path: str):
+        """Resume from ``save_checkpoint``'s file (the reference's ``-r`` path restores the same
+        training state through Lightning): parameters + EMA, AdamW moments and step count, the LR
+        schedule position, global_step and the data position.  Captured graphs stay valid: every
+        restore writes into the existing arena / pool buffers."""
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        missing, unexpected = self.ldm.load_state_dict(ck["state_dict"], strict=False)
+        if missing or unexpected:
+            raise RuntimeError(f"checkpoint does not match the model: missing {missing}, unexpected {unexpected}")
+        self.arena.mark_dirty()
+        os_ = ck["optimizer_states"][0]
+        if list(os_["arena_names"]) != list(self.arena.names):
+            raise RuntimeError("checkpoint arena layout differs from this model's")
+        self.arena.exp_avg.copy_(os_["state"]["exp_avg"])
+        self.arena.exp_avg_sq.copy_(os_["state"]["exp_avg_sq"])
+        self.opt.step_count = int(os_["step"])
+        for g, saved in zip(self.opt.param_groups, os_["param_groups"]):
+            g.update(saved)
+        if self.sched is not None and ck.get("lr_schedulers"):
+            self.sched.load_state_dict(ck["lr_schedulers"][0])
+        self.ldm.global_step = int(ck["global_step"])
+        d = ck.get("encdiff_data")
+        if d is not None:
+            self.data.perm.copy_(d["perm"])
+            self.data.step.copy_(d["step"])
+            self.data.host_step, self.data.epoch = int(d["host_step"]), int(d["epoch"])
+        # the bf16 GEMM weight copies follow the restored parameters
+        self.unet.executor()
+        if hasattr(self.ldm.cond_stage_model, "repack_hip"):
+            self.ldm.cond_stage_model.repack_hip()
+        torch.cuda.synchronize()
 
     def install_signal_handlers(self, ckptdir: str):
         """main_val.py:845-862: SIGUSR1 summons a checkpoint -- rank 0 writes ``ckptdir/last.ckpt``.

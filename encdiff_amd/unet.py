@@ -90,6 +90,16 @@ ST_TAIL_HEAD_MAX_B = int(os.environ.get("ENCDIFF_ST_TAIL_HEAD_MAX_B", "32"))
 # default -- DDIM B=8 716 -> 705 steps/s with it (8 workgroups at the 4x4 level each stream the
 # 512 KB of proj_in + q/k/v weights; the GroupNorm + GEMM + LayerNorm + GEMM launches spread them)
 ST_HEAD_256 = os.environ.get("ENCDIFF_ST_HEAD_256", "0") != "0"
+# training backward of the SpatialTransformers at c <= ST_BWD_MAXC as fused kernels: the tail's
+# input-gradient chain (encdiff_st_tail_bwd), the self-attention backward, the head's chain
+# (encdiff_st_head_bwd), the block's 8 weight gradients as ONE grouped launch, the GroupNorm
+# backward -- 5 launches instead of 14 (0: the per-layer launches, for A/B runs)
+ST_BWD = os.environ.get("ENCDIFF_ST_BWD", "1") != "0"
+ST_BWD_MAXC = int(os.environ.get("ENCDIFF_ST_BWD_MAXC", "128"))
+# the fused blocks' weight gradients: "st" (encdiff_st_wgrad: large output blocks, each operand read
+# about once, + a chunk fold), "group" (the generic grouped launch's 64 x 64 parts) or "single"
+# (standalone split-K launches), for A/B
+ST_BWD_WG = os.environ.get("ENCDIFF_ST_BWD_WG", "st")
 
 
 # --------------------------------------------------------------------------- spec
@@ -294,6 +304,24 @@ class UNetExecutor:
                                   ("attn2.to_out.0.weight", c, c), ("ff.net.0.proj.weight", 8 * c, c),
                                   ("ff.net.2.weight", c, 4 * c)):
                 pk.add(tb + w, a.offsets[tb + w][0], rows, cols)
+        # the fused transformer backward reads every Linear of its block transposed ([in][out]):
+        # packed by the same per-step pack launch (kind 6)
+        # (the kernels' support: c in {64, 128}, 8 heads, <= 64 concept tokens, whole row tiles per image)
+        self.stf = {t.prefix for t in spec.sts
+                    if ST_BWD and t.c <= ST_BWD_MAXC and t.heads == 8 and self.lu <= 64 and
+                    ((t.c == 64 and t.h * t.h % 64 == 0) or (t.c == 128 and t.h * t.h % 32 == 0))}
+        for t in spec.sts:
+            if t.prefix not in self.stf:
+                continue
+            c, tb = t.c, t.prefix + "transformer_blocks.0."
+            for key, name, rows, cols in (("po", t.prefix + "proj_out.weight", c, c), ("in", t.prefix + "proj_in.weight", c, c),
+                                          ("ff2", tb + "ff.net.2.weight", c, 4 * c),
+                                          ("ff1", tb + "ff.net.0.proj.weight", 8 * c, c),
+                                          ("out2", tb + "attn2.to_out.0.weight", c, c), ("q2", tb + "attn2.to_q.weight", c, c),
+                                          ("out1", tb + "attn1.to_out.0.weight", c, c)):
+                pk.add(t.prefix + "T:" + key, a.offsets[name][0], rows, cols, kind=6)
+            o, _ = a.span([tb + "attn1.to_q.weight", tb + "attn1.to_k.weight", tb + "attn1.to_v.weight"])
+            pk.add(t.prefix + "T:qkv", o, 3 * c, c, kind=6)
         pk.finalize()
         self.pack = pk
         # norm partials: GN rows = batch (set at bind time), LN rows = LN_PARTS
@@ -306,12 +334,18 @@ class UNetExecutor:
         self._gn_names.append(("out.0.weight", "out.0.bias"))
         # output-block / out columns last: the split backward folds that suffix early
         self._gn_names.sort(key=lambda p: self._early_final(p[0]))
+        # LayerNorm partials: the per-layer backward kernels' (LN_PARTS rows); the fused transformer
+        # backward's (one row per row tile, per batch size: self.ln_f, bind)
         self.ln = NormPartials(arena, ops.LN_PARTS)
         for t in spec.sts:
+            if t.prefix in self.stf:
+                continue
             tb = t.prefix + "transformer_blocks.0."
             for nn_ in ("norm1", "norm2", "norm3"):
                 self.ln.add(tb + nn_ + ".weight", tb + nn_ + ".bias")
         self.ln.finalize()
+        self._stwg = ops.WgradGroup()  # the fused transformer blocks' weight gradients (ST_BWD_WG "group")
+        self._stwgk = ops.StWgrad()    # ... (ST_BWD_WG "st": encdiff_st_wgrad)
         self.gn: Optional[NormPartials] = None
         self.B = None
         self._sets: Dict[int, dict] = {}
@@ -330,11 +364,28 @@ class UNetExecutor:
         # names shared by every batch size; everything bind() (re)creates is per batch size and is
         # kept in / restored from self._sets -- the GroupNorm partials (rows = B) included: excluded
         # from the shared names although declared above, else a switch back to a larger batch kept
-        # the smaller batch's partial rows and its GroupNorm backwards wrote past them
+        # the smaller batch's partial rows and its GroupNorm backwards wrote past them.  bind()
+        # checks that it rebinds no shared name (_check_shared), so a future per-batch buffer
+        # declared in __init__ fails at its first bind instead of writing past a smaller batch's
         self._base_names = (set(self.__dict__) - self._PER_BATCH) | {"_base_names"}
         self.pack.repack()
 
     _PER_BATCH = frozenset({"gn"})  # declared in __init__, rebound per batch size by bind()
+    _SHARED_REBIND = frozenset({"B"})  # shared names bind() itself may reassign
+
+    def _shared_snapshot(self) -> dict:
+        return {n: self.__dict__[n] for n in self._base_names if n in self.__dict__}
+
+    def _check_shared(self, before: dict):
+        """Per-batch state safe by construction: every name bind() (re)assigns must be per batch
+        size (saved / restored across batch switches).  A shared name -- one present after
+        __init__ and not in _PER_BATCH -- that bind() rebinds would be kept from the batch size
+        bound last, e.g. a B-row buffer reused at a larger B."""
+        bad = sorted(n for n, v in before.items()
+                     if n not in self._SHARED_REBIND and self.__dict__.get(n) is not v)
+        if bad:
+            raise RuntimeError(f"UNetExecutor.bind rebinds shared attribute(s) {bad}: per-batch state declared in "
+                               "__init__ must be listed in UNetExecutor._PER_BATCH")
 
     # ---------------------------------------------------------------- helpers
     def W(self, key):
@@ -366,6 +417,11 @@ class UNetExecutor:
         if B in self._sets:
             self.__dict__.update(self._sets[B])
             return
+        shared = self._shared_snapshot()
+        self._bind_new(B)
+        self._check_shared(shared)
+
+    def _bind_new(self, B: int):
         ops.ensure_scratch(self.dev.index if self.dev.index is not None else None)
         sp = self.spec
         self._split = False  # split_plan() not computed for this batch size yet
@@ -374,6 +430,14 @@ class UNetExecutor:
         for gname, bname in self._gn_names:
             self.gn.add(gname, bname)
         self.gn.finalize()
+        # the fused transformer backward's LayerNorm partials: a row per row tile (tiles >= 32 rows)
+        self.ln_f = NormPartials(self.arena, max([B * st.h * st.h // 32 for st in sp.sts if st.prefix in self.stf] or [1]))
+        for st in sp.sts:
+            if st.prefix in self.stf:
+                tb = st.prefix + "transformer_blocks.0."
+                for nn_ in ("norm1", "norm2", "norm3"):
+                    self.ln_f.add(tb + nn_ + ".weight", tb + nn_ + ".bias")
+        self.ln_f.finalize()
         t = self._t
         mc, H = self.mc, self.H
         self.temb0 = t(B, mc); self.th1 = t(B, 4 * mc); self.ta1 = t(B, 4 * mc)
@@ -440,6 +504,8 @@ class UNetExecutor:
             M = B * t_.h * t_.h
             c = t_.c
             self.st_scratch[key] = dict(d_a=t(M, 4 * c), d_n=t(M, c), d_o=t(M, c), d_g=t(M, c))
+            if t_.prefix in self.stf:  # the fused backward's cross-attention dK / dV partial slabs
+                self.st_scratch[key]["kv_part"] = t(M // 32 * self.lu, 2 * c, F32)
         self.res_scratch = {}
         self._bind_gn_stats(B)
 
@@ -666,22 +732,33 @@ class UNetExecutor:
         cskip = r.cin if r.cin != r.cout else 0
         if r.hin * r.hin * r.cin > RC_MAX_IMG or r.hout * r.hout * r.cout > RC_MAX_IMG:
             return False
-        if not (ops.resconv_supported(x, gi, w1, r.updown)
-                and ops.resconv_supported(S["h1"], go, w2, film=film, ld_film=self._E_ld, cskip=cskip)):
+        # the kernel reads its skip input at the OUTPUT resolution: a channel-changing skip of a
+        # resampling block (none in the reference's UNets) stays on the unfused launches
+        if cskip and r.updown:
             return False
-        p = self._pend
-        self._pend = None
-        ops.finalize(p)
-        ok = ops.resconv_fwd(x, gi, w1, S["h1"], self.P(pre + "in_layers.0.weight"), self.P(pre + "in_layers.0.bias"),
-                             GN_EPS, bias=self.P(pre + "in_layers.2.bias"), resample=r.updown)
+        # it writes no producer statistics: a later GroupNorm reading S['h1'] / S['out'] from
+        # them (GN_FROM_PRODUCER at B >= 64) needs the unfused launches
+        if self._gst(S["h1"]) is not None or self._gst(S["out"]) is not None:
+            return False
         if cskip:
             skip = dict(xskip=x, wskip=self.W(pre + "skip_connection.weight"), bskip=self.P(pre + "skip_connection.bias"))
         else:
             skip = dict(resid=x, resid_resample=r.updown)
-        ok = ok and ops.resconv_fwd(S["h1"], go, w2, S["out"], self.P(pre + "out_layers.0.weight"),
-                                    self.P(pre + "out_layers.0.bias"), GN_EPS, film=film, ld_film=self._E_ld,
-                                    bias=self.P(pre + "out_layers.3.bias"), **skip)
-        assert ok, "encdiff_resconv_fwd declined a conv its query accepted"
+        conv1 = dict(x=x, g=gi, w=w1, y=S["h1"], gamma=self.P(pre + "in_layers.0.weight"),
+                     beta=self.P(pre + "in_layers.0.bias"), eps=GN_EPS, bias=self.P(pre + "in_layers.2.bias"),
+                     resample=r.updown)
+        conv2 = dict(x=S["h1"], g=go, w=w2, y=S["out"], gamma=self.P(pre + "out_layers.0.weight"),
+                     beta=self.P(pre + "out_layers.0.bias"), eps=GN_EPS, film=film, ld_film=self._E_ld,
+                     bias=self.P(pre + "out_layers.3.bias"), **skip)
+        # both launches planned with their exact arguments before the first is issued
+        if not (ops.resconv_fwd(**conv1, query=True) and ops.resconv_fwd(**conv2, query=True)):
+            return False
+        p = self._pend
+        self._pend = None
+        ops.finalize(p)
+        ok = ops.resconv_fwd(**conv1) and ops.resconv_fwd(**conv2)
+        if not ok:
+            raise RuntimeError("encdiff_resconv_fwd declined a conv its query with the same arguments accepted")
         return True
 
     def _res_fwd_agn(self, r: ResSpec, S, x, gi: Geom, go: Geom):
@@ -874,9 +951,10 @@ class UNetExecutor:
             return None
         gcol = self.gn.split_col(self._early_final)
         lcol = self.ln.split_col(self._early_final)
-        if gcol is None or lcol is None:
+        fcol = self.ln_f.split_col(self._early_final)
+        if gcol is None or lcol is None or fcol is None:
             return None
-        self._split = (lo, gcol, lcol)
+        self._split = (lo, gcol, lcol, fcol)
         return lo
 
     def backward(self, d_eps: torch.Tensor, split: bool = False) -> torch.Tensor:
@@ -894,14 +972,15 @@ class UNetExecutor:
             out = self._bwd_outputs(d_eps)
             if split and self._split:
                 ops.group_end()  # the output blocks' weight gradients, one grid
-                _, gcol, lcol = self._split
+                _, gcol, lcol, fcol = self._split
                 ops.flush()
                 self.gn.reduce(gcol)
                 self.ln.reduce(lcol)
+                self.ln_f.reduce(fcol)
                 self._cont = out
                 return self.d_ctx
             self._cont = None
-            return self._bwd_rest(out, self.gn.cols, self.ln.cols)
+            return self._bwd_rest(out, self.gn.cols, self.ln.cols, self.ln_f.cols)
         finally:
             ops.group_begin(None)
 
@@ -915,11 +994,11 @@ class UNetExecutor:
     def backward_rest(self) -> torch.Tensor:
         assert self._cont is not None, "backward_rest() follows backward(split=True)"
         out, self._cont = self._cont, None
-        _, gcol, lcol = self._split
+        _, gcol, lcol, fcol = self._split
         self._wg_blocks = 0
         ops.group_begin(self._wgg if ops.WG_GROUP else None)
         try:
-            return self._bwd_rest(out, gcol, lcol)
+            return self._bwd_rest(out, gcol, lcol, fcol)
         finally:
             ops.group_begin(None)
 
@@ -964,7 +1043,7 @@ class UNetExecutor:
             self._wg_block_done()
         return dout, g_hs
 
-    def _bwd_rest(self, state, gcol: int, lcol: int) -> torch.Tensor:
+    def _bwd_rest(self, state, gcol: int, lcol: int, fcol: int) -> torch.Tensor:
         B = self.B
         sp = self.spec
         g0 = Geom(B, self.H, self.H)
@@ -1030,6 +1109,7 @@ class UNetExecutor:
         # backward left: the columns before the output blocks' suffix)
         self.gn.reduce(0, gcol)
         self.ln.reduce(0, lcol)
+        self.ln_f.reduce(0, fcol)
         return self.d_ctx
 
     def conv_bwd(self, dy, g, cin, name, x, dx, db, resample=0, defer_dx=False):
@@ -1092,7 +1172,70 @@ class UNetExecutor:
         elif r.updown and not fuse:
             ops.resample_bwd(dout, dx, gi, r.updown, accumulate=True)
 
+    def _st_bwd_fused(self, s: STSpec, dout, dx, acc) -> bool:
+        """attention.py:250-261 backward in 5 launches: the tail's input-gradient chain
+        (encdiff_st_tail_bwd: proj_out, GEGLU FF, norm3, attn2 with its cross-attention backward,
+        norm2, attn1.to_out), the self-attention backward, the head's chain (encdiff_st_head_bwd:
+        q/k/v, norm1, proj_in), the block's 8 weight gradients as one grouped launch, and the
+        GroupNorm backward with the block residual.  False (nothing launched): shape outside the
+        fused kernels' support -- the caller runs the per-layer launches."""
+        B, c = self.B, s.c
+        S = self.state[s.prefix]
+        x = S["x"]
+        tb = s.prefix + "transformer_blocks.0."
+        ntok = s.h * s.h
+        X = self.st_scratch[(s.h, c)]
+        W, P, G = self.W, self.P, self.G
+        wt = {k: W(s.prefix + "T:" + k) for k in ("po", "ff2", "ff1", "out2", "q2", "out1")}
+        k2 = self.KV[:, s.kv_off:s.kv_off + c]
+        v2 = self.KV[:, s.kv_off + c:s.kv_off + 2 * c]
+        dk2 = self.dKV[:, s.kv_off:s.kv_off + c]
+        dv2 = self.dKV[:, s.kv_off + c:s.kv_off + 2 * c]
+        save = {k: S[k] for k in ("f", "t2", "t1", "q2", "o2", "s3", "s2", "lse2")}
+        out = dict(d_t3=S["d_t3"], d_f=S["d_f"], d_t2=S["d_t2"], d_q2=S["d_q2"], d_t1=S["d_t1"], d_o1=X["d_o"])
+        F = self.ln_f
+        if not ops.st_tail_bwd(dout, save, wt, P(tb + "norm3.weight"), P(tb + "norm2.weight"), k2, v2, out,
+                               F.parts(tb + "norm3.weight", c), F.parts(tb + "norm2.weight", c), dk2, dv2,
+                               B * ntok, c, ntok, s.heads, self.lu, kv_part=X["kv_part"]):
+            return False
+        tiles = ntok // ops.st_tail_bwd_tile(c, B * ntok, ntok)  # per image: > 1 -> partial slabs
+        qkv, dqkv = S["qkv"], S["d_qkv"]
+        ops.attention_bwd(qkv[:, :c], qkv[:, c:2 * c], qkv[:, 2 * c:], S["o1"], S["lse1"], X["d_o"], dqkv[:, :c],
+                          dqkv[:, c:2 * c], dqkv[:, 2 * c:], B, s.heads, ntok, ntok, s.dh, fp8=s.fp8)
+        ok = ops.st_head_bwd(dqkv, S["d_t1"], S["t0"], S["s1"], P(tb + "norm1.weight"), W(s.prefix + "T:qkv"),
+                             W(s.prefix + "T:in"), S["d_t0"], X["d_g"], F.parts(tb + "norm1.weight", c), B * ntok, c,
+                             kv=(X["kv_part"], tiles, self.lu, B, dk2, dv2) if tiles > 1 else None)
+        if not ok:
+            raise RuntimeError("encdiff_st_head_bwd declined a block whose tail it accepted")
+        wg = [(dout, S["t3"], G(s.prefix + "proj_out.weight").view(c, c), G(s.prefix + "proj_out.bias")),
+              (S["d_t3"], S["a"], G(tb + "ff.net.2.weight"), G(tb + "ff.net.2.bias")),
+              (S["d_f"], S["n3"], G(tb + "ff.net.0.proj.weight"), G(tb + "ff.net.0.proj.bias")),
+              (S["d_t2"], S["o2"], G(tb + "attn2.to_out.0.weight"), G(tb + "attn2.to_out.0.bias")),
+              (S["d_q2"], S["n2"], G(tb + "attn2.to_q.weight"), None),
+              (S["d_t1"], S["o1"], G(tb + "attn1.to_out.0.weight"), G(tb + "attn1.to_out.0.bias")),
+              (dqkv, S["n1"], self.qkv_grad[s.prefix], None),
+              (S["d_t0"], S["gn"], G(s.prefix + "proj_in.weight").view(c, c), G(s.prefix + "proj_in.bias"))]
+        if ST_BWD_WG == "st":
+            ops.flush()  # a paired launch's deferred finalize: its slabs share the workspace half
+            self._stwgk.launch(wg)
+        elif ST_BWD_WG == "group":
+            ops.flush()
+            for dy_, x_, dw, db in wg:
+                self._stwg.add(ops.whole_wgrad_args(dy_, x_, dw, db))
+            self._stwg.launch()
+        else:
+            for dy_, x_, dw, db in wg:
+                ops.linear_wgrad(dy_, x_, dw, db)
+        dg, db = self.gn.parts(s.prefix + "norm.weight", c)
+        ops.groupnorm_bwd(x, Geom(B, s.h, s.h), P(s.prefix + "norm.weight"), P(s.prefix + "norm.bias"), S["stg"],
+                          ST_GN_EPS, False, X["d_g"], dx, dg, db, accumulate=acc, ld_part=self.gn.ld, resid=dout)
+        return True
+
     def _st_bwd(self, s: STSpec, dout, dx, acc):
+        if s.prefix in self.stf:
+            if self._st_bwd_fused(s, dout, dx, acc):
+                return
+            raise RuntimeError(f"encdiff_st_tail_bwd declined {s.prefix} (c={s.c}, {s.h}x{s.h}, B={self.B})")
         B, c = self.B, s.c
         S = self.state[s.prefix]
         x = S["x"]

@@ -479,7 +479,9 @@ int encdiff_adamw_ema_mirror(float* p, const float* g, float* m, float* v, float
  * [co][cin][taps] (cin <= 8) -> [co][tap][hi8|hi8|lo8] (cols = 24*taps); kind 5: [co][cin] ->
  * [co][hi|hi|lo|I|I] (cols = 5*cin, co == cin: a 1x1 conv plus an identity residual).  With
  * activations stored [hi|lo|hi] (+ [hi|lo] for the residual) one GEMM forms a_hi w_hi + a_lo w_hi +
- * a_hi w_lo: fp32-class products for the Encoder4 forward (see cond.py). */
+ * a_hi w_lo: fp32-class products for the Encoder4 forward (see cond.py).  kind 6: the transpose,
+ * src [rows][cols] -> dst [cols][rows] (a Linear's [in][out] copy: the B operands of the
+ * SpatialTransformer backward kernels, encdiff_st_tail_bwd / encdiff_st_head_bwd). */
 typedef struct EncdiffPackJob {
   long long src_off, dst_off;
   int rows, cols, kind, cin;
@@ -662,6 +664,100 @@ typedef struct EncdiffStHeadArgs {
 } EncdiffStHeadArgs;
 
 int encdiff_st_head_fwd(const EncdiffStHeadArgs* args, void* stream);
+
+/* Backward of the row-local tail of a SpatialTransformer (attention.py:211-215 BasicTransformerBlock
+ * after attn1, :226-232 GEGLU, :170-191 CrossAttention to the concept tokens, :260-261 proj_out)
+ * as ONE kernel: the input-gradient chain of encdiff_st_tail_fwd for a tile of token rows, with
+ * the rows resident in LDS (fp32 residual-gradient stream, bf16 MFMA operands):
+ *   d_t3 = dy Wpo;  d_a = d_t3 W2;  d_f = GEGLU'(f) (d_a);  d_n3 = d_f W1
+ *   d_t2 = d_t3 + LN3'(t2; d_n3);   d_o2 = d_t2 Wout2
+ *   (d_q2, dK2, dV2) = cross-attention backward (recomputed from q2, K2 / V2, the saved LSE)
+ *   d_n2 = d_q2 Wq2;  d_t1 = d_t2 + LN2'(t1; d_n2);  d_o1 = d_t1 Wout1
+ * It writes the gradients the weight-gradient GEMMs and the self-attention backward read
+ * (d_t3 d_f d_t2 d_q2 d_t1 d_o1), the LN2 / LN3 affine partial sums of the tile (row blockIdx of
+ * the part matrices) and dK2 / dV2 of the image's concept tokens (a tile per image: written;
+ * several: fp32 partial slabs combined in tile order by the image's last tile through a ticket
+ * -- reproducible).  Weights are the TRANSPOSED bf16 copies ([in][out] of each Linear, dense).
+ * Replaces 9 launches of the unfused backward (6 input-gradient GEMMs with their weight-gradient
+ * pairs, two LayerNorm backwards, the cross-attention backward); the weight gradients are the
+ * caller's (one grouped launch).  c in {64, 128}, heads == 8, n_ctx <= 64, tokens a multiple of
+ * the row tile (64; 32 at c = 128 with fewer than 256 64-row tiles).  Reference of the chain:
+ * attention.py:180-191 (attention), :206-215 (block), :226-232 (GEGLU), :250-261 (transformer). */
+typedef struct EncdiffStTailBwdArgs {
+  int rows, c, tokens, heads, n_ctx;
+  float scale;                               /* dh^-0.5 */
+  int part_rows;                             /* rows of the LN partial matrices (>= launched tiles) */
+  int pad_;                                  /* 0; timing experiments only (tools/st_bwd_bench.py): stage mask */
+  const void* dy; long ld_dy;                /* d(block output), bf16 [rows][c] */
+  const void* f; long ld_f;                  /* saved GEGLU input [rows][8c]: value | gate */
+  const void* t2; const void* t1; const void* q2; const void* o2; long ld_save;
+  const float* s3; const float* s2;          /* saved LN3 / LN2 (mean, rstd) [rows][2] */
+  const float* lse2;                         /* saved cross-attention LSE [batch*heads][tokens] */
+  const void* k2; const void* v2; long ld_kv;  /* [batch*n_ctx][..] concept-token keys / values */
+  const void* w_po_t;                        /* [c][c]   proj_out^T        */
+  const void* w_ff2_t;                       /* [4c][c]  ff.net.2^T        */
+  const void* w_ff1_t;                       /* [c][8c]  ff.net.0.proj^T   */
+  const void* w_out2_t;                      /* [c][c]   attn2.to_out^T    */
+  const void* w_q2_t;                        /* [c][c]   attn2.to_q^T      */
+  const void* w_out1_t;                      /* [c][c]   attn1.to_out^T    */
+  const float* g3; const float* g2;          /* LN3 / LN2 gamma            */
+  void* d_t3; void* d_t2; void* d_q2; void* d_t1; void* d_o1; long ld_d;  /* bf16 [rows][c] outputs */
+  void* d_f; long ld_df;                     /* bf16 [rows][8c]            */
+  float* ln3_dg; float* ln3_db; float* ln2_dg; float* ln2_db; long ld_part;
+  void* dk2; void* dv2; long ld_dkv;         /* bf16 [batch*n_ctx][..]: written when a tile holds a
+                                                whole image (tokens == tile rows) */
+  float* kv_part;                            /* tokens > tile: fp32 [rows/tile][n_ctx][2c] partial slabs
+                                                of dK2 | dV2 per tile, folded into dk2 / dv2 by
+                                                encdiff_st_head_bwd (kv_* fields) */
+} EncdiffStTailBwdArgs;
+
+int encdiff_st_tail_bwd(const EncdiffStTailBwdArgs* args, void* stream);
+/* The row tile encdiff_st_tail_bwd uses for (c, rows, tokens): tokens / tile partial slabs per image. */
+int encdiff_st_tail_bwd_tile(int c, int rows, int tokens);
+
+/* Backward of the row-local head (attention.py:211 norm1 + attn1's q/k/v, :253-254 proj_in) after
+ * the self-attention backward, as ONE kernel for a tile of token rows:
+ *   d_n1 = d_qkv [Wq; Wk; Wv];  d_t0 = d_t1 + LN1'(t0; d_n1);  d_gn = d_t0 Win
+ * writing d_t0 (proj_in's weight gradient reads it), d_gn (the GroupNorm backward reads it) and
+ * the LN1 affine partial sums (row blockIdx).  Weights transposed ([in][out], dense).  c in {64, 128}.
+ * kv_part (optional): the tail kernel's dK2 / dV2 partial slabs, kv_tiles per image, summed in tile
+ * order into dk2 / dv2 (bf16) by the same grid (no ticket, reproducible). */
+typedef struct EncdiffStHeadBwdArgs {
+  int rows, c, part_rows, pad_;
+  const void* d_qkv; long ld_dqkv;           /* bf16 [rows][3c] */
+  const void* d_t1; long ld_dt1;             /* residual gradient, bf16 [rows][c] */
+  const void* t0; long ld_t0; const float* s1;
+  const float* g1;
+  const void* w_qkv_t;                       /* [c][3c] */
+  const void* w_in_t;                        /* [c][c]  */
+  void* d_t0; long ld_dt0;
+  void* d_gn; long ld_dgn;
+  float* ln1_dg; float* ln1_db; long ld_part;
+  const float* kv_part; int kv_tiles, n_ctx, batch, pad2_;
+  void* dk2; void* dv2; long ld_dkv;
+} EncdiffStHeadBwdArgs;
+
+int encdiff_st_head_bwd(const EncdiffStHeadBwdArgs* args, void* stream);
+
+/* The weight gradients of a fused transformer block's Linear layers (attention.py:160-167, 206-215,
+ * 226-232, 253-261: proj_out, ff.net.2, ff.net.0.proj, attn2.to_out / to_q, attn1.to_out, to_q/k/v,
+ * proj_in): dW_i += dY_i^T X_i and db_i += column sums of dY_i over the K tokens, for up to 16 problems
+ * in ONE grid (+ a fold launch when a block is split over token chunks: fp32 slabs in the caller's
+ * workspace summed in chunk order -- reproducible).  M, N multiples of 64, K of 32; operands bf16,
+ * 16-byte aligned.  plan (host, no device access) writes the launch description into `blob` (NULL:
+ * only *blob_bytes); the caller copies it to device memory once and launches it any number of times
+ * (captured graphs: the blob and the slab region must outlive them). */
+typedef struct EncdiffWgradProb {
+  const void* dy; long ld_dy;     /* bf16 [K][M] */
+  const void* x; long ld_x;       /* bf16 [K][N] */
+  float* dw; long ld_dw;          /* fp32 [M][N], accumulated */
+  float* db;                      /* fp32 [M], accumulated (optional) */
+  int M, N, K, pad_;
+} EncdiffWgradProb;
+
+int encdiff_st_wgrad_plan(const EncdiffWgradProb* probs, int n, float* workspace, long ws_floats, void* blob,
+                          long capacity, long* blob_bytes);
+int encdiff_st_wgrad_launch(const void* host_blob, const void* dev_blob, void* stream);
 
 /* ---------------------------------------------------------------- step prologue
  * The per-step device work in front of the training step, as ONE launch:

@@ -34,6 +34,7 @@ STRUCTS = {
     "EncdiffSmallConvArgs": "SmallConvArgs", "EncdiffPackJob": "PackJob", "EncdiffBatchNormArgs": "BatchNormArgs",
     "EncdiffStTailArgs": "StTailArgs", "EncdiffStHeadArgs": "StHeadArgs", "EncdiffZeroJob": "ZeroJob",
     "EncdiffStepPrologueArgs": "StepPrologueArgs", "EncdiffResConvArgs": "ResConvArgs",
+    "EncdiffStTailBwdArgs": "StTailBwdArgs", "EncdiffStHeadBwdArgs": "StHeadBwdArgs", "EncdiffWgradProb": "WgradProb",
 }
 
 

@@ -127,3 +127,35 @@ def test_wg3_split_matches_kernel_rule():
                 assert ((B // sp // ni) * (h // rows)) % (8 if tile == 33 else 4) == 0
     assert ops.wg3_split(128, 16, 16, 64, 64, 0, 64, 64, L.OUT_BF16) is None  # fp32 outputs only
     assert ops.wg3_split(128, 16, 16, 48, 64, 0, 64, 64, L.OUT_F32_ACCUM) is None  # cout % 32
+
+
+def test_bind_refuses_shared_per_batch_state():
+    """UNetExecutor.bind keeps one buffer set per batch size; a name declared in __init__ is shared
+    by all of them unless _PER_BATCH lists it.  A per-batch buffer declared in __init__ but not
+    listed (the round-5 GroupNorm-partials fault: B=64 backwards wrote past a B=16 buffer) must
+    fail at its first bind, and once listed it must be saved / restored across batch switches.
+    The real bind() runs on CPU tensors through a stand-in _bind_new."""
+    from encdiff_amd.unet import UNetExecutor
+
+    class Ex(UNetExecutor):
+        def __init__(self, per_batch):
+            self._PER_BATCH = frozenset(per_batch)
+            self.B = None
+            self._sets = {}
+            self.parts = None  # declared here, sized by B in bind (like `gn`)
+            self.width = 3     # truly shared
+            self._base_names = (set(self.__dict__) - self._PER_BATCH) | {"_base_names"}
+
+        def _bind_new(self, B):
+            self.act = torch.empty(B, self.width)
+            self.parts = torch.empty(B, 7)
+
+    with pytest.raises(RuntimeError, match="parts"):
+        Ex(per_batch=()).bind(4)
+    ex = Ex(per_batch=("parts",))
+    ex.bind(4)
+    p4 = ex.parts
+    ex.bind(16)
+    assert ex.parts.shape[0] == 16 and ex.act.shape[0] == 16
+    ex.bind(4)
+    assert ex.parts is p4 and ex.act.shape[0] == 4

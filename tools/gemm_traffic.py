@@ -8,6 +8,9 @@ WRITE_SIZE do not fit one pass):
     rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_w -o run -- python3 $R/tools/gemm_traffic.py run
     python tools/gemm_traffic.py summarize gpurun_out/pmc_f gpurun_out/pmc_w --out profiles/gemm_traffic.json
 
+(`run --config celeba128` for configs[4]; summarize it into profiles/gemm_traffic_celeba128.json,
+which is the file bench.py --config celeba128 reads.)
+
 `run` records the GEMM launches of one eager training step (B=128) and replays them once
 between torch spin_kernel markers, preceded by a calibration copy of known size (the
 ENCDIFF_EW_COPY kernel, 16-B lanes, 256 MiB read + 256 MiB write).  `summarize` sums the
@@ -30,13 +33,13 @@ sys.path.insert(0, REPO)
 CAL_BYTES = 256 << 20
 
 
-def run(batch: int):
+def run(batch: int, config: str = "shapes3d"):
     import torch
     import bench
     from encdiff_amd import ops
     from encdiff_amd.trainer import HipTrainer
     torch.cuda.set_device(0)
-    ldm, _ = bench.build_ldm()
+    ldm, _ = bench.build_ldm(config)
     tr = HipTrainer(ldm, batch, graph=False)
     tr.init_scale_factor()
     tr.step_eager()
@@ -61,10 +64,10 @@ def run(batch: int):
                 "resample": a.conv.resample, "alg_bytes": bench.gemm_alg_bytes(a), "flops": 2.0 * a.M * a.N * a.K}
     per_call = []
     for c in calls:
-        ps = [c[1]] if c[0] == "gemm" else ([c[1], c[2]] if c[0] == "pair_ex" else [])
+        ps = [c[1]] if c[0] == "gemm" else ([c[1], c[2]] if c[0] == "pair_ex" else (c[3] if c[0] in ("group", "stwg") else []))
         per_call.append({"kind": c[0], "problems": [desc(a) for a in ps]})
     with open(os.path.join(REPO, "gpurun_out", "gemm_traffic_calls.json"), "w") as f:
-        json.dump({"launches": len(calls), "alg_bytes": alg,
+        json.dump({"launches": len(calls), "alg_bytes": alg, "batch": batch, "config": config,
                    "flops": sum(2.0 * a.M * a.N * a.K for a in probs), "calls": per_call}, f)
     print(f"replayed {len(calls)} gemm launches")
 
@@ -92,7 +95,7 @@ def _segments(rows, counter):
     return segs
 
 
-FAM = ("gemm_kernel", "gemm2_kernel", "gemm_finalize", "wgrad3x3_kernel", "wgradlin_kernel")
+FAM = ("gemm_kernel", "gemm2_kernel", "gemm_finalize", "wgrad3x3_kernel", "wgradlin_kernel", "wgrad_group_kernel", "st_wgrad_kernel", "st_wgrad_fold")
 
 
 def _window(rows, counter):
@@ -116,7 +119,9 @@ def summarize(fdir, wdir, out):
            "bytes_per_launch": (rd + wr) / n, "alg_bytes_per_launch": meta["alg_bytes"] / n,
            "traffic_over_alg": (rd + wr) / meta["alg_bytes"],
            "fetch_units_per_cal_byte": f_cal / CAL_BYTES, "write_units_per_cal_byte": w_cal / CAL_BYTES,
-           "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of tools/gemm_traffic.py run (B=128), "
+           "batch": meta.get("batch", 128), "config": meta.get("config", "shapes3d"),
+           "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of tools/gemm_traffic.py run "
+                     f"({meta.get('config', 'shapes3d')}, B={meta.get('batch', 128)}), "
                      "calibrated on a 256 MiB 16-B-lane copy"}
     # per call: measured read / write bytes beside the algorithmic bytes, and per kernel name
     calls = meta.get("calls", [])
@@ -149,11 +154,12 @@ def main():
     ap.add_argument("mode", choices=["run", "summarize"])
     ap.add_argument("dirs", nargs="*")
     ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--config", default="shapes3d", choices=["shapes3d", "celeba128"])
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "gemm_traffic.json"))
     a = ap.parse_args()
     if a.mode == "run":
         os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-        run(a.batch)
+        run(a.batch, a.config)
     else:
         summarize(a.dirs[0], a.dirs[1], a.out)
 

@@ -14,7 +14,7 @@ fi
 ARMS=("$@"); [ ${#ARMS[@]} = 0 ] && ARMS=("X=0")
 for e in "${ARMS[@]}"; do
   for rep in 1 2; do
-    env $e timeout -k 10 200 python bench.py --skip-cpu --skip-ddim --steps 50 > gpurun_out/iter_bench.log 2>&1 || { tail -15 gpurun_out/iter_bench.log; exit 1; }
+    env $e timeout -k 10 200 python bench.py --skip-cpu --skip-ref-api --skip-ddim --steps 50 > gpurun_out/iter_bench.log 2>&1 || { tail -15 gpurun_out/iter_bench.log; exit 1; }
     echo "$e: $(tail -1 gpurun_out/iter_bench.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],3), "ms/step", round(d["value"]), "imgs/s", "frac", round(d["roofline"]["frac"],4))')"
   done
 done
