@@ -59,7 +59,7 @@ class GroupNormArgs(C.Structure):
                 ("dgamma_part", vp), ("dbeta_part", vp), ("ld_part", C.c_long), ("dfilm", vp),
                 ("ld_dfilm", C.c_long), ("resid", vp), ("ld_resid", C.c_long), ("in_stats", vp),
                 ("ld_in_stats", C.c_long), ("x_from", vp), ("dy_resample", C.c_int), ("resid_resample", C.c_int),
-                ("w", C.c_int), ("pad_rs_", C.c_int)]
+                ("w", C.c_int), ("pad_rs_", C.c_int), ("dsilu", vp), ("ld_dsilu", C.c_long)]
 
 
 class LayerNormArgs(C.Structure):

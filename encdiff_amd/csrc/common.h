@@ -68,6 +68,12 @@ ED_DEV float silu_grad(float z) {
   const float s = sigmoid_f(z);
   return s * (1.0f + z * (1.0f - s));
 }
+// SiLU(z) (bitwise silu_f) and, in g, silu_grad(z) from the one sigmoid
+ED_DEV float silu_and_grad(float z, float& g) {
+  const float s = sigmoid_f(z);
+  g = s * (1.0f + z * (1.0f - s));
+  return z * s;
+}
 
 ED_DEV float wave_sum(float v) {
 #pragma unroll

@@ -307,6 +307,19 @@ __global__ __launch_bounds__(GN_THREADS) void gn_fwd_kernel(const EncdiffGroupNo
   }
   bf16_t* Y = (bf16_t*)p.y + (long)L.b * HW * p.ldy + L.cb;
   const bool silu = p.silu;
+  bf16_t* DS = silu && p.dsilu ? (bf16_t*)p.dsilu + (long)L.b * HW * p.ld_dsilu + L.cb : nullptr;
+  if (DS) {  // training: silu'(z) for the backward too
+#pragma unroll 2
+    for (int px = L.tp; px < HW; px += L.np) {
+      float v[8], g[8];
+      unpack8(gn_row(L, tile, X, p.ldx, px), v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = silu_and_grad(v[i] * mul[i] + add[i], g[i]);
+      *(uint4*)(Y + (long)px * p.ldy) = pack8(v);
+      *(uint4*)(DS + (long)px * p.ld_dsilu) = pack8(g);
+    }
+    return;
+  }
 #pragma unroll 2
   for (int px = L.tp; px < HW; px += L.np) {
     float v[8];
@@ -381,13 +394,21 @@ __global__ __launch_bounds__(GN_THREADS) void gn_fwd_stats_kernel(const EncdiffG
   }
   bf16_t* Y = (bf16_t*)p.y + (long)L.b * HW * p.ldy + L.cb;
   const bool silu = p.silu;
+  bf16_t* DS = silu && p.dsilu ? (bf16_t*)p.dsilu + (long)L.b * HW * p.ld_dsilu + L.cb : nullptr;
   auto emit = [&](const uint4& u, int px) {
     float v[8];
     unpack8(u, v);
+    if (DS) {  // training: silu'(z) for the backward too
+      float g[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float z = v[i] * mul[i] + add[i];
-      v[i] = silu ? silu_f(z) : z;
+      for (int i = 0; i < 8; ++i) v[i] = silu_and_grad(v[i] * mul[i] + add[i], g[i]);
+      *(uint4*)(DS + (long)px * p.ld_dsilu) = pack8(g);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float z = v[i] * mul[i] + add[i];
+        v[i] = silu ? silu_f(z) : z;
+      }
     }
     *(uint4*)(Y + (long)px * p.ldy) = pack8(v);
   };
@@ -472,6 +493,19 @@ __global__ __launch_bounds__(GN_THREADS) void gn_apply_kernel(const EncdiffGroup
   const bf16_t* X = (const bf16_t*)p.x + (long)b * p.hw * p.ldx + cb;
   bf16_t* Y = (bf16_t*)p.y + (long)b * p.hw * p.ldy + cb;
   const bool silu = p.silu;
+  bf16_t* DS = silu && p.dsilu ? (bf16_t*)p.dsilu + (long)b * p.hw * p.ld_dsilu + cb : nullptr;
+  if (DS) {  // training: silu'(z) for the backward too
+#pragma unroll 4
+    for (int px = r0 + tp; px < r1; px += np) {
+      float v[8], g[8];
+      unpack8(*(const uint4*)(X + (long)px * p.ldx), v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = silu_and_grad(v[i] * mul[i] + add[i], g[i]);
+      *(uint4*)(Y + (long)px * p.ldy) = pack8(v);
+      *(uint4*)(DS + (long)px * p.ld_dsilu) = pack8(g);
+    }
+    return;
+  }
 #pragma unroll 4
   for (int px = r0 + tp; px < r1; px += np) {
     float v[8];
@@ -535,7 +569,8 @@ ED_DEV int gn_rs_hw(int mode, int hw) { return mode == ENCDIFF_RESAMPLE_DOWN2 ? 
 
 // RS: the resampled-operand variant (dy and / or resid through gn_resample_adj); separate so the
 // common instantiations keep their registers
-template <bool SLAB, bool RS = false>
+// DSL: the SiLU gradient is read from the forward's dsilu rows instead of recomputed from z
+template <bool SLAB, bool RS = false, bool DSL = false>
 __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNormArgs p, int cs, const GnSlabs sl) {
   __shared__ uint4 tx[GN_TILE], td[GN_TILE];
   __shared__ float red[4 * 2048], chs[4 * 512], gam_sh[512];
@@ -563,6 +598,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   };
   const bf16_t* RSA = RS && rsrs ? (const bf16_t*)p.resid + (long)L.b * gn_rs_hw(rsrs, HW) * p.ld_resid + L.cb
                                  : nullptr;
+  const bf16_t* DSR = DSL ? (const bf16_t*)p.dsilu + off * p.ld_dsilu + L.cb : nullptr;
   // per-channel constants
   float xm[8], xr[8], ga[8], be[8], sc1[8], sf[8];
   load8f(p.gamma + L.cb, ga);
@@ -620,46 +656,54 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   for (int k = 0; k < 2; ++k)
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[k][i] = 0.f;
-  auto row1 = [&](const uint4 ux, const uint4 ud, const int u, const bool keep) {
-    float v[8], d[8];
+  auto row1 = [&](const uint4 ux, const uint4 ud, const uint4 us, const int u, const bool keep) {
+    float v[8], d[8], sg1[8];
     unpack8(ux, v);
     unpack8(ud, d);
+    if constexpr (DSL) unpack8(us, sg1);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float xh = v[i] * xr[i] + xo[i];
-      const float z = xh * zg[i] + zb[i];
-      const float dz = silu ? d[i] * silu_grad(z) : d[i];
+      float dz;
+      if constexpr (DSL) {
+        dz = d[i] * sg1[i];
+      } else {
+        const float z = xh * zg[i] + zb[i];
+        dz = silu ? d[i] * silu_grad(z) : d[i];
+      }
       acc[0][i] += dz; acc[1][i] += dz * xh;
       if (keep) { cdz[u][i] = dz; cxh[u][i] = xh; }
     }
   };
   if (L.active) {
     if (one) {
-      uint4 bx[U1], bd[U1];
+      uint4 bx[U1], bd[U1], bs[U1];
 #pragma unroll
       for (int u = 0; u < U1; ++u) {
         const int px = L.tp + u * L.np;
-        bx[u] = bd[u] = gr0[u] = (uint4){0u, 0u, 0u, 0u};
+        bx[u] = bd[u] = bs[u] = gr0[u] = (uint4){0u, 0u, 0u, 0u};
         if (px < HW) {
           bx[u] = *(const uint4*)(X + (long)px * p.ldx);
           bd[u] = dy_row(px);
+          if constexpr (DSL) bs[u] = *(const uint4*)(DSR + (long)px * p.ld_dsilu);
           if (RES) gr0[u] = *(const uint4*)(RES + (long)px * p.ld_resid);
           else if (accum) gr0[u] = *(const uint4*)(DX + (long)px * p.lddx);
         }
       }
 #pragma unroll
       for (int u = 0; u < U1; ++u) {
-        if (L.tp + u * L.np < HW) row1(bx[u], bd[u], u, true);
+        if (L.tp + u * L.np < HW) row1(bx[u], bd[u], bs[u], u, true);
       }
     } else {
       for (int px0 = L.tp; px0 < HW; px0 += U1 * L.np) {
-        uint4 bx[U1], bd[U1];
+        uint4 bx[U1], bd[U1], bs[U1];
 #pragma unroll
         for (int u = 0; u < U1; ++u) {
           const int px = px0 + u * L.np;
-          bx[u] = bd[u] = (uint4){0u, 0u, 0u, 0u};
+          bx[u] = bd[u] = bs[u] = (uint4){0u, 0u, 0u, 0u};
           if (px < HW) {
             bx[u] = *(const uint4*)(X + (long)px * p.ldx);
+            if constexpr (DSL) bs[u] = *(const uint4*)(DSR + (long)px * p.ld_dsilu);
             if constexpr (SLAB) {  // dy combined from its producer's slabs and written back
               bd[u] = gn_slab_row(sl, off + px, p.c, L.cb);
               *(uint4*)(const_cast<bf16_t*>(DY) + (long)px * p.lddy) = bd[u];
@@ -673,7 +717,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
           const int px = px0 + u * L.np;
           if (px >= HW) break;
           if (L.tiled) { tx[px * L.nvc + L.tv] = bx[u]; td[px * L.nvc + L.tv] = bd[u]; }
-          row1(bx[u], bd[u], u, false);
+          row1(bx[u], bd[u], bs[u], u, false);
         }
       }
     }
@@ -780,14 +824,19 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
       for (int u = 0; u < U; ++u) {
         const int px = px0 + u * L.np;
         if (px >= HW) break;
-        float v[8], d[8], dz[8], xh[8];
+        float v[8], d[8], dz[8], xh[8], sg1[8];
         unpack8(gn_row(L, tx, X, p.ldx, px), v);
         unpack8(RS && dyrs && !L.tiled ? dy_row(px) : gn_row(L, td, DY, p.lddy, px), d);
+        if constexpr (DSL) unpack8(*(const uint4*)(DSR + (long)px * p.ld_dsilu), sg1);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           xh[i] = v[i] * xr[i] + xo[i];
-          const float z = xh[i] * zg[i] + zb[i];
-          dz[i] = silu ? d[i] * silu_grad(z) : d[i];
+          if constexpr (DSL) {
+            dz[i] = d[i] * sg1[i];
+          } else {
+            const float z = xh[i] * zg[i] + zb[i];
+            dz[i] = silu ? d[i] * silu_grad(z) : d[i];
+          }
         }
         out_row(px, gr[u], dz, xh);
       }
@@ -953,6 +1002,7 @@ int gn_check(const EncdiffGroupNormArgs* a) {
 extern "C" int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* a, void* stream) {
   if (a && a->dtype == ENCDIFF_DT_F32) return a->x_from ? ENCDIFF_ERR_UNSUPPORTED : ed_groupnorm_fwd_f32(a, (hipStream_t)stream);
   if (!a || a->dtype != ENCDIFF_DT_BF16 || !a->x || !a->y || !a->stats || !a->gamma || !a->beta) return ENCDIFF_ERR_ARG;
+  if (a->silu && a->dsilu && (((uintptr_t)a->dsilu & 15) || a->ld_dsilu % 8)) return ENCDIFF_ERR_ARG;
   const int cs = gn_check(a);
   if (cs < 0) return cs;
   GnSlabs sl{};
@@ -1011,6 +1061,8 @@ extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream
     if (rc != ENCDIFF_OK) return rc;
   }
   const bool rs = a->dy_resample || a->resid_resample;
+  const bool dsl = a->silu && a->dsilu != nullptr;
+  if (dsl && (((uintptr_t)a->dsilu & 15) || a->ld_dsilu % 8)) return ENCDIFF_ERR_ARG;
   if (rs) {  // operands at a following resample's resolution (read through its adjoint)
     auto ok_mode = [](int m) { return m == 0 || m == ENCDIFF_RESAMPLE_DOWN2 || m == ENCDIFF_RESAMPLE_UP2; };
     if (!ok_mode(a->dy_resample) || !ok_mode(a->resid_resample) || sl.ws || a->w <= 0 || a->hw % a->w ||
@@ -1019,14 +1071,26 @@ extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream
     const int h = a->hw / a->w;
     if ((a->dy_resample == ENCDIFF_RESAMPLE_DOWN2 || a->resid_resample == ENCDIFF_RESAMPLE_DOWN2) && ((h | a->w) & 1))
       return ENCDIFF_ERR_SHAPE;
-    hipLaunchKernelGGL((gn_bwd_kernel<false, true>), dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0,
-                       (hipStream_t)stream, *a, cs, sl);
+    if (dsl)
+      hipLaunchKernelGGL((gn_bwd_kernel<false, true, true>), dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0,
+                         (hipStream_t)stream, *a, cs, sl);
+    else
+      hipLaunchKernelGGL((gn_bwd_kernel<false, true>), dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0,
+                         (hipStream_t)stream, *a, cs, sl);
   } else if (sl.ws) {
-    hipLaunchKernelGGL(gn_bwd_kernel<true>, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream,
-                       *a, cs, sl);
+    if (dsl)
+      hipLaunchKernelGGL((gn_bwd_kernel<true, false, true>), dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0,
+                         (hipStream_t)stream, *a, cs, sl);
+    else
+      hipLaunchKernelGGL(gn_bwd_kernel<true>, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream,
+                         *a, cs, sl);
   } else {
-    hipLaunchKernelGGL(gn_bwd_kernel<false>, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream,
-                       *a, cs, sl);
+    if (dsl)
+      hipLaunchKernelGGL((gn_bwd_kernel<false, false, true>), dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0,
+                         (hipStream_t)stream, *a, cs, sl);
+    else
+      hipLaunchKernelGGL(gn_bwd_kernel<false>, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0,
+                         (hipStream_t)stream, *a, cs, sl);
   }
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;

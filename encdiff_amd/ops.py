@@ -795,23 +795,26 @@ def conv4x4s2_bwd_cl(dy, g_out: Geom, wf, x, cin, dw_cl, dx, db=None):
 
 # ------------------------------------------------------------------ normalisation
 def groupnorm_fwd(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_film=0, groups=32, in_stats=None,
-                  x_from=None):
+                  x_from=None, dsilu=None):
     """in_stats: the segment sums x's producer GEMM wrote (gn_stats), else a reduction pass.
     x_from: the GemmArgs a deferred conv3x3_fwd returned for x -- its slabs are combined here
-    (x written, bitwise the finalize's result), one launch instead of two."""
+    (x written, bitwise the finalize's result), one launch instead of two.  dsilu (training, with
+    silu): bf16 rows [pixels][c] that receive silu'(z) for the backward (groupnorm_bwd(dsilu=))."""
     c = x.shape[1]
     a = L.GroupNormArgs(batch=g.batch, hw=g.h * g.w, c=c, groups=groups, eps=eps, silu=int(silu),
                         x=_p(x), ldx=_ld(x), gamma=_p(gamma), beta=_p(beta), film=_p(film), ld_film=ld_film,
                         y=_p(y), ldy=_ld(y), stats=_p(stats), in_stats=_p(in_stats),
                         ld_in_stats=_ld(in_stats) if in_stats is not None else 0,
-                        x_from=None if x_from is None else C.addressof(x_from))
+                        x_from=None if x_from is None else C.addressof(x_from),
+                        dsilu=_p(dsilu), ld_dsilu=_ld(dsilu) if dsilu is not None else 0)
     check(lib.encdiff_groupnorm_fwd(C.byref(a), _s()), "encdiff_groupnorm_fwd")
 
 
 def groupnorm_bwd(x, g: Geom, gamma, beta, stats, eps, silu, dy, dx, dgamma_part, dbeta_part, film=None,
                   ld_film=0, dfilm=None, ld_dfilm=0, accumulate=False, groups=32, ld_part=None, resid=None,
-                  dy_from=None, dy_resample=0, resid_resample=0):
+                  dy_from=None, dy_resample=0, resid_resample=0, dsilu=None):
     """dx (+)= GN_bwd(dy) (+ resid: the block's skip-branch gradient, added in the same pass).
+    dsilu: the forward's silu'(z) rows (groupnorm_fwd(dsilu=)), read instead of recomputed.
     dy_from: the GemmArgs of dy's producer whose finalize gemm_pair deferred (dy written here).
     dy_resample / resid_resample: dy / resid are at the resolution of that 2x resample following
     the GroupNorm (L.RESAMPLE_DOWN2 / UP2); their adjoint is applied on the fly."""
@@ -823,7 +826,8 @@ def groupnorm_bwd(x, g: Geom, gamma, beta, stats, eps, silu, dy, dx, dgamma_part
                         ld_part=c if ld_part is None else ld_part, dfilm=_p(dfilm), ld_dfilm=ld_dfilm,
                         resid=_p(resid), ld_resid=_ld(resid) if resid is not None else 0,
                         x_from=None if dy_from is None else C.addressof(dy_from), dy_resample=dy_resample,
-                        resid_resample=resid_resample, w=g.w)
+                        resid_resample=resid_resample, w=g.w,
+                        dsilu=_p(dsilu), ld_dsilu=_ld(dsilu) if dsilu is not None else 0)
     check(lib.encdiff_groupnorm_bwd(C.byref(a), _s()), "encdiff_groupnorm_bwd")
 
 

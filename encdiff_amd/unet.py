@@ -100,6 +100,9 @@ ST_BWD_MAXC = int(os.environ.get("ENCDIFF_ST_BWD_MAXC", "128"))
 # about once, + a chunk fold), "group" (the generic grouped launch's 64 x 64 parts) or "single"
 # (standalone split-K launches), for A/B
 ST_BWD_WG = os.environ.get("ENCDIFF_ST_BWD_WG", "st")
+# training forward: the SiLU GroupNorms also store silu'(z) (bf16), which their backward reads instead
+# of recomputing two transcendentals per element in its VALU-bound first pass (0: recompute, A/B)
+GN_DSILU = os.environ.get("ENCDIFF_GN_DSILU", "0") == "1"
 
 
 # --------------------------------------------------------------------------- spec
@@ -490,6 +493,7 @@ class UNetExecutor:
         self.dw_out = t(8, 9 * sp.out_ch, F32)
         self.db_out = torch.zeros(8, device=self.dev, dtype=F32)  # bias-gradient accumulator (left zero)
         self.a_out = t(g0.pixels, sp.out_ch)
+        self.ds_out = t(g0.pixels, sp.out_ch) if GN_DSILU else None
         self.st_out = t(B, 64, F32)
         self.d_aout = t(g0.pixels, sp.out_ch)
         self.d_hlast = t(g0.pixels, sp.out_ch)
@@ -552,6 +556,8 @@ class UNetExecutor:
         Mi, Mo = B * r.hin * r.hin, B * r.hout * r.hout
         d = dict(a1=t(Mi, r.cin), st1=t(B, 64, F32), h1=t(Mo, r.cout), a2=t(Mo, r.cout), st2=t(B, 64, F32),
                  out=t(Mo, r.cout), d_a2=t(Mo, r.cout), d_h1=t(Mo, r.cout), d_in=t(Mi, r.cin), d_a1=t(Mi, r.cin))
+        if GN_DSILU:  # silu'(z) of GN1 / GN2 (training forward -> backward)
+            d["ds1"], d["ds2"] = t(Mi, r.cin), t(Mo, r.cout)
         if r.updown:
             d["d_a1r"] = t(Mo, r.cin)
         if r.updown == L.RESAMPLE_DOWN2:
@@ -659,7 +665,7 @@ class UNetExecutor:
                 h = self._layer_fwd(layer, h)
         self._h_last = h
         ops.groupnorm_fwd(h, g0, self.P("out.0.weight"), self.P("out.0.bias"), self.a_out, self.st_out, GN_EPS, True,
-                          in_stats=self._gst(h), x_from=self._take_pend(h))
+                          in_stats=self._gst(h), x_from=self._take_pend(h), dsilu=None if self.infer else self.ds_out)
         ops.small_conv_out_fwd(self.a_out, g0, self.P("out.2.weight"), self.P("out.2.bias"), self.eps)
         return self.eps
 
@@ -692,7 +698,8 @@ class UNetExecutor:
         if self.infer and AGN and AGN_RES and B <= AGN_MAX_B:
             return self._res_fwd_agn(r, S, x, gi, go)
         ops.groupnorm_fwd(x, gi, self.P(r.prefix + "in_layers.0.weight"), self.P(r.prefix + "in_layers.0.bias"),
-                          S["a1"], S["st1"], GN_EPS, True, in_stats=self._gst(x), x_from=self._take_pend(x))
+                          S["a1"], S["st1"], GN_EPS, True, in_stats=self._gst(x), x_from=self._take_pend(x),
+                          dsilu=None if self.infer else S.get("ds1"))
         a1, rs = self._conv1_input(r, S, go)
         f1 = ops.conv3x3_fwd(a1, go, r.cin, self.W(r.prefix + "in_layers.2.weight"), S["h1"],
                              bias=self.P(r.prefix + "in_layers.2.bias"), resample=rs, gn_stats=self._gst(S["h1"]),
@@ -700,7 +707,7 @@ class UNetExecutor:
         film = self._E_use[:, r.film_off:]
         ops.groupnorm_fwd(S["h1"], go, self.P(r.prefix + "out_layers.0.weight"), self.P(r.prefix + "out_layers.0.bias"),
                           S["a2"], S["st2"], GN_EPS, True, film=film, ld_film=self._E_ld,
-                          in_stats=self._gst(S["h1"]), x_from=f1)
+                          in_stats=self._gst(S["h1"]), x_from=f1, dsilu=None if self.infer else S.get("ds2"))
         # skip path into the output buffer, then conv2 adds onto it
         out = S["out"]
         if r.cin != r.cout:
@@ -1022,7 +1029,7 @@ class UNetExecutor:
                       self.G("out.2.bias"))
         dg, db = self.gn.parts("out.0.weight", sp.out_ch)
         ops.groupnorm_bwd(self._h_last, g0, self.P("out.0.weight"), self.P("out.0.bias"), self.st_out, GN_EPS, True,
-                          self.d_aout, self.d_hlast, dg, db, ld_part=self.gn.ld)
+                          self.d_aout, self.d_hlast, dg, db, ld_part=self.gn.ld, dsilu=self.ds_out)
         dout = self.d_hlast
         hs = self._hs
         nhs = len(hs)
@@ -1144,7 +1151,7 @@ class UNetExecutor:
         ops.groupnorm_bwd(S["h1"], go, self.P(pre + "out_layers.0.weight"), self.P(pre + "out_layers.0.bias"),
                           S["st2"], GN_EPS, True, S["d_a2"], S["d_h1"], dg, db, film=self.E[:, r.film_off:],
                           ld_film=self.E.shape[1], dfilm=self.dE[:, r.film_off:], ld_dfilm=self.dE.shape[1],
-                          ld_part=self.gn.ld, dy_from=f2)
+                          ld_part=self.gn.ld, dy_from=f2, dsilu=S.get("ds2"))
         # conv1 (on the resampled GN1 output)
         if r.updown == L.RESAMPLE_DOWN2:
             a1, rs = S["a1r"], L.RESAMPLE_NONE
@@ -1163,7 +1170,8 @@ class UNetExecutor:
         ops.groupnorm_bwd(x, gi, self.P(pre + "in_layers.0.weight"), self.P(pre + "in_layers.0.bias"), S["st1"],
                           GN_EPS, True, S["d_a1r"] if fuse else d_a1, dx, dg, db, accumulate=acc, ld_part=self.gn.ld,
                           resid=dout if (identity or fuse) else None, dy_from=f1,
-                          dy_resample=r.updown if fuse else 0, resid_resample=r.updown if fuse else 0)
+                          dy_resample=r.updown if fuse else 0, resid_resample=r.updown if fuse else 0,
+                          dsilu=S.get("ds1"))
         # skip path
         if r.cin != r.cout:
             ops.linear_bwd(dout, self.W(pre + "skip_connection.weight"), x, dx,

@@ -288,6 +288,10 @@ typedef struct EncdiffGroupNormArgs {
      w: the image width at this GroupNorm's resolution (hw = h * w), needed with either mode. */
   int dy_resample, resid_resample;
   int w, pad_rs_;
+  /* optional (bf16, silu): the SiLU gradient at z, silu'(z) = s (1 + z (1 - s)), s = sigmoid(z), one
+     bf16 [batch*hw][c] row per pixel (ld_dsilu): the training forward writes it beside y, the backward
+     reads it instead of recomputing z's two transcendentals per element (its VALU-bound pass 1) */
+  void* dsilu; long ld_dsilu;
 } EncdiffGroupNormArgs;
 
 int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* args, void* stream);

@@ -648,6 +648,28 @@ def test_groupnorm(O, C, H, film, silu, eps):
     assert rel(dbp.sum(0), br.grad) < 2e-3
     if film:
         assert rel(dE[:, :2 * C], Er.grad[:, :2 * C]) < 2e-3
+    if silu:
+        # training form: the forward also stores silu'(z) (bf16); y is bitwise the plain forward's,
+        # and the backward reading it matches the reference like the recomputing one
+        ds = torch.empty_like(x)
+        y2 = torch.empty_like(x)
+        O.groupnorm_fwd(x, g, gamma, beta, y2, stats, eps, silu, film=E, ld_film=E.shape[1] if film else 0, dsilu=ds)
+        assert torch.equal(y2, y)
+        z = F.group_norm(nhwc(x, g).float(), 32, gamma, beta, eps)
+        if film:
+            z = z * (1 + E[:, :C, None, None]) + E[:, C:2 * C, None, None]
+        sz = torch.sigmoid(z)
+        assert rel(nhwc(ds, g), sz * (1 + z * (1 - sz))) < 1e-2
+        dx2 = torch.empty_like(x)
+        dgp2, dbp2 = torch.empty(B, C, device=dev), torch.empty(B, C, device=dev)
+        dE2 = torch.zeros(B, 2 * C + 32, device=dev) if film else None
+        O.groupnorm_bwd(x, g, gamma, beta, stats, eps, silu, dy, dx2, dgp2, dbp2, film=E,
+                        ld_film=E.shape[1] if film else 0, dfilm=dE2, ld_dfilm=dE2.shape[1] if film else 0, dsilu=ds)
+        assert rel(nhwc(dx2, g), xr.grad) < 1e-2
+        assert rel(dgp2.sum(0), gr.grad) < 5e-3
+        assert rel(dbp2.sum(0), br.grad) < 5e-3
+        if film:
+            assert rel(dE2[:, :2 * C], Er.grad[:, :2 * C]) < 5e-3
 
 
 @pytest.mark.parametrize("rows,C", [(32768, 64), (8192, 128), (2048, 256), (512, 256), (1000, 128)])
