@@ -663,12 +663,22 @@ constexpr int STWG_MAXP = 16;
 // (WM, WN) kinds: 16-row tiles per wave x 16-column tiles (acc WM * WN * 4 VGPRs <= 128)
 constexpr int STWG_KINDS[][2] = {{1, 4}, {1, 16}, {4, 4}, {3, 4}, {2, 8}, {2, 16}, {4, 8}, {3, 8}};
 
+#ifndef STWG_PF
+#define STWG_PF 1
+#endif
+#ifndef STWG_FOLD_UNROLL
+#define STWG_FOLD_UNROLL 4
+#endif
+#ifndef STWG_PF_TILES
+#define STWG_PF_TILES 16
+#endif
 template <int WM, int WN>
 struct WgShape {
   static constexpr int BM = 64 * WM, BN = 16 * WN, LDA = BM + 8, LDB = BN + 8;
   static constexpr int STAGE = 32 * (LDA + LDB);      // bf16 elements per stage
   static constexpr int NL = (BM + BN) / 64;           // 16-byte loads per thread per stage
   static constexpr size_t LDS = 2 * (size_t)STAGE * 2 + 16 * 4 * WM * 4;  // + bias reduction
+  static constexpr int PF = WM * WN <= STWG_PF_TILES ? STWG_PF : 1;    // stages in flight (registers)
 };
 
 template <int WM, int WN>
@@ -728,36 +738,46 @@ __device__ __forceinline__ void st_wgrad_body(const StWg& p, int mblk, int nblk,
   float bs[WM];
 #pragma unroll
   for (int i = 0; i < WM; ++i) bs[i] = 0.f;
-  v4u32 r[NL];
-  load(r, 0);
-  store(r, 0);
+  // register ring of PF stages in flight (PF - 1 stage loads outstanding while a stage is stored
+  // to LDS): a stage is one global-load round trip, the kernel's critical path
+  constexpr int PF = T::PF;
+  v4u32 r[PF][NL];
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u < ns) load(r[u], u);
+  store(r[0], 0);
   __syncthreads();
   const int wm0 = wave * 16 * WM;  // this wave's rows of the block
-  for (int s = 0; s < ns; ++s) {
-    if (s + 1 < ns) load(r, s + 1);
-    const bf16_t* A = buf + (s & 1) * T::STAGE;
-    const bf16_t* Bt = A + 32 * LDA;
-    v8bf af[WM], bf[WN];
+  for (int s0 = 0; s0 < ns; s0 += PF) {
 #pragma unroll
-    for (int i = 0; i < WM; ++i) af[i] = frag(A, LDA, wm0 + 16 * i);
+    for (int u = 0; u < PF; ++u) {
+      const int s = s0 + u;
+      if (s >= ns) break;
+      if (s + PF < ns) load(r[u], s + PF);  // r[u]'s stage s is already in LDS
+      const bf16_t* A = buf + (s & 1) * T::STAGE;
+      const bf16_t* Bt = A + 32 * LDA;
+      v8bf af[WM], bf[WN];
 #pragma unroll
-    for (int j = 0; j < WN; ++j) bf[j] = frag(Bt, LDB, 16 * j);
+      for (int i = 0; i < WM; ++i) af[i] = frag(A, LDA, wm0 + 16 * i);
 #pragma unroll
-    for (int i = 0; i < WM; ++i)
+      for (int j = 0; j < WN; ++j) bf[j] = frag(Bt, LDB, 16 * j);
 #pragma unroll
-      for (int j = 0; j < WN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-    if (bias) {
+      for (int i = 0; i < WM; ++i)
 #pragma unroll
-      for (int i = 0; i < WM; ++i) {
-        const v8s a = __builtin_bit_cast(v8s, af[i]);
-        float t = 0.f;
+        for (int j = 0; j < WN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      if (bias) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) t += bf2f((bf16_t)a[e]);
-        bs[i] += t;
+        for (int i = 0; i < WM; ++i) {
+          const v8s a = __builtin_bit_cast(v8s, af[i]);
+          float t = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t += bf2f((bf16_t)a[e]);
+          bs[i] += t;
+        }
       }
+      if (s + 1 < ns) store(r[(u + 1) % PF], (s + 1) & 1);
+      __syncthreads();
     }
-    if (s + 1 < ns) store(r, (s + 1) & 1);
-    __syncthreads();
   }
   // accumulator (i, j, q): row wm0 + 16 i + 4 g4 + q of the block, column 16 j + l16
   const bool direct = p.kb == 1;
@@ -829,7 +849,7 @@ __global__ __launch_bounds__(256) void st_wgrad_fold_kernel(const StWg* __restri
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     if (e < n4) {
       const float* s = p.slab + 4 * e;
-#pragma unroll 4
+#pragma unroll STWG_FOLD_UNROLL
       for (int z = g; z < p.kb; z += 8) {
         const float4 v = *(const float4*)(s + (long)z * MN);
         a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;

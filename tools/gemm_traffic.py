@@ -149,9 +149,81 @@ def summarize(fdir, wdir, out):
     print(json.dumps({k: v for k, v in res.items() if k not in ("worst_calls",)}, indent=1))
 
 
+def _kname(n):
+    return n.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+
+
+def pmc(adir, bdir, out, traffic):
+    """Per-kernel-class SQ / L2 counters of the replay (two --pmc passes, each with --kernel-trace):
+    MFMA pipe utilisation, occupancy, wait shares and L2 hit rate beside the measured HBM traffic.
+
+    util  = SQ_INSTS_MFMA * 16 cyc / (duration * 2.4 GHz * 1024 SIMDs)  (16x16x32 bf16: 16 cycles;
+            the busy/N column = SQ_VALU_MFMA_BUSY_CYCLES / SQ_INSTS_MFMA checks that reading)
+    occ   = SQ_WAVE_CYCLES * 4 / (duration cycles * 256 CUs): mean resident waves per CU
+            (SQ_WAVE_CYCLES counts quad-cycles, MI355X_MICROARCH.md)
+    wait  = SQ_WAIT_ANY / SQ_WAVE_CYCLES, issue = SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES,
+    ldsw  = SQ_WAIT_INST_LDS / SQ_WAVE_CYCLES, L2hit = TCC_HIT / (TCC_HIT + TCC_MISS)."""
+    agg = {}
+
+    def add(d):
+        kt = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+        assert kt, f"no kernel_trace.csv under {d}"
+        names, dur = {}, {}
+        for r in csv.DictReader(open(kt[0])):
+            names[int(r["Dispatch_Id"])] = r["Kernel_Name"]
+            dur[int(r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        marks = sorted(i for i, n in names.items() if "spin_kernel" in n)
+        lo, hi = marks[1], marks[-1]            # skip the calibration segment
+        rows = _rows(d)
+        seen = set()
+        for i, n, c, v in rows:
+            if not (lo < i < hi) or not any(k in n for k in FAM):
+                continue
+            e = agg.setdefault(_kname(n), {"calls": {}, "ctr": {}})
+            e["ctr"][c] = e["ctr"].get(c, 0.0) + v
+            if i not in seen and d == adir:
+                seen.add(i)
+                e["calls"][i] = dur.get(i, 0)
+    add(adir)
+    add(bdir)
+    byk = {}
+    if traffic and os.path.exists(traffic):
+        byk = json.load(open(traffic)).get("by_kernel", {})
+    lines = [pmc.__doc__.split("\n\n")[0].strip(), "",
+             f"{'kernel':52s} {'calls':>5s} {'us':>7s} {'util':>6s} {'busy/N':>6s} {'occ':>5s} {'wait':>5s} "
+             f"{'issue':>5s} {'ldsw':>5s} {'L2hit':>5s} {'valu/mfma':>9s} {'traffic/alg':>11s} {'GB/s':>6s}"]
+    tot_ns = tot_m = 0.0
+    for k, e in sorted(agg.items(), key=lambda kv: -sum(kv[1]["calls"].values())):
+        ns = float(sum(e["calls"].values()))
+        if not ns:
+            continue
+        c = e["ctr"]
+        nm = c.get("SQ_INSTS_MFMA", 0.0)
+        wc = c.get("SQ_WAVE_CYCLES", 0.0) or 1.0
+        cyc = ns * 2.4
+        hit, miss = c.get("TCC_HIT_sum", 0.0), c.get("TCC_MISS_sum", 0.0)
+        t = byk.get(k, {})
+        rw = t.get("read", 0.0) + t.get("write", 0.0)
+        ratio = f"{rw / t['alg']:11.2f}" if t.get("alg") else f"{'-':>11s}"
+        gbs = rw / ns if rw else 0.0
+        lines.append(f"{k[:52]:52s} {len(e['calls']):5d} {ns / 1e3:7.1f} {nm * 16 / (cyc * 1024):6.3f} "
+                     f"{(c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0) / nm if nm else 0.0):6.1f} "
+                     f"{wc * 4 / (cyc * 256):5.1f} {c.get('SQ_WAIT_ANY', 0.0) / wc:5.2f} "
+                     f"{c.get('SQ_ACTIVE_INST_ANY', 0.0) / wc:5.2f} {c.get('SQ_WAIT_INST_LDS', 0.0) / wc:5.2f} "
+                     f"{(hit / (hit + miss) if hit + miss else 0.0):5.2f} "
+                     f"{(c.get('SQ_INSTS_VALU', 0.0) / nm if nm else 0.0):9.2f} {ratio} {gbs:6.0f}")
+        tot_ns += ns
+        tot_m += nm
+    lines.append(f"{'GEMM family':52s} {'':5s} {tot_ns / 1e3:7.1f} {tot_m * 16 / (tot_ns * 2.4 * 1024):6.3f}")
+    txt = "\n".join(lines) + "\n"
+    print(txt)
+    with open(out, "w") as f:
+        f.write(txt)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["run", "summarize"])
+    ap.add_argument("mode", choices=["run", "summarize", "pmc"])
     ap.add_argument("dirs", nargs="*")
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--config", default="shapes3d", choices=["shapes3d", "celeba128"])
@@ -160,6 +232,8 @@ def main():
     if a.mode == "run":
         os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
         run(a.batch, a.config)
+    elif a.mode == "pmc":
+        pmc(a.dirs[0], a.dirs[1], a.out, a.dirs[2] if len(a.dirs) > 2 else "")
     else:
         summarize(a.dirs[0], a.dirs[1], a.out)
 
