@@ -17,8 +17,11 @@
 // transposed bf16 copies (B fragments need 8 consecutive reduction elements per lane) streamed from
 // L2 one stage ahead.  The gradients the weight-gradient GEMMs read are written out (bf16, as the
 // unfused launches store them); the LayerNorm affine partials of a tile are summed over its rows in
-// row order (one partial row per workgroup); dK2 / dV2 of an image spread over several tiles are
-// combined by the image's last tile (write-through slabs + ticket, summed in tile order).
+// row order (one partial row per workgroup); dK2 / dV2 of an image whose tokens span several tiles
+// are written per tile as plain fp32 slabs that st_head_bwd_kernel folds in tile order before it
+// uses them (a last-arriver ticket with write-through slabs cost ~7 us per launch).  The weight
+// gradients of the block's eight Linears run as ONE grouped launch (st_wgrad_kernel: token-chunk
+// partials of every problem, folded in chunk order by st_wgrad_fold_kernel).
 #include <algorithm>
 #include <cstring>
 
