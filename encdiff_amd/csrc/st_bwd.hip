@@ -158,12 +158,32 @@ struct TailBwd {
     const size_t m = a > b ? (a > c ? a : c) : (b > c ? b : c);
     return (m + 15) / 16 * 16;
   }
-  static size_t lds_bytes(int nctx) {
-    return (size_t)R * LDT * 4 + 2 * (size_t)R * LDX * 2 + ubytes() + (size_t)2 * nctx * C * 2 + (size_t)2 * R * 8 * 4 + 16;
+  // MF: the per-(row, head) P / dS tiles of one round of heads (NTH / R heads: 256 pairs) for the
+  // MFMA key-gradient pass, [2][NTH / R][R][JP] bf16 (JP = n_ctx rounded up to 4), + a 64-B tail the
+  // last fragment reads may touch; otherwise per (row, head) LSE / D for the VALU (head, key) pass
+  // Layout: Tr | Xa | Xb | KV | U (| AT); the P / dS round starts in U right after the q2 rows the
+  // cross-attention keeps there (the rest of U is free during the attention) and may run past U.
+  static constexpr int jp(int nctx) { return (nctx + 3) & ~3; }
+  static constexpr size_t qbytes() { return (size_t)R * LDX * 2; }
+  static size_t lds_bytes(int nctx, bool mf) {
+    const size_t ps = (size_t)256 * jp(nctx) * 2 * 2 + 64;
+    const size_t u = mf ? std::max(ubytes(), qbytes() + ps) : ubytes() + (size_t)2 * R * 8 * 4;
+    return (size_t)R * LDT * 4 + 2 * (size_t)R * LDX * 2 + (size_t)2 * nctx * C * 2 + u + 16;
   }
 };
 
-template <int C, int R>
+// k-outer fragment (8 consecutive k of column col + l16) of a k-major bf16 tile in LDS: two
+// transposed 4 x 16 reads (ds_read_b64_tr_b16); rows g4 * 8 .. + 8 of the tile
+ED_DEV v8bf frag_tr(const bf16_t* tile, int ld, int col, int lane) {
+  typedef __attribute__((address_space(3))) v4s lds_v4s;
+  const int l16 = lane & 15, g4 = lane >> 4, tq = l16 >> 2, tp = l16 & 3;
+  const bf16_t* a0 = tile + (g4 * 8 + tq) * ld + col + 4 * tp;
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a0));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a0 + 4 * ld));
+  return __builtin_bit_cast(v8bf, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int C, int R, bool MF>
 __global__ __launch_bounds__(256, (C == 128 && R == 64) ? 1 : 2) void st_tail_bwd_kernel(const EncdiffStTailBwdArgs p) {
   using T = TailBwd<C, R>;
   constexpr int NWV = 4, NTH = 256, TM = R / 16, NT = C / (16 * NWV);
@@ -172,13 +192,14 @@ __global__ __launch_bounds__(256, (C == 128 && R == 64) ? 1 : 2) void st_tail_bw
   float* Tr = (float*)smem_raw;                          // [R][LDT] fp32 residual-gradient stream
   bf16_t* Xa = (bf16_t*)(Tr + R * LDT);                  // [R][LDX] bf16 operand
   bf16_t* Xb = Xa + R * LDX;                             // [R][LDX] bf16 operand
-  unsigned char* U = (unsigned char*)(Xb + R * LDX);     // union: GEGLU chunk | LN terms | q2 rows
+  const int nctx = p.n_ctx;
+  bf16_t* KV = Xb + R * LDX;                             // [2][nctx][C] the image's concept K / V
+  unsigned char* U = (unsigned char*)(KV + 2 * nctx * C);  // union: GEGLU chunk | LN terms | q2 rows
   bf16_t* Xh = (bf16_t*)U;                               //   [R][LDH] f chunk -> d_f chunk (value | gate)
   float* S = (float*)U;                                  //   [R][LDT] d * xh of a LayerNorm backward
   bf16_t* Q = (bf16_t*)U;                                //   [R][LDX] q2 rows (cross-attention)
-  const int nctx = p.n_ctx;
-  bf16_t* KV = (bf16_t*)(U + T::ubytes());               // [2][nctx][C] the image's concept K / V
-  float* AT = (float*)(KV + 2 * nctx * C);               // [2][R][8]: lse, D per (row, head)
+  float* AT = (float*)(U + T::ubytes());                 // [2][R][8]: lse, D per (row, head) (!MF)
+  bf16_t* PS = (bf16_t*)(U + T::qbytes());               // [2][NTH / R][R][JP]: P, dS of a head round (MF)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, g4 = lane >> 4;
@@ -360,6 +381,104 @@ __global__ __launch_bounds__(256, (C == 128 && R == 64) ? 1 : 2) void st_tail_bw
   }
   __syncthreads();
 
+  const int tpi = p.tokens / R;  // tiles per image
+  if constexpr (MF) {
+    // ---- cross-attention backward with the key gradients on MFMA.  Per round of HPR = NTH / R heads
+    // (one (row, head) pair per thread): D = do . o, p_j = exp(s_j - lse), ds_j = p_j (do . v_j - D),
+    // dq = scale sum_j ds_j k_j (VALU, as the forward), P and dS rows -> LDS (bf16, [head][row][key]);
+    // then dV_h = P_h^T dO_h and dK_h = scale dS_h^T Q_h as 16 (keys) x 16 (head columns) MFMA tiles
+    // over the tile's rows (k), the k-major P / dS and the row-major dO / Q read as k-outer fragments
+    // with ds_read_b64_tr_b16.  Key rows >= n_ctx of the last key tile and, at head dim 8, the 8
+    // columns of the neighbouring head are computed and dropped.
+    constexpr int HPR = NTH / R;
+    const int JP = T::jp(nctx), JT = (nctx + 15) / 16;
+    bf16_t* Pb = PS;
+    bf16_t* Db = PS + HPR * R * JP;
+#pragma unroll
+    for (int u = 0; u < PPT; ++u) {
+      const int r = tid % R, hl = tid / R, h = u * HPR + hl;
+      if (!(dbg & 2)) {
+        float q[DH], dout[DH], dq[DH], o[DH];
+#pragma unroll
+        for (int v = 0; v < DV; ++v) {
+          unpack8(*(const uint4*)(Q + r * LDX + h * DH + 8 * v), q + 8 * v);
+          unpack8(*(const uint4*)(Xa + r * LDX + h * DH + 8 * v), dout + 8 * v);
+          unpack8(make_uint4(o2r[u][v][0], o2r[u][v][1], o2r[u][v][2], o2r[u][v][3]), o + 8 * v);
+        }
+        float D = 0.f;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+          D += dout[d] * o[d];
+          dq[d] = 0.f;
+        }
+        bf16_t* prow = Pb + (hl * R + r) * JP;
+        bf16_t* drow = Db + (hl * R + r) * JP;
+        for (int j = 0; j < JP; j += 2) {
+          float pj[2], ds[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int jj = j + e < nctx ? j + e : 0;
+            float kf[DH], vf[DH];
+#pragma unroll
+            for (int v = 0; v < DV; ++v) {
+              unpack8(*(const uint4*)(KV + jj * C + h * DH + 8 * v), kf + 8 * v);
+              unpack8(*(const uint4*)(KV + (nctx + jj) * C + h * DH + 8 * v), vf + 8 * v);
+            }
+            float s0 = 0.f, s1 = 0.f, p0 = 0.f, p1 = 0.f;
+#pragma unroll
+            for (int d = 0; d < DH; d += 2) {
+              s0 += q[d] * kf[d];
+              s1 += q[d + 1] * kf[d + 1];
+              p0 += dout[d] * vf[d];
+              p1 += dout[d + 1] * vf[d + 1];
+            }
+            const float pe = j + e < nctx ? __expf((s0 + s1) * p.scale - lse_r[u]) : 0.f;
+            pj[e] = pe;
+            ds[e] = pe * ((p0 + p1) - D);
+#pragma unroll
+            for (int d = 0; d < DH; ++d) dq[d] += ds[e] * kf[d];
+          }
+          *(unsigned*)(prow + j) = pack2(pj[0], pj[1]);
+          *(unsigned*)(drow + j) = pack2(ds[0], ds[1]);
+        }
+#pragma unroll
+        for (int v = 0; v < DV; ++v) {
+          float y[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) y[k] = dq[8 * v + k] * p.scale;
+          *(uint4*)(Xb + r * LDX + h * DH + 8 * v) = pack8(y);
+        }
+      }
+      __syncthreads();
+      // key-gradient tiles of this round: (head, key tile, dV | dK), round-robin over the waves
+      for (int t = (dbg & 4) ? HPR * JT * 2 : wave; t < HPR * JT * 2; t += NWV) {
+        const int kind = t & 1, jt = (t >> 1) % JT, hh = (t >> 1) / JT, hg = u * HPR + hh;
+        const bf16_t* A = (kind ? Db : Pb) + hh * R * JP;
+        const bf16_t* B = kind ? Q : Xa;
+        v4f a = (v4f){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < R / 32; ++ks)
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr(A + 32 * ks * JP, JP, 16 * jt, lane),
+                                                      frag_tr(B + 32 * ks * LDX, LDX, hg * DH, lane), a, 0, 0, 0);
+        const int d = l16;
+        if (d < DH && !(dbg & 32)) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int j = 16 * jt + 4 * g4 + q;
+            if (j >= nctx) continue;
+            const float val = kind ? a[q] * p.scale : a[q];
+            if (tpi == 1) {
+              bf16_t* dst = (bf16_t*)(kind ? p.dk2 : p.dv2) + (long)(img * nctx + j) * p.ld_dkv + hg * DH + d;
+              *dst = f2bf(val);
+            } else {  // fp32 partial slab of this tile; encdiff_st_head_bwd folds an image's slabs in tile order
+              p.kv_part[((long)blockIdx.x * nctx + j) * 2 * C + (kind ? 0 : C) + hg * DH + d] = val;
+            }
+          }
+        }
+      }
+      __syncthreads();  // P / dS rewritten by the next round; Xa / Q read by the tiles above
+    }
+  } else {
   // ---- cross-attention backward (attention.py:180-191 with the softmax recomputed from the LSE):
   // per (row, head): D = do . o, p_j = exp(s_j - lse), ds_j = p_j (do . v_j - D), dq = scale sum ds_j k_j.
   // A thread's PPT pairs run interleaved (independent chains per key).
@@ -428,7 +547,6 @@ __global__ __launch_bounds__(256, (C == 128 && R == 64) ? 1 : 2) void st_tail_bw
   __syncthreads();
   // dK_j = scale sum_r ds_rj q_r, dV_j = sum_r p_rj do_r over the tile's rows, per (head, key); four
   // rows per step with independent score chains
-  const int tpi = p.tokens / R;  // tiles per image
   {
     for (int t = (dbg & 4) ? 8 * nctx : tid; t < 8 * nctx; t += NTH) {
       const int h = t / nctx, j = t - h * nctx;
@@ -508,6 +626,7 @@ __global__ __launch_bounds__(256, (C == 128 && R == 64) ? 1 : 2) void st_tail_bw
       }
     }
   }
+  }
   // ---- d_n2 = d_q2 Wq2 -> Xa   (Xb = d_q2 out; Xa's d_o2 rows are read by the dK / dV loop above)
   __syncthreads();
   if (!(dbg & 16)) rows_to_global<C, R, NTH>((bf16_t*)p.d_q2 + (long)row0 * p.ld_d, p.ld_d, Xb, LDX, tid);
@@ -529,6 +648,31 @@ __global__ __launch_bounds__(256, (C == 128 && R == 64) ? 1 : 2) void st_tail_bw
   if (!(dbg & 16)) rows_to_global<C, R, NTH>((bf16_t*)p.d_o1 + (long)row0 * p.ld_d, p.ld_d, Xa, LDX, tid);
 }
 
+// the MFMA key-gradient form where its P / dS round fits the occupancy the tile was sized for
+// (2 workgroups per CU, 1 for the c = 128 64-row tile); ENCDIFF_ST_BWD_MF=0: the VALU form, A/B
+template <int C, int R>
+bool tail_bwd_mf(int nctx) {
+  static const bool on = [] {
+    const char* e = getenv("ENCDIFF_ST_BWD_MF");
+    return !e || atoi(e) != 0;
+  }();
+  const size_t cap = (C == 128 && R == 64) ? 160 * 1024 : 80 * 1024;
+  return on && TailBwd<C, R>::lds_bytes(nctx, true) <= cap;
+}
+
+template <int C, int R, bool MF>
+int launch_tail_bwd_mf(const EncdiffStTailBwdArgs& p, hipStream_t s) {
+  using T = TailBwd<C, R>;
+  const size_t lds = T::lds_bytes(p.n_ctx, MF);
+  if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
+  static const hipError_t attr_ok = hipFuncSetAttribute((const void*)st_tail_bwd_kernel<C, R, MF>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr_ok != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)attr_ok;
+  hipLaunchKernelGGL((st_tail_bwd_kernel<C, R, MF>), dim3((unsigned)(p.rows / R)), dim3(256), lds, s, p);
+  ED_CHECK_LAUNCH();
+  return ENCDIFF_OK;
+}
+
 template <int C, int R>
 int launch_tail_bwd(const EncdiffStTailBwdArgs& p, hipStream_t s) {
   using T = TailBwd<C, R>;
@@ -536,14 +680,8 @@ int launch_tail_bwd(const EncdiffStTailBwdArgs& p, hipStream_t s) {
   if (p.rows / R > p.part_rows) return ENCDIFF_ERR_SHAPE;
   if (p.tokens / R > 1 && (!p.kv_part || ((uintptr_t)p.kv_part & 15))) return ENCDIFF_ERR_ARG;
   if ((long)(p.rows / R) * p.n_ctx * 2 * C * 4 >= 0x7FFFFFF0L) return ENCDIFF_ERR_SHAPE;
-  const size_t lds = T::lds_bytes(p.n_ctx);
-  if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
-  static const hipError_t attr_ok = hipFuncSetAttribute((const void*)st_tail_bwd_kernel<C, R>,
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (attr_ok != hipSuccess) return ENCDIFF_ERR_LAUNCH - (int)attr_ok;
-  hipLaunchKernelGGL((st_tail_bwd_kernel<C, R>), dim3((unsigned)(p.rows / R)), dim3(256), lds, s, p);
-  ED_CHECK_LAUNCH();
-  return ENCDIFF_OK;
+  (void)sizeof(T);
+  return tail_bwd_mf<C, R>(p.n_ctx) ? launch_tail_bwd_mf<C, R, true>(p, s) : launch_tail_bwd_mf<C, R, false>(p, s);
 }
 
 // ---------------------------------------------------------------------------------------------
