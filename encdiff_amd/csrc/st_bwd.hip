@@ -172,6 +172,16 @@ struct TailBwd {
   }
 };
 
+#ifndef ST_BWD_JU
+#define ST_BWD_JU 2  // key pairs per iteration of the (row, head) pass (LDS reads of K / V in flight)
+#endif
+typedef __bf16 v2bf_t __attribute__((ext_vector_type(2)));
+typedef float v2f __attribute__((ext_vector_type(2)));
+// c + a.lo * b.lo + a.hi * b.hi over bf16 pairs (v_dot2_f32_bf16)
+ED_DEV float dot2bf(unsigned a, unsigned b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf_t, a), __builtin_bit_cast(v2bf_t, b), c, false);
+}
+
 // k-outer fragment (8 consecutive k of column col + l16) of a k-major bf16 tile in LDS: two
 // transposed 4 x 16 reads (ds_read_b64_tr_b16); rows g4 * 8 .. + 8 of the tile
 ED_DEV v8bf frag_tr(const bf16_t* tile, int ld, int col, int lane) {
@@ -398,45 +408,55 @@ __global__ __launch_bounds__(256, (C == 128 && R == 64) ? 1 : 2) void st_tail_bw
     for (int u = 0; u < PPT; ++u) {
       const int r = tid % R, hl = tid / R, h = u * HPR + hl;
       if (!(dbg & 2)) {
-        float q[DH], dout[DH], dq[DH], o[DH];
+        // bf16 pairs as loaded: the dot products on v_dot2_f32_bf16 (fp32 accumulation of the exact
+        // bf16 products), dq accumulated as packed fp32 pairs
+        constexpr int DP = DH / 2;
+        unsigned qv[DP], dov[DP], ov[DP];
 #pragma unroll
         for (int v = 0; v < DV; ++v) {
-          unpack8(*(const uint4*)(Q + r * LDX + h * DH + 8 * v), q + 8 * v);
-          unpack8(*(const uint4*)(Xa + r * LDX + h * DH + 8 * v), dout + 8 * v);
-          unpack8(make_uint4(o2r[u][v][0], o2r[u][v][1], o2r[u][v][2], o2r[u][v][3]), o + 8 * v);
+          const uint4 a = *(const uint4*)(Q + r * LDX + h * DH + 8 * v);
+          const uint4 b = *(const uint4*)(Xa + r * LDX + h * DH + 8 * v);
+          qv[4 * v] = a.x; qv[4 * v + 1] = a.y; qv[4 * v + 2] = a.z; qv[4 * v + 3] = a.w;
+          dov[4 * v] = b.x; dov[4 * v + 1] = b.y; dov[4 * v + 2] = b.z; dov[4 * v + 3] = b.w;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) ov[4 * v + k] = o2r[u][v][k];
         }
         float D = 0.f;
 #pragma unroll
-        for (int d = 0; d < DH; ++d) {
-          D += dout[d] * o[d];
-          dq[d] = 0.f;
-        }
+        for (int i = 0; i < DP; ++i) D = dot2bf(dov[i], ov[i], D);
+        v2f dq[DP];
+#pragma unroll
+        for (int i = 0; i < DP; ++i) dq[i] = (v2f){0.f, 0.f};
         bf16_t* prow = Pb + (hl * R + r) * JP;
         bf16_t* drow = Db + (hl * R + r) * JP;
+#pragma unroll ST_BWD_JU
         for (int j = 0; j < JP; j += 2) {
           float pj[2], ds[2];
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             const int jj = j + e < nctx ? j + e : 0;
-            float kf[DH], vf[DH];
+            unsigned kv[DP], vv[DP];
 #pragma unroll
             for (int v = 0; v < DV; ++v) {
-              unpack8(*(const uint4*)(KV + jj * C + h * DH + 8 * v), kf + 8 * v);
-              unpack8(*(const uint4*)(KV + (nctx + jj) * C + h * DH + 8 * v), vf + 8 * v);
+              const uint4 a = *(const uint4*)(KV + jj * C + h * DH + 8 * v);
+              const uint4 b = *(const uint4*)(KV + (nctx + jj) * C + h * DH + 8 * v);
+              kv[4 * v] = a.x; kv[4 * v + 1] = a.y; kv[4 * v + 2] = a.z; kv[4 * v + 3] = a.w;
+              vv[4 * v] = b.x; vv[4 * v + 1] = b.y; vv[4 * v + 2] = b.z; vv[4 * v + 3] = b.w;
             }
             float s0 = 0.f, s1 = 0.f, p0 = 0.f, p1 = 0.f;
 #pragma unroll
-            for (int d = 0; d < DH; d += 2) {
-              s0 += q[d] * kf[d];
-              s1 += q[d + 1] * kf[d + 1];
-              p0 += dout[d] * vf[d];
-              p1 += dout[d + 1] * vf[d + 1];
+            for (int i = 0; i < DP; i += 2) {
+              s0 = dot2bf(qv[i], kv[i], s0);
+              s1 = dot2bf(qv[i + 1], kv[i + 1], s1);
+              p0 = dot2bf(dov[i], vv[i], p0);
+              p1 = dot2bf(dov[i + 1], vv[i + 1], p1);
             }
             const float pe = j + e < nctx ? __expf((s0 + s1) * p.scale - lse_r[u]) : 0.f;
             pj[e] = pe;
             ds[e] = pe * ((p0 + p1) - D);
 #pragma unroll
-            for (int d = 0; d < DH; ++d) dq[d] += ds[e] * kf[d];
+            for (int i = 0; i < DP; ++i)
+              dq[i] += ds[e] * (v2f){__uint_as_float(kv[i] << 16), __uint_as_float(kv[i] & 0xffff0000u)};
           }
           *(unsigned*)(prow + j) = pack2(pj[0], pj[1]);
           *(unsigned*)(drow + j) = pack2(ds[0], ds[1]);
@@ -445,7 +465,10 @@ __global__ __launch_bounds__(256, (C == 128 && R == 64) ? 1 : 2) void st_tail_bw
         for (int v = 0; v < DV; ++v) {
           float y[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) y[k] = dq[8 * v + k] * p.scale;
+          for (int k = 0; k < 4; ++k) {
+            y[2 * k] = dq[4 * v + k].x * p.scale;
+            y[2 * k + 1] = dq[4 * v + k].y * p.scale;
+          }
           *(uint4*)(Xb + r * LDX + h * DH + 8 * v) = pack8(y);
         }
       }
