@@ -175,13 +175,6 @@ struct TailBwd {
 #ifndef ST_BWD_JU
 #define ST_BWD_JU 2  // key pairs per iteration of the (row, head) pass (LDS reads of K / V in flight)
 #endif
-typedef __bf16 v2bf_t __attribute__((ext_vector_type(2)));
-typedef float v2f __attribute__((ext_vector_type(2)));
-// c + a.lo * b.lo + a.hi * b.hi over bf16 pairs (v_dot2_f32_bf16)
-ED_DEV float dot2bf(unsigned a, unsigned b, float c) {
-  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf_t, a), __builtin_bit_cast(v2bf_t, b), c, false);
-}
-
 // k-outer fragment (8 consecutive k of column col + l16) of a k-major bf16 tile in LDS: two
 // transposed 4 x 16 reads (ds_read_b64_tr_b16); rows g4 * 8 .. + 8 of the tile
 ED_DEV v8bf frag_tr(const bf16_t* tile, int ld, int col, int lane) {

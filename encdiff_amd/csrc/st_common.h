@@ -6,6 +6,13 @@
 
 namespace {
 
+typedef __bf16 v2bf_t __attribute__((ext_vector_type(2)));
+// c + a.lo * b.lo + a.hi * b.hi over bf16 pairs as stored (v_dot2_f32_bf16: the exact products,
+// fp32 accumulation)
+ED_DEV float dot2bf(unsigned a, unsigned b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf_t, a), __builtin_bit_cast(v2bf_t, b), c, false);
+}
+
 // GELU (erf form, F.gelu's default) with a branch-free erf: Abramowitz-Stegun 7.1.26, |error| <=
 // 1.5e-7 -- far below the bf16 rounding of a -- instead of ocml erff's range branches, which made
 // the GEGLU chunk the tail kernel's longest stage.

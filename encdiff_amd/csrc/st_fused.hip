@@ -142,31 +142,57 @@ __global__ __launch_bounds__(64 * NWV) void st_tail_kernel(const EncdiffStTailAr
   for (int pr = (dbg & 1) ? NPR : tid / SPL; pr < NPR; pr += NTH / SPL) {
     const int r = pr % R, h = pr / R;
     const int il = (row0 + r) / p.tokens - img0;
-    float q[DH], o[DH];
+    // two passes over the keys (all of them are in LDS): the scaled scores' max, then p = exp(s - m)
+    // with the scores recomputed bit-identically -- one exp per key and no rescale of o; the dot
+    // products on v_dot2_f32_bf16 (bf16 pairs as stored), o accumulated as packed fp32 pairs
+    constexpr int DP = DH / 2;
+    unsigned qv[DP];
 #pragma unroll
-    for (int d8 = 0; d8 < DH; d8 += 8) unpack8(*(const uint4*)(Xb + r * LDX + h * DH + d8), q + d8);
+    for (int d8 = 0; d8 < DH; d8 += 8) {
+      const uint4 a = *(const uint4*)(Xb + r * LDX + h * DH + d8);
+      qv[d8 / 2] = a.x; qv[d8 / 2 + 1] = a.y; qv[d8 / 2 + 2] = a.z; qv[d8 / 2 + 3] = a.w;
+    }
     const bf16_t* Ks = KV + (long)(il * 2) * nctx * C + h * DH;
     const bf16_t* Vs = Ks + (long)nctx * C;
-    float m = -INFINITY, l = 0.f;
-#pragma unroll
-    for (int d = 0; d < DH; ++d) o[d] = 0.f;
-    for (int j = part; j < nctx; j += SPL) {
-      float kf[DH], vf[DH];
+    auto score = [&](int j) {
+      unsigned kv[DP];
 #pragma unroll
       for (int d8 = 0; d8 < DH; d8 += 8) {
-        unpack8(*(const uint4*)(Ks + j * C + d8), kf + d8);
-        unpack8(*(const uint4*)(Vs + j * C + d8), vf + d8);
+        const uint4 a = *(const uint4*)(Ks + j * C + d8);
+        kv[d8 / 2] = a.x; kv[d8 / 2 + 1] = a.y; kv[d8 / 2 + 2] = a.z; kv[d8 / 2 + 3] = a.w;
       }
-      float s = 0.f;
+      float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-      for (int d = 0; d < DH; ++d) s += q[d] * kf[d];
-      s *= p.scale;
-      const float mn = fmaxf(m, s);
-      const float cr = __expf(m - mn), pe = __expf(s - mn);
-      l = l * cr + pe;
+      for (int i = 0; i < DP; i += 2) {
+        s0 = dot2bf(qv[i], kv[i], s0);
+        s1 = dot2bf(qv[i + 1], kv[i + 1], s1);
+      }
+      return (s0 + s1) * p.scale;
+    };
+    float m = -INFINITY, l = 0.f;
+#pragma unroll 4
+    for (int j = part; j < nctx; j += SPL) m = fmaxf(m, score(j));
+    v2f o2[DP];
 #pragma unroll
-      for (int d = 0; d < DH; ++d) o[d] = o[d] * cr + pe * vf[d];
-      m = mn;
+    for (int i = 0; i < DP; ++i) o2[i] = (v2f){0.f, 0.f};
+#pragma unroll 2
+    for (int j = part; j < nctx; j += SPL) {
+      const float pe = __expf(score(j) - m);
+      l += pe;
+#pragma unroll
+      for (int d8 = 0; d8 < DH; d8 += 8) {
+        const uint4 b = *(const uint4*)(Vs + j * C + d8);
+        const unsigned vv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          o2[d8 / 2 + k] += pe * (v2f){__uint_as_float(vv[k] << 16), __uint_as_float(vv[k] & 0xffff0000u)};
+      }
+    }
+    float o[DH];
+#pragma unroll
+    for (int i = 0; i < DP; ++i) {
+      o[2 * i] = o2[i].x;
+      o[2 * i + 1] = o2[i].y;
     }
     if constexpr (SPL > 1) {
 #pragma unroll
