@@ -118,7 +118,8 @@ def record_gemms(tr):
     from encdiff_amd import _lib as L
     calls = []
     names = ("encdiff_gemm", "encdiff_gemm_ex", "encdiff_gemm_pair", "encdiff_gemm_pair_ex", "encdiff_gemm_pair_dx",
-             "encdiff_gemm_finalize", "encdiff_wgrad_group_launch", "encdiff_st_wgrad_launch")
+             "encdiff_gemm_finalize", "encdiff_wgrad_group_launch", "encdiff_st_wgrad_launch",
+             "encdiff_st_wgrad_launch_nofold")
     orig = {n: getattr(L.lib, n) for n in names}
 
     def rec(name):
@@ -133,7 +134,8 @@ def record_gemms(tr):
             elif name == "encdiff_wgrad_group_launch":  # grouped weight gradients (blobs kept by the group)
                 from encdiff_amd import ops
                 calls.append(("group", a[0], a[1], [L.GemmArgs.from_buffer_copy(bytes(x)) for x in ops.GROUP_PROBS[a[0]]]))
-            elif name == "encdiff_st_wgrad_launch":  # a fused transformer block's weight gradients
+            elif name.startswith("encdiff_st_wgrad_launch"):  # a fused transformer block's weight gradients
+                # (replayed with its chunk fold, which the step carries in the GroupNorm backward's grid)
                 from encdiff_amd import ops
                 calls.append(("stwg", a[0], a[1], [L.GemmArgs.from_buffer_copy(bytes(x)) for x in ops.STWG_PROBS[a[0]]]))
             else:

@@ -59,7 +59,8 @@ class GroupNormArgs(C.Structure):
                 ("dgamma_part", vp), ("dbeta_part", vp), ("ld_part", C.c_long), ("dfilm", vp),
                 ("ld_dfilm", C.c_long), ("resid", vp), ("ld_resid", C.c_long), ("in_stats", vp),
                 ("ld_in_stats", C.c_long), ("x_from", vp), ("dy_resample", C.c_int), ("resid_resample", C.c_int),
-                ("w", C.c_int), ("pad_rs_", C.c_int), ("dsilu", vp), ("ld_dsilu", C.c_long)]
+                ("w", C.c_int), ("pad_rs_", C.c_int), ("dsilu", vp), ("ld_dsilu", C.c_long),
+                ("fold_plan", vp), ("fold_blocks", C.c_int), ("pad_fold_", C.c_int)]
 
 
 class LayerNormArgs(C.Structure):
@@ -239,6 +240,7 @@ _PROTOS = {
     "encdiff_st_tail_bwd_tile": [C.c_int, C.c_int, C.c_int],
     "encdiff_st_wgrad_plan": [vp, C.c_int, vp, C.c_long, vp, C.c_long, vp],
     "encdiff_st_wgrad_launch": [vp, vp, vp],
+    "encdiff_st_wgrad_launch_nofold": [vp, vp, vp, C.POINTER(vp), C.POINTER(C.c_int)],
     "encdiff_resconv_fwd": [C.POINTER(ResConvArgs), vp],
     "encdiff_resconv_query": [C.POINTER(ResConvArgs), C.POINTER(C.c_int), C.POINTER(C.c_int)],
     "encdiff_step_prologue": [C.POINTER(StepPrologueArgs), vp],

@@ -10,6 +10,7 @@
 #include <stdlib.h>
 
 #include "common.h"
+#include "stwg.h"
 
 namespace {
 
@@ -46,10 +47,10 @@ ED_DEV int gn_xcd_index(int i, int n) { return (n & 7) ? i : (i & 7) * (n >> 3) 
 struct GnSlice {
   int S, b, c0, cs, nvc, np, tv, tp, cpg, gs, g0, cb;
   bool active, tiled;
-  ED_DEV GnSlice(const EncdiffGroupNormArgs& p, int cs_, int tile_cap = GN_TILE) {
+  ED_DEV GnSlice(const EncdiffGroupNormArgs& p, int cs_, int tile_cap = GN_TILE, int nblk = 0) {
     cs = cs_;
     S = p.c / cs;
-    const int bid = gn_xcd_index(blockIdx.x, gridDim.x);
+    const int bid = gn_xcd_index(blockIdx.x, nblk ? nblk : gridDim.x);
     b = bid / S;
     c0 = (bid - b * S) * cs;
     nvc = cs >> 3;
@@ -574,9 +575,15 @@ template <bool SLAB, bool RS = false, bool DSL = false>
 __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNormArgs p, int cs, const GnSlabs sl) {
   __shared__ uint4 tx[GN_TILE], td[GN_TILE];
   __shared__ float red[4 * 2048], chs[4 * 512], gam_sh[512];
+  // workgroups past the GroupNorm's: the weight-gradient fold riding in this launch
+  const int gnb = p.batch * (p.c / cs);
+  if ((int)blockIdx.x >= gnb) {
+    stwg_fold_from_blob(p.fold_plan, blockIdx.x - gnb, (float4(*)[32])red);
+    return;
+  }
   GN_STAMP_RT(0);
   GN_STAMP(1);
-  const GnSlice L(p, cs);
+  const GnSlice L(p, cs, GN_TILE, gnb);
   const int HW = p.hw;
   const bool film = p.film != nullptr, silu = p.silu;
   const float inv_n = 1.f / ((float)HW * L.cpg);
@@ -1048,6 +1055,7 @@ extern "C" int encdiff_debug_gn_stamps(void* dst, int nblocks) {
 #endif
 
 extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream) {
+  if (a && a->dtype == ENCDIFF_DT_F32 && a->fold_plan) return ENCDIFF_ERR_UNSUPPORTED;
   if (a && a->dtype == ENCDIFF_DT_F32)
     return (a->dy_resample || a->resid_resample) ? ENCDIFF_ERR_UNSUPPORTED : ed_groupnorm_bwd_f32(a, (hipStream_t)stream);
   if (a && a->dtype != ENCDIFF_DT_BF16) return ENCDIFF_ERR_UNSUPPORTED;
@@ -1060,6 +1068,8 @@ extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream
     const int rc = gn_slabs_of(*a->x_from, a->dy, a->lddy, a, sl);
     if (rc != ENCDIFF_OK) return rc;
   }
+  if ((a->fold_plan != nullptr) != (a->fold_blocks > 0) || a->fold_blocks < 0) return ENCDIFF_ERR_ARG;
+  const int fold = a->fold_plan ? a->fold_blocks : 0;
   const bool rs = a->dy_resample || a->resid_resample;
   const bool dsl = a->silu && a->dsilu != nullptr;
   if (dsl && (((uintptr_t)a->dsilu & 15) || a->ld_dsilu % 8)) return ENCDIFF_ERR_ARG;
@@ -1072,24 +1082,24 @@ extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream
     if ((a->dy_resample == ENCDIFF_RESAMPLE_DOWN2 || a->resid_resample == ENCDIFF_RESAMPLE_DOWN2) && ((h | a->w) & 1))
       return ENCDIFF_ERR_SHAPE;
     if (dsl)
-      hipLaunchKernelGGL((gn_bwd_kernel<false, true, true>), dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0,
+      hipLaunchKernelGGL((gn_bwd_kernel<false, true, true>), dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), 0,
                          (hipStream_t)stream, *a, cs, sl);
     else
-      hipLaunchKernelGGL((gn_bwd_kernel<false, true>), dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0,
+      hipLaunchKernelGGL((gn_bwd_kernel<false, true>), dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), 0,
                          (hipStream_t)stream, *a, cs, sl);
   } else if (sl.ws) {
     if (dsl)
-      hipLaunchKernelGGL((gn_bwd_kernel<true, false, true>), dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0,
+      hipLaunchKernelGGL((gn_bwd_kernel<true, false, true>), dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), 0,
                          (hipStream_t)stream, *a, cs, sl);
     else
-      hipLaunchKernelGGL(gn_bwd_kernel<true>, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0, (hipStream_t)stream,
+      hipLaunchKernelGGL(gn_bwd_kernel<true>, dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), 0, (hipStream_t)stream,
                          *a, cs, sl);
   } else {
     if (dsl)
-      hipLaunchKernelGGL((gn_bwd_kernel<false, false, true>), dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0,
+      hipLaunchKernelGGL((gn_bwd_kernel<false, false, true>), dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), 0,
                          (hipStream_t)stream, *a, cs, sl);
     else
-      hipLaunchKernelGGL(gn_bwd_kernel<false>, dim3(a->batch * (a->c / cs)), dim3(GN_THREADS), 0,
+      hipLaunchKernelGGL(gn_bwd_kernel<false>, dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), 0,
                          (hipStream_t)stream, *a, cs, sl);
   }
   ED_CHECK_LAUNCH();

@@ -27,6 +27,7 @@
 
 #include "common.h"
 #include "st_common.h"
+#include "stwg.h"
 
 namespace {
 
@@ -806,25 +807,11 @@ int launch_head_bwd(const EncdiffStHeadBwdArgs& p, hipStream_t s) {
 // read k-outer with the gfx950 transpose read ds_read_b64_tr_b16; the 4 waves split BM.  Chunks
 // write fp32 slabs that st_wgrad_fold_kernel sums in chunk order (reproducible); a single-chunk
 // block accumulates straight into dW.
-struct StWg {
-  const bf16_t* dy; const bf16_t* x; float* dw; float* db; float* slab;
-  long ld_dy, ld_x, ld_dw;
-  int M, N, K, kc, kb, mb, nb, item0, fold0, kind, bm, bn;
-};
-struct StWgHead {
-  int magic, nprob, nitems, nfold;
-  long probs_off, bytes;
-};
-constexpr int STWG_MAGIC = 0x53545747;  // "STWG"
-constexpr int STWG_MAXP = 16;
 // (WM, WN) kinds: 16-row tiles per wave x 16-column tiles (acc WM * WN * 4 VGPRs <= 128)
 constexpr int STWG_KINDS[][2] = {{1, 4}, {1, 16}, {4, 4}, {3, 4}, {2, 8}, {2, 16}, {4, 8}, {3, 8}};
 
 #ifndef STWG_PF
 #define STWG_PF 1
-#endif
-#ifndef STWG_FOLD_UNROLL
-#define STWG_FOLD_UNROLL 4
 #endif
 #ifndef STWG_PF_TILES
 #define STWG_PF_TILES 16
@@ -986,59 +973,11 @@ __global__ __launch_bounds__(256, 2) void st_wgrad_kernel(const StWg* __restrict
   st_wgrad_dispatch<0>(p, blk % p.mb, blk / p.mb, z, smem_raw);
 }
 
-// dW += sum_z slab[z] (and db): a workgroup owns 32 float4 of one problem's dW (or 128 bias
-// entries); its 8 thread groups sum chunks z = g, g + 8, ... (independent loads in flight), and the
-// 8 group sums are added in group order through LDS -- a fixed order, reproducible
+// the fold as its own launch (encdiff_st_wgrad_launch); encdiff_st_wgrad_launch_nofold leaves it to
+// the next GroupNorm backward, whose grid carries the same blocks (norm.hip, stwg_fold_block)
 __global__ __launch_bounds__(256) void st_wgrad_fold_kernel(const StWg* __restrict__ probs, int nprob) {
   __shared__ float4 red[8][32];
-  int pi = 0;
-  for (int q = 1; q < nprob; ++q)
-    if ((int)blockIdx.x >= probs[q].fold0) pi = q;
-  const StWg p = probs[pi];
-  if (p.kb == 1) return;
-  const int g = threadIdx.x >> 5, l = threadIdx.x & 31;
-  const long n4 = (long)p.M * p.N / 4;
-  const long nw = (n4 + 31) / 32;  // workgroups of the weight part
-  const long blk = blockIdx.x - p.fold0;
-  const long MN = (long)p.M * p.N;
-  if (blk < nw) {
-    const long e = blk * 32 + l;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e < n4) {
-      const float* s = p.slab + 4 * e;
-#pragma unroll STWG_FOLD_UNROLL
-      for (int z = g; z < p.kb; z += 8) {
-        const float4 v = *(const float4*)(s + (long)z * MN);
-        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-      }
-    }
-    red[g][l] = a;
-    __syncthreads();
-    if (g == 0 && e < n4) {
-      float4 t = red[0][l];
-#pragma unroll
-      for (int k = 1; k < 8; ++k) {
-        const float4 v = red[k][l];
-        t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
-      }
-      const long m = 4 * e / p.N, n = 4 * e % p.N;
-      float* o = p.dw + m * p.ld_dw + n;
-      o[0] += t.x; o[1] += t.y; o[2] += t.z; o[3] += t.w;
-    }
-  } else if (p.db) {  // bias: 32 entries per workgroup, the same group split
-    const long m = (blk - nw) * 32 + l;
-    float a = 0.f;
-    if (m < p.M)
-      for (int z = g; z < p.kb; z += 8) a += p.slab[(long)p.kb * MN + (long)z * p.M + m];
-    red[g][l].x = a;
-    __syncthreads();
-    if (g == 0 && m < p.M) {
-      float t = red[0][l].x;
-#pragma unroll
-      for (int k = 1; k < 8; ++k) t += red[k][l].x;
-      p.db[m] += t;
-    }
-  }
+  stwg_fold_block(probs, nprob, blockIdx.x, red);
 }
 
 size_t stwg_lds(int kind) {
@@ -1185,7 +1124,8 @@ extern "C" int encdiff_st_wgrad_plan(const EncdiffWgradProb* in, int n, float* w
   return ENCDIFF_OK;
 }
 
-extern "C" int encdiff_st_wgrad_launch(const void* host_blob, const void* dev_blob, void* stream) {
+namespace {
+int stwg_launch(const void* host_blob, const void* dev_blob, void* stream, bool fold, int* nfold) {
   if (!host_blob || !dev_blob) return ENCDIFF_ERR_ARG;
   StWgHead h;
   std::memcpy(&h, host_blob, sizeof(h));
@@ -1199,7 +1139,22 @@ extern "C" int encdiff_st_wgrad_launch(const void* host_blob, const void* dev_bl
   const StWg* dp = (const StWg*)((const char*)dev_blob + h.probs_off);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(st_wgrad_kernel, dim3((unsigned)h.nitems), dim3(256), lds, s, dp, h.nprob);
-  if (h.nfold > 0) hipLaunchKernelGGL(st_wgrad_fold_kernel, dim3((unsigned)h.nfold), dim3(256), 0, s, dp, h.nprob);
+  if (fold && h.nfold > 0) hipLaunchKernelGGL(st_wgrad_fold_kernel, dim3((unsigned)h.nfold), dim3(256), 0, s, dp, h.nprob);
+  if (nfold) *nfold = h.nfold;
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
+}
+}  // namespace
+
+extern "C" int encdiff_st_wgrad_launch(const void* host_blob, const void* dev_blob, void* stream) {
+  return stwg_launch(host_blob, dev_blob, stream, true, nullptr);
+}
+
+extern "C" int encdiff_st_wgrad_launch_nofold(const void* host_blob, const void* dev_blob, void* stream,
+                                              const void** fold_plan, int* fold_blocks) {
+  if (!fold_plan || !fold_blocks) return ENCDIFF_ERR_ARG;
+  const int rc = stwg_launch(host_blob, dev_blob, stream, false, fold_blocks);
+  *fold_plan = rc == ENCDIFF_OK && *fold_blocks > 0 ? dev_blob : nullptr;
+  if (rc != ENCDIFF_OK || !*fold_plan) *fold_blocks = 0;
+  return rc;
 }

@@ -812,9 +812,11 @@ def groupnorm_fwd(x, g: Geom, gamma, beta, y, stats, eps, silu, film=None, ld_fi
 
 def groupnorm_bwd(x, g: Geom, gamma, beta, stats, eps, silu, dy, dx, dgamma_part, dbeta_part, film=None,
                   ld_film=0, dfilm=None, ld_dfilm=0, accumulate=False, groups=32, ld_part=None, resid=None,
-                  dy_from=None, dy_resample=0, resid_resample=0, dsilu=None):
+                  dy_from=None, dy_resample=0, resid_resample=0, dsilu=None, fold=None):
     """dx (+)= GN_bwd(dy) (+ resid: the block's skip-branch gradient, added in the same pass).
     dsilu: the forward's silu'(z) rows (groupnorm_fwd(dsilu=)), read instead of recomputed.
+    fold: (device plan, blocks) of StWgrad.launch(..., ride=True): that plan's chunk fold runs as
+    extra workgroups of this launch.
     dy_from: the GemmArgs of dy's producer whose finalize gemm_pair deferred (dy written here).
     dy_resample / resid_resample: dy / resid are at the resolution of that 2x resample following
     the GroupNorm (L.RESAMPLE_DOWN2 / UP2); their adjoint is applied on the fly."""
@@ -827,7 +829,8 @@ def groupnorm_bwd(x, g: Geom, gamma, beta, stats, eps, silu, dy, dx, dgamma_part
                         resid=_p(resid), ld_resid=_ld(resid) if resid is not None else 0,
                         x_from=None if dy_from is None else C.addressof(dy_from), dy_resample=dy_resample,
                         resid_resample=resid_resample, w=g.w,
-                        dsilu=_p(dsilu), ld_dsilu=_ld(dsilu) if dsilu is not None else 0)
+                        dsilu=_p(dsilu), ld_dsilu=_ld(dsilu) if dsilu is not None else 0,
+                        fold_plan=fold[0] if fold else None, fold_blocks=fold[1] if fold else 0)
     check(lib.encdiff_groupnorm_bwd(C.byref(a), _s()), "encdiff_groupnorm_bwd")
 
 
@@ -1070,8 +1073,11 @@ class StWgrad:
     def __init__(self):
         self._plans = {}
 
-    def launch(self, probs):
-        """probs: [(dy [K][M], x [K][N], dw [M][N] fp32 (+=), db [M] fp32 or None)]."""
+    def launch(self, probs, ride=False):
+        """probs: [(dy [K][M], x [K][N], dw [M][N] fp32 (+=), db [M] fp32 or None)].
+        ride=True: only the weight-gradient grid is launched; returns (device plan, fold blocks) for
+        the next GroupNorm backward to carry (groupnorm_bwd(fold=)), or None when there is no fold
+        (every problem in one chunk).  The fold must be launched before the gradients are read."""
         arr = (L.WgradProb * len(probs))(*[
             L.WgradProb(dy=_p(dy), ld_dy=_ld(dy), x=_p(x), ld_x=_ld(x), dw=_p(dw), ld_dw=_ld(dw), db=_p(db),
                         M=dy.shape[1], N=x.shape[1], K=dy.shape[0])
@@ -1092,7 +1098,13 @@ class StWgrad:
                               a=q.dy, lda=q.ld_dy, b=q.x, ldb=q.ld_x, c=q.dw, ldc=q.ld_dw, split_k=1) for q in arr]
             ent = self._plans[key] = (host, dev)
             STWG_PROBS[C.addressof(host)] = gem
-        check(lib.encdiff_st_wgrad_launch(C.addressof(ent[0]), ent[1].data_ptr(), _s()), "encdiff_st_wgrad_launch")
+        if not ride:
+            check(lib.encdiff_st_wgrad_launch(C.addressof(ent[0]), ent[1].data_ptr(), _s()), "encdiff_st_wgrad_launch")
+            return None
+        plan, nb = C.c_void_p(), C.c_int(0)
+        check(lib.encdiff_st_wgrad_launch_nofold(C.addressof(ent[0]), ent[1].data_ptr(), _s(), C.byref(plan),
+                                                 C.byref(nb)), "encdiff_st_wgrad_launch_nofold")
+        return (plan.value, nb.value) if nb.value > 0 else None
 
 
 def whole_wgrad_args(dy, x, dw, db=None):

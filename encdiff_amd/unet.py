@@ -93,15 +93,20 @@ ST_HEAD_256 = os.environ.get("ENCDIFF_ST_HEAD_256", "0") != "0"
 # training backward of the SpatialTransformers at c <= ST_BWD_MAXC as fused kernels: the tail's
 # input-gradient chain (encdiff_st_tail_bwd), the self-attention backward, the head's chain
 # (encdiff_st_head_bwd), the block's 8 weight gradients as ONE grouped launch, the GroupNorm
-# backward -- 5 launches instead of 14 (0: the per-layer launches, for A/B runs)
+# backward -- 5 launches instead of 14 (the weight-gradient fold rides in the GroupNorm backward;
+# 0: the per-layer launches, for A/B runs)
 ST_BWD = os.environ.get("ENCDIFF_ST_BWD", "1") != "0"
 ST_BWD_MAXC = int(os.environ.get("ENCDIFF_ST_BWD_MAXC", "128"))
 # the fused blocks' weight gradients: "st" (encdiff_st_wgrad: large output blocks, each operand read
 # about once, + a chunk fold), "group" (the generic grouped launch's 64 x 64 parts) or "single"
 # (standalone split-K launches), for A/B
 ST_BWD_WG = os.environ.get("ENCDIFF_ST_BWD_WG", "st")
+# ... and their chunk fold as extra workgroups of the block's GroupNorm backward (the next launch;
+# the fold is off its critical path) instead of a launch of its own (0: separate, A/B)
+ST_FOLD_RIDE = os.environ.get("ENCDIFF_ST_FOLD_RIDE", "1") != "0"
 # training forward: the SiLU GroupNorms also store silu'(z) (bf16), which their backward reads instead
-# of recomputing two transcendentals per element in its VALU-bound first pass (0: recompute, A/B)
+# of recomputing two transcendentals per element in its VALU-bound first pass -- measured slower
+# (8.93 -> 8.975 ms/step: the backward stayed at ~8.3 us per call, the forward grew), so off by default
 GN_DSILU = os.environ.get("ENCDIFF_GN_DSILU", "0") == "1"
 
 
@@ -1223,9 +1228,10 @@ class UNetExecutor:
               (S["d_t1"], S["o1"], G(tb + "attn1.to_out.0.weight"), G(tb + "attn1.to_out.0.bias")),
               (dqkv, S["n1"], self.qkv_grad[s.prefix], None),
               (S["d_t0"], S["gn"], G(s.prefix + "proj_in.weight").view(c, c), G(s.prefix + "proj_in.bias"))]
+        fold = None
         if ST_BWD_WG == "st":
             ops.flush()  # a paired launch's deferred finalize: its slabs share the workspace half
-            self._stwgk.launch(wg)
+            fold = self._stwgk.launch(wg, ride=ST_FOLD_RIDE)
         elif ST_BWD_WG == "group":
             ops.flush()
             for dy_, x_, dw, db in wg:
@@ -1236,7 +1242,8 @@ class UNetExecutor:
                 ops.linear_wgrad(dy_, x_, dw, db)
         dg, db = self.gn.parts(s.prefix + "norm.weight", c)
         ops.groupnorm_bwd(x, Geom(B, s.h, s.h), P(s.prefix + "norm.weight"), P(s.prefix + "norm.bias"), S["stg"],
-                          ST_GN_EPS, False, X["d_g"], dx, dg, db, accumulate=acc, ld_part=self.gn.ld, resid=dout)
+                          ST_GN_EPS, False, X["d_g"], dx, dg, db, accumulate=acc, ld_part=self.gn.ld, resid=dout,
+                          fold=fold)
         return True
 
     def _st_bwd(self, s: STSpec, dout, dx, acc):

@@ -292,6 +292,11 @@ typedef struct EncdiffGroupNormArgs {
      bf16 [batch*hw][c] row per pixel (ld_dsilu): the training forward writes it beside y, the backward
      reads it instead of recomputing z's two transcendentals per element (its VALU-bound pass 1) */
   void* dsilu; long ld_dsilu;
+  /* backward, optional: a device weight-gradient plan of encdiff_st_wgrad_plan whose chunk fold rides
+     in this launch as fold_blocks extra workgroups after the GroupNorm's (encdiff_st_wgrad_launch_nofold
+     launched its grid before; the fold is off the GroupNorm's critical path) -- one launch fewer per
+     fused transformer block */
+  const void* fold_plan; int fold_blocks, pad_fold_;
 } EncdiffGroupNormArgs;
 
 int encdiff_groupnorm_fwd(const EncdiffGroupNormArgs* args, void* stream);
@@ -762,6 +767,10 @@ typedef struct EncdiffWgradProb {
 int encdiff_st_wgrad_plan(const EncdiffWgradProb* probs, int n, float* workspace, long ws_floats, void* blob,
                           long capacity, long* blob_bytes);
 int encdiff_st_wgrad_launch(const void* host_blob, const void* dev_blob, void* stream);
+/* the weight-gradient grid alone (no fold): the caller hands the plan's fold to the next GroupNorm
+   backward (EncdiffGroupNormArgs.fold_plan = dev_blob, fold_blocks = *fold_blocks) */
+int encdiff_st_wgrad_launch_nofold(const void* host_blob, const void* dev_blob, void* stream, const void** fold_plan,
+                                   int* fold_blocks);
 
 /* ---------------------------------------------------------------- step prologue
  * The per-step device work in front of the training step, as ONE launch:

@@ -209,3 +209,61 @@ def test_st_wgrad_matches_torch(c, K):
     torch.cuda.synchronize()
     for (_, _, dw, db), (w1, b1) in zip(probs, out1):
         assert torch.equal(dw, w1) and (db is None or torch.equal(db, b1))
+
+
+@pytest.mark.parametrize("c,K", [(64, 32768), (128, 8192)])
+def test_st_wgrad_fold_rides_in_groupnorm_bwd(c, K):
+    """StWgrad.launch(ride=True) launches only the weight-gradient grid; its chunk fold runs as extra
+    workgroups of the next GroupNorm backward (groupnorm_bwd(fold=)).  Both results must be bitwise
+    those of the separate launches (the fold sums the chunk slabs in the same order)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from encdiff_amd import ops
+    from encdiff_amd.ops import Geom
+    dev, bf = "cuda", torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(5 * c + 1)
+    shapes = [(c, c, True), (c, 4 * c, True), (8 * c, c, True), (3 * c, c, False)]
+    probs = []
+    for M, N, has_b in shapes:
+        dy = (torch.randn(K, M, device=dev, generator=g) * 0.1).to(bf)
+        x = torch.randn(K, N, device=dev, generator=g).to(bf)
+        dw = torch.randn(M, N, device=dev, generator=g)
+        db = torch.randn(M, device=dev, generator=g) if has_b else None
+        probs.append((dy, x, dw, db))
+    init = [(dw.clone(), None if db is None else db.clone()) for _, _, dw, db in probs]
+    # a GroupNorm backward of the block's shape (B images of hw tokens, c channels)
+    hw = 256 if c == 64 else 64
+    B = K // hw
+    gg = Geom(B, int(hw ** 0.5), int(hw ** 0.5))
+    xg = (torch.randn(B * hw, c, device=dev, generator=g) + 0.3).to(bf)
+    gam = 1 + 0.1 * torch.randn(c, device=dev, generator=g)
+    bet = 0.1 * torch.randn(c, device=dev, generator=g)
+    yg = torch.empty_like(xg)
+    st = torch.empty(B, 32, 2, device=dev)
+    ops.groupnorm_fwd(xg, gg, gam, bet, yg, st, 1e-6, False)
+    dyg = (torch.randn(B * hw, c, device=dev, generator=g) * 0.1).to(bf)
+    res = []
+    for ride in (False, True):
+        for (_, _, dw, db), (w0, b0) in zip(probs, init):
+            dw.copy_(w0)
+            if db is not None:
+                db.copy_(b0)
+        dx = torch.empty_like(xg)
+        dgp = torch.empty(B, c, device=dev)
+        dbp = torch.empty(B, c, device=dev)
+        wg = ops.StWgrad()
+        fold = wg.launch(probs, ride=ride)
+        assert (fold is not None) == ride
+        ops.groupnorm_bwd(xg, gg, gam, bet, st, 1e-6, False, dyg, dx, dgp, dbp, fold=fold)
+        torch.cuda.synchronize()
+        res.append(([dw.clone() for _, _, dw, _ in probs], [None if db is None else db.clone() for *_, db in probs],
+                    dx, dgp, dbp))
+    (w0, b0, dx0, g0, be0), (w1, b1, dx1, g1, be1) = res
+    for a, b in zip(w0, w1):
+        assert torch.equal(a, b)
+    for a, b in zip(b0, b1):
+        assert (a is None and b is None) or torch.equal(a, b)
+    assert torch.equal(dx0, dx1) and torch.equal(g0, g1) and torch.equal(be0, be1)
+    # and the gradients are right: dW = W0 + dY^T X
+    for (dy, x, dw, db), (wi, bi), got in zip(probs, init, w1):
+        assert _rel(got, wi + dy.float().t() @ x.float()) < 1e-5
