@@ -367,7 +367,7 @@ __global__ __launch_bounds__(64 * NWV) void st_tail_kernel(const EncdiffStTailAr
 template <int C, int RR, int NWV>
 int launch_tail_w(const EncdiffStTailArgs& p, hipStream_t s) {
   using T = Tail<C, RR>;
-  if (p.head_n3 && (!p.head_t2 || p.save_t1 || p.gn_stats || p.ld_head % 8)) return ENCDIFF_ERR_ARG;
+  if (p.head_n3 && (!p.head_t2 || p.gn_stats || p.ld_head % 8)) return ENCDIFF_ERR_ARG;
   if (p.rows % T::R || (T::R % p.tokens && p.tokens % T::R)) return ENCDIFF_ERR_SHAPE;
   const int nimg = T::R > p.tokens ? T::R / p.tokens : 1;
   const size_t lds = T::lds_bytes(nimg, p.n_ctx);
@@ -604,7 +604,11 @@ extern "C" int encdiff_st_tail_fwd(const EncdiffStTailArgs* a, void* stream) {
                       p.save_t3, p.save_s2, p.save_s3, p.save_lse2};
   int nsave = 0;
   for (const void* q : sv) nsave += q != nullptr;
-  if (nsave != 0 && (nsave != 12 || p.ld_save % 8)) return ENCDIFF_ERR_ARG;
+  // head mode with training saves: the nine activations up to norm3 (the kernel stops there; t2 /
+  // n3 go to the save rows, which must be the head rows)
+  const bool head_save = p.head_n3 && nsave == 9 && !p.save_f && !p.save_a && !p.save_t3 &&
+                         p.save_t2 == p.head_t2 && p.save_n3 == p.head_n3 && p.ld_save == p.ld_head;
+  if (nsave != 0 && ((nsave != 12 && !head_save) || p.ld_save % 8)) return ENCDIFF_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   // row tile: 64 rows (32 at c = 256); 16 when the batch is too small for it or the tile's images'
   // concept-token K / V would not fit the LDS (the 2x2 middle block: 4 tokens per image)

@@ -930,8 +930,9 @@ def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps
     250-261) as one kernel.  w: dict of the bf16 GEMM weights / fp32 biases and LayerNorm affines
     (keys out1, b_out1, g2, be2, q2, out2, b_out2, g3, be3, ff1, b_ff1, ff2, b_ff2, po, b_po).
     save: None (inference) or a dict of the training activations (t1 n2 q2 o2 t2 n3 f a t3 s2 s3
-    lse2).  head: None or (t2, n3) -- inference only: the kernel stops after norm3 and writes t2
-    and n3 = LN3(t2) there (bf16 rows), the feed-forward and proj_out being the caller's launches.
+    lse2).  head: None or (t2, n3): the kernel stops after norm3 and writes t2 and n3 = LN3(t2)
+    there (bf16 rows), the feed-forward and proj_out being the caller's launches; in training with
+    save = the nine activations up to norm3 (t1 n2 q2 o2 t2 n3 s2 s3 lse2; t2 / n3 the head rows).
     Returns False when the shape is outside the fused kernel's support (the caller issues the
     separate launches); any other error raises."""
     a = L.StTailArgs(rows=rows, c=c, tokens=tokens, heads=heads, n_ctx=n_ctx, ln_eps=ln_eps,
@@ -946,10 +947,12 @@ def st_tail_fwd(o1, t0, x, k2, v2, w, out, rows, c, tokens, heads, n_ctx, ln_eps
                      w_po=_p(w["po"]), ld_po=_ld(w["po"]), b_po=_p(w["b_po"]), out=_p(out), ld_out=_ld(out))
     if save is not None:
         for k in ("t1", "n2", "q2", "o2", "t2", "n3", "f", "a", "t3", "s2", "s3", "lse2"):
-            setattr(a, "save_" + k, _p(save[k]))
+            if k in save:
+                setattr(a, "save_" + k, _p(save[k]))
         a.ld_save = _ld(save["t1"])
     if head is not None:
-        assert save is None and gn_stats is None
+        # training (save): the nine activations up to norm3, t2 / n3 being the head rows
+        assert gn_stats is None and (save is None or (save["t2"] is head[0] and save["n3"] is head[1]))
         a.head_t2, a.head_n3, a.ld_head = _p(head[0]), _p(head[1]), _ld(head[1])
         assert _ld(head[0]) == a.ld_head
     if gn_stats is not None:  # the next GroupNorm's producer statistics of out

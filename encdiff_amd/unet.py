@@ -86,6 +86,8 @@ ST_TAIL_TRAIN = os.environ.get("ENCDIFF_ST_TAIL_TRAIN", "1") != "0"
 ST_TAIL_HEAD = os.environ.get("ENCDIFF_ST_TAIL_HEAD", "1") != "0"
 ST_TAIL_HEAD_MAXC = int(os.environ.get("ENCDIFF_ST_TAIL_HEAD_MAXC", "256"))
 ST_TAIL_HEAD_MAX_B = int(os.environ.get("ENCDIFF_ST_TAIL_HEAD_MAX_B", "32"))
+# ... and in the training forward, saving the activations up to norm3 for the (unfused) backward
+ST_TAIL_HEAD_TRAIN = os.environ.get("ENCDIFF_ST_TAIL_HEAD_TRAIN", "1") != "0"
 # ... and their head (GroupNorm statistics from x, proj_in, norm1, q/k/v) as one kernel too: off by
 # default -- DDIM B=8 716 -> 705 steps/s with it (8 workgroups at the 4x4 level each stream the
 # 512 KB of proj_in + q/k/v weights; the GroupNorm + GEMM + LayerNorm + GEMM launches spread them)
@@ -878,6 +880,11 @@ class UNetExecutor:
                 and B <= ST_TAIL_HEAD_MAX_B
                 and ops.st_tail_fwd(S["o1"], S["t0"], x, k2, v2, self._tail_weights(s), S["out"], B * ntok, c,
                                     ntok, s.heads, self.lu, LN_EPS, head=(S["t2"], S["n3"]))):
+            return self._st_ff(s, x, S)
+        if (ST_TAIL_FUSED and ST_TAIL_HEAD_TRAIN and not self.infer and ST_TAIL_MAXC < c <= ST_TAIL_HEAD_MAXC
+                and ops.st_tail_fwd(S["o1"], S["t0"], x, k2, v2, self._tail_weights(s), S["out"], B * ntok, c,
+                                    ntok, s.heads, self.lu, LN_EPS, head=(S["t2"], S["n3"]),
+                                    save={k: S[k] for k in ("t1", "n2", "q2", "o2", "t2", "n3", "s2", "s3", "lse2")})):
             return self._st_ff(s, x, S)
         # cross-attention to the concept tokens (norm2 in the to_out epilogue, or at inference for
         # wide blocks in to_q's A staging)
