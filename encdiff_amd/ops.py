@@ -59,6 +59,10 @@ _RETIRED = []  # outgrown scratch stays allocated: graphs captured earlier still
 SPLIT_FOLD = int(os.environ.get("ENCDIFF_SPLIT_FOLD", "1"))
 WS_FLOATS = 64 * 1024 * 1024         # fp32 split-K scratch per device, 256 MB (two halves, see gemm_pair)
 WS_HALF = WS_FLOATS // 2
+# the fused transformer blocks' grouped weight-gradient slabs (StWgrad): a scratch of their own, so
+# a paired launch's deferred finalize (whose slabs sit in a split-K workspace half) can stay pending
+# across a fused block's backward instead of being flushed as a launch of its own
+STWG_WS_FLOATS = 24 * 1024 * 1024    # 96 MB (c = 64 / 128 at B = 128: 42 MB; larger batches: longer chunks)
 COUNTERS = 1 << 16                   # split-K tickets per device (one int per output tile)
 _TILES = None
 _TILE_SHAPES = {1: (128, 128), 2: (128, 64), 3: (64, 128), 4: (64, 64)}
@@ -1071,7 +1075,8 @@ class StWgrad:
     """The weight gradients of a fused transformer block's Linear layers (encdiff_st_wgrad_*: one
     grid of large output blocks + a chunk fold), planned once per distinct problem list (the
     executor's buffers are static per batch size) and kept for the life of the object: captured
-    graphs read the device description at replay.  Slabs live in the workspace's second half."""
+    graphs read the device description at replay.  Slabs live in a scratch of their own
+    (STWG_WS_FLOATS), not in the split-K workspace halves."""
 
     def __init__(self):
         self._plans = {}
@@ -1090,12 +1095,13 @@ class StWgrad:
         if ent is None:
             if torch.cuda.is_current_stream_capturing():
                 raise RuntimeError("encdiff_st_wgrad first planned inside a graph capture: run an eager step first")
-            ws = _workspace().data_ptr() + 4 * WS_HALF
+            ws = scratch("stwg_ws", STWG_WS_FLOATS).data_ptr()
             nb = C.c_long(0)
-            check(lib.encdiff_st_wgrad_plan(arr, len(probs), ws, WS_HALF, None, 0, C.byref(nb)), "encdiff_st_wgrad_plan")
-            host = (C.c_longlong * ((nb.value + 7) // 8))()
-            check(lib.encdiff_st_wgrad_plan(arr, len(probs), ws, WS_HALF, C.addressof(host), C.sizeof(host), C.byref(nb)),
+            check(lib.encdiff_st_wgrad_plan(arr, len(probs), ws, STWG_WS_FLOATS, None, 0, C.byref(nb)),
                   "encdiff_st_wgrad_plan")
+            host = (C.c_longlong * ((nb.value + 7) // 8))()
+            check(lib.encdiff_st_wgrad_plan(arr, len(probs), ws, STWG_WS_FLOATS, C.addressof(host), C.sizeof(host),
+                                            C.byref(nb)), "encdiff_st_wgrad_plan")
             dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(torch.cuda.current_device())
             gem = [L.GemmArgs(M=q.M, N=q.N, K=q.K, a_mode=L.OPA_ROWM, b_mode=L.OPB_ROWN, c_mode=L.OUT_F32_ACCUM,
                               a=q.dy, lda=q.ld_dy, b=q.x, ldb=q.ld_x, c=q.dw, ldc=q.ld_dw, split_k=1) for q in arr]

@@ -1237,7 +1237,7 @@ class UNetExecutor:
               (S["d_t0"], S["gn"], G(s.prefix + "proj_in.weight").view(c, c), G(s.prefix + "proj_in.bias"))]
         fold = None
         if ST_BWD_WG == "st":
-            ops.flush()  # a paired launch's deferred finalize: its slabs share the workspace half
+            # (slabs in a scratch of their own: a paired launch's deferred finalize stays pending)
             fold = self._stwgk.launch(wg, ride=ST_FOLD_RIDE)
         elif ST_BWD_WG == "group":
             ops.flush()
