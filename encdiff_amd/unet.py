@@ -690,9 +690,7 @@ class UNetExecutor:
     def _layer_fwd(self, layer, x):
         if isinstance(layer, ResSpec):
             return self._res_fwd(layer, x)
-        ops.finalize(self._pend)  # the transformer reads x directly
-        self._pend = None
-        return self._st_fwd(layer, x)
+        return self._st_fwd(layer, x)  # (it takes or finalizes a pending finalize of x)
 
     def _res_fwd(self, r: ResSpec, x):
         """openaimodel_enc.py:255-275 with use_scale_shift_norm."""
@@ -839,6 +837,13 @@ class UNetExecutor:
         in_st = self._gst(x)
         # inference at sampling batches: the fused head computes the GroupNorm statistics itself
         self_st = hfused and in_st is None and self.infer and AGN and B <= AGN_MAX_B
+        # x's producer deferred its split-K finalize: the unfused head's self-reducing GroupNorm
+        # combines the slabs (and writes x); every other path reads x directly, so it is finalized now
+        pend, self._pend = self._pend, None
+        x_from = pend if (pend is not None and not hfused and in_st is None and pend.c == x.data_ptr()
+                          and pend.N == x.shape[1] and pend.ldc == x.stride(0)) else None
+        if x_from is None:
+            ops.finalize(pend)
         if hfused and in_st is None and not self_st:  # no producer statistics: the GroupNorm kernel reduces them
             ops.groupnorm_fwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["gn"],
                               S["stg"], ST_GN_EPS, False)
@@ -851,7 +856,8 @@ class UNetExecutor:
                 n1=None if self.infer else S["n1"], s1=None if self.infer else S["s1"], self_stats=self_st)):
             if not hfused or in_st is not None or self_st:
                 ops.groupnorm_fwd(x, g, self.P(s.prefix + "norm.weight"), self.P(s.prefix + "norm.bias"), S["gn"],
-                                  S["stg"], ST_GN_EPS, False, in_stats=in_st)
+                                  S["stg"], ST_GN_EPS, False, in_stats=in_st, x_from=x_from)
+                x_from = None
             if lna:  # norm1 applied in q/k/v's A staging (no LayerNorm launch)
                 ops.linear_fwd(S["gn"], self.W(s.prefix + "proj_in.weight"), S["t0"],
                                bias=self.P(s.prefix + "proj_in.bias"))
@@ -863,6 +869,7 @@ class UNetExecutor:
                                   self.P(tb + "norm1.bias"), S["n1"], S["s1"], LN_EPS,
                                   bias=self.P(s.prefix + "proj_in.bias"))
                 ops.linear_fwd(S["n1"], self.W(s.prefix + "qkv"), S["qkv"])
+        assert x_from is None, "a deferred finalize of the transformer input was neither combined nor run"
         q, k, v = S["qkv"][:, :c], S["qkv"][:, c:2 * c], S["qkv"][:, 2 * c:]
         ops.attention_fwd(q, k, v, S["o1"], S["lse1"], B, s.heads, ntok, ntok, s.dh, fp8=s.fp8)
         k2 = self.KV[:, s.kv_off:s.kv_off + c]
