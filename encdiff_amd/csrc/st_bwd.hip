@@ -692,12 +692,10 @@ int launch_tail_bwd_mf(const EncdiffStTailBwdArgs& p, hipStream_t s) {
 
 template <int C, int R>
 int launch_tail_bwd(const EncdiffStTailBwdArgs& p, hipStream_t s) {
-  using T = TailBwd<C, R>;
   if (p.tokens % R || p.rows % R) return ENCDIFF_ERR_SHAPE;
   if (p.rows / R > p.part_rows) return ENCDIFF_ERR_SHAPE;
   if (p.tokens / R > 1 && (!p.kv_part || ((uintptr_t)p.kv_part & 15))) return ENCDIFF_ERR_ARG;
   if ((long)(p.rows / R) * p.n_ctx * 2 * C * 4 >= 0x7FFFFFF0L) return ENCDIFF_ERR_SHAPE;
-  (void)sizeof(T);
   return tail_bwd_mf<C, R>(p.n_ctx) ? launch_tail_bwd_mf<C, R, true>(p, s) : launch_tail_bwd_mf<C, R, false>(p, s);
 }
 
