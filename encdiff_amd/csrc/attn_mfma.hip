@@ -403,8 +403,11 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
     }
   };
   if (KR == SKP) {  // every head's K / V resident: waves loop over their tasks
+    // (tasks split over blockIdx.y when the host spread a small grid over query blocks: workgroup
+    // y takes tasks y, y + nqb, ...)
+    const int ty = blockIdx.y, tny = gridDim.y, t0 = ty + tny * wave;
     // the first task's Q loads are issued with the K / V staging loads (one round trip)
-    if (wave < hpb * npairs) init(wave);
+    if (t0 < hpb * npairs) init(t0);
     if (tid < hpb) kn[tid] = 0.f;
     stage_kv_u<DH, DP, 2, ONES>((const bf16_t*)p.k, p.ldk, (const bf16_t*)p.v, p.ldv, SK, SKP, H, bh0, hpb, Ks, Vs,
                                 SKP * DP, 0);
@@ -420,8 +423,8 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const EncdiffAttnArgs p, in
       }
       __syncthreads();
     }
-    for (int task = wave; task < hpb * npairs; task += 4) {
-      if (task != wave) init(task);
+    for (int task = t0; task < hpb * npairs; task += 4 * tny) {
+      if (task != t0) init(task);
       if constexpr (F8 || DH > 32) {
         consume(BoundTag<false>{}, 0, SKP);
       } else {
@@ -949,6 +952,9 @@ int mfma_hpb(const EncdiffAttnArgs& a) {
   return hpb;
 }
 
+#ifndef ATTN_FWD_QSPLIT
+#define ATTN_FWD_QSPLIT 1
+#endif
 template <int DH, bool F8>
 int launch_mfma_fwd(const EncdiffAttnArgs& a, hipStream_t s) {
   constexpr int DP = DH < 16 ? 16 : DH;
@@ -966,6 +972,15 @@ int launch_mfma_fwd(const EncdiffAttnArgs& a, hipStream_t s) {
     const int npairs = (((a.sq + 15) >> 4) + NT - 1) / NT;
     nqb = (npairs + 3) / 4;
     lds = (size_t)2 * kch * DP * sizeof(bf16_t);
+  }
+  // wide single-head blocks with few (image, head) workgroups (the VQ AttnBlock at 16x16: 128
+  // workgroups of 128 KB K / V): query tasks spread over blockIdx.y, each workgroup staging the
+  // head's K / V, so every CU takes one (up to 4 tasks per workgroup, one per wave)
+  if (nqb == 1 && DH >= 64 && hpb == 1 && ATTN_FWD_QSPLIT) {
+    constexpr int NT = fwd_tiles_per_task(DH);
+    const int npairs = (((a.sq + 15) >> 4) + NT - 1) / NT;
+    const int nx = a.batch * a.heads;
+    while (nqb * 2 * nx <= 256 && npairs >= 4 * nqb * 2) nqb *= 2;
   }
   const dim3 grid(a.batch * a.heads / hpb, nqb);
   const bool mask = a.sk % 32 != 0;
