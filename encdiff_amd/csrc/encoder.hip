@@ -300,7 +300,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* r, long ldr,
     const int b = blockIdx.x;
     for (int j = threadIdx.x; j < UM; j += 256) sdu[j] = j < units ? du[(long)b * lddu + j] : 0.f;
     __syncthreads();
-    for (int k = threadIdx.x; k < K; k += 256) {
+#pragma unroll 4
+    for (int k = threadIdx.x; k < K; k += 256) {  // (4 outputs' W loads in flight per thread)
       const int c = k / HPIX, p = k - c * HPIX;
       float a = 0.f;
 #pragma unroll
@@ -309,9 +310,33 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* r, long ldr,
     }
     return;
   }
+  // a dW block: 64 channels c of one pixel p (k = c * HPIX + p), lanes channel-fastest so the rows
+  // of r are read coalesced (256 B per wave per image instead of one 64-B line per lane)
   const int blk = blockIdx.x - batch;
+  if (blk == (int)gridDim.x - batch - 1) {
+    // the last workgroup: db = sum over images of du, 4 image groups per unit summed in parallel
+    // (16 loads in flight per thread) and the group sums added in group order -- a fixed order
+    const int j = threadIdx.x & 63, gi = threadIdx.x >> 6, per = (batch + 3) / 4;
+    const int i0 = gi * per, i1 = min(batch, i0 + per);
+    float a = 0.f;
+    if (j < units) {
+#pragma unroll 16
+      for (int b = i0; b < i1; ++b) a += du[(long)b * lddu + j];
+    }
+    sdu[gi * 64 + j] = a;
+    __syncthreads();
+    if (threadIdx.x < units) {
+      float t = sdu[threadIdx.x];
+#pragma unroll
+      for (int k = 1; k < 4; ++k) t += sdu[k * 64 + threadIdx.x];
+      db[threadIdx.x] += t;
+    }
+    return;
+  }
   const int kl = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int k = blk * 64 + kl;
+  const int pp = blk % HPIX, cc = (blk / HPIX) * 64 + kl;
+  const bool kv = cc < d;
+  const int k = cc * HPIX + pp;
   const int qb = (batch + 3) / 4, b0 = q * qb, b1 = min(batch, b0 + qb);
   float acc[UM];  // UM >= units, compile-time indices only (registers)
 #pragma unroll
@@ -321,17 +346,17 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* r, long ldr,
   for (int c0 = 0; c0 < batch; c0 += HEAD_CB) {
     const int c1 = min(batch, c0 + HEAD_CB);
     __syncthreads();  // the previous chunk is consumed
-    for (int e = threadIdx.x; e < (c1 - c0) * UM; e += 256) {
+#pragma unroll 8
+    for (int e = threadIdx.x; e < (c1 - c0) * UM; e += 256) {  // (loads in flight, not one per round trip)
       const int b = e / UM, j = e - b * UM;
       sdu[e] = j < units ? du[(long)(c0 + b) * lddu + j] : 0.f;
     }
     __syncthreads();
-    if (k < K) {
-      const int c = k / HPIX, p = k - c * HPIX;
+    if (kv) {
       const int bs = max(b0, c0), be = min(b1, c1);
 #pragma unroll 8
       for (int b = bs; b < be; ++b) {
-        const float xv = r[((long)b * HPIX + p) * ldr + c];
+        const float xv = r[((long)b * HPIX + pp) * ldr + cc];
 #pragma unroll
         for (int j = 0; j < UM; ++j) acc[j] += sdu[(b - c0) * UM + j] * xv;
       }
@@ -342,17 +367,12 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* r, long ldr,
 #pragma unroll
   for (int j = 0; j < UM; ++j) part[(q * UM + j) * 64 + kl] = acc[j];
   __syncthreads();
-  if (q == 0 && k < K) {
+  if (q == 0 && kv) {
 #pragma unroll
     for (int j = 0; j < UM; ++j)
       if (j < units)
         dW[(long)j * K + k] += ((part[j * 64 + kl] + part[(UM + j) * 64 + kl]) + part[(2 * UM + j) * 64 + kl]) +
                                part[(3 * UM + j) * 64 + kl];
-  }
-  if (blk == 0 && threadIdx.x < units) {
-    float a = 0.f;
-    for (int b = 0; b < batch; ++b) a += du[(long)b * lddu + threadIdx.x];
-    db[threadIdx.x] += a;
   }
 }
 
@@ -375,9 +395,9 @@ extern "C" int encdiff_encoder_head_bwd(const float* r, long ldr, int batch, int
   const int um = units <= 20 ? 20 : (units <= 40 ? 40 : 64);
   size_t lds = (size_t)(batch < HEAD_CB ? batch : HEAD_CB) * um * sizeof(float);
   if (lds < (size_t)4 * um * 64 * sizeof(float)) lds = (size_t)4 * um * 64 * sizeof(float);  // <= 64 KB
-  const int kb = (d * HPIX + 63) / 64;
+  const int kb = HPIX * ((d + 63) / 64);  // dW blocks: (64-channel chunk, pixel)
   auto kern = units <= 20 ? head_bwd_kernel<20> : (units <= 40 ? head_bwd_kernel<40> : head_bwd_kernel<64>);
-  hipLaunchKernelGGL(kern, dim3(batch + kb), dim3(256), lds, (hipStream_t)stream, r, ldr, d, W, units, batch, du, lddu,
+  hipLaunchKernelGGL(kern, dim3(batch + kb + 1), dim3(256), lds, (hipStream_t)stream, r, ldr, d, W, units, batch, du, lddu,
                      (bf16_t*)dr, lddr, dW, db);
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
