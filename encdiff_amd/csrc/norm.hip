@@ -23,6 +23,9 @@ namespace {
 #ifndef ED_LN_BWD_U
 #define ED_LN_BWD_U 2  // LayerNorm backward rows per thread in flight (4 measured slower: 9.09 -> 9.11 ms/step)
 #endif
+#ifndef GN_BWD_LDS_FULL
+#define GN_BWD_LDS_FULL 0
+#endif
 #ifndef ED_GN_BWD_U
 #define ED_GN_BWD_U 4  // backward rows per load batch (code size vs loads in flight)
 #endif
@@ -571,10 +574,19 @@ ED_DEV int gn_rs_hw(int mode, int hw) { return mode == ENCDIFF_RESAMPLE_DOWN2 ? 
 // RS: the resampled-operand variant (dy and / or resid through gn_resample_adj); separate so the
 // common instantiations keep their registers
 // DSL: the SiLU gradient is read from the forward's dsilu rows instead of recomputed from z
+// LDS is dynamic, sized per launch (gn_bwd_lds): the pixel tiles only where pass 2 reads them (not
+// for register-cached single-batch slices), the reduction rows for the slice's channel count -- a
+// few KB for most UNet calls instead of a static ~74 KB, so the launch packs more workgroups per
+// CU (the weight-gradient fold riding in it included)
 template <bool SLAB, bool RS = false, bool DSL = false>
-__global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNormArgs p, int cs, const GnSlabs sl) {
-  __shared__ uint4 tx[GN_TILE], td[GN_TILE];
-  __shared__ float red[4 * 2048], chs[4 * 512], gam_sh[512];
+__global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNormArgs p, int cs, const GnSlabs sl,
+                                                            int ntile, int nred) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char gn_smem[];
+  uint4* tx = (uint4*)gn_smem;   // [ntile] x rows of the slice (tiled pass 2)
+  uint4* td = tx + ntile;        // [ntile] dy rows
+  float* red = (float*)(td + ntile);  // [nred] reduction rows, then the group-term scratch
+  float* chs = red + nred;            // [2][cs] channel totals
+  float* gam_sh = chs + 2 * cs;       // [cs]
   // workgroups past the GroupNorm's: the weight-gradient fold riding in this launch
   const int gnb = p.batch * (p.c / cs);
   if ((int)blockIdx.x >= gnb) {
@@ -583,7 +595,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_bwd_kernel(const EncdiffGroupNo
   }
   GN_STAMP_RT(0);
   GN_STAMP(1);
-  const GnSlice L(p, cs, GN_TILE, gnb);
+  const GnSlice L(p, cs, ntile, gnb);
   const int HW = p.hw;
   const bool film = p.film != nullptr, silu = p.silu;
   const float inv_n = 1.f / ((float)HW * L.cpg);
@@ -1072,6 +1084,35 @@ extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream
   const int fold = a->fold_plan ? a->fold_blocks : 0;
   const bool rs = a->dy_resample || a->resid_resample;
   const bool dsl = a->silu && a->dsilu != nullptr;
+  // dynamic LDS: pixel tiles only where pass 2 reads them (not register-cached single-batch slices,
+  // gn_bwd_kernel's `one`), reduction rows (slice_partials: 4 wave rows for power-of-two vector
+  // counts, one per pixel lane otherwise; >= the group-term scratch [2][cs] + [2][64] and the fold's
+  // [8][32] float4)
+  const int nvc = cs / 8, np = GN_THREADS / nvc;
+  const bool one = !sl.ws && a->hw <= ED_GN_BWD_U * np;
+  const int ntile = (!one && nvc * a->hw <= GN_TILE) ? nvc * a->hw : 0;
+  const bool pow2 = (nvc & (nvc - 1)) == 0;
+  const int rows = pow2 ? (nvc >= 64 ? GN_THREADS / nvc : GN_THREADS / 64) : np;
+  int nred = std::max(rows * 2 * cs, 2 * cs + 128);
+  if (a->fold_plan) nred = std::max(nred, 8 * 32 * 4);
+  nred = (nred + 3) & ~3;
+#if GN_BWD_LDS_FULL  // A/B: the former static sizing (tiles for every tiled slice, 8192 reduction floats)
+  const int ntile_ = nvc * a->hw <= GN_TILE ? GN_TILE : 0;
+  nred = 4 * 2048;
+#else
+  const int ntile_ = ntile;
+#endif
+  const size_t lds = (size_t)2 * ntile_ * 16 + (size_t)(nred + 3 * cs) * 4;
+  if (lds > 160 * 1024) return ENCDIFF_ERR_SHAPE;
+  static const bool attr_ok = [] {
+    const void* ks[] = {(const void*)gn_bwd_kernel<false>, (const void*)gn_bwd_kernel<true>,
+                        (const void*)gn_bwd_kernel<false, true>, (const void*)gn_bwd_kernel<false, false, true>,
+                        (const void*)gn_bwd_kernel<true, false, true>, (const void*)gn_bwd_kernel<false, true, true>};
+    bool ok = true;
+    for (const void* k : ks) ok = ok && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    return ok;
+  }();
+  if (!attr_ok) return ENCDIFF_ERR_LAUNCH;
   if (dsl && (((uintptr_t)a->dsilu & 15) || a->ld_dsilu % 8)) return ENCDIFF_ERR_ARG;
   if (rs) {  // operands at a following resample's resolution (read through its adjoint)
     auto ok_mode = [](int m) { return m == 0 || m == ENCDIFF_RESAMPLE_DOWN2 || m == ENCDIFF_RESAMPLE_UP2; };
@@ -1082,25 +1123,25 @@ extern "C" int encdiff_groupnorm_bwd(const EncdiffGroupNormArgs* a, void* stream
     if ((a->dy_resample == ENCDIFF_RESAMPLE_DOWN2 || a->resid_resample == ENCDIFF_RESAMPLE_DOWN2) && ((h | a->w) & 1))
       return ENCDIFF_ERR_SHAPE;
     if (dsl)
-      hipLaunchKernelGGL((gn_bwd_kernel<false, true, true>), dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), 0,
-                         (hipStream_t)stream, *a, cs, sl);
+      hipLaunchKernelGGL((gn_bwd_kernel<false, true, true>), dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), lds,
+                         (hipStream_t)stream, *a, cs, sl, ntile_, nred);
     else
-      hipLaunchKernelGGL((gn_bwd_kernel<false, true>), dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), 0,
-                         (hipStream_t)stream, *a, cs, sl);
+      hipLaunchKernelGGL((gn_bwd_kernel<false, true>), dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), lds,
+                         (hipStream_t)stream, *a, cs, sl, ntile_, nred);
   } else if (sl.ws) {
     if (dsl)
-      hipLaunchKernelGGL((gn_bwd_kernel<true, false, true>), dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), 0,
-                         (hipStream_t)stream, *a, cs, sl);
+      hipLaunchKernelGGL((gn_bwd_kernel<true, false, true>), dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), lds,
+                         (hipStream_t)stream, *a, cs, sl, ntile_, nred);
     else
-      hipLaunchKernelGGL(gn_bwd_kernel<true>, dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), 0, (hipStream_t)stream,
-                         *a, cs, sl);
+      hipLaunchKernelGGL(gn_bwd_kernel<true>, dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), lds, (hipStream_t)stream,
+                         *a, cs, sl, ntile_, nred);
   } else {
     if (dsl)
-      hipLaunchKernelGGL((gn_bwd_kernel<false, false, true>), dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), 0,
-                         (hipStream_t)stream, *a, cs, sl);
+      hipLaunchKernelGGL((gn_bwd_kernel<false, false, true>), dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), lds,
+                         (hipStream_t)stream, *a, cs, sl, ntile_, nred);
     else
-      hipLaunchKernelGGL(gn_bwd_kernel<false>, dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), 0,
-                         (hipStream_t)stream, *a, cs, sl);
+      hipLaunchKernelGGL(gn_bwd_kernel<false>, dim3(a->batch * (a->c / cs) + fold), dim3(GN_THREADS), lds,
+                         (hipStream_t)stream, *a, cs, sl, ntile_, nred);
   }
   ED_CHECK_LAUNCH();
   return ENCDIFF_OK;
