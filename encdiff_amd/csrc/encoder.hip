@@ -286,7 +286,11 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* r, long ldr,
 // image each (thread per column k, the image's du in LDS); the remaining blocks own 64 weight
 // columns each, 4 batch quarters per column (256 threads): dW[j][k] += sum_b du[b][j] x[b][k], the
 // quarters added in order through LDS (deterministic, no atomics); the first of them adds db.
-constexpr int HEAD_CB = 256;  // images of du staged in LDS at a time by the dW blocks
+constexpr int HEAD_CB = 256;
+constexpr int HEAD_CW = 16;  // channels per weight-gradient workgroup (x 16 image groups)
+#ifndef HEADBWD_SKIP
+#define HEADBWD_SKIP 0  // timing builds only (tools/head_bwd_bench.py): 1 no dr blocks, 2 no dW blocks, 4 no db
+#endif  // images of du staged in LDS at a time by the dW blocks
 
 template <int UM>
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float* r, long ldr, int d, const float* W, int units,
@@ -297,6 +301,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* r, long ldr,
   // loads are never predicated (a runtime-conditional load is branched around and waited for one
   // at a time): du is zero-padded to UM units in LDS, W rows beyond `units` clamp to row 0
   if ((int)blockIdx.x < batch) {
+    if (HEADBWD_SKIP & 1) return;
     const int b = blockIdx.x;
     for (int j = threadIdx.x; j < UM; j += 256) sdu[j] = j < units ? du[(long)b * lddu + j] : 0.f;
     __syncthreads();
@@ -314,6 +319,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* r, long ldr,
   // of r are read coalesced (256 B per wave per image instead of one 64-B line per lane)
   const int blk = blockIdx.x - batch;
   if (blk == (int)gridDim.x - batch - 1) {
+    if (HEADBWD_SKIP & 4) return;
     // the last workgroup: db = sum over images of du, 4 image groups per unit summed in parallel
     // (16 loads in flight per thread) and the group sums added in group order -- a fixed order
     const int j = threadIdx.x & 63, gi = threadIdx.x >> 6, per = (batch + 3) / 4;
@@ -333,23 +339,27 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* r, long ldr,
     }
     return;
   }
-  const int kl = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int pp = blk % HPIX, cc = (blk / HPIX) * 64 + kl;
+  if (HEADBWD_SKIP & 2) return;
+  // 16 channels x 16 image groups per workgroup (4 x the workgroups of 64-channel blocks, a quarter
+  // of the per-thread image chain); the group partials are added in group order -- a fixed order
+  constexpr int CW = HEAD_CW, NG = 256 / CW;
+  const int kl = threadIdx.x % CW, q = threadIdx.x / CW;
+  const int pp = blk % HPIX, cc = (blk / HPIX) * CW + kl;
   const bool kv = cc < d;
   const int k = cc * HPIX + pp;
-  const int qb = (batch + 3) / 4, b0 = q * qb, b1 = min(batch, b0 + qb);
+  const int qb = (batch + NG - 1) / NG, b0 = q * qb, b1 = min(batch, b0 + qb);
   float acc[UM];  // UM >= units, compile-time indices only (registers)
 #pragma unroll
   for (int j = 0; j < UM; ++j) acc[j] = 0.f;
-  // du staged HEAD_CB images at a time (any batch fits the LDS); each quarter still adds its images
+  // du staged HEAD_CB images at a time (any batch fits the LDS); each group still adds its images
   // in increasing order, so the chunking does not change a bit of the result
   for (int c0 = 0; c0 < batch; c0 += HEAD_CB) {
     const int c1 = min(batch, c0 + HEAD_CB);
     __syncthreads();  // the previous chunk is consumed
 #pragma unroll 8
     for (int e = threadIdx.x; e < (c1 - c0) * UM; e += 256) {  // (loads in flight, not one per round trip)
-      const int b = e / UM, j = e - b * UM;
-      sdu[e] = j < units ? du[(long)(c0 + b) * lddu + j] : 0.f;
+      const int b = e / UM, jj = e - b * UM;
+      sdu[e] = jj < units ? du[(long)(c0 + b) * lddu + jj] : 0.f;
     }
     __syncthreads();
     if (kv) {
@@ -358,21 +368,22 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* r, long ldr,
       for (int b = bs; b < be; ++b) {
         const float xv = r[((long)b * HPIX + pp) * ldr + cc];
 #pragma unroll
-        for (int j = 0; j < UM; ++j) acc[j] += sdu[(b - c0) * UM + j] * xv;
+        for (int jj = 0; jj < UM; ++jj) acc[jj] += sdu[(b - c0) * UM + jj] * xv;
       }
     }
   }
   __syncthreads();  // sdu is reused for the partials
-  float* part = sdu;  // [4][UM][64]
+  float* part = sdu;  // [NG][UM][CW]
 #pragma unroll
-  for (int j = 0; j < UM; ++j) part[(q * UM + j) * 64 + kl] = acc[j];
+  for (int jj = 0; jj < UM; ++jj) part[(q * UM + jj) * CW + kl] = acc[jj];
   __syncthreads();
-  if (q == 0 && kv) {
+  for (int e = threadIdx.x; e < units * CW; e += 256) {
+    const int jj = e / CW, kc = e - jj * CW, c2 = (blk / HPIX) * CW + kc;
+    if (c2 >= d) continue;
+    float t = part[jj * CW + kc];
 #pragma unroll
-    for (int j = 0; j < UM; ++j)
-      if (j < units)
-        dW[(long)j * K + k] += ((part[j * 64 + kl] + part[(UM + j) * 64 + kl]) + part[(2 * UM + j) * 64 + kl]) +
-                               part[(3 * UM + j) * 64 + kl];
+    for (int g = 1; g < NG; ++g) t += part[(g * UM + jj) * CW + kc];
+    dW[(long)jj * K + c2 * HPIX + pp] += t;
   }
 }
 
@@ -395,7 +406,7 @@ extern "C" int encdiff_encoder_head_bwd(const float* r, long ldr, int batch, int
   const int um = units <= 20 ? 20 : (units <= 40 ? 40 : 64);
   size_t lds = (size_t)(batch < HEAD_CB ? batch : HEAD_CB) * um * sizeof(float);
   if (lds < (size_t)4 * um * 64 * sizeof(float)) lds = (size_t)4 * um * 64 * sizeof(float);  // <= 64 KB
-  const int kb = HPIX * ((d + 63) / 64);  // dW blocks: (64-channel chunk, pixel)
+  const int kb = HPIX * ((d + HEAD_CW - 1) / HEAD_CW);  // dW blocks: (channel chunk, pixel)
   auto kern = units <= 20 ? head_bwd_kernel<20> : (units <= 40 ? head_bwd_kernel<40> : head_bwd_kernel<64>);
   hipLaunchKernelGGL(kern, dim3(batch + kb + 1), dim3(256), lds, (hipStream_t)stream, r, ldr, d, W, units, batch, du, lddu,
                      (bf16_t*)dr, lddr, dW, db);
