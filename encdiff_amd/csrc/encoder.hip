@@ -274,18 +274,18 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* r, long ldr,
   const float* w = W + (long)j * K;
   float a = 0.f;
 #pragma unroll 8
-  for (int k = lane; k < K; k += 64) {
-    const int c = k / HPIX, p = k - c * HPIX;
-    a += x[(long)p * ldr + c] * w[k];
+  for (int e = lane; e < K; e += 64) {  // channel-fastest: the lanes read x rows coalesced
+    const int p = e / d, c = e - p * d;
+    a += x[(long)p * ldr + c] * w[c * HPIX + p];
   }
   a = wave_sum(a);
   if (lane == 0) u[(long)b * ldu + j] = a + bias[j];
 }
 
 // backward, one launch: blocks [0, batch) write dr (bf16 NHWC, the trunk's output gradient) of one
-// image each (thread per column k, the image's du in LDS); the remaining blocks own 64 weight
-// columns each, 4 batch quarters per column (256 threads): dW[j][k] += sum_b du[b][j] x[b][k], the
-// quarters added in order through LDS (deterministic, no atomics); the first of them adds db.
+// image each (thread per column k, the image's du in LDS); the next blocks own 16 channels of one
+// pixel each, 16 image groups per channel (256 threads): dW[j][k] += sum_b du[b][j] x[b][k], the
+// groups added in order through LDS (deterministic, no atomics); the last block adds db.
 constexpr int HEAD_CB = 256;
 constexpr int HEAD_CW = 16;  // channels per weight-gradient workgroup (x 16 image groups)
 #ifndef HEADBWD_SKIP
