@@ -19,6 +19,9 @@
 #include "common.h"
 #include "st_common.h"
 
+#ifndef ED_HEAD128_R32
+#define ED_HEAD128_R32 1
+#endif
 #ifndef ED_HEAD128_NWV
 #define ED_HEAD128_NWV 4  // waves of the c = 128 head at sampling tiles (8: DDIM 717.8 vs 716.9, no change)
 #endif
@@ -661,6 +664,12 @@ extern "C" int encdiff_st_head_fwd(const EncdiffStHeadArgs* a, void* stream) {
   const bool big = p.rows / 64 >= 256;
   int rc = big ? (p.c == 64 ? launch_head<64, 64>(p, s) : launch_head<128, 64>(p, s)) : ENCDIFF_ERR_SHAPE;
   if (rc != ENCDIFF_ERR_SHAPE) return rc;
+  // c = 128 at the 8x8 training level (8192 rows): 32-row tiles, 256 workgroups (each streams the
+  // 128 KB of proj_in + q/k/v weights for twice the rows of a 16-row tile)
+  if (ED_HEAD128_R32 && p.c == 128 && p.rows / 32 >= 256) {
+    rc = launch_head<128, 32>(p, s);
+    if (rc != ENCDIFF_ERR_SHAPE) return rc;
+  }
   if (p.c == 256) return launch_head<256, 16, 8>(p, s);
   return p.c == 64 ? launch_head<64, 16>(p, s) : launch_head<128, 16, ED_HEAD128_NWV>(p, s);
 }
