@@ -811,6 +811,9 @@ constexpr int STWG_KINDS[][2] = {{1, 4}, {1, 16}, {4, 4}, {3, 4}, {2, 8}, {2, 16
 #ifndef STWG_PF
 #define STWG_PF 1
 #endif
+#ifndef ED_HEADBWD64_R32
+#define ED_HEADBWD64_R32 0  // A/B: the c = 64 head backward on 32-row tiles at training batches too
+#endif
 #ifndef STWG_PF_TILES
 #define STWG_PF_TILES 16
 #endif
@@ -1040,7 +1043,9 @@ extern "C" int encdiff_st_head_bwd(const EncdiffStHeadBwdArgs* a, void* stream) 
                     ((uintptr_t)p.dk2 & 7) || ((uintptr_t)p.dv2 & 7) || p.ld_dkv % 4))
     return ENCDIFF_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  if (p.c == 64) return p.rows % 64 == 0 && p.rows / 64 >= 256 ? launch_head_bwd<64, 64>(p, s) : launch_head_bwd<64, 32>(p, s);
+  if (p.c == 64)
+    return !ED_HEADBWD64_R32 && p.rows % 64 == 0 && p.rows / 64 >= 256 ? launch_head_bwd<64, 64>(p, s)
+                                                                        : launch_head_bwd<64, 32>(p, s);
   return launch_head_bwd<128, 32>(p, s);
 }
 
