@@ -19,6 +19,9 @@
 #include "common.h"
 #include "st_common.h"
 
+#ifndef ED_HEAD64_R32
+#define ED_HEAD64_R32 0  // A/B: the c = 64 head on 32-row tiles at training batches
+#endif
 #ifndef ED_HEAD128_R32
 #define ED_HEAD128_R32 1
 #endif
@@ -662,7 +665,9 @@ extern "C" int encdiff_st_head_fwd(const EncdiffStHeadArgs* a, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   // 64-row tiles at training batches, 16 rows when that leaves most CUs idle (sampling)
   const bool big = p.rows / 64 >= 256;
-  int rc = big ? (p.c == 64 ? launch_head<64, 64>(p, s) : launch_head<128, 64>(p, s)) : ENCDIFF_ERR_SHAPE;
+  int rc = big ? (p.c == 64 ? (ED_HEAD64_R32 ? launch_head<64, 32>(p, s) : launch_head<64, 64>(p, s))
+                             : launch_head<128, 64>(p, s))
+                : ENCDIFF_ERR_SHAPE;
   if (rc != ENCDIFF_ERR_SHAPE) return rc;
   // c = 128 at the 8x8 training level (8192 rows): 32-row tiles, 256 workgroups (each streams the
   // 128 KB of proj_in + q/k/v weights for twice the rows of a 16-row tile)
