@@ -154,7 +154,9 @@ def main():
     if rt is None:
         sys.exit("no libclang_rt.asan-x86_64.so under /opt/rocm/lib/llvm")
     lib = build()
-    env = dict(os.environ, LD_PRELOAD=rt, ENCDIFF_LIB=lib,
+    # the ASan runtime goes first; whatever the environment already preloads stays preloaded
+    pre = " ".join(x for x in (rt, os.environ.get("LD_PRELOAD", "")) if x)
+    env = dict(os.environ, LD_PRELOAD=pre, ENCDIFF_LIB=lib,
                ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0:alloc_dealloc_mismatch=0:"
                             "detect_odr_violation=0:halt_on_error=1")
     r = subprocess.run([sys.executable, os.path.abspath(__file__), "--checks"], env=env, capture_output=True, text=True)
