@@ -88,6 +88,9 @@ ST_TAIL_HEAD_MAXC = int(os.environ.get("ENCDIFF_ST_TAIL_HEAD_MAXC", "256"))
 ST_TAIL_HEAD_MAX_B = int(os.environ.get("ENCDIFF_ST_TAIL_HEAD_MAX_B", "32"))
 # ... and in the training forward, saving the activations up to norm3 for the (unfused) backward
 ST_TAIL_HEAD_TRAIN = os.environ.get("ENCDIFF_ST_TAIL_HEAD_TRAIN", "1") != "0"
+# A/B: the c = 128 training tail in head mode too (up to norm3; the GEGLU feed-forward and proj_out
+# as GEMM launches, which share the weights across row tiles instead of streaming them per tile)
+ST_TAIL_C128_HEAD = os.environ.get("ENCDIFF_ST_TAIL_C128_HEAD", "0") == "1"
 # ... and their head (GroupNorm statistics from x, proj_in, norm1, q/k/v) as one kernel too: off by
 # default -- DDIM B=8 716 -> 705 steps/s with it (8 workgroups at the 4x4 level each stream the
 # 512 KB of proj_in + q/k/v weights; the GroupNorm + GEMM + LayerNorm + GEMM launches spread them)
@@ -874,6 +877,11 @@ class UNetExecutor:
         ops.attention_fwd(q, k, v, S["o1"], S["lse1"], B, s.heads, ntok, ntok, s.dh, fp8=s.fp8)
         k2 = self.KV[:, s.kv_off:s.kv_off + c]
         v2 = self.KV[:, s.kv_off + c:s.kv_off + 2 * c]
+        if (ST_TAIL_FUSED and ST_TAIL_C128_HEAD and not self.infer and c == 128
+                and ops.st_tail_fwd(S["o1"], S["t0"], x, k2, v2, self._tail_weights(s), S["out"], B * ntok, c,
+                                    ntok, s.heads, self.lu, LN_EPS, head=(S["t2"], S["n3"]),
+                                    save={k: S[k] for k in ("t1", "n2", "q2", "o2", "t2", "n3", "s2", "s3", "lse2")})):
+            return self._st_ff(s, x, S)
         if ST_TAIL_FUSED and c <= ST_TAIL_MAXC and (self.infer or ST_TAIL_TRAIN):
             save = None if self.infer else {k: S[k] for k in ("t1", "n2", "q2", "o2", "t2", "n3", "f", "a", "t3",
                                                              "s2", "s3")}
